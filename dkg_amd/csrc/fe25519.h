@@ -1,0 +1,318 @@
+// GF(2^255-19) arithmetic for gfx950 in 32-bit VALU ops.
+//
+// Representation: ten unsigned 32-bit limbs in radix 2^25.5 (limb i holds 26 bits for even i,
+// 25 bits for odd i; bit offsets 0,26,51,77,102,128,153,179,204,230).  A product limb pair is
+// one v_mad_u64_u32 (32x32 -> 64 plus a 64-bit addend), which the microbenchmark in
+// tools/ubench/intrate2.hip measured at the same issue cost as v_mul_lo_u32 / v_mul_hi_u32, so a
+// field multiply is 100 MADs + 9 x19 pre-multiplies + one 64-bit carry pass (a square is 55 MADs).
+// The pseudo-Mersenne fold 2^255 = 19 is applied inside the product (no Montgomery form: the
+// x19 fold is cheaper for this prime than a Montgomery reduction; see DESIGN.md "field").
+//
+// Bounds (checked by tools/fe_bounds.py): a "tight" element has limbs <= 2^26 (even) /
+// 2^25 (odd) plus a carry remainder < 2^18; fe_mul/fe_sq accept inputs with limbs < 2^27.585 on
+// both sides (sum over one output limb of the ten 19/38-weighted products stays < 2^64), and
+// produce tight output.  fe_add of two tight values and fe_sub(a, b) = a + 2p - b with tight b are
+// valid mul inputs; anything looser goes through fe_carry first.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DKG_DEV __device__ __forceinline__
+
+struct fe {
+  uint32_t v[10];
+};
+
+namespace fe_const {
+// 2*p in radix 2^25.5 (limbwise), the bias added by fe_sub.
+constexpr uint32_t P2_0 = 0x7ffffdau;  // 2*(2^26 - 19)
+constexpr uint32_t P2_E = 0x7fffffeu;  // 2*(2^26 - 1)
+constexpr uint32_t P2_O = 0x3fffffeu;  // 2*(2^25 - 1)
+}  // namespace fe_const
+
+DKG_DEV void fe_set(fe& r, const uint32_t (&c)[10]) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = c[i];
+}
+DKG_DEV void fe_zero(fe& r) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = 0;
+}
+DKG_DEV void fe_one(fe& r) {
+  fe_zero(r);
+  r.v[0] = 1;
+}
+DKG_DEV void fe_copy(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = a.v[i];
+}
+DKG_DEV void fe_add(fe& r, const fe& a, const fe& b) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = a.v[i] + b.v[i];
+}
+// r = a - b + 2p  (b must be tight)
+DKG_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
+  r.v[0] = a.v[0] + fe_const::P2_0 - b.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; i++) r.v[i] = a.v[i] + ((i & 1) ? fe_const::P2_O : fe_const::P2_E) - b.v[i];
+}
+// r = 2p - a  (a tight)
+DKG_DEV void fe_neg(fe& r, const fe& a) {
+  r.v[0] = fe_const::P2_0 - a.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; i++) r.v[i] = ((i & 1) ? fe_const::P2_O : fe_const::P2_E) - a.v[i];
+}
+
+// One parallel carry pass on 32-bit limbs: output limbs <= 2^26/2^25 + 2^7 (tight).
+DKG_DEV void fe_carry(fe& r, const fe& a) {
+  uint32_t c[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) c[i] = a.v[i] >> ((i & 1) ? 25 : 26);
+  r.v[0] = (a.v[0] & 0x3ffffffu) + 19u * c[9];
+#pragma unroll
+  for (int i = 1; i < 10; i++) r.v[i] = (a.v[i] & ((i & 1) ? 0x1ffffffu : 0x3ffffffu)) + c[i - 1];
+}
+
+DKG_DEV uint64_t mul32(uint32_t a, uint32_t b) { return (uint64_t)a * (uint64_t)b; }
+
+// Carry the ten 64-bit column sums into a tight element.
+DKG_DEV void fe_carry64(fe& r, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4,
+                        uint64_t h5, uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+  uint64_t c;
+  c = h0 >> 26; h1 += c; h0 &= 0x3ffffff;
+  c = h4 >> 26; h5 += c; h4 &= 0x3ffffff;
+  c = h1 >> 25; h2 += c; h1 &= 0x1ffffff;
+  c = h5 >> 25; h6 += c; h5 &= 0x1ffffff;
+  c = h2 >> 26; h3 += c; h2 &= 0x3ffffff;
+  c = h6 >> 26; h7 += c; h6 &= 0x3ffffff;
+  c = h3 >> 25; h4 += c; h3 &= 0x1ffffff;
+  c = h7 >> 25; h8 += c; h7 &= 0x1ffffff;
+  c = h4 >> 26; h5 += c; h4 &= 0x3ffffff;
+  c = h8 >> 26; h9 += c; h8 &= 0x3ffffff;
+  c = h9 >> 25; h0 += c * 19; h9 &= 0x1ffffff;
+  c = h0 >> 26; h1 += c; h0 &= 0x3ffffff;
+  r.v[0] = (uint32_t)h0; r.v[1] = (uint32_t)h1; r.v[2] = (uint32_t)h2; r.v[3] = (uint32_t)h3;
+  r.v[4] = (uint32_t)h4; r.v[5] = (uint32_t)h5; r.v[6] = (uint32_t)h6; r.v[7] = (uint32_t)h7;
+  r.v[8] = (uint32_t)h8; r.v[9] = (uint32_t)h9;
+}
+
+DKG_DEV void fe_mul(fe& r, const fe& f, const fe& g) {
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
+  const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
+  const uint32_t g1_19 = 19u * g1, g2_19 = 19u * g2, g3_19 = 19u * g3, g4_19 = 19u * g4;
+  const uint32_t g5_19 = 19u * g5, g6_19 = 19u * g6, g7_19 = 19u * g7, g8_19 = 19u * g8;
+  const uint32_t g9_19 = 19u * g9;
+  const uint32_t f1_2 = 2u * f1, f3_2 = 2u * f3, f5_2 = 2u * f5, f7_2 = 2u * f7, f9_2 = 2u * f9;
+  uint64_t h0 = mul32(f0, g0) + mul32(f1_2, g9_19) + mul32(f2, g8_19) + mul32(f3_2, g7_19) +
+                mul32(f4, g6_19) + mul32(f5_2, g5_19) + mul32(f6, g4_19) + mul32(f7_2, g3_19) +
+                mul32(f8, g2_19) + mul32(f9_2, g1_19);
+  uint64_t h1 = mul32(f0, g1) + mul32(f1, g0) + mul32(f2, g9_19) + mul32(f3, g8_19) +
+                mul32(f4, g7_19) + mul32(f5, g6_19) + mul32(f6, g5_19) + mul32(f7, g4_19) +
+                mul32(f8, g3_19) + mul32(f9, g2_19);
+  uint64_t h2 = mul32(f0, g2) + mul32(f1_2, g1) + mul32(f2, g0) + mul32(f3_2, g9_19) +
+                mul32(f4, g8_19) + mul32(f5_2, g7_19) + mul32(f6, g6_19) + mul32(f7_2, g5_19) +
+                mul32(f8, g4_19) + mul32(f9_2, g3_19);
+  uint64_t h3 = mul32(f0, g3) + mul32(f1, g2) + mul32(f2, g1) + mul32(f3, g0) + mul32(f4, g9_19) +
+                mul32(f5, g8_19) + mul32(f6, g7_19) + mul32(f7, g6_19) + mul32(f8, g5_19) +
+                mul32(f9, g4_19);
+  uint64_t h4 = mul32(f0, g4) + mul32(f1_2, g3) + mul32(f2, g2) + mul32(f3_2, g1) + mul32(f4, g0) +
+                mul32(f5_2, g9_19) + mul32(f6, g8_19) + mul32(f7_2, g7_19) + mul32(f8, g6_19) +
+                mul32(f9_2, g5_19);
+  uint64_t h5 = mul32(f0, g5) + mul32(f1, g4) + mul32(f2, g3) + mul32(f3, g2) + mul32(f4, g1) +
+                mul32(f5, g0) + mul32(f6, g9_19) + mul32(f7, g8_19) + mul32(f8, g7_19) +
+                mul32(f9, g6_19);
+  uint64_t h6 = mul32(f0, g6) + mul32(f1_2, g5) + mul32(f2, g4) + mul32(f3_2, g3) + mul32(f4, g2) +
+                mul32(f5_2, g1) + mul32(f6, g0) + mul32(f7_2, g9_19) + mul32(f8, g8_19) +
+                mul32(f9_2, g7_19);
+  uint64_t h7 = mul32(f0, g7) + mul32(f1, g6) + mul32(f2, g5) + mul32(f3, g4) + mul32(f4, g3) +
+                mul32(f5, g2) + mul32(f6, g1) + mul32(f7, g0) + mul32(f8, g9_19) + mul32(f9, g8_19);
+  uint64_t h8 = mul32(f0, g8) + mul32(f1_2, g7) + mul32(f2, g6) + mul32(f3_2, g5) + mul32(f4, g4) +
+                mul32(f5_2, g3) + mul32(f6, g2) + mul32(f7_2, g1) + mul32(f8, g0) +
+                mul32(f9_2, g9_19);
+  uint64_t h9 = mul32(f0, g9) + mul32(f1, g8) + mul32(f2, g7) + mul32(f3, g6) + mul32(f4, g5) +
+                mul32(f5, g4) + mul32(f6, g3) + mul32(f7, g2) + mul32(f8, g1) + mul32(f9, g0);
+  fe_carry64(r, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+DKG_DEV void fe_sq(fe& r, const fe& f) {
+  // Symmetric products counted once; x19 factors kept on limbs 5..9 (19 * 2^27.585 < 2^32) and
+  // the extra 2 / 4 weights moved onto the partner limb so every operand fits in 32 bits.
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t f0_2 = 2u * f0, f1_2 = 2u * f1, f2_2 = 2u * f2, f3_2 = 2u * f3, f4_2 = 2u * f4;
+  const uint32_t f5_2 = 2u * f5, f6_2 = 2u * f6, f7_2 = 2u * f7, f8_2 = 2u * f8, f9_2 = 2u * f9;
+  const uint32_t f1_4 = 4u * f1, f3_4 = 4u * f3, f5_4 = 4u * f5, f7_4 = 4u * f7;
+  const uint32_t f5_19 = 19u * f5, f6_19 = 19u * f6, f7_19 = 19u * f7, f8_19 = 19u * f8;
+  const uint32_t f9_19 = 19u * f9;
+  uint64_t h0 = mul32(f0, f0) + mul32(f1_4, f9_19) + mul32(f2_2, f8_19) + mul32(f3_4, f7_19) +
+                mul32(f4_2, f6_19) + mul32(f5_2, f5_19);
+  uint64_t h1 = mul32(f0_2, f1) + mul32(f2_2, f9_19) + mul32(f3_2, f8_19) + mul32(f4_2, f7_19) +
+                mul32(f5_2, f6_19);
+  uint64_t h2 = mul32(f0_2, f2) + mul32(f1_2, f1) + mul32(f3_4, f9_19) + mul32(f4_2, f8_19) +
+                mul32(f5_4, f7_19) + mul32(f6, f6_19);
+  uint64_t h3 = mul32(f0_2, f3) + mul32(f1_2, f2) + mul32(f4_2, f9_19) + mul32(f5_2, f8_19) +
+                mul32(f6_2, f7_19);
+  uint64_t h4 = mul32(f0_2, f4) + mul32(f1_2, f3_2) + mul32(f2, f2) + mul32(f5_4, f9_19) +
+                mul32(f6_2, f8_19) + mul32(f7_2, f7_19);
+  uint64_t h5 = mul32(f0_2, f5) + mul32(f1_2, f4) + mul32(f2_2, f3) + mul32(f6_2, f9_19) +
+                mul32(f7_2, f8_19);
+  uint64_t h6 = mul32(f0_2, f6) + mul32(f1_2, f5_2) + mul32(f2_2, f4) + mul32(f3_2, f3) +
+                mul32(f7_4, f9_19) + mul32(f8, f8_19);
+  uint64_t h7 = mul32(f0_2, f7) + mul32(f1_2, f6) + mul32(f2_2, f5) + mul32(f3_2, f4) +
+                mul32(f8_2, f9_19);
+  uint64_t h8 = mul32(f0_2, f8) + mul32(f1_2, f7_2) + mul32(f2_2, f6) + mul32(f3_2, f5_2) +
+                mul32(f4, f4) + mul32(f9_2, f9_19);
+  uint64_t h9 = mul32(f0_2, f9) + mul32(f1_2, f8) + mul32(f2_2, f7) + mul32(f3_2, f6) +
+                mul32(f4_2, f5);
+  fe_carry64(r, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+// r = a * k for a small constant k < 2^12 (a tight).
+DKG_DEV void fe_mul_small(fe& r, const fe& a, uint32_t k) {
+  uint64_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = mul32(a.v[i], k);
+  fe_carry64(r, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+}
+
+DKG_DEV void fe_sqn(fe& r, const fe& a, int n) {
+  fe_sq(r, a);
+  for (int i = 1; i < n; i++) fe_sq(r, r);
+}
+
+// z^(2^252 - 3), the exponent of sqrt_ratio (RFC 9496 section 4.2 / ref10 pow22523).
+DKG_DEV void fe_pow22523(fe& out, const fe& z) {
+  fe t0, t1, t2;
+  fe_sq(t0, z);             // 2
+  fe_sqn(t1, t0, 2);        // 8
+  fe_mul(t1, z, t1);        // 9
+  fe_mul(t0, t0, t1);       // 11
+  fe_sq(t0, t0);            // 22
+  fe_mul(t0, t1, t0);       // 2^5 - 1
+  fe_sqn(t1, t0, 5);
+  fe_mul(t0, t1, t0);       // 2^10 - 1
+  fe_sqn(t1, t0, 10);
+  fe_mul(t1, t1, t0);       // 2^20 - 1
+  fe_sqn(t2, t1, 20);
+  fe_mul(t1, t2, t1);       // 2^40 - 1
+  fe_sqn(t1, t1, 10);
+  fe_mul(t0, t1, t0);       // 2^50 - 1
+  fe_sqn(t1, t0, 50);
+  fe_mul(t1, t1, t0);       // 2^100 - 1
+  fe_sqn(t2, t1, 100);
+  fe_mul(t1, t2, t1);       // 2^200 - 1
+  fe_sqn(t1, t1, 50);
+  fe_mul(t0, t1, t0);       // 2^250 - 1
+  fe_sqn(t0, t0, 2);        // 2^252 - 4
+  fe_mul(out, t0, z);       // 2^252 - 3
+}
+
+// z^(p-2) = 1/z
+DKG_DEV void fe_invert(fe& out, const fe& z) {
+  fe t0, t1, t2, t3;
+  fe_sq(t0, z);             // 2
+  fe_sqn(t1, t0, 2);        // 8
+  fe_mul(t1, z, t1);        // 9
+  fe_mul(t0, t0, t1);       // 11
+  fe_sq(t2, t0);            // 22
+  fe_mul(t1, t1, t2);       // 2^5 - 1
+  fe_sqn(t2, t1, 5);
+  fe_mul(t1, t2, t1);       // 2^10 - 1
+  fe_sqn(t2, t1, 10);
+  fe_mul(t2, t2, t1);       // 2^20 - 1
+  fe_sqn(t3, t2, 20);
+  fe_mul(t2, t3, t2);       // 2^40 - 1
+  fe_sqn(t2, t2, 10);
+  fe_mul(t1, t2, t1);       // 2^50 - 1
+  fe_sqn(t2, t1, 50);
+  fe_mul(t2, t2, t1);       // 2^100 - 1
+  fe_sqn(t3, t2, 100);
+  fe_mul(t2, t3, t2);       // 2^200 - 1
+  fe_sqn(t2, t2, 50);
+  fe_mul(t1, t2, t1);       // 2^250 - 1
+  fe_sqn(t1, t1, 5);        // 2^255 - 32
+  fe_mul(out, t1, t0);      // 2^255 - 21
+}
+
+// Fully reduce to the canonical representative and pack little-endian into 8 words.
+DKG_DEV void fe_tobytes32(uint32_t (&s)[8], const fe& a) {
+  fe t;
+  fe_carry(t, a);
+  fe_carry(t, t);
+  // t < 2^255 + small; compute q = floor((t + 19) / 2^255) in {0,1}
+  uint32_t q = (t.v[0] + 19u) >> 26;
+  q = (t.v[1] + q) >> 25;
+  q = (t.v[2] + q) >> 26;
+  q = (t.v[3] + q) >> 25;
+  q = (t.v[4] + q) >> 26;
+  q = (t.v[5] + q) >> 25;
+  q = (t.v[6] + q) >> 26;
+  q = (t.v[7] + q) >> 25;
+  q = (t.v[8] + q) >> 26;
+  q = (t.v[9] + q) >> 25;
+  t.v[0] += 19u * q;
+  uint32_t c;
+  c = t.v[0] >> 26; t.v[1] += c; t.v[0] &= 0x3ffffffu;
+  c = t.v[1] >> 25; t.v[2] += c; t.v[1] &= 0x1ffffffu;
+  c = t.v[2] >> 26; t.v[3] += c; t.v[2] &= 0x3ffffffu;
+  c = t.v[3] >> 25; t.v[4] += c; t.v[3] &= 0x1ffffffu;
+  c = t.v[4] >> 26; t.v[5] += c; t.v[4] &= 0x3ffffffu;
+  c = t.v[5] >> 25; t.v[6] += c; t.v[5] &= 0x1ffffffu;
+  c = t.v[6] >> 26; t.v[7] += c; t.v[6] &= 0x3ffffffu;
+  c = t.v[7] >> 25; t.v[8] += c; t.v[7] &= 0x1ffffffu;
+  c = t.v[8] >> 26; t.v[9] += c; t.v[8] &= 0x3ffffffu;
+  t.v[9] &= 0x1ffffffu;
+  // pack: bit offsets 0,26,51,77,102,128,153,179,204,230
+  s[0] = t.v[0] | (t.v[1] << 26);
+  s[1] = (t.v[1] >> 6) | (t.v[2] << 19);
+  s[2] = (t.v[2] >> 13) | (t.v[3] << 13);
+  s[3] = (t.v[3] >> 19) | (t.v[4] << 6);
+  s[4] = t.v[5] | (t.v[6] << 25);
+  s[5] = (t.v[6] >> 7) | (t.v[7] << 19);
+  s[6] = (t.v[7] >> 13) | (t.v[8] << 12);
+  s[7] = (t.v[8] >> 20) | (t.v[9] << 6);
+}
+
+// Unpack 255 bits (bit 255 ignored, as dalek FieldElement::from_bytes); result may be >= p.
+DKG_DEV void fe_frombytes32(fe& r, const uint32_t (&s)[8]) {
+  r.v[0] = s[0] & 0x3ffffffu;
+  r.v[1] = ((s[0] >> 26) | (s[1] << 6)) & 0x1ffffffu;
+  r.v[2] = ((s[1] >> 19) | (s[2] << 13)) & 0x3ffffffu;
+  r.v[3] = ((s[2] >> 13) | (s[3] << 19)) & 0x1ffffffu;
+  r.v[4] = (s[3] >> 6) & 0x3ffffffu;
+  r.v[5] = s[4] & 0x1ffffffu;
+  r.v[6] = ((s[4] >> 25) | (s[5] << 7)) & 0x3ffffffu;
+  r.v[7] = ((s[5] >> 19) | (s[6] << 13)) & 0x1ffffffu;
+  r.v[8] = ((s[6] >> 12) | (s[7] << 20)) & 0x3ffffffu;
+  r.v[9] = (s[7] >> 6) & 0x1ffffffu;
+}
+
+// Canonical low bit (RFC 9496 IS_NEGATIVE) and zero test.
+DKG_DEV uint32_t fe_isneg(const fe& a) {
+  uint32_t s[8];
+  fe_tobytes32(s, a);
+  return s[0] & 1u;
+}
+DKG_DEV bool fe_iszero(const fe& a) {
+  uint32_t s[8];
+  fe_tobytes32(s, a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= s[i];
+  return o == 0;
+}
+DKG_DEV void fe_cmov(fe& r, const fe& a, bool c) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = c ? a.v[i] : r.v[i];
+}
+// r = |a| (non-negative representative), a tight
+DKG_DEV void fe_abs(fe& r, const fe& a) {
+  fe n;
+  fe_neg(n, a);
+  fe_carry(n, n);
+  bool neg = fe_isneg(a);
+  fe_copy(r, a);
+  fe_cmov(r, n, neg);
+}

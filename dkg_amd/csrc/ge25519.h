@@ -1,0 +1,352 @@
+// Edwards25519 group law (a = -1, twisted Edwards, extended coordinates) and Ristretto255
+// encode / decode / equality on gfx950.  Formulas: Hisil-Wong-Carter-Dawson 2008 unified
+// addition ("add-2008-hwcd-3") and doubling ("dbl-2008-hwcd"); Ristretto per RFC 9496 section 4.
+// The reference reaches the same group through curve25519-dalek (groups.rs:55-90): every value
+// that leaves the device is a canonical 32-byte encoding, so results are implementation-independent.
+//
+// Operand-bound rules for fe_mul(f, g) (see fe25519.h): f limbs <= 2^31, g limbs <= 2^27.75,
+// max(f) * max(g) <= 2^55.9.  The comments "<= 2^x" below track the worst limb bound.
+#pragma once
+#include "fe25519.h"
+
+struct ge_p3 {  // extended (X : Y : Z : T), x = X/Z, y = Y/Z, xy = T/Z; all tight
+  fe X, Y, Z, T;
+};
+struct ge_cached {  // (Y+X, Y-X, 2Z, 2dT), all tight: an addend prepared for ge_add
+  fe YpX, YmX, Z2, T2d;
+};
+struct ge_aff {  // affine Niels (y+x, y-x, 2dxy), tight: fixed-base table entries (Z = 1)
+  fe ypx, ymx, xy2d;
+};
+
+namespace ge_const {
+__device__ static const uint32_t D[10] = {0x35978a3u, 0xd37284u, 0x3156ebdu, 0x6a0a0eu, 0x1c029u,
+                                          0x179e898u, 0x3a03cbbu, 0x1ce7198u, 0x2e2b6ffu, 0x1480db3u};
+__device__ static const uint32_t D2[10] = {0x2b2f159u, 0x1a6e509u, 0x22add7au, 0xd4141du, 0x38052u,
+                                           0xf3d130u, 0x3407977u, 0x19ce331u, 0x1c56dffu, 0x901b67u};
+__device__ static const uint32_t SQRT_M1[10] = {0x20ea0b0u, 0x186c9d2u, 0x8f189du, 0x35697fu,
+                                                0xbd0c60u, 0x1fbd7a7u, 0x2804c9eu, 0x1e16569u,
+                                                0x4fc1du, 0xae0c92u};
+__device__ static const uint32_t SQRT_AD_MINUS_ONE[10] = {
+    0x17b2e1bu, 0x1fda812u, 0x297afd2u, 0x60dbc2u, 0x2be7638u,
+    0x1f5d1fdu, 0x27e6498u, 0x11581e7u, 0x3f2b834u, 0xdda4c6u};
+__device__ static const uint32_t INVSQRT_A_MINUS_D[10] = {
+    0x5d40eau, 0x3f6aa0u, 0x257d339u, 0xbad20bu, 0x274bc58u,
+    0x1d840u, 0x13dc8ffu, 0x19442d8u, 0x5cfaffu, 0x1e1b224u};
+__device__ static const uint32_t ONE_MINUS_D_SQ[10] = {
+    0x5fc176u, 0x1027065u, 0x2a1fc4fu, 0x1c66af1u, 0xb20684u,
+    0x70dfe4u, 0x255eedfu, 0x1af332u, 0x28b2b3eu, 0xa41cau};
+__device__ static const uint32_t D_MINUS_ONE_SQ[10] = {
+    0xed4d20u, 0x156aa91u, 0x3332635u, 0x16580f0u, 0x34a7928u,
+    0x9b4eebu, 0x26997a9u, 0x48299bu, 0x3af66c2u, 0x165a2cdu};
+}  // namespace ge_const
+
+DKG_DEV void fe_ld(fe& r, const uint32_t* c) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = c[i];
+}
+
+DKG_DEV void ge_identity(ge_p3& p) {
+  fe_zero(p.X);
+  fe_one(p.Y);
+  fe_one(p.Z);
+  fe_zero(p.T);
+}
+
+DKG_DEV void ge_to_cached(ge_cached& c, const ge_p3& p) {
+  fe t;
+  fe_add(t, p.Y, p.X);
+  fe_carry(c.YpX, t);
+  fe_sub(t, p.Y, p.X);
+  fe_carry(c.YmX, t);
+  fe_add(t, p.Z, p.Z);
+  fe_carry(c.Z2, t);
+  fe d2;
+  fe_ld(d2, ge_const::D2);
+  fe_mul(c.T2d, p.T, d2);
+}
+
+DKG_DEV void ge_cached_neg(ge_cached& r, const ge_cached& c) {
+  fe_copy(r.YpX, c.YmX);
+  fe_copy(r.YmX, c.YpX);
+  fe_copy(r.Z2, c.Z2);
+  fe_neg(r.T2d, c.T2d);
+  fe_carry(r.T2d, r.T2d);
+}
+
+// r = p + q  (8M).  r may alias p.
+DKG_DEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
+  fe a, b, c, d, e, f, g, h, t;
+  fe_sub(t, p.Y, p.X);      // <= 1.5*2^27
+  fe_mul(a, t, q.YmX);
+  fe_add(t, p.Y, p.X);      // <= 2^27
+  fe_mul(b, t, q.YpX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(d, p.Z, q.Z2);
+  fe_sub(e, b, a);          // <= 1.5*2^27
+  fe_sub(f, d, c);          // <= 1.5*2^27
+  fe_add(g, d, c);          // <= 2^27
+  fe_add(h, b, a);          // <= 2^27
+  fe_mul(r.X, e, f);
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, f, g);
+  fe_mul(r.T, e, h);
+}
+
+// r = p - q
+DKG_DEV void ge_sub(ge_p3& r, const ge_p3& p, const ge_cached& q) {
+  fe a, b, c, d, e, f, g, h, t;
+  fe_sub(t, p.Y, p.X);
+  fe_mul(a, t, q.YpX);
+  fe_add(t, p.Y, p.X);
+  fe_mul(b, t, q.YmX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(d, p.Z, q.Z2);
+  fe_sub(e, b, a);
+  fe_add(f, d, c);          // sign of c flipped for -q
+  fe_sub(g, d, c);
+  fe_add(h, b, a);
+  fe_mul(r.X, e, f);
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, f, g);
+  fe_mul(r.T, e, h);
+}
+
+// r = p + q with q affine Niels (Z = 1): 7M.
+DKG_DEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_aff& q) {
+  fe a, b, c, d, e, f, g, h, t;
+  fe_sub(t, p.Y, p.X);
+  fe_mul(a, t, q.ymx);
+  fe_add(t, p.Y, p.X);
+  fe_mul(b, t, q.ypx);
+  fe_mul(c, p.T, q.xy2d);
+  fe_add(d, p.Z, p.Z);      // <= 2^27
+  fe_sub(e, b, a);
+  fe_sub(f, d, c);          // <= 2^27 + 2^27
+  fe_add(g, d, c);          // <= 1.5*2^27
+  fe_add(h, b, a);
+  fe_mul(r.X, f, e);        // f <= 2^28 as first operand
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, f, g);
+  fe_mul(r.T, e, h);
+}
+
+DKG_DEV void ge_msub(ge_p3& r, const ge_p3& p, const ge_aff& q) {
+  fe a, b, c, d, e, f, g, h, t;
+  fe_sub(t, p.Y, p.X);
+  fe_mul(a, t, q.ypx);
+  fe_add(t, p.Y, p.X);
+  fe_mul(b, t, q.ymx);
+  fe_mul(c, p.T, q.xy2d);
+  fe_add(d, p.Z, p.Z);
+  fe_sub(e, b, a);
+  fe_add(f, d, c);
+  fe_sub(g, d, c);          // <= 2^28
+  fe_add(h, b, a);
+  fe_mul(r.X, f, e);
+  fe_mul(r.Y, g, h);        // g <= 2^28 first operand
+  fe_mul(r.Z, g, f);
+  fe_mul(r.T, e, h);
+}
+
+// r = 2p (4S + 4M); with_t = false skips T (valid when the next op is another doubling).
+template <bool with_t = true>
+DKG_DEV void ge_dbl(ge_p3& r, const ge_p3& p) {
+  fe a, b, c, e, f, g, h, t;
+  fe_sq(a, p.X);
+  fe_sq(b, p.Y);
+  fe_sq(c, p.Z);
+  fe_add(c, c, c);          // <= 2^27
+  fe_add(t, p.X, p.Y);      // <= 2^27
+  fe_sq(t, t);
+  fe_add(h, a, b);          // <= 2^27             (= -H_std)
+  fe_sub(e, h, t);          // <= 2^28             (= -E_std)
+  fe_sub(g, a, b);          // <= 1.5*2^27         (= -G_std)
+  fe_add(f, c, g);          // <= 2.5*2^27
+  fe_carry(f, f);           // tight               (= -F_std)
+  fe_mul(r.X, e, f);
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, f, g);
+  if (with_t) fe_mul(r.T, e, h);
+}
+
+// ---- Ristretto255 (RFC 9496 section 4.3) ----
+
+// (was_square, r) = SQRT_RATIO_M1(u, v); u, v tight.
+DKG_DEV bool fe_sqrt_ratio_m1(fe& r, const fe& u, const fe& v) {
+  fe v3, v7, t, chk, neg_u, neg_u_i, sqrtm1;
+  fe_ld(sqrtm1, ge_const::SQRT_M1);
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);        // v^3
+  fe_sq(v7, v3);
+  fe_mul(v7, v7, v);        // v^7
+  fe_mul(t, u, v7);
+  fe_pow22523(t, t);        // (u v^7)^((p-5)/8)
+  fe_mul(t, t, v3);
+  fe_mul(r, t, u);          // r = u v^3 (u v^7)^((p-5)/8)
+  fe_sq(chk, r);
+  fe_mul(chk, chk, v);      // v r^2
+  fe_neg(neg_u, u);
+  fe_carry(neg_u, neg_u);
+  fe_mul(neg_u_i, neg_u, sqrtm1);
+  fe d;
+  fe_sub(d, chk, u);
+  bool correct = fe_iszero(d);
+  fe_sub(d, chk, neg_u);
+  bool flipped = fe_iszero(d);
+  fe_sub(d, chk, neg_u_i);
+  bool flipped_i = fe_iszero(d);
+  fe r_prime;
+  fe_mul(r_prime, r, sqrtm1);
+  fe_cmov(r, r_prime, flipped || flipped_i);
+  fe_abs(r, r);
+  return correct || flipped;
+}
+
+// Decode 32 bytes (as 8 LE words).  Returns false for a non-canonical / invalid encoding
+// (dalek CompressedRistretto::decompress -> None, groups.rs:78-81).
+DKG_DEV bool ristretto_decode(ge_p3& p, const uint32_t (&w)[8]) {
+  // canonical: s < p and s even
+  fe s;
+  fe_frombytes32(s, w);
+  uint32_t chk[8];
+  fe_tobytes32(chk, s);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) diff |= chk[i] ^ w[i];
+  bool ok = (diff == 0) && ((w[0] & 1u) == 0);
+  fe ss, u1, u2, u2sq, v, one, t, inv, den_x, den_y, dd;
+  fe_one(one);
+  fe_sq(ss, s);
+  fe_sub(u1, one, ss);
+  fe_carry(u1, u1);
+  fe_add(u2, one, ss);
+  fe_carry(u2, u2);
+  fe_sq(u2sq, u2);
+  fe_ld(dd, ge_const::D);
+  fe_sq(t, u1);
+  fe_mul(t, t, dd);          // D u1^2
+  fe_add(t, t, u2sq);
+  fe_carry(t, t);
+  fe_neg(v, t);              // v = -(D u1^2) - u2^2
+  fe_carry(v, v);
+  fe_mul(t, v, u2sq);
+  bool was_sq = fe_sqrt_ratio_m1(inv, one, t);
+  fe_mul(den_x, inv, u2);
+  fe_mul(den_y, inv, den_x);
+  fe_mul(den_y, den_y, v);
+  fe_add(t, s, s);
+  fe_carry(t, t);
+  fe_mul(t, t, den_x);
+  fe_abs(p.X, t);
+  fe_mul(p.Y, u1, den_y);
+  fe_one(p.Z);
+  fe_mul(p.T, p.X, p.Y);
+  ok = ok && was_sq && !fe_isneg(p.T) && !fe_iszero(p.Y);
+  return ok;
+}
+
+// Encode to 8 LE words (RFC 9496 ENCODE).
+DKG_DEV void ristretto_encode(uint32_t (&w)[8], const ge_p3& p) {
+  fe u1, u2, t, inv, den1, den2, z_inv, ix0, iy0, ench, x, y, den_inv, sqrtm1, one;
+  fe_ld(sqrtm1, ge_const::SQRT_M1);
+  fe_one(one);
+  fe_add(t, p.Z, p.Y);
+  fe_sub(u1, p.Z, p.Y);
+  fe_mul(u1, t, u1);                 // (Z+Y)(Z-Y)
+  fe_mul(u2, p.X, p.Y);
+  fe_sq(t, u2);
+  fe_mul(t, t, u1);
+  fe_sqrt_ratio_m1(inv, one, t);
+  fe_mul(den1, inv, u1);
+  fe_mul(den2, inv, u2);
+  fe_mul(z_inv, den1, den2);
+  fe_mul(z_inv, z_inv, p.T);
+  fe_mul(ix0, p.X, sqrtm1);
+  fe_mul(iy0, p.Y, sqrtm1);
+  fe_ld(t, ge_const::INVSQRT_A_MINUS_D);
+  fe_mul(ench, den1, t);
+  fe_mul(t, p.T, z_inv);
+  bool rotate = fe_isneg(t);
+  fe_copy(x, p.X);
+  fe_copy(y, p.Y);
+  fe_cmov(x, iy0, rotate);
+  fe_cmov(y, ix0, rotate);
+  fe_copy(den_inv, den2);
+  fe_cmov(den_inv, ench, rotate);
+  fe_mul(t, x, z_inv);
+  if (fe_isneg(t)) {
+    fe_neg(y, y);
+    fe_carry(y, y);
+  }
+  fe_sub(t, p.Z, y);
+  fe_mul(t, den_inv, t);
+  fe_abs(t, t);
+  fe_tobytes32(w, t);
+}
+
+// Ristretto equality (RFC 9496 EQUALS): X1 Y2 == Y1 X2 or Y1 Y2 == X1 X2.
+DKG_DEV bool ristretto_eq(const ge_p3& p, const ge_p3& q) {
+  fe a, b, d;
+  fe_mul(a, p.X, q.Y);
+  fe_mul(b, p.Y, q.X);
+  fe_sub(d, a, b);
+  bool e1 = fe_iszero(d);
+  fe_mul(a, p.Y, q.Y);
+  fe_mul(b, p.X, q.X);
+  fe_sub(d, a, b);
+  return e1 || fe_iszero(d);
+}
+
+// Elligator one-way map (RFC 9496 MAP) of 255 bits given as 8 words (bit 255 masked).
+DKG_DEV void ristretto_elligator(ge_p3& p, const uint32_t (&w)[8]) {
+  uint32_t m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = w[i];
+  m[7] &= 0x7fffffffu;
+  fe t0, r, u, v, s, s_prime, c, n, w0, w1, w2, w3, one, dd, tmp, tmp2, sqrtm1;
+  fe_frombytes32(t0, m);
+  fe_carry(t0, t0);
+  fe_one(one);
+  fe_ld(dd, ge_const::D);
+  fe_ld(sqrtm1, ge_const::SQRT_M1);
+  fe_sq(r, t0);
+  fe_mul(r, r, sqrtm1);                       // r = i t^2
+  fe_add(tmp, r, one);
+  fe_ld(tmp2, ge_const::ONE_MINUS_D_SQ);
+  fe_mul(u, tmp, tmp2);                       // u = (r+1)(1-d^2)
+  fe_mul(tmp, r, dd);
+  fe_add(tmp, tmp, one);
+  fe_neg(tmp, tmp);
+  fe_carry(tmp, tmp);                         // -1 - r d
+  fe_add(tmp2, r, dd);
+  fe_mul(v, tmp, tmp2);                       // v = (-1 - r d)(r + d)
+  bool was_sq = fe_sqrt_ratio_m1(s, u, v);
+  fe_mul(s_prime, s, t0);
+  fe_abs(s_prime, s_prime);
+  fe_neg(s_prime, s_prime);
+  fe_carry(s_prime, s_prime);
+  if (!was_sq) fe_copy(s, s_prime);
+  fe_neg(c, one);
+  fe_carry(c, c);
+  if (!was_sq) fe_copy(c, r);
+  fe_sub(tmp, r, one);
+  fe_mul(n, c, tmp);
+  fe_ld(tmp2, ge_const::D_MINUS_ONE_SQ);
+  fe_mul(n, n, tmp2);
+  fe_sub(n, n, v);
+  fe_carry(n, n);                             // N = c (r-1) (d-1)^2 - v
+  fe_add(tmp, s, s);
+  fe_carry(tmp, tmp);
+  fe_mul(w0, tmp, v);                         // 2 s v
+  fe_ld(tmp2, ge_const::SQRT_AD_MINUS_ONE);
+  fe_mul(w1, n, tmp2);
+  fe_sq(tmp, s);
+  fe_sub(w2, one, tmp);
+  fe_carry(w2, w2);
+  fe_add(w3, one, tmp);
+  fe_mul(p.X, w0, w3);
+  fe_mul(p.Y, w2, w1);
+  fe_mul(p.Z, w1, w3);
+  fe_mul(p.T, w0, w2);
+}
