@@ -1,0 +1,167 @@
+"""Pin the CPU oracle against the golden fixtures (libsodium-generated, tools/gen_golden.py).
+
+These run on CPU only.  They are the reason the oracle may be trusted as the checker for the HIP
+path: every group / scalar / ceremony output it produces equals an independent implementation.
+"""
+import ctypes
+
+import pytest
+
+from tests import oracle_lib as O
+
+H = bytes.fromhex
+
+
+def chunks(hexstr, size=32):
+    b = H(hexstr)
+    return [b[i:i + size] for i in range(0, len(b), size)]
+
+
+def test_base_multiples(golden):
+    g = golden("kat_group.json")
+    for e in g["base_multiples"]:
+        k = e["k"].to_bytes(32, "little")
+        assert O.base_mul(k).hex() == e["P"], e["k"]
+    for e in g["base_mul"]:
+        assert O.base_mul(H(e["k"])).hex() == e["P"]
+
+
+def test_hash_to_group_and_uniform(golden):
+    g = golden("kat_group.json")
+    for e in g["hash_to_group"]:
+        m = H(e["msg"])
+        out, _ = O.call32("or_pt_hash_to_group", m, len(m))
+        assert out.hex() == e["P"]
+    # CommitmentKey::generate(b"Example of a shared string.") (commitment.rs:13-17)
+    assert g["hash_to_group"][0]["P"].startswith("242496c4")
+    for e in g["from_uniform_bytes"]:
+        out, _ = O.call32("or_pt_from_uniform_bytes", H(e["in"]))
+        assert out.hex() == e["P"]
+
+
+def test_point_ops(golden):
+    g = golden("kat_group.json")
+    for e in g["add"]:
+        assert O.call32("or_pt_add", H(e["P"]), H(e["Q"]))[0].hex() == e["sum"]
+        assert O.call32("or_pt_sub", H(e["P"]), H(e["Q"]))[0].hex() == e["diff"]
+        assert O.call32("or_pt_neg", H(e["P"]))[0].hex() == e["neg_P"]
+        assert O.lib().or_pt_eq(H(e["P"]), H(e["P"])) == 1
+        assert O.lib().or_pt_eq(H(e["P"]), H(e["Q"])) == 0
+    for e in g["mul"]:
+        assert O.call32("or_pt_mul", H(e["P"]), H(e["k"]))[0].hex() == e["kP"]
+
+
+def test_invalid_encodings(golden):
+    for b in golden("kat_group.json")["invalid_encodings"]:
+        assert O.lib().or_pt_valid(H(b)) == 0, b
+    assert O.lib().or_pt_valid(bytes(32)) == 1  # identity decodes
+
+
+@pytest.mark.parametrize("idx", range(10))
+def test_msm(golden, idx):
+    c = golden("kat_group.json")["msm"][idx]
+    assert O.msm(H(c["scalars"]), H(c["points"])).hex() == c["out"], c["N"]
+
+
+def test_scalar_ops(golden):
+    s = golden("kat_scalar.json")
+    for e in s["reduce_wide"]:
+        assert O.call32("or_sc_reduce_wide", H(e["in"]))[0].hex() == e["out"]
+    for e in s["ops"]:
+        a, b = H(e["a"]), H(e["b"])
+        assert O.call32("or_sc_add", a, b)[0].hex() == e["add"]
+        assert O.call32("or_sc_sub", a, b)[0].hex() == e["sub"]
+        assert O.call32("or_sc_mul", a, b)[0].hex() == e["mul"]
+        assert O.call32("or_sc_neg", a)[0].hex() == e["neg_a"]
+        assert O.call32("or_sc_invert", a)[0].hex() == e["inv_a"]
+
+
+def test_polynomial_kats(golden):
+    s = golden("kat_scalar.json")
+    # polynomial.rs:240-249: (1 + 3x) of degree 4 at 3 == 10
+    kt = s["poly_tests"]
+    coeffs = b"".join(c.to_bytes(32, "little") for c in kt["coeffs"])
+    assert O.poly_eval(coeffs, kt["x"].to_bytes(32, "little")) == kt["value"].to_bytes(32, "little")
+    for e in s["poly_eval"]:
+        for x, v in zip(e["points"], e["values"]):
+            assert O.poly_eval(H(e["coeffs"]), x.to_bytes(32, "little")).hex() == v
+    lg = s["lagrange"]
+    xs = b"".join(x.to_bytes(32, "little") for x in lg["xs"])
+    ys = b"".join(y.to_bytes(32, "little") for y in lg["ys"])
+    out = ctypes.create_string_buffer(32)
+    O.lib().or_lagrange(out, bytes(32), ys, xs, 3)
+    assert int.from_bytes(out.raw, "little") == lg["at_zero"] == 13
+
+
+def test_dealer_rng(golden):
+    r = golden("kat_scalar.json")["dealer_rng"]
+    seed = O.dealer_seed(H(r["master"]), r["ceremony"], r["dealer"])
+    assert seed.hex() == r["seed"]
+    out = ctypes.create_string_buffer(128)
+    O.lib().or_chacha20_stream(seed, 0, out, 128)
+    assert out.raw.hex() == r["stream_head"]
+    a, b = O.dealer_coeffs(seed, r["t"])
+    assert chunks(a.hex()) == [H(x) for x in r["a"]]
+    assert chunks(b.hex()) == [H(x) for x in r["b"]]
+
+
+CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.json",
+              "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
+FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
+          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json"]
+
+
+@pytest.mark.parametrize("name", CEREMONIES)
+def test_share_gen(golden, name):
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    master = H(c["master_seed"])
+    a = b"".join(O.dealer_coeffs(O.dealer_seed(master, c["ceremony"], i), t)[0] for i in range(n))
+    b = b"".join(O.dealer_coeffs(O.dealer_seed(master, c["ceremony"], i), t)[1] for i in range(n))
+    assert a.hex() == c["a"] and b.hex() == c["b"]
+    E, A, s, sp = O.share_gen(n, n, t, a, b, H(c["h"]))
+    assert E.hex() == c["E"]
+    assert A.hex() == c["A"]
+    assert s.hex() == c["s"]
+    assert sp.hex() == c["s_prime"]
+
+
+def _decisions(c, rnd):
+    n, t = c["n"], c["t"]
+    C = H(c["E"] if rnd == 2 else c["A"])
+    acc, rc = O.verify_pairs(n, t, rnd, C, H(c["h"]), H(c["s"]), H(c["s_prime"]), 0, n, 0, n)
+    return acc, rc
+
+
+@pytest.mark.parametrize("name", CEREMONIES + FAULTS)
+def test_round2_round4_decisions(golden, name):
+    c = golden(name)
+    n = c["n"]
+    acc, rc = _decisions(c, 2)
+    assert rc == 0
+    assert "".join(str(x) for x in acc) == c["dec2"]
+    acc4, rc = _decisions(c, 4)
+    exp4 = c["dec4"]
+    got4 = "".join(str(x) for x in acc4)
+    # dec4 marks disqualified dealers "3" (skipped, committee.rs:522); the oracle checks every pair
+    for i in range(n * n):
+        if exp4[i] != "3":
+            assert got4[i] == exp4[i], (name, i // n, i % n)
+
+
+def test_ceremony_n64(golden):
+    c = golden("ceremony_n64_t31.json")
+    acc, rc = _decisions(c, 2)
+    assert rc == 0 and "".join(str(x) for x in acc) == c["dec2"]
+
+
+def test_spot_n256(golden):
+    sp = golden("spot_n256_t127.json")
+    n, t = sp["n"], sp["t"]
+    for d in sp["dealers"]:
+        # per-pair reference check on the committed vector (vartime MSM over t+1 = 128 points)
+        for pr in d["pairs"]:
+            j = pr["receiver"]
+            pw = b"".join(pow(j + 1, k, 2**252 + 27742317777372353535851937790883648493).to_bytes(32, "little")
+                          for k in range(t + 1))
+            assert O.msm(pw, H(d["E"])).hex() == pr["rhs2"]

@@ -1,0 +1,390 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ (container-only; needs libsodium 1.0.18).
+
+This is an independent restatement of the reference's plaintext-mode ceremony
+(/root/reference/src/dkg/committee.rs rounds 1-5, src/polynomial.rs, src/groups.rs) written on
+libsodium's ristretto255 (RFC 9496) and Python big-int arithmetic mod l.  It shares no code with
+the C oracle (oracle/) or the HIP path (dkg_amd/csrc/), so agreement of all three pins parity.
+libsodium is NOT shipped and is never loaded by tests, smoke() or bench.py: only the JSON files it
+writes travel.
+
+Run:  python tools/gen_golden.py            (about a minute)
+"""
+import ctypes
+import hashlib
+import json
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import r255  # noqa: E402  (pure-Python RFC 9496 restatement, used as a second cross-check)
+
+L = r255.L
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+SO = ctypes.CDLL("/opt/conda/lib/libsodium.so")
+assert SO.sodium_init() >= 0
+
+CK_BYTES = b"Example of a shared string."  # every reference test (committee.rs:1079 ...)
+
+
+def hx(b):
+    return b.hex()
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+# ---------------- group via libsodium (identity = 32 zero bytes) ----------------
+ID = bytes(32)
+
+
+def scb(x):
+    return (x % L).to_bytes(32, "little")
+
+
+def gmul_base(k):
+    k %= L
+    if k == 0:
+        return ID
+    o = buf(32)
+    SO.crypto_scalarmult_ristretto255_base(o, scb(k))
+    return o.raw
+
+
+def gmul(p, k):
+    k %= L
+    if k == 0 or p == ID:
+        return ID
+    o = buf(32)
+    SO.crypto_scalarmult_ristretto255(o, scb(k), p)  # rc = -1 only for an identity result
+    return o.raw
+
+
+def gadd(p, q):
+    if p == ID:
+        return q
+    if q == ID:
+        return p
+    o = buf(32)
+    assert SO.crypto_core_ristretto255_add(o, p, q) == 0
+    return o.raw
+
+
+def gneg(p):
+    return gmul(p, L - 1)
+
+
+def hash_to_group(msg):
+    h = hashlib.blake2b(msg, digest_size=64).digest()
+    o = buf(32)
+    SO.crypto_core_ristretto255_from_hash(o, h)
+    return o.raw
+
+
+def valid(p):
+    return SO.crypto_core_ristretto255_is_valid_point(p) == 1 or p == ID
+
+
+def msm(scalars, points):
+    acc = ID
+    for s, p in zip(scalars, points):
+        acc = gadd(acc, gmul(p, s))
+    return acc
+
+
+# ---------------- RNG (rand_chacha ChaCha20Rng == IETF ChaCha20, zero nonce) ----------------
+def chacha_stream(key, nbytes):
+    o = buf(nbytes)
+    SO.crypto_stream_chacha20_ietf(o, ctypes.c_ulonglong(nbytes), bytes(12), key)
+    return o.raw
+
+
+def wide_reduce(b64):
+    o = buf(32)
+    SO.crypto_core_ristretto255_scalar_reduce(o, b64)
+    assert o.raw == scb(int.from_bytes(b64, "little"))
+    return int.from_bytes(o.raw, "little")
+
+
+def dealer_seed(master, ceremony, dealer):
+    return hashlib.blake2b(b"dkg-amd/v1/dealer" + master + ceremony.to_bytes(4, "little")
+                           + dealer.to_bytes(4, "little"), digest_size=32).digest()
+
+
+def dealer_coeffs(seed, t):
+    """committee.rs:143-146: hiding polynomial (b) drawn first, then sharing polynomial (a)."""
+    st = chacha_stream(seed, 2 * (t + 1) * 64)
+    b = [wide_reduce(st[64 * k:64 * k + 64]) for k in range(t + 1)]
+    a = [wide_reduce(st[64 * (t + 1 + k):64 * (t + 2 + k)]) for k in range(t + 1)]
+    return a, b
+
+
+def evaluate(coeffs, x):
+    """polynomial.rs:68-74 power-sum."""
+    acc, xp = 0, 1
+    for c in coeffs:
+        acc = (acc + c * xp) % L
+        xp = xp * x % L
+    return acc
+
+
+def lagrange_at_zero(ys, xs):
+    """polynomial.rs:162-184 at evaluation point 0."""
+    res = 0
+    for xa, ya in zip(xs, ys):
+        coef = 1
+        for xb in xs:
+            if xb != xa:
+                coef = coef * (0 - xb) * pow(xa - xb, -1, L) % L
+        res = (res + coef * ya) % L
+    return res
+
+
+# ---------------- the ceremony (plaintext-share mode) ----------------
+def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True):
+    """Returns a dict of inputs/outputs.  faults: list of dicts
+       {"kind": "E_identity", "dealer": i} (committee.rs:1127-1128 style),
+       {"kind": "share_flip", "dealer": i, "receiver": j}   s_ij += 1,
+       {"kind": "rand_flip", "dealer": i, "receiver": j}    s'_ij += 1,
+       {"kind": "A_generator", "dealer": i}                  round-3 broadcast := [g; t+1] (:1303-1306).
+       Dealers / receivers are 1-based as in the reference."""
+    faults = faults or []
+    assert t < (n + 1) // 2, "Environment::init asserts threshold < (nr_members + 1) / 2"
+    h = hash_to_group(CK_BYTES)
+    g = gmul_base(1)
+    A, B, E, Apub, S, SP = [], [], [], [], [], []
+    for i in range(n):
+        a, b = dealer_coeffs(dealer_seed(master, ceremony_id, i), t)
+        A.append(a)
+        B.append(b)
+        ap = [gmul_base(ak) for ak in a]                                # committee.rs:155
+        E.append([gadd(gmul(h, bk), apk) for bk, apk in zip(b, ap)])  # committee.rs:156
+        Apub.append(ap)
+        S.append([evaluate(a, j + 1) for j in range(n)])                # committee.rs:165-167
+        SP.append([evaluate(b, j + 1) for j in range(n)])
+    # wire values after fault injection
+    Ew = [list(e) for e in E]
+    Aw = [list(x) for x in Apub]
+    Sw = [list(s) for s in S]
+    SPw = [list(s) for s in SP]
+    for f in faults:
+        i = f["dealer"] - 1
+        if f["kind"] == "E_identity":
+            Ew[i] = [ID] * (t + 1)
+        elif f["kind"] == "share_flip":
+            Sw[i][f["receiver"] - 1] = (Sw[i][f["receiver"] - 1] + 1) % L
+        elif f["kind"] == "rand_flip":
+            SPw[i][f["receiver"] - 1] = (SPw[i][f["receiver"] - 1] + 1) % L
+        elif f["kind"] == "A_generator":
+            Aw[i] = [g] * (t + 1)
+        else:
+            raise ValueError(f)
+    # round 2 (committee.rs:273-338): decision[i][j] = receiver j accepts dealer i
+    dec2 = [[2] * n for _ in range(n)]
+    for j in range(n):
+        pw = [pow(j + 1, k, L) for k in range(t + 1)]                  # :287-290
+        for i in range(n):
+            if i == j:
+                continue
+            lhs = gadd(gmul(h, SPw[i][j]), gmul_base(Sw[i][j]))        # :292-294
+            rhs = msm(pw, Ew[i])                                       # :295-296
+            dec2[i][j] = int(lhs == rhs)                               # :305
+    complaints2 = [sum(1 for i in range(n) if i != j and dec2[i][j] == 0) for j in range(n)]
+    r2_error = [c > t for c in complaints2]                             # :340-347
+    # round 3: a valid complaint disqualifies the accused everywhere (committee.rs:370-398)
+    qualified = [int(all(dec2[i][j] != 0 for j in range(n))) for i in range(n)]
+    final_share = [sum(Sw[i][j] for i in range(n) if qualified[i]) % L for j in range(n)]  # :454-462
+    public_share = [gmul_base(s) for s in final_share]                 # :464-466
+    # round 4 (committee.rs:520-559)
+    dec4 = [[2] * n for _ in range(n)]
+    for j in range(n):
+        pw = [pow(j + 1, k, L) for k in range(t + 1)]
+        for i in range(n):
+            if i == j:
+                continue
+            if not qualified[i]:
+                dec4[i][j] = 3  # not checked: disqualified dealer is skipped (:522)
+                continue
+            lhs = gmul_base(Sw[i][j])                                  # :537
+            rhs = msm(pw, Aw[i])                                       # :538-539
+            dec4[i][j] = int(lhs == rhs)                               # :541
+    # round 5 / finalise (committee.rs:625-805): accused-and-valid dealers are reconstructed
+    recon = [int(qualified[i] and any(dec4[i][j] == 0 for j in range(n) if j != i)) for i in range(n)]
+    mpk = ID
+    for i in range(n):
+        if recon[i]:
+            xs = [j + 1 for j in range(n) if j != i and not recon[j]][: t + 1]
+            ys = [Sw[i][x - 1] for x in xs]
+            secret = lagrange_at_zero(ys, xs)                          # :784-788
+            assert secret == A[i][0]
+            mpk = gadd(mpk, gmul_base(secret))                         # :789
+        elif qualified[i]:
+            mpk = gadd(mpk, Aw[i][0])                                  # :790-795
+    # property of the honest run (committee.rs:1633-1647): mpk == g * sum of qualified secrets
+    assert mpk == gmul_base(sum(A[i][0] for i in range(n) if qualified[i]))
+    out = {
+        "n": n, "t": t, "ceremony": ceremony_id, "master_seed": hx(master), "ck_bytes": hx(CK_BYTES),
+        "h": hx(h), "faults": faults,
+        "E": "".join(hx(p) for e in Ew for p in e),
+        "A": "".join(hx(p) for e in Aw for p in e),
+        "s": "".join(hx(scb(x)) for row in Sw for x in row),
+        "s_prime": "".join(hx(scb(x)) for row in SPw for x in row),
+        "dec2": "".join(str(d) for row in dec2 for d in row),
+        "dec4": "".join(str(d) for row in dec4 for d in row),
+        "complaints2": complaints2, "r2_error": r2_error, "qualified": qualified,
+        "reconstruct": recon,
+        "final_share": "".join(hx(scb(x)) for x in final_share),
+        "public_share": "".join(hx(p) for p in public_share),
+        "mpk": hx(mpk),
+    }
+    if with_coeffs:
+        out["a"] = "".join(hx(scb(x)) for row in A for x in row)
+        out["b"] = "".join(hx(scb(x)) for row in B for x in row)
+        out["dealer_seeds"] = [hx(dealer_seed(master, ceremony_id, i)) for i in range(n)]
+    return out
+
+
+def kat_group(rng):
+    out = {}
+    out["base_multiples"] = [{"k": k, "P": hx(gmul_base(k))} for k in range(0, 17)]
+    ks = [rng.randrange(L) for _ in range(8)] + [L - 1, L - 2, 2**252, 2**128 + 7]
+    out["base_mul"] = [{"k": hx(scb(k)), "P": hx(gmul_base(k))} for k in ks]
+    for k in ks[:4]:
+        assert r255.encode(r255.mul(r255.BASE, k)) == gmul_base(k)
+    out["hash_to_group"] = [{"msg": hx(m), "P": hx(hash_to_group(m))}
+                            for m in [CK_BYTES, b"\x00", b"", bytes(range(200))]]
+    uni = []
+    for _ in range(8):
+        u = bytes(rng.getrandbits(8) for _ in range(64))
+        o = buf(32)
+        SO.crypto_core_ristretto255_from_hash(o, u)
+        assert r255.encode(r255.from_uniform_bytes(u)) == o.raw
+        uni.append({"in": hx(u), "P": hx(o.raw)})
+    out["from_uniform_bytes"] = uni
+    adds = []
+    for _ in range(8):
+        p, q = gmul_base(rng.randrange(L)), gmul_base(rng.randrange(L))
+        adds.append({"P": hx(p), "Q": hx(q), "sum": hx(gadd(p, q)), "diff": hx(gadd(p, gneg(q))),
+                     "neg_P": hx(gneg(p))})
+    out["add"] = adds
+    muls = []
+    for _ in range(8):
+        p, k = gmul_base(rng.randrange(L)), rng.randrange(L)
+        muls.append({"P": hx(p), "k": hx(scb(k)), "kP": hx(gmul(p, k))})
+    out["mul"] = muls
+    # encodings that must fail to decode (CompressedRistretto::decompress -> None)
+    P = r255.P
+    bad = [(P).to_bytes(32, "little"), (P + 2).to_bytes(32, "little"), (2**255 - 2).to_bytes(32, "little"),
+           (1).to_bytes(32, "little"), bytes([0xff] * 32), bytes(31) + b"\x80"]
+    for _ in range(40):
+        cand = bytes(rng.getrandbits(8) for _ in range(32))
+        if not valid(cand) and cand not in bad:
+            bad.append(cand)
+        if len(bad) >= 16:
+            break
+    for b in bad:
+        # dalek (and RFC 9496) reject a set bit 255 via the canonical re-encoding check;
+        # libsodium 1.0.18 masks that bit in its canonicity test, so it only arbitrates the rest.
+        assert r255.decode(b) is None, b.hex()
+        assert b[31] & 0x80 or not valid(b), b.hex()
+    out["invalid_encodings"] = [hx(b) for b in bad]
+    # MSM (vartime_multiscalar_multiplication) at sizes on both sides of dalek's Straus/Pippenger
+    # switch (190) and window thresholds (500, 800)
+    cases = []
+    for N in [0, 1, 2, 5, 32, 189, 190, 256, 512]:
+        sc = [rng.randrange(L) for _ in range(N)]
+        pts = [gmul_base(rng.randrange(L)) for _ in range(N)]
+        cases.append({"N": N, "scalars": "".join(hx(scb(x)) for x in sc),
+                      "points": "".join(hx(p) for p in pts), "out": hx(msm(sc, pts))})
+    # a vector with identity points and zero / l-1 scalars (fault-injection shapes)
+    sc = [0, 1, L - 1, 5]
+    pts = [ID, gmul_base(3), gmul_base(9), ID]
+    cases.append({"N": 4, "scalars": "".join(hx(scb(x)) for x in sc), "points": "".join(hx(p) for p in pts),
+                  "out": hx(msm(sc, pts))})
+    out["msm"] = cases
+    return out
+
+
+def kat_scalar(rng):
+    out = {}
+    wides = [bytes([0xff] * 64), bytes(64), (L).to_bytes(64, "little"), (2 * L + 5).to_bytes(64, "little")]
+    wides += [bytes(rng.getrandbits(8) for _ in range(64)) for _ in range(8)]
+    out["reduce_wide"] = [{"in": hx(w), "out": hx(scb(int.from_bytes(w, "little")))} for w in wides]
+    ops = []
+    for _ in range(12):
+        a, b = rng.randrange(L), rng.randrange(L)
+        ops.append({"a": hx(scb(a)), "b": hx(scb(b)), "add": hx(scb(a + b)), "sub": hx(scb(a - b)),
+                    "mul": hx(scb(a * b)), "neg_a": hx(scb(-a)), "inv_a": hx(scb(pow(a, -1, L)))})
+    out["ops"] = ops
+    # polynomial.rs:240-279 KATs
+    out["poly_tests"] = {"coeffs": [1, 3, 0, 0, 0], "x": 3, "value": 10}
+    # polynomial.rs:190-211: 13 + 2x through x in {5, 7, 2}
+    xs = [5, 7, 2]
+    ys = [evaluate([13, 2], x) for x in xs]
+    out["lagrange"] = {"xs": xs, "ys": ys, "at_zero": lagrange_at_zero(ys, xs)}
+    evals = []
+    for deg in [0, 1, 4, 31, 127]:
+        c = [rng.randrange(L) for _ in range(deg + 1)]
+        xs = [1, 2, 3, 1023, 4096, rng.randrange(1, 2**32)]
+        evals.append({"coeffs": "".join(hx(scb(x)) for x in c),
+                      "points": xs, "values": [hx(scb(evaluate(c, x))) for x in xs]})
+    out["poly_eval"] = evals
+    # the RNG convention (committee.rs:143-146 draw order) on one seed
+    seed = dealer_seed(bytes(32), 0, 0)
+    a, b = dealer_coeffs(seed, 3)
+    out["dealer_rng"] = {"master": hx(bytes(32)), "ceremony": 0, "dealer": 0, "seed": hx(seed), "t": 3,
+                         "a": [hx(scb(x)) for x in a], "b": [hx(scb(x)) for x in b],
+                         "stream_head": hx(chacha_stream(seed, 128))}
+    return out
+
+
+def spot(n, t, master, dealers, receivers):
+    """Per-pair spot vectors for a large config: full E/A of a few dealers plus chosen shares."""
+    h = hash_to_group(CK_BYTES)
+    res = {"n": n, "t": t, "master_seed": hx(master), "h": hx(h), "dealers": []}
+    for i in dealers:
+        a, b = dealer_coeffs(dealer_seed(master, 0, i), t)
+        ap = [gmul_base(x) for x in a]
+        E = [gadd(gmul(h, y), x) for x, y in zip(ap, b)]
+        d = {"dealer": i, "E": "".join(hx(p) for p in E), "A": "".join(hx(p) for p in ap), "pairs": []}
+        for j in receivers:
+            s, sp = evaluate(a, j + 1), evaluate(b, j + 1)
+            pw = [pow(j + 1, k, L) for k in range(t + 1)]
+            rhs2, rhs4 = msm(pw, E), msm(pw, ap)
+            assert rhs2 == gadd(gmul(h, sp), gmul_base(s)) and rhs4 == gmul_base(s)
+            d["pairs"].append({"receiver": j, "s": hx(scb(s)), "s_prime": hx(scb(sp)), "rhs2": hx(rhs2)})
+        res["dealers"].append(d)
+    return res
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    rng = random.Random(20250117)
+    files = {}
+    files["kat_group.json"] = kat_group(rng)
+    files["kat_scalar.json"] = kat_scalar(rng)
+    m = hashlib.blake2b(b"golden/master", digest_size=32).digest()
+    for n, t in [(2, 0), (3, 1), (10, 4), (11, 5), (16, 7)]:
+        files[f"ceremony_n{n}_t{t}.json"] = ceremony(n, t, m)
+    files["ceremony_n64_t31.json"] = ceremony(64, 31, m, ceremony_id=7, with_coeffs=False)
+    faults = {
+        "e_identity": [{"kind": "E_identity", "dealer": 3}],
+        "share_flip": [{"kind": "share_flip", "dealer": 5, "receiver": 2},
+                       {"kind": "rand_flip", "dealer": 7, "receiver": 9}],
+        "a_generator": [{"kind": "A_generator", "dealer": 6}],
+        "over_threshold": [{"kind": "E_identity", "dealer": d} for d in (1, 2, 4, 8, 9)],
+    }
+    for name, fs in faults.items():
+        files[f"fault_{name}_n10_t4.json"] = ceremony(10, 4, m, ceremony_id=1, faults=fs)
+    files["spot_n256_t127.json"] = spot(256, 127, m, [0, 200], [1, 17, 255])
+    files["spot_n1024_t511.json"] = spot(1024, 511, m, [513], [0, 1023])
+    for name, obj in files.items():
+        with open(os.path.join(OUT, name), "w") as f:
+            json.dump(obj, f, separators=(",", ":"))
+        print(name, os.path.getsize(os.path.join(OUT, name)))
+
+
+if __name__ == "__main__":
+    main()
