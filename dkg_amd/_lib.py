@@ -1,0 +1,84 @@
+"""ctypes binding of the in-tree HIP library dkg_amd/libdkg_amd.so (C ABI: include/dkg_amd.h).
+
+The product path always runs the HIP kernels: there is no CPU fallback.  If the library is missing
+or no GPU is visible, the calls below raise instead of silently computing something else.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DKG_AMD_LIB", os.path.join(HERE, "libdkg_amd.so"))
+
+DKG_OK = 0
+DKG_E_ARG = -1
+DKG_E_DECODE = -2
+DKG_E_DEVICE = -3
+DKG_E_NOMEM = -4
+REJECT, ACCEPT, SELF, SKIPPED = 0, 1, 2, 3
+
+_lib = None
+
+
+class DkgError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        names = {DKG_E_ARG: "DKG_E_ARG", DKG_E_DECODE: "DKG_E_DECODE", DKG_E_DEVICE: "DKG_E_DEVICE",
+                 DKG_E_NOMEM: "DKG_E_NOMEM"}
+        super().__init__(f"{names.get(code, code)}: {msg}")
+
+
+class CeremonyOut(ctypes.Structure):
+    _fields_ = [
+        ("E", ctypes.c_void_p), ("A", ctypes.c_void_p),
+        ("s", ctypes.c_void_p), ("s_prime", ctypes.c_void_p),
+        ("dec2", ctypes.c_void_p), ("dec4", ctypes.c_void_p),
+        ("qualified", ctypes.c_void_p), ("r2_error", ctypes.c_void_p),
+        ("complaints2", ctypes.c_void_p), ("reconstruct", ctypes.c_void_p),
+        ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
+        ("mpk", ctypes.c_uint8 * 32),
+        ("n_qualified", ctypes.c_int32),
+        ("ms_round1", ctypes.c_double), ("ms_round2", ctypes.c_double), ("ms_round3", ctypes.c_double),
+        ("ms_round4", ctypes.c_double), ("ms_finalise", ctypes.c_double), ("ms_total", ctypes.c_double),
+    ]
+
+
+def lib():
+    """Load libdkg_amd.so (raises if it is absent: the HIP path is mandatory)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C dkg_amd` or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    sz, p, u8p = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
+    L.dkg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(p)]
+    L.dkg_ctx_destroy.argtypes = [p]
+    L.dkg_ctx_destroy.restype = None
+    L.dkg_ctx_last_error.argtypes = [p]
+    L.dkg_ctx_last_error.restype = ctypes.c_char_p
+    L.dkg_device_count.argtypes = []
+    L.dkg_env_check.argtypes = [sz, sz]
+    L.dkg_env_init.argtypes = [p, sz, sz, u8p, sz, p]
+    L.dkg_msm_batch.argtypes = [p, sz, sz, u8p, u8p, p]
+    L.dkg_fixed_base_batch.argtypes = [p, p, sz, u8p, p]
+    L.dkg_poly_eval_batch.argtypes = [p, sz, sz, u8p, sz, p, p]
+    L.dkg_points_valid_batch.argtypes = [p, sz, u8p, p]
+    L.dkg_share_gen.argtypes = [p, sz, sz, sz, u8p, u8p, p, p, p, p]
+    L.dkg_verify_pairs.argtypes = [p, sz, sz, ctypes.c_int, sz, sz, u8p, u8p, p, p]
+    L.dkg_verify_receiver.argtypes = [p, sz, sz, ctypes.c_int, sz, u8p, u8p, p, p]
+    L.dkg_ceremony_run.argtypes = [p, sz, sz, u8p, u8p, ctypes.POINTER(CeremonyOut)]
+    L.dkg_ceremony_verify.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
+    L.dkg_ceremony_run_device.argtypes = [p, sz, sz, p, p, ctypes.POINTER(CeremonyOut)]
+    L.dkg_ceremony_shard_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]
+    L.dkg_dealer_coeffs.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, p, p]
+    _lib = L
+    return L
+
+
+EXPORTED = [
+    "dkg_ctx_create", "dkg_ctx_destroy", "dkg_ctx_last_error", "dkg_device_count", "dkg_env_init",
+    "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
+    "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
+    "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
+    "dkg_dealer_coeffs",
+]

@@ -1,0 +1,215 @@
+"""Python host API over the C ABI, mirroring the reference's operator surface for this path.
+
+Reference interface -> here:
+  Environment::init(threshold, nr_members, ck_gen_bytes)      committee.rs:72-83  -> Environment
+  PrimeGroupElement::vartime_multiscalar_multiplication        traits.rs:234-237   -> Backend.msm_batch
+  Mul<Scalar> (generator / h)                                  traits.rs:212       -> Backend.fixed_base_batch
+  Polynomial::evaluate                                         polynomial.rs:68-74 -> Backend.poly_eval_batch
+  PrimeGroupElement::from_bytes (validity)                     groups.rs:78-81     -> Backend.points_valid
+  Phases<Initialise>::init (all dealers)                       committee.rs:124-216 -> Backend.share_gen
+  Phases<Phase1>::proceed / Phases<Phase3>::proceed checks     committee.rs:273-338, 520-559
+                                                               -> Backend.verify_pairs / verify_receiver
+  the all-parties test driver (full_valid_run)                 committee.rs:1518-1656 -> Backend.ceremony
+Scalars and points are 32-byte encodings (bytes), exactly the reference's wire values.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+from . import _lib
+from ._lib import CeremonyOut, DkgError
+
+CK_DEFAULT = b"Example of a shared string."
+
+
+def _check(ctx, rc):
+    if rc != _lib.DKG_OK:
+        msg = _lib.lib().dkg_ctx_last_error(ctx).decode() if ctx else ""
+        raise DkgError(rc, msg)
+
+
+def env_check(threshold: int, nr_members: int) -> None:
+    """committee.rs:73 `assert!(threshold < (nr_members + 1) / 2)` -> DkgError(DKG_E_ARG)."""
+    rc = _lib.lib().dkg_env_check(threshold, nr_members)
+    if rc != _lib.DKG_OK:
+        raise DkgError(rc, f"threshold {threshold} must be < (nr_members + 1) / 2 = {(nr_members + 1) // 2}")
+
+
+def dealer_coefficients(master: bytes, ceremony: int, d0: int, D: int, t: int):
+    """Seeded Polynomial::random pair per dealer (hiding first, committee.rs:143-146): (a, b)."""
+    N = t + 1
+    a = ctypes.create_string_buffer(32 * D * N)
+    b = ctypes.create_string_buffer(32 * D * N)
+    rc = _lib.lib().dkg_dealer_coeffs(master, ceremony, d0, D, t, a, b)
+    if rc != _lib.DKG_OK:
+        raise DkgError(rc, "dealer_coeffs")
+    return a.raw, b.raw
+
+
+@dataclass
+class CeremonyResult:
+    n: int
+    t: int
+    mpk: bytes
+    qualified: List[int]
+    r2_error: List[int]
+    complaints2: List[int]
+    reconstruct: List[int]
+    n_qualified: int
+    ms: dict
+    E: Optional[bytes] = None
+    A: Optional[bytes] = None
+    s: Optional[bytes] = None
+    s_prime: Optional[bytes] = None
+    dec2: Optional[bytes] = None
+    dec4: Optional[bytes] = None
+    final_share: Optional[bytes] = None
+    public_share: Optional[bytes] = None
+
+
+class Backend:
+    """One GPU (one process per GPU).  Owns a dkg_ctx."""
+
+    def __init__(self, device: int = 0):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        rc = L.dkg_ctx_create(device, ctypes.byref(h))
+        if rc != _lib.DKG_OK:
+            raise DkgError(rc, f"dkg_ctx_create(device={device}) failed (is a gfx950 GPU visible?)")
+        self._ctx = h
+        self.h: Optional[bytes] = None
+
+    def close(self):
+        if self._ctx:
+            _lib.lib().dkg_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def env_init(self, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        _check(self._ctx, _lib.lib().dkg_env_init(self._ctx, threshold, nr_members, ck_gen_bytes,
+                                                   len(ck_gen_bytes), out))
+        self.h = out.raw
+        return out.raw
+
+    # ---- trait-level batches
+    def msm_batch(self, scalars: bytes, points: bytes, B: int, N: int) -> bytes:
+        out = ctypes.create_string_buffer(32 * max(B, 1))
+        _check(self._ctx, _lib.lib().dkg_msm_batch(self._ctx, B, N, scalars, points, out))
+        return out.raw[: 32 * B]
+
+    def fixed_base_batch(self, scalars: bytes, base: Optional[bytes] = None) -> bytes:
+        count = len(scalars) // 32
+        out = ctypes.create_string_buffer(32 * max(count, 1))
+        _check(self._ctx, _lib.lib().dkg_fixed_base_batch(self._ctx, base, count, scalars, out))
+        return out.raw[: 32 * count]
+
+    def poly_eval_batch(self, coeffs: bytes, D: int, N: int, xs: List[int]) -> bytes:
+        M = len(xs)
+        arr = (ctypes.c_uint32 * max(M, 1))(*xs)
+        out = ctypes.create_string_buffer(32 * max(D * M, 1))
+        _check(self._ctx, _lib.lib().dkg_poly_eval_batch(self._ctx, D, N, coeffs, M, arr, out))
+        return out.raw[: 32 * D * M]
+
+    def points_valid(self, points: bytes) -> bytes:
+        count = len(points) // 32
+        out = ctypes.create_string_buffer(max(count, 1))
+        _check(self._ctx, _lib.lib().dkg_points_valid_batch(self._ctx, count, points, out))
+        return out.raw[:count]
+
+    # ---- round 1
+    def share_gen(self, a: bytes, b: bytes, D: int, n: int, t: int):
+        N = t + 1
+        E, A = ctypes.create_string_buffer(32 * D * N), ctypes.create_string_buffer(32 * D * N)
+        s, sp = ctypes.create_string_buffer(32 * D * n), ctypes.create_string_buffer(32 * D * n)
+        _check(self._ctx, _lib.lib().dkg_share_gen(self._ctx, D, n, t, a, b, E, A, s, sp))
+        return E.raw, A.raw, s.raw, sp.raw
+
+    # ---- rounds 2 / 4
+    def verify_pairs(self, n: int, t: int, rnd: int, d0: int, d1: int, C: bytes, s: bytes,
+                     s_prime: Optional[bytes] = None) -> bytes:
+        dec = ctypes.create_string_buffer(max((d1 - d0) * n, 1))
+        _check(self._ctx, _lib.lib().dkg_verify_pairs(self._ctx, n, t, rnd, d0, d1, C, s, s_prime, dec))
+        return dec.raw[: (d1 - d0) * n]
+
+    def verify_receiver(self, n: int, t: int, rnd: int, j: int, C: bytes, s_col: bytes,
+                        sp_col: Optional[bytes] = None) -> bytes:
+        dec = ctypes.create_string_buffer(max(n, 1))
+        _check(self._ctx, _lib.lib().dkg_verify_receiver(self._ctx, n, t, rnd, j, C, s_col, sp_col, dec))
+        return dec.raw[:n]
+
+    # ---- whole ceremony
+    def _ceremony_out(self, n, t, big):
+        N = t + 1
+        bufs = {}
+        o = CeremonyOut()
+        sizes = {"qualified": n, "r2_error": n, "complaints2": 4 * n, "reconstruct": n}
+        if big:
+            sizes.update({"E": 32 * n * N, "A": 32 * n * N, "s": 32 * n * n, "s_prime": 32 * n * n,
+                          "dec2": n * n, "dec4": n * n, "final_share": 32 * n, "public_share": 32 * n})
+        for k, v in sizes.items():
+            bufs[k] = ctypes.create_string_buffer(v)
+            setattr(o, k, ctypes.cast(bufs[k], ctypes.c_void_p))
+        return o, bufs
+
+    def _result(self, n, t, o, bufs, big):
+        import struct
+        r = CeremonyResult(
+            n=n, t=t, mpk=bytes(o.mpk), qualified=list(bufs["qualified"].raw[:n]),
+            r2_error=list(bufs["r2_error"].raw[:n]),
+            complaints2=list(struct.unpack(f"<{n}i", bufs["complaints2"].raw[: 4 * n])),
+            reconstruct=list(bufs["reconstruct"].raw[:n]), n_qualified=o.n_qualified,
+            ms={"round1": o.ms_round1, "round2": o.ms_round2, "round3": o.ms_round3, "round4": o.ms_round4,
+                "finalise": o.ms_finalise, "total": o.ms_total})
+        if big:
+            for k in ("E", "A", "s", "s_prime", "dec2", "dec4", "final_share", "public_share"):
+                setattr(r, k, bufs[k].raw)
+        return r
+
+    def ceremony(self, a: bytes, b: bytes, n: int, t: int) -> CeremonyResult:
+        o, bufs = self._ceremony_out(n, t, True)
+        _check(self._ctx, _lib.lib().dkg_ceremony_run(self._ctx, n, t, a, b, ctypes.byref(o)))
+        return self._result(n, t, o, bufs, True)
+
+    def ceremony_verify(self, E: bytes, A: bytes, s: bytes, s_prime: bytes, n: int, t: int) -> CeremonyResult:
+        o, bufs = self._ceremony_out(n, t, True)
+        for k in ("E", "A", "s", "s_prime"):
+            setattr(o, k, None)
+        _check(self._ctx, _lib.lib().dkg_ceremony_verify(self._ctx, n, t, E, A, s, s_prime, ctypes.byref(o)))
+        r = self._result(n, t, o, bufs, True)
+        r.E, r.A, r.s, r.s_prime = E, A, s, s_prime
+        return r
+
+    def ceremony_device(self, d_a: int, d_b: int, n: int, t: int) -> CeremonyResult:
+        """d_a, d_b: device pointers (e.g. torch tensor .data_ptr()) to [n][t+1][32] scalars."""
+        o, bufs = self._ceremony_out(n, t, False)
+        _check(self._ctx, _lib.lib().dkg_ceremony_run_device(self._ctx, n, t, ctypes.c_void_p(d_a),
+                                                              ctypes.c_void_p(d_b), ctypes.byref(o)))
+        return self._result(n, t, o, bufs, False)
+
+    def ceremony_shard_device(self, n, t, d0, d1, d_a, d_b, d_dec2, d_dec4, d_A0, d_partial) -> float:
+        ms = ctypes.c_double()
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_ceremony_shard_device(self._ctx, n, t, d0, d1, vp(d_a), vp(d_b),
+                                                                vp(d_dec2), vp(d_dec4), vp(d_A0),
+                                                                vp(d_partial), ctypes.byref(ms)))
+        return ms.value
+
+
+class Environment:
+    """committee.rs:24-28 / :72-83 — threshold, nr_members and the Pedersen commitment key h."""
+
+    def __init__(self, backend: Backend, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT):
+        env_check(threshold, nr_members)
+        self.threshold = threshold
+        self.nr_members = nr_members
+        self.commitment_key = backend.env_init(threshold, nr_members, ck_gen_bytes)

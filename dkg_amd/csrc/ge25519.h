@@ -74,78 +74,80 @@ DKG_DEV void ge_cached_neg(ge_cached& r, const ge_cached& c) {
   fe_carry(r.T2d, r.T2d);
 }
 
+// Additions are written so that (a, b) collapse into (e, h) before (c, d) are formed: at most
+// four field temporaries are live next to the operands (keeps the kernels at <= 128 VGPRs).
 // r = p + q  (8M).  r may alias p.
 DKG_DEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
-  fe a, b, c, d, e, f, g, h, t;
+  fe a, b, e, h, t;
   fe_sub(t, p.Y, p.X);      // <= 1.5*2^27
   fe_mul(a, t, q.YmX);
   fe_add(t, p.Y, p.X);      // <= 2^27
   fe_mul(b, t, q.YpX);
-  fe_mul(c, p.T, q.T2d);
-  fe_mul(d, p.Z, q.Z2);
   fe_sub(e, b, a);          // <= 1.5*2^27
-  fe_sub(f, d, c);          // <= 1.5*2^27
-  fe_add(g, d, c);          // <= 2^27
   fe_add(h, b, a);          // <= 2^27
-  fe_mul(r.X, e, f);
-  fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
+  fe_mul(a, p.T, q.T2d);    // c
+  fe_mul(b, p.Z, q.Z2);     // d
+  fe_sub(t, b, a);          // f = d - c <= 1.5*2^27
+  fe_add(b, b, a);          // g = d + c <= 2^27
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, t, b);
   fe_mul(r.T, e, h);
 }
 
 // r = p - q
 DKG_DEV void ge_sub(ge_p3& r, const ge_p3& p, const ge_cached& q) {
-  fe a, b, c, d, e, f, g, h, t;
+  fe a, b, e, h, t;
   fe_sub(t, p.Y, p.X);
   fe_mul(a, t, q.YpX);
   fe_add(t, p.Y, p.X);
   fe_mul(b, t, q.YmX);
-  fe_mul(c, p.T, q.T2d);
-  fe_mul(d, p.Z, q.Z2);
   fe_sub(e, b, a);
-  fe_add(f, d, c);          // sign of c flipped for -q
-  fe_sub(g, d, c);
   fe_add(h, b, a);
-  fe_mul(r.X, e, f);
-  fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
+  fe_mul(a, p.T, q.T2d);    // c
+  fe_mul(b, p.Z, q.Z2);     // d
+  fe_add(t, b, a);          // f = d + c (sign of c flipped for -q)
+  fe_sub(b, b, a);          // g = d - c
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, t, b);
   fe_mul(r.T, e, h);
 }
 
 // r = p + q with q affine Niels (Z = 1): 7M.
 DKG_DEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_aff& q) {
-  fe a, b, c, d, e, f, g, h, t;
+  fe a, b, e, h, t;
   fe_sub(t, p.Y, p.X);
   fe_mul(a, t, q.ymx);
   fe_add(t, p.Y, p.X);
   fe_mul(b, t, q.ypx);
-  fe_mul(c, p.T, q.xy2d);
-  fe_add(d, p.Z, p.Z);      // <= 2^27
   fe_sub(e, b, a);
-  fe_sub(f, d, c);          // <= 2^27 + 2^27
-  fe_add(g, d, c);          // <= 1.5*2^27
   fe_add(h, b, a);
-  fe_mul(r.X, f, e);        // f <= 2^28 as first operand
-  fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
+  fe_mul(a, p.T, q.xy2d);   // c
+  fe_add(b, p.Z, p.Z);      // d <= 2^27
+  fe_sub(t, b, a);          // f = d - c <= 2^27 + 2^27
+  fe_add(b, b, a);          // g = d + c <= 1.5*2^27
+  fe_mul(r.X, t, e);        // f <= 2^28 as first operand
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, t, b);
   fe_mul(r.T, e, h);
 }
 
 DKG_DEV void ge_msub(ge_p3& r, const ge_p3& p, const ge_aff& q) {
-  fe a, b, c, d, e, f, g, h, t;
+  fe a, b, e, h, t;
   fe_sub(t, p.Y, p.X);
   fe_mul(a, t, q.ypx);
   fe_add(t, p.Y, p.X);
   fe_mul(b, t, q.ymx);
-  fe_mul(c, p.T, q.xy2d);
-  fe_add(d, p.Z, p.Z);
   fe_sub(e, b, a);
-  fe_add(f, d, c);
-  fe_sub(g, d, c);          // <= 2^28
   fe_add(h, b, a);
-  fe_mul(r.X, f, e);
-  fe_mul(r.Y, g, h);        // g <= 2^28 first operand
-  fe_mul(r.Z, g, f);
+  fe_mul(a, p.T, q.xy2d);   // c
+  fe_add(b, p.Z, p.Z);      // d
+  fe_add(t, b, a);          // f = d + c <= 1.5*2^27
+  fe_sub(b, b, a);          // g = d - c <= 2^28
+  fe_mul(r.X, t, e);
+  fe_mul(r.Y, b, h);        // g <= 2^28 first operand
+  fe_mul(r.Z, b, t);
   fe_mul(r.T, e, h);
 }
 
@@ -168,6 +170,55 @@ DKG_DEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, f, g);
   if (with_t) fe_mul(r.T, e, h);
+}
+
+// Doubling with a run-time (wave-uniform) choice of whether T is produced.
+DKG_DEV void ge_dbl_rt(ge_p3& r, const ge_p3& p, bool with_t) {
+  fe a, b, c, t, h, e, g;
+  fe_sq(a, p.X);
+  fe_sq(b, p.Y);
+  fe_sq(c, p.Z);
+  fe_add(c, c, c);          // <= 2^27
+  fe_add(t, p.X, p.Y);      // <= 2^27
+  fe_sq(t, t);              // (X+Y)^2
+  fe_add(h, a, b);          // <= 2^27             (= -H_std)
+  fe_sub(e, h, t);          // <= 2^28             (= -E_std)
+  fe_sub(g, a, b);          // <= 1.5*2^27         (= -G_std)
+  fe_add(c, c, g);          // f <= 2.5*2^27
+  fe_carry(c, c);           // tight               (= -F_std)
+  fe_mul(r.X, e, c);
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, c, g);
+  if (with_t) fe_mul(r.T, e, h);
+}
+
+// r = p + q (neg = false) or p - q (neg = true) with one code path: the sign only selects
+// which of (Y+X, Y-X) multiplies which, and the sign of the 2dT product.
+DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg) {
+  fe a, b, e, h, t, qa, qb;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    qa.v[i] = neg ? q.YpX.v[i] : q.YmX.v[i];
+    qb.v[i] = neg ? q.YmX.v[i] : q.YpX.v[i];
+  }
+  fe_sub(t, p.Y, p.X);
+  fe_mul(a, t, qa);
+  fe_add(t, p.Y, p.X);
+  fe_mul(b, t, qb);
+  fe_sub(e, b, a);
+  fe_add(h, b, a);
+  fe_mul(a, p.T, q.T2d);    // c  (the term whose sign flips with q)
+  fe_mul(b, p.Z, q.Z2);     // d
+  fe na;
+  fe_neg(na, a);            // -c <= 2^27
+  fe_cmov(a, na, neg);      // a = +/-c (limbs <= 2^27)
+  fe_carry(a, a);           // tight again (fe_sub needs a tight subtrahend)
+  fe_sub(t, b, a);          // f = d - (+/-c) <= 1.5*2^27
+  fe_add(b, b, a);          // g <= 2^27
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, t, b);
+  fe_mul(r.T, e, h);
 }
 
 // ---- Ristretto255 (RFC 9496 section 4.3) ----

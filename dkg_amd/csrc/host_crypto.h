@@ -1,0 +1,26 @@
+// Host-side helpers of the product library (not the oracle): BLAKE2b-512 for the commitment key
+// (commitment.rs:13-17), the ChaCha20Rng stream for seeded synthetic coefficients, and small
+// Z_l arithmetic for the (cold) reconstruction path of finalise (polynomial.rs:162-184).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dkgh {
+
+void blake2b(uint8_t* out, size_t outlen, const uint8_t* in, size_t inlen);
+// ChaCha20 keystream (key = seed, 64-bit block counter from `block`, zero stream id)
+void chacha20(const uint8_t key[32], uint64_t block, uint8_t* out, size_t len);
+
+struct Zl {  // canonical element of Z_l, little-endian 64-bit limbs
+  uint64_t w[4];
+};
+Zl zl_from_bytes_wide(const uint8_t* in, size_t len);  // any length, big-endian fold of LE bytes
+Zl zl_from_u64(uint64_t x);
+void zl_to_bytes(uint8_t out[32], const Zl& a);
+Zl zl_add(const Zl& a, const Zl& b);
+Zl zl_sub(const Zl& a, const Zl& b);
+Zl zl_mul(const Zl& a, const Zl& b);
+Zl zl_inv(const Zl& a);
+bool zl_is_zero(const Zl& a);
+
+}  // namespace dkgh

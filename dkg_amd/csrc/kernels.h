@@ -1,0 +1,70 @@
+// Host-side launchers for the gfx950 kernels (kernels.hip).  All pointers are device pointers;
+// all launches go to `stream`.  Layouts are documented in points.h and DESIGN.md.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dkgk {
+
+// K5: 32-byte encodings [count][8 words] -> extended SoA [40][stride]; ok[e] = 1 if valid.
+void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t stride, uint8_t* ok,
+                   hipStream_t stream);
+// extended SoA -> encodings [count][8]
+void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream);
+// comb table of the decoded point ext[.., e0] into tab (30 x 512 words)
+void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream);
+
+// K2: A_k = g a_k, E_k = A_k + h b_k for D*N coefficients (scalars [D*N][8]); outputs SoA [40][DN].
+void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g,
+            const uint32_t* tab_h, uint32_t* A_ext, uint32_t* E_ext, hipStream_t stream);
+// K1: s[i][j] = f_i(j+1), s'[i][j] = f'_i(j+1) (scalars [D][n][8]); coefficients [D][N][8].
+void share_eval(size_t D, size_t n, size_t N, const uint32_t* a, const uint32_t* b, uint32_t* s,
+                uint32_t* sp, hipStream_t stream);
+// Polynomial::evaluate for D polynomials at M small integer points x[m] (< 2^24).
+void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint32_t* xs, uint32_t* out,
+               hipStream_t stream);
+
+// K3a: binomial-basis Horner.  C: decoded commitments SoA [40][N][npad] (position-major,
+// dealer-minor); e0/e1 ping-pong buffers of the same shape.  Returns the buffer holding
+// e_m = Delta^m P_i(0), m = 0..t.
+uint32_t* binomial(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
+                   hipStream_t stream);
+// K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][ndealers*nrecv].
+// stream_a / stream_b: scratch for the inter-block boundary streams, each >= ndealers*nrecv*160 B
+// (unused when N <= 256).
+void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
+              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream);
+// K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);
+// dealer_ok[i] == 0 forces 0; i == j (self, index i + dealer_base == j) gives 2.
+void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round, const uint32_t* s,
+           const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
+           const uint8_t* dealer_ok, uint8_t* decision, hipStream_t stream);
+// per-dealer validity: dealer_ok[i] = AND of point_ok over its N commitments (dealer-major [D][N])
+void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream);
+// Horner in the exponent for receivers x0 .. x0+nrecv-1 (1-based indices): R [40][ndealers*nrecv]
+void horner(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t x0, size_t nrecv, uint32_t* R,
+            hipStream_t stream);
+// out (one SoA point, stride 1) = sum of mask[e] * P_e (mask may be NULL)
+void sum_points(size_t count, const uint32_t* pts, size_t stride, const uint8_t* mask, uint32_t* out, size_t ostride, size_t col,
+                hipStream_t stream);
+// hash_to_group tail: from_uniform_bytes(64 bytes as 16 LE words) -> SoA point (stride 1)
+void from_uniform(const uint32_t* in16, uint32_t* out, hipStream_t stream);
+
+// Generic batched MSM (trait boundary): out[b] = sum_k scalars[b][k] * points[b][k];
+// points given decoded SoA [40][B*N] (element b*N + k), scalars [B*N][8].
+void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts, size_t stride,
+               uint32_t* out_ext, hipStream_t stream);
+// Fixed-base batch: out = s * base via comb table; out SoA [40][count]
+void fixed_base(size_t count, const uint32_t* scalars, const uint32_t* tab, uint32_t* out_ext,
+                hipStream_t stream);
+// Transpose dealer-major point SoA [40][D*N] (element i*N+k) to position-major [40][N][npad].
+void to_position_major(size_t D, size_t N, size_t npad, const uint32_t* in, uint32_t* out,
+                       hipStream_t stream);
+// Scalar reduction of 256-bit inputs to canonical (from_bits semantics, groups.rs:29-36).
+void reduce_scalars(size_t count, const uint32_t* in, uint32_t* out, hipStream_t stream);
+// Modular sum over dealers with mask: out[j] = sum_i mask[i] * s[i][j]  (round-3 final share)
+void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out,
+                hipStream_t stream);
+
+}  // namespace dkgk

@@ -1,0 +1,653 @@
+// gfx950 kernels for the DKG share-generation / share-verification hot path.
+// Reference loops replaced (file:line in /root/reference):
+//   K1 share_eval   <- committee.rs:164-167 -> polynomial.rs:68-74
+//   K2 commit       <- committee.rs:151-159
+//   K3 binomial / stepping / check  <- committee.rs:287-305 (round 2), :532-548 (round 4)
+//   K5 decode / encode              <- groups.rs:72-81
+// See DESIGN.md for the algorithm (exact finite-difference evaluation of the committed
+// polynomial in the exponent) and the roofline of each kernel.
+#include "kernels.h"
+#include "points.h"
+
+namespace dkgk {
+
+constexpr int COMB_WORDS = AFF_WORDS * COMB_ENTRIES;  // 15360 words = 61440 B per base
+
+// ------------------------------------------------------------------ K5 decode / encode
+__global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ comp, size_t count,
+                                                uint32_t* __restrict__ ext, size_t stride,
+                                                uint8_t* __restrict__ ok) {
+  size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  uint32_t w[8];
+  ld_words8(w, comp + 8 * e);
+  ge_p3 p;
+  bool v = ristretto_decode(p, w);
+  if (!v) ge_identity(p);
+  pt_store(ext, stride, e, p);
+  ok[e] = v ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
+                                                size_t count, uint32_t* __restrict__ comp) {
+  size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  ge_p3 p;
+  pt_load(p, ext, stride, e);
+  uint32_t w[8];
+  ristretto_encode(w, p);
+  st_words8(comp + 8 * e, w);
+}
+
+void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t stride, uint8_t* ok,
+                   hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count,
+                     ext, stride, ok);
+}
+
+void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_encode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, ext, stride,
+                     count, comp);
+}
+
+// ------------------------------------------------------------------ comb tables
+// Thread w (0..63) builds window w: B_w = 16^w B, entries d B_w (d = 1..8) in affine Niels form.
+__global__ __launch_bounds__(64) void k_build_comb(const uint32_t* __restrict__ ext, size_t stride, size_t e0,
+                                                   uint32_t* __restrict__ tab) {
+  const int w = threadIdx.x;
+  ge_p3 b;
+  pt_load(b, ext, stride, e0);
+  for (int i = 0; i < 4 * w; i++) ge_dbl<true>(b, b);
+  ge_cached bc;
+  ge_to_cached(bc, b);
+  ge_p3 m = b;
+  fe d2;
+  fe_ld(d2, ge_const::D2);
+  for (int d = 1; d <= 8; d++) {
+    if (d > 1) ge_add(m, m, bc);
+    fe zi, x, y, t;
+    fe_invert(zi, m.Z);
+    fe_mul(x, m.X, zi);
+    fe_mul(y, m.Y, zi);
+    const int e = w * 8 + d - 1;
+    fe_add(t, y, x);
+    fe_carry(t, t);
+#pragma unroll
+    for (int i = 0; i < 10; i++) tab[i * COMB_ENTRIES + e] = t.v[i];
+    fe_sub(t, y, x);
+    fe_carry(t, t);
+#pragma unroll
+    for (int i = 0; i < 10; i++) tab[(10 + i) * COMB_ENTRIES + e] = t.v[i];
+    fe_mul(t, x, y);
+    fe_mul(t, t, d2);
+#pragma unroll
+    for (int i = 0; i < 10; i++) tab[(20 + i) * COMB_ENTRIES + e] = t.v[i];
+  }
+}
+
+void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream) {
+  hipLaunchKernelGGL(k_build_comb, dim3(1), dim3(64), 0, stream, ext, stride, e0, tab);
+}
+
+__device__ __forceinline__ void lds_fill(uint32_t* lds, const uint32_t* __restrict__ g, int words) {
+  const uint4* src = reinterpret_cast<const uint4*>(g);
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  for (int i = threadIdx.x; i < words / 4; i += blockDim.x) dst[i] = src[i];
+}
+
+static int comb_grid(size_t items, int threads) {
+  size_t want = (items + threads - 1) / threads;
+  size_t cap = 256 * 2;  // one 1024-thread workgroup per CU holds the 120 KB of tables
+  return (int)(want < cap ? (want ? want : 1) : cap);
+}
+
+// ------------------------------------------------------------------ K2 commitments
+__global__ __launch_bounds__(1024) void k_commit(size_t count, const uint32_t* __restrict__ a,
+                                                 const uint32_t* __restrict__ b,
+                                                 const uint32_t* __restrict__ tab_g,
+                                                 const uint32_t* __restrict__ tab_h,
+                                                 uint32_t* __restrict__ A_ext, uint32_t* __restrict__ E_ext) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  lds_fill(lds, tab_g, COMB_WORDS);
+  lds_fill(lds + COMB_WORDS, tab_h, COMB_WORDS);
+  __syncthreads();
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count;
+       e += (size_t)gridDim.x * blockDim.x) {
+    sc sa, sb;
+    sc_load(sa, a + 8 * e);
+    sc_load(sb, b + 8 * e);
+    ge_p3 acc;
+    ge_identity(acc);
+    comb_mul_add(acc, sa, lds);                 // apub = G::generator() * a   (committee.rs:155)
+    pt_store(A_ext, count, e, acc);
+    comb_mul_add(acc, sb, lds + COMB_WORDS);    // coeff_comm = h * b + apub   (committee.rs:156)
+    pt_store(E_ext, count, e, acc);
+  }
+}
+
+void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g, const uint32_t* tab_h,
+            uint32_t* A_ext, uint32_t* E_ext, hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_commit, dim3(comb_grid(count, 1024)), dim3(1024), 2 * COMB_WORDS * 4, stream, count,
+                     a, b, tab_g, tab_h, A_ext, E_ext);
+}
+
+// ------------------------------------------------------------------ K1 share evaluation
+// Horner at x = j+1: identical field value to the power-sum of polynomial.rs:68-74.
+__global__ __launch_bounds__(256) void k_share_eval(size_t n, size_t N, const uint32_t* __restrict__ a,
+                                                    const uint32_t* __restrict__ b, uint32_t* __restrict__ s,
+                                                    uint32_t* __restrict__ sp) {
+  const size_t i = blockIdx.y;
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t x = (uint32_t)(j + 1);
+  const uint32_t* ai = a + 8 * i * N;
+  const uint32_t* bi = b + 8 * i * N;
+  sc fa, fb, c;
+  sc_load(fa, ai + 8 * (N - 1));
+  sc_load(fb, bi + 8 * (N - 1));
+  for (size_t k = N - 1; k-- > 0;) {
+    sc_load(c, ai + 8 * k);
+    sc_mul_small_add(fa, fa, x, c);
+    sc_load(c, bi + 8 * k);
+    sc_mul_small_add(fb, fb, x, c);
+  }
+  st_words8(s + 8 * (i * n + j), fa.v);
+  st_words8(sp + 8 * (i * n + j), fb.v);
+}
+
+void share_eval(size_t D, size_t n, size_t N, const uint32_t* a, const uint32_t* b, uint32_t* s, uint32_t* sp,
+                hipStream_t stream) {
+  if (!D || !n) return;
+  hipLaunchKernelGGL(k_share_eval, dim3((unsigned)((n + 255) / 256), (unsigned)D), dim3(256), 0, stream, n, N,
+                     a, b, s, sp);
+}
+
+__global__ __launch_bounds__(256) void k_poly_eval(size_t D, size_t N, const uint32_t* __restrict__ coeffs,
+                                                   size_t M, const uint32_t* __restrict__ xs,
+                                                   uint32_t* __restrict__ out) {
+  const size_t i = blockIdx.y;
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const uint32_t* ci = coeffs + 8 * i * N;
+  sc f, c;
+  sc_load(f, ci + 8 * (N - 1));
+  for (size_t k = N - 1; k-- > 0;) {
+    sc_load(c, ci + 8 * k);
+    sc_mul_small_add(f, f, xs[m], c);
+  }
+  st_words8(out + 8 * (i * M + m), f.v);
+}
+
+void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint32_t* xs, uint32_t* out,
+               hipStream_t stream) {
+  if (!D || !M) return;
+  hipLaunchKernelGGL(k_poly_eval, dim3((unsigned)((M + 255) / 256), (unsigned)D), dim3(256), 0, stream, D, N,
+                     coeffs, M, xs, out);
+}
+
+// ------------------------------------------------------------------ K3a binomial-basis Horner
+// y = m * x for a wave-uniform small m (non-adjacent form, left to right).
+__device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint32_t m) {
+  uint32_t pos = 0, neg = 0;
+  int len = 0;
+  uint32_t v = m;
+  while (v) {
+    if (v & 1u) {
+      if ((v & 3u) == 1u) {
+        pos |= 1u << len;
+        v -= 1;
+      } else {
+        neg |= 1u << len;
+        v += 1;
+      }
+    }
+    v >>= 1;
+    len++;
+  }
+  y = x;
+  if (len <= 1) return;
+  ge_cached xc;
+  ge_to_cached(xc, x);
+  for (int i = len - 2; i >= 0; i--) {
+    const uint32_t bit = 1u << i;
+    const bool nz = ((pos | neg) & bit) != 0;
+    ge_dbl_rt(y, y, nz || i == 0);           // T only when an addition (or the result) needs it
+    if (nz) ge_add_signed(y, y, xc, (neg & bit) != 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy_pos(size_t npad, size_t N, const uint32_t* __restrict__ C,
+                                                  size_t kpos, uint32_t* __restrict__ e) {
+  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= npad) return;
+  const size_t S = N * npad;
+#pragma unroll 8
+  for (int w = 0; w < PT_WORDS; w++) e[w * S + d] = C[w * S + kpos * npad + d];
+}
+
+// One Horner step in the binomial basis: e'_0 = C_k, e'_m = m (e_{m-1} + e_m), m = 1..r.
+// Lanes = dealers (so m is uniform per wave); blockIdx.x = block of POS consecutive positions.
+constexpr int BINOM_POS = 4;
+__global__ __launch_bounds__(64, 3) void k_binom_step(int r, size_t npad, size_t N, const uint32_t* __restrict__ ein,
+                                                    uint32_t* __restrict__ eout) {
+  const size_t d = (size_t)blockIdx.y * blockDim.x + threadIdx.x;
+  const size_t S = N * npad;
+  const int lo = blockIdx.x * BINOM_POS + 1;
+  const int hi = min(r, (int)(blockIdx.x + 1) * BINOM_POS);
+  for (int m = hi; m >= lo; m--) {
+    // both operands re-read from HBM/L2 each position: keeps one point live, not two
+    ge_p3 x;
+    ge_cached cc;
+    {
+      ge_p3 cur;
+      if (m == r) ge_identity(cur);  // degree r-1 input: position r is zero
+      else pt_load(cur, ein, S, (size_t)m * npad + d);
+      ge_to_cached(cc, cur);
+    }
+    pt_load(x, ein, S, (size_t)(m - 1) * npad + d);
+    ge_add(x, x, cc);
+    mul_small_uniform(x, x, (uint32_t)m);
+    pt_store(eout, S, (size_t)m * npad + d, x);
+  }
+}
+
+uint32_t* binomial(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
+                   hipStream_t stream) {
+  (void)ndealers;
+  const size_t t = N - 1;
+  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, stream, npad, N, C, t, e0);
+  uint32_t* in = e0;
+  uint32_t* out = e1;
+  for (size_t r = 1; r <= t; r++) {
+    const size_t k = t - r;
+    hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, stream, npad, N, C, k,
+                       out);
+    const unsigned nblk = (unsigned)((r + BINOM_POS - 1) / BINOM_POS);
+    // npad is a multiple of 64: one wave per (position block, 64 dealers)
+    hipLaunchKernelGGL(k_binom_step, dim3(nblk, (unsigned)(npad / 64)), dim3(64), 0, stream, (int)r, npad, N, in,
+                       out);
+    uint32_t* tmp = in;
+    in = out;
+    out = tmp;
+  }
+  return in;
+}
+
+// ------------------------------------------------------------------ K3b stepping
+// D_m <- D_m + D_{m+1} (m = 0..t-1) once per receiver; D_0 after step j is P_i(j+1).
+// Positions are cut into blocks of STEP_BS (one lane each, registers only).  D_m depends only on
+// D_{m+1}, so block b never waits on block b-1: blocks run as separate launches from the top
+// block down, and each launch streams its lowest position's per-step value (cached form,
+// [dealer][step][40]) to the launch below.  Inside a block the neighbour value crosses lanes by
+// shuffle and waves by a double-buffered LDS slot; one workgroup per dealer.
+constexpr int STEP_BS = 256;
+
+__device__ __forceinline__ void cached_identity(ge_cached& c) {
+  fe_one(c.YpX);
+  fe_one(c.YmX);
+  fe_zero(c.Z2);
+  c.Z2.v[0] = 2;
+  fe_zero(c.T2d);
+}
+
+__global__ __launch_bounds__(STEP_BS, 2) void k_stepping(size_t npad, size_t N, const uint32_t* __restrict__ e,
+                                                         size_t nrecv, size_t pos0,
+                                                         const uint32_t* __restrict__ up,   // NULL: top block
+                                                         uint32_t* __restrict__ down,       // NULL: block 0
+                                                         uint32_t* __restrict__ R, size_t rstride) {
+  __shared__ uint32_t slot[2][STEP_BS / 64][PT_WORDS];
+  const size_t d = blockIdx.x;
+  const int l = threadIdx.x;
+  const int lane = l & 63, wave = l >> 6, nwaves = blockDim.x >> 6;
+  const size_t S = N * npad;
+  const size_t pos = pos0 + l;
+  ge_p3 D;
+  if (pos < N) pt_load(D, e, S, pos * npad + d);
+  else ge_identity(D);
+  const bool top_lane = (l == (int)blockDim.x - 1);
+  const uint4* upd = up ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
+  uint4* downd = down ? reinterpret_cast<uint4*>(down + d * nrecv * PT_WORDS) : nullptr;
+  for (size_t j = 0; j < nrecv; j++) {
+    ge_cached c0, nb;
+    ge_to_cached(c0, D);
+    uint32_t* w = reinterpret_cast<uint32_t*>(&c0);
+    uint32_t* nw = reinterpret_cast<uint32_t*>(&nb);
+#pragma unroll
+    for (int k = 0; k < PT_WORDS; k++) nw[k] = __shfl_down(w[k], 1, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < PT_WORDS; k++) slot[j & 1][wave][k] = w[k];
+      if (l == 0 && downd) {
+        const uint4* w4 = reinterpret_cast<const uint4*>(w);
+#pragma unroll
+        for (int k = 0; k < PT_WORDS / 4; k++) downd[j * (PT_WORDS / 4) + k] = w4[k];
+      }
+    }
+    __syncthreads();
+    if (lane == 63) {
+      if (wave + 1 < nwaves) {
+#pragma unroll
+        for (int k = 0; k < PT_WORDS; k++) nw[k] = slot[j & 1][wave + 1][k];
+      } else if (top_lane && upd) {
+        uint4* n4 = reinterpret_cast<uint4*>(nw);
+#pragma unroll
+        for (int k = 0; k < PT_WORDS / 4; k++) n4[k] = upd[j * (PT_WORDS / 4) + k];
+      } else {
+        cached_identity(nb);
+      }
+    }
+    if (pos + 1 < N) ge_add(D, D, nb);
+    if (l == 0 && R) pt_store(R, rstride, d * nrecv + j, D);
+  }
+}
+
+void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
+              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream) {
+  if (!ndealers || !nrecv) return;
+  const size_t rstride = ndealers * nrecv;
+  const size_t bs = N >= STEP_BS ? STEP_BS : ((N + 63) / 64) * 64;
+  const size_t nblk = (N + bs - 1) / bs;
+  uint32_t* up = nullptr;
+  for (size_t b = nblk; b-- > 0;) {
+    uint32_t* down = b ? ((nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
+    hipLaunchKernelGGL(k_stepping, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream, npad, N, e, nrecv,
+                       b * bs, up, down, b ? nullptr : R, rstride);
+    up = down;
+  }
+}
+
+// ------------------------------------------------------------------ K3c check
+__global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round,
+                                                const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
+                                                const uint32_t* __restrict__ R, const uint32_t* __restrict__ tab_g,
+                                                const uint32_t* __restrict__ tab_h,
+                                                const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  lds_fill(lds, tab_g, COMB_WORDS);
+  if (round == 2) lds_fill(lds + COMB_WORDS, tab_h, COMB_WORDS);
+  __syncthreads();
+  const size_t total = ndealers * nrecv;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = p / nrecv, j = p % nrecv;
+    ge_p3 acc, r;
+    ge_identity(acc);
+    sc x;
+    sc_load(x, s + 8 * p);
+    comb_mul_add(acc, x, lds);                       // G::generator() * s       (committee.rs:294, :537)
+    if (round == 2) {
+      sc_load(x, sp + 8 * p);
+      comb_mul_add(acc, x, lds + COMB_WORDS);        // + h * s'                 (committee.rs:292-293)
+    }
+    pt_load(r, R, total, p);
+    const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
+    uint8_t v = (dok[i] && eq) ? 1 : 0;
+    if (i + dealer_base == j + recv_base) v = 2;
+    dec[p] = v;
+  }
+}
+
+void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round, const uint32_t* s,
+           const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h, const uint8_t* dok,
+           uint8_t* dec, hipStream_t stream) {
+  const size_t total = ndealers * nrecv;
+  if (!total) return;
+  const size_t lds = (round == 2 ? 2 : 1) * COMB_WORDS * 4;
+  hipLaunchKernelGGL(k_check, dim3(comb_grid(total, 1024)), dim3(1024), lds, stream, ndealers, nrecv, dealer_base,
+                     recv_base, round, s, sp, R, tab_g, tab_h, dok, dec);
+}
+
+__global__ void k_dealer_ok(size_t ndealers, size_t N, const uint8_t* __restrict__ pok, uint8_t* __restrict__ ok) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ndealers) return;
+  uint8_t v = 1;
+  for (size_t k = 0; k < N; k++) v &= pok[i * N + k];
+  ok[i] = v;
+}
+
+void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream) {
+  if (!ndealers) return;
+  hipLaunchKernelGGL(k_dealer_ok, dim3((unsigned)((ndealers + 255) / 256)), dim3(256), 0, stream, ndealers, N,
+                     point_ok, ok);
+}
+
+// Horner in the exponent for one receiver index x per blockIdx.y (x = x0 + blockIdx.y, uniform per
+// wave): R[i][y] = sum_k x^k C_i[k] = C_0 + x (C_1 + x (...)), lanes = dealers.  This is the
+// single-party view of committee.rs:287-296 (t small-scalar multiplications instead of an MSM).
+__global__ __launch_bounds__(64, 3) void k_horner(size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ C,
+                                                uint32_t x0, size_t nrecv, uint32_t* __restrict__ R) {
+  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t x = x0 + blockIdx.y;
+  if (d >= npad) return;
+  const size_t S = N * npad;
+  ge_p3 acc, c;
+  pt_load(acc, C, S, (N - 1) * npad + d);
+  for (size_t k = N - 1; k-- > 0;) {
+    mul_small_uniform(acc, acc, x);
+    pt_load(c, C, S, k * npad + d);
+    ge_cached cc;
+    ge_to_cached(cc, c);
+    ge_add(acc, acc, cc);
+  }
+  if (d < ndealers) pt_store(R, ndealers * nrecv, d * nrecv + blockIdx.y, acc);
+}
+
+void horner(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t x0, size_t nrecv, uint32_t* R,
+            hipStream_t stream) {
+  if (!ndealers || !nrecv) return;
+  hipLaunchKernelGGL(k_horner, dim3((unsigned)(npad / 64), (unsigned)nrecv), dim3(64), 0, stream, ndealers, npad, N,
+                     C, x0, nrecv, R);
+}
+
+// Sum of the masked points of an SoA vector (one workgroup, tree reduction): out = sum mask[e] P_e.
+__global__ __launch_bounds__(256) void k_sum_points(size_t count, const uint32_t* __restrict__ pts, size_t stride,
+                                                    const uint8_t* __restrict__ mask, uint32_t* __restrict__ out,
+                                                    size_t ostride, size_t col) {
+  __shared__ uint32_t red[256][PT_WORDS];
+  ge_p3 acc;
+  ge_identity(acc);
+  for (size_t e = threadIdx.x; e < count; e += blockDim.x) {
+    if (mask && !mask[e]) continue;
+    ge_p3 p;
+    pt_load(p, pts, stride, e);
+    ge_cached pc;
+    ge_to_cached(pc, p);
+    ge_add(acc, acc, pc);
+  }
+  uint32_t* aw = reinterpret_cast<uint32_t*>(&acc);
+  for (int w = 0; w < PT_WORDS; w++) red[threadIdx.x][w] = aw[w];
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      ge_p3 x, y;
+      uint32_t* xw = reinterpret_cast<uint32_t*>(&x);
+      uint32_t* yw = reinterpret_cast<uint32_t*>(&y);
+      for (int w = 0; w < PT_WORDS; w++) {
+        xw[w] = red[threadIdx.x][w];
+        yw[w] = red[threadIdx.x + h][w];
+      }
+      ge_cached yc;
+      ge_to_cached(yc, y);
+      ge_add(x, x, yc);
+      for (int w = 0; w < PT_WORDS; w++) red[threadIdx.x][w] = xw[w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int w = 0; w < PT_WORDS; w++) out[w * ostride + col] = red[0][w];
+}
+
+void sum_points(size_t count, const uint32_t* pts, size_t stride, const uint8_t* mask, uint32_t* out,
+                size_t ostride, size_t col, hipStream_t stream) {
+  hipLaunchKernelGGL(k_sum_points, dim3(1), dim3(256), 0, stream, count, pts, stride, mask, out, ostride, col);
+}
+
+// RistrettoPoint::from_uniform_bytes of 64 hash bytes (hash_to_group, groups.rs:68-70) -> SoA point.
+__global__ void k_from_uniform(const uint32_t* __restrict__ in16, uint32_t* __restrict__ out) {
+  uint32_t a[8], b[8];
+  for (int i = 0; i < 8; i++) {
+    a[i] = in16[i];
+    b[i] = in16[8 + i];
+  }
+  ge_p3 p, q;
+  ristretto_elligator(p, a);
+  ristretto_elligator(q, b);
+  ge_cached qc;
+  ge_to_cached(qc, q);
+  ge_add(p, p, qc);
+  pt_store(out, 1, 0, p);
+}
+
+void from_uniform(const uint32_t* in16, uint32_t* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_from_uniform, dim3(1), dim3(1), 0, stream, in16, out);
+}
+
+// ------------------------------------------------------------------ generic MSM / fixed base
+// One workgroup per MSM; each lane accumulates s_k P_k over a strided subset of terms with a
+// uniform double-and-add (the addend is selected, never branched on), then a tree reduction.
+__global__ __launch_bounds__(256) void k_msm(size_t N, const uint32_t* __restrict__ scalars,
+                                             const uint32_t* __restrict__ pts, size_t stride,
+                                             uint32_t* __restrict__ out, size_t ostride) {
+  __shared__ uint32_t red[256][PT_WORDS];
+  const size_t b = blockIdx.x;
+  ge_p3 acc;
+  ge_identity(acc);
+  for (size_t k = threadIdx.x; k < N; k += blockDim.x) {
+    ge_p3 p, q;
+    pt_load(p, pts, stride, b * N + k);
+    sc s;
+    sc_load(s, scalars + 8 * (b * N + k));
+    ge_cached pc, idc;
+    ge_to_cached(pc, p);
+    cached_identity(idc);
+    ge_identity(q);
+    for (int bit = 252; bit >= 0; bit--) {
+      ge_dbl<true>(q, q);
+      const bool on = (s.v[bit >> 5] >> (bit & 31)) & 1u;
+      ge_cached sel;
+      uint32_t* sw = reinterpret_cast<uint32_t*>(&sel);
+      const uint32_t* pw = reinterpret_cast<const uint32_t*>(&pc);
+      const uint32_t* iw = reinterpret_cast<const uint32_t*>(&idc);
+#pragma unroll
+      for (int w = 0; w < PT_WORDS; w++) sw[w] = on ? pw[w] : iw[w];
+      ge_add(q, q, sel);
+    }
+    ge_cached qc;
+    ge_to_cached(qc, q);
+    ge_add(acc, acc, qc);
+  }
+  uint32_t* aw = reinterpret_cast<uint32_t*>(&acc);
+  for (int w = 0; w < PT_WORDS; w++) red[threadIdx.x][w] = aw[w];
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      ge_p3 x, y;
+      uint32_t* xw = reinterpret_cast<uint32_t*>(&x);
+      uint32_t* yw = reinterpret_cast<uint32_t*>(&y);
+      for (int w = 0; w < PT_WORDS; w++) {
+        xw[w] = red[threadIdx.x][w];
+        yw[w] = red[threadIdx.x + h][w];
+      }
+      ge_cached yc;
+      ge_to_cached(yc, y);
+      ge_add(x, x, yc);
+      for (int w = 0; w < PT_WORDS; w++) red[threadIdx.x][w] = xw[w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    ge_p3 r;
+    uint32_t* rw = reinterpret_cast<uint32_t*>(&r);
+    for (int w = 0; w < PT_WORDS; w++) rw[w] = red[0][w];
+    pt_store(out, ostride, b, r);
+  }
+}
+
+void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts, size_t stride, uint32_t* out_ext,
+               hipStream_t stream) {
+  if (!B) return;
+  hipLaunchKernelGGL(k_msm, dim3((unsigned)B), dim3(256), 0, stream, N, scalars, pts, stride, out_ext, B);
+}
+
+__global__ __launch_bounds__(1024) void k_fixed_base(size_t count, const uint32_t* __restrict__ scalars,
+                                                     const uint32_t* __restrict__ tab, uint32_t* __restrict__ out) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  lds_fill(lds, tab, COMB_WORDS);
+  __syncthreads();
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
+    sc x;
+    sc_load(x, scalars + 8 * e);
+    ge_p3 acc;
+    ge_identity(acc);
+    comb_mul_add(acc, x, lds);
+    pt_store(out, count, e, acc);
+  }
+}
+
+void fixed_base(size_t count, const uint32_t* scalars, const uint32_t* tab, uint32_t* out_ext, hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_fixed_base, dim3(comb_grid(count, 1024)), dim3(1024), COMB_WORDS * 4, stream, count, scalars,
+                     tab, out_ext);
+}
+
+// ------------------------------------------------------------------ layout / scalar helpers
+__global__ void k_to_pos_major(size_t D, size_t N, size_t npad, const uint32_t* __restrict__ in,
+                               uint32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = k * npad + i
+  if (e >= N * npad) return;
+  const size_t k = e / npad, i = e % npad;
+  const size_t S = N * npad, Sin = D * N;
+  for (int w = 0; w < PT_WORDS; w++) {
+    uint32_t v;
+    if (i < D) v = in[w * Sin + i * N + k];
+    else v = (w == 10 || w == 20) ? 1u : 0u;  // padded dealers hold the identity (0 : 1 : 1 : 0)
+    out[w * S + e] = v;
+  }
+}
+
+void to_position_major(size_t D, size_t N, size_t npad, const uint32_t* in, uint32_t* out, hipStream_t stream) {
+  const size_t tot = N * npad;
+  if (!tot) return;
+  hipLaunchKernelGGL(k_to_pos_major, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, D, N, npad, in, out);
+}
+
+__global__ void k_reduce_scalars(size_t count, const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  uint32_t w[8];
+  ld_words8(w, in + 8 * e);
+  sc r;
+  sc_reduce256(r, w);
+  st_words8(out + 8 * e, r.v);
+}
+
+void reduce_scalars(size_t count, const uint32_t* in, uint32_t* out, hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_reduce_scalars, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, in, out);
+}
+
+__global__ void k_sum_shares(size_t D, size_t n, const uint32_t* __restrict__ s, const uint8_t* __restrict__ mask,
+                             uint32_t* __restrict__ out) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  sc acc, x;
+  sc_zero(acc);
+  for (size_t i = 0; i < D; i++) {
+    if (!mask[i]) continue;
+    sc_load(x, s + 8 * (i * n + j));
+    sc_add(acc, acc, x);
+  }
+  st_words8(out + 8 * j, acc.v);
+}
+
+void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out, hipStream_t stream) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_sum_shares, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, D, n, s, mask, out);
+}
+
+}  // namespace dkgk

@@ -1,0 +1,93 @@
+// Device-memory layouts for group elements and the LDS fixed-base (comb) tables.
+//
+// Extended points live in HBM as structure-of-arrays: word w (0..39: X0..X9, Y0..Y9, Z0..Z9,
+// T0..T9) of element e at base[w * stride + e], so a wave reading 64 consecutive elements issues
+// 40 fully coalesced 256-byte loads.  Comb tables (affine Niels, 30 words per entry) use the same
+// SoA shape with 512 entries per base: entry (window w, digit d) = d * 16^w * B, d = 1..8.
+#pragma once
+#include "ge25519.h"
+#include "sc25519.h"
+
+constexpr int PT_WORDS = 40;
+constexpr int AFF_WORDS = 30;
+constexpr int COMB_ENTRIES = 512;  // 64 windows x 8 digits
+
+DKG_DEV void pt_load(ge_p3& p, const uint32_t* __restrict__ base, size_t stride, size_t e) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    p.X.v[i] = base[(size_t)(i)*stride + e];
+    p.Y.v[i] = base[(size_t)(10 + i) * stride + e];
+    p.Z.v[i] = base[(size_t)(20 + i) * stride + e];
+    p.T.v[i] = base[(size_t)(30 + i) * stride + e];
+  }
+}
+
+DKG_DEV void pt_store(uint32_t* __restrict__ base, size_t stride, size_t e, const ge_p3& p) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    base[(size_t)(i)*stride + e] = p.X.v[i];
+    base[(size_t)(10 + i) * stride + e] = p.Y.v[i];
+    base[(size_t)(20 + i) * stride + e] = p.Z.v[i];
+    base[(size_t)(30 + i) * stride + e] = p.T.v[i];
+  }
+}
+
+DKG_DEV void ld_words8(uint32_t (&w)[8], const uint32_t* __restrict__ p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+DKG_DEV void st_words8(uint32_t* __restrict__ p, const uint32_t (&w)[8]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+DKG_DEV void sc_load(sc& s, const uint32_t* __restrict__ p) {
+  uint32_t w[8];
+  ld_words8(w, p);
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.v[i] = w[i];
+}
+
+// Read comb entry e (SoA, 512 entries) from LDS / global.
+DKG_DEV void aff_load(ge_aff& q, const uint32_t* tab, int e) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    q.ypx.v[i] = tab[i * COMB_ENTRIES + e];
+    q.ymx.v[i] = tab[(10 + i) * COMB_ENTRIES + e];
+    q.xy2d.v[i] = tab[(20 + i) * COMB_ENTRIES + e];
+  }
+}
+
+// acc += s * B using the 64-window signed radix-16 comb of B (no doublings: one mixed
+// addition per window).  Digits are recentred on the fly exactly as dalek's to_radix_16.
+DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
+  int carry = 0;
+  for (int w = 0; w < 64; w++) {
+    const int wi = w >> 3;
+    uint32_t word = s.v[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) word = (wi == k) ? s.v[k] : word;
+    int d = (int)((word >> (4 * (w & 7))) & 15u) + carry;
+    carry = (d + 8) >> 4;
+    d -= carry << 4;
+    const int ad = d < 0 ? -d : d;
+    // Branch-free select (lanes carry independent scalars): identity for d = 0, and -Q =
+    // (y-x, y+x, -2dxy) for d < 0, so every lane runs the same single mixed addition.
+    ge_aff q, r;
+    aff_load(q, tab, w * 8 + (ad == 0 ? 0 : ad - 1));
+    fe nxy;
+    fe_neg(nxy, q.xy2d);
+    const bool neg = d < 0, zero = ad == 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      r.ypx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? q.ymx.v[i] : q.ypx.v[i]);
+      r.ymx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? q.ypx.v[i] : q.ymx.v[i]);
+      r.xy2d.v[i] = zero ? 0u : (neg ? nxy.v[i] : q.xy2d.v[i]);
+    }
+    ge_madd(acc, acc, r);
+  }
+}

@@ -1,0 +1,692 @@
+// Host runtime of the MI355X DKG backend: device context, buffer arena, the C ABI of
+// include/dkg_amd.h, and the ceremony driver that plays the reference's rounds 1-5
+// (committee.rs:124-805) for all parties in one process on one GPU.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dkg_amd.h"
+#include "host_crypto.h"
+#include "kernels.h"
+
+struct dkg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<std::string, std::pair<void*, size_t>> bufs;
+  uint32_t* tab_g = nullptr;  // comb table of the generator (15360 words)
+  uint32_t* tab_h = nullptr;  // comb table of the commitment key h
+  uint8_t h[32] = {0};
+  bool have_h = false;
+  size_t threshold = 0, nr_members = 0;
+  hipEvent_t ev[8] = {};
+};
+
+namespace {
+
+constexpr size_t PTB = 160;  // bytes of one extended point (40 words)
+constexpr size_t COMB_BYTES = 30 * 512 * 4;
+const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
+                               0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
+                               0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
+
+struct Fail {
+  int code;
+};
+
+#define HCK(call)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      ctx->err = std::string(#call) + ": " + hipGetErrorString(e_);                    \
+      throw Fail{DKG_E_DEVICE};                                                        \
+    }                                                                                  \
+  } while (0)
+
+template <typename T = void>
+T* buf(dkg_ctx* ctx, const char* name, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  auto it = ctx->bufs.find(name);
+  if (it != ctx->bufs.end() && it->second.second >= bytes) return reinterpret_cast<T*>(it->second.first);
+  if (it != ctx->bufs.end()) {
+    HCK(hipStreamSynchronize(ctx->stream));
+    HCK(hipFree(it->second.first));
+    ctx->bufs.erase(it);
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    ctx->err = std::string("hipMalloc(") + name + ", " + std::to_string(bytes) + "): " + hipGetErrorString(e);
+    throw Fail{DKG_E_NOMEM};
+  }
+  ctx->bufs[name] = {p, bytes};
+  return reinterpret_cast<T*>(p);
+}
+
+void h2d(dkg_ctx* ctx, void* d, const void* h, size_t n) {
+  if (n) HCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, ctx->stream));
+}
+void d2h(dkg_ctx* ctx, void* h, const void* d, size_t n) {
+  if (n) HCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->stream));
+}
+void sync(dkg_ctx* ctx) { HCK(hipStreamSynchronize(ctx->stream)); }
+void check_launch(dkg_ctx* ctx) { HCK(hipGetLastError()); }
+
+size_t pad64(size_t x) { return (x + 63) / 64 * 64; }
+
+template <typename F>
+int guarded(dkg_ctx* ctx, F&& f) {
+  if (!ctx) return DKG_E_ARG;
+  try {
+    HCK(hipSetDevice(ctx->device));
+    int rc = f();
+    return rc;
+  } catch (const Fail& x) {
+    return x.code;
+  } catch (const std::exception& x) {
+    ctx->err = x.what();
+    return DKG_E_NOMEM;
+  }
+}
+
+// Decode one 32-byte point and build its comb table into `tab`.
+void comb_for_point(dkg_ctx* ctx, const uint8_t p[32], uint32_t* tab, bool* ok) {
+  uint32_t* comp = buf<uint32_t>(ctx, "comb_in", 32);
+  uint32_t* ext = buf<uint32_t>(ctx, "comb_ext", PTB);
+  uint8_t* okd = buf<uint8_t>(ctx, "comb_ok", 1);
+  h2d(ctx, comp, p, 32);
+  dkgk::decode_points(comp, 1, ext, 1, okd, ctx->stream);
+  dkgk::build_comb(ext, 1, 0, tab, ctx->stream);
+  check_launch(ctx);
+  uint8_t v = 0;
+  d2h(ctx, &v, okd, 1);
+  sync(ctx);
+  *ok = v != 0;
+}
+
+// Upload scalars (32-byte encodings) and reduce them mod l (from_bits semantics, groups.rs:29-36).
+uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, size_t count) {
+  uint32_t* raw = buf<uint32_t>(ctx, "scalar_raw", 32 * count);
+  uint32_t* red = buf<uint32_t>(ctx, name, 32 * count);
+  h2d(ctx, raw, host, 32 * count);
+  dkgk::reduce_scalars(count, raw, red, ctx->stream);
+  return red;
+}
+
+// Rounds 2 / 4 for dealers [dealer_base, dealer_base + D) against receivers 0..n-1, all on device.
+// Ccomp [D][N][8] compressed commitments; s, sp [D][n][8] canonical; dec [D][n].
+void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t dealer_base,
+                   const uint32_t* Ccomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec) {
+  const size_t N = t + 1, npad = pad64(D);
+  uint32_t* Cext = buf<uint32_t>(ctx, "Cext", PTB * D * N);
+  uint8_t* pok = buf<uint8_t>(ctx, "pok", D * N);
+  uint8_t* dok = buf<uint8_t>(ctx, "dok", D);
+  uint32_t* Cpm = buf<uint32_t>(ctx, "Cpm", PTB * N * npad);
+  dkgk::decode_points(Ccomp, D * N, Cext, D * N, pok, ctx->stream);  // K5 (groups.rs:78-81)
+  dkgk::dealer_ok(D, N, pok, dok, ctx->stream);
+  dkgk::to_position_major(D, N, npad, Cext, Cpm, ctx->stream);
+  uint32_t* e0 = buf<uint32_t>(ctx, "binom0", PTB * N * npad);
+  uint32_t* e1 = buf<uint32_t>(ctx, "binom1", PTB * N * npad);
+  uint32_t* e = dkgk::binomial(D, npad, N, Cpm, e0, e1, ctx->stream);
+  uint32_t* R = buf<uint32_t>(ctx, "R", PTB * D * n);
+  uint32_t *sa = nullptr, *sb = nullptr;
+  if (N > 256) {
+    sa = buf<uint32_t>(ctx, "step_a", PTB * D * n);
+    sb = buf<uint32_t>(ctx, "step_b", PTB * D * n);
+  }
+  dkgk::stepping(D, npad, N, e, n, R, sa, sb, ctx->stream);
+  dkgk::check(D, n, dealer_base, 0, round, s, sp, R, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
+  check_launch(ctx);
+}
+
+double ev_ms(dkg_ctx* ctx, int a, int b) {
+  float ms = 0;
+  HCK(hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]));
+  return ms;
+}
+
+// Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
+void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
+                      const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big) {
+  const size_t N = t + 1;
+  uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
+  uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
+  // ---- round 2 (committee.rs:260-366)
+  verify_device(ctx, n, t, 2, n, 0, Ecomp, s, sp, dec2);
+  std::vector<uint8_t> h2(n * n);
+  d2h(ctx, h2.data(), dec2, n * n);
+  HCK(hipEventRecord(ctx->ev[2], ctx->stream));
+  sync(ctx);
+  std::vector<uint8_t> qualified(n, 1), r2err(n, 0);
+  std::vector<int32_t> complaints(n, 0);
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < n; j++)
+      if (h2[i * n + j] == DKG_REJECT) {
+        complaints[j]++;     // receiver j accuses dealer i (committee.rs:311-316)
+        qualified[i] = 0;    // a valid complaint disqualifies i for everyone (:370-398)
+      }
+  for (size_t j = 0; j < n; j++) r2err[j] = complaints[j] > (int32_t)t;  // :340-347
+  // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
+  uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
+  h2d(ctx, qmask, qualified.data(), n);
+  uint32_t* fs = buf<uint32_t>(ctx, "final_share", 32 * n);
+  dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
+  uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
+  dkgk::fixed_base(n, fs, ctx->tab_g, pub, ctx->stream);
+  uint32_t* pubc = buf<uint32_t>(ctx, "pub_comp", 32 * n);
+  dkgk::encode_points(pub, n, n, pubc, ctx->stream);
+  HCK(hipEventRecord(ctx->ev[3], ctx->stream));
+  // ---- round 4 (committee.rs:508-580)
+  verify_device(ctx, n, t, 4, n, 0, Acomp, s, nullptr, dec4);
+  std::vector<uint8_t> h4(n * n);
+  d2h(ctx, h4.data(), dec4, n * n);
+  HCK(hipEventRecord(ctx->ev[4], ctx->stream));
+  sync(ctx);
+  std::vector<uint8_t> recon(n, 0);
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < n; j++) {
+      if (i == j) continue;
+      if (!qualified[i]) h4[i * n + j] = DKG_SKIPPED;  // disqualified dealers are skipped (:522)
+      else if (h4[i * n + j] == DKG_REJECT) recon[i] = 1;  // -> reconstructable set (:660-670)
+    }
+  // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
+  std::vector<uint8_t> honest_mask(n);
+  size_t nrecon = 0;
+  for (size_t i = 0; i < n; i++) {
+    honest_mask[i] = qualified[i] && !recon[i];
+    nrecon += recon[i];
+  }
+  uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
+  HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
+  uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
+  uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
+  dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
+  uint8_t* hmask = buf<uint8_t>(ctx, "hmask", n);
+  h2d(ctx, hmask, honest_mask.data(), n);
+  uint32_t* parts = buf<uint32_t>(ctx, "mpk_parts", PTB * 2);
+  dkgk::sum_points(n, A0, n, hmask, parts, 2, 0, ctx->stream);
+  if (nrecon) {
+    // Lagrange reconstruction from t+1 shares of parties outside the reconstructable set
+    // (polynomial.rs:172-184 at 0; the reference interpolates the disclosed shares, :748-789).
+    std::vector<size_t> xs;
+    for (size_t j = 0; j < n && xs.size() < t + 1; j++)
+      if (!recon[j]) xs.push_back(j);
+    std::vector<dkgh::Zl> lambda(xs.size());
+    for (size_t a = 0; a < xs.size(); a++) {
+      dkgh::Zl num = dkgh::zl_from_u64(1), den = dkgh::zl_from_u64(1);
+      for (size_t b = 0; b < xs.size(); b++) {
+        if (a == b) continue;
+        num = dkgh::zl_mul(num, dkgh::zl_sub(dkgh::zl_from_u64(0), dkgh::zl_from_u64(xs[b] + 1)));
+        den = dkgh::zl_mul(den, dkgh::zl_sub(dkgh::zl_from_u64(xs[a] + 1), dkgh::zl_from_u64(xs[b] + 1)));
+      }
+      lambda[a] = dkgh::zl_mul(num, dkgh::zl_inv(den));
+    }
+    std::vector<uint8_t> hs(32 * n * n);
+    d2h(ctx, hs.data(), s, 32 * n * n);
+    sync(ctx);
+    std::vector<uint8_t> secrets;
+    for (size_t i = 0; i < n; i++) {
+      if (!recon[i]) continue;
+      dkgh::Zl acc = dkgh::zl_from_u64(0);
+      for (size_t a = 0; a < xs.size(); a++) {
+        dkgh::Zl y = dkgh::zl_from_bytes_wide(&hs[32 * (i * n + xs[a])], 32);
+        acc = dkgh::zl_add(acc, dkgh::zl_mul(lambda[a], y));
+      }
+      uint8_t b[32];
+      dkgh::zl_to_bytes(b, acc);
+      secrets.insert(secrets.end(), b, b + 32);
+    }
+    uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
+    h2d(ctx, sec, secrets.data(), secrets.size());
+    uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
+    dkgk::fixed_base(nrecon, sec, ctx->tab_g, gsec, ctx->stream);
+    dkgk::sum_points(nrecon, gsec, nrecon, nullptr, parts, 2, 1, ctx->stream);
+  } else {
+    dkgk::sum_points(0, A0, n, nullptr, parts, 2, 1, ctx->stream);  // identity
+  }
+  uint32_t* mpk_ext = buf<uint32_t>(ctx, "mpk_ext", PTB);
+  dkgk::sum_points(2, parts, 2, nullptr, mpk_ext, 1, 0, ctx->stream);
+  uint32_t* mpk_c = buf<uint32_t>(ctx, "mpk_comp", 32);
+  dkgk::encode_points(mpk_ext, 1, 1, mpk_c, ctx->stream);
+  check_launch(ctx);
+  d2h(ctx, out->mpk, mpk_c, 32);
+  HCK(hipEventRecord(ctx->ev[5], ctx->stream));
+  // ---- outputs
+  if (out->qualified) memcpy(out->qualified, qualified.data(), n);
+  if (out->r2_error) memcpy(out->r2_error, r2err.data(), n);
+  if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * n);
+  if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
+  int32_t nq = 0;
+  for (auto q : qualified) nq += q;
+  out->n_qualified = nq;
+  if (copy_big) {
+    if (out->dec2) memcpy(out->dec2, h2.data(), n * n);
+    if (out->dec4) memcpy(out->dec4, h4.data(), n * n);
+    if (out->final_share) d2h(ctx, out->final_share, fs, 32 * n);
+    if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * n);
+  }
+  sync(ctx);
+}
+
+// Round 1 for D dealers on device: a, b canonical [D][N][8] -> Ecomp, Acomp [D][N][8], s, sp [D][n][8].
+void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a, const uint32_t* b,
+                   uint32_t* Ecomp, uint32_t* Acomp, uint32_t* s, uint32_t* sp) {
+  const size_t N = t + 1;
+  uint32_t* Aext = buf<uint32_t>(ctx, "Aext", PTB * D * N);
+  uint32_t* Eext = buf<uint32_t>(ctx, "Eext", PTB * D * N);
+  dkgk::commit(D * N, a, b, ctx->tab_g, ctx->tab_h, Aext, Eext, ctx->stream);  // K2 (committee.rs:151-159)
+  dkgk::encode_points(Eext, D * N, D * N, Ecomp, ctx->stream);                    // broadcast encodings
+  dkgk::encode_points(Aext, D * N, D * N, Acomp, ctx->stream);
+  dkgk::share_eval(D, n, N, a, b, s, sp, ctx->stream);                            // K1 (:164-167)
+  check_launch(ctx);
+}
+
+int need_env(dkg_ctx* ctx) {
+  if (!ctx->have_h) {
+    ctx->err = "dkg_env_init has not been called (commitment key unknown)";
+    return DKG_E_ARG;
+  }
+  return DKG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dkg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int dkg_ctx_create(int device, dkg_ctx** out) {
+  if (!out) return DKG_E_ARG;
+  *out = nullptr;
+  dkg_ctx* ctx = new dkg_ctx();
+  ctx->device = device;
+  int rc = guarded(ctx, [&] {
+    HCK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    for (auto& e : ctx->ev) HCK(hipEventCreate(&e));
+    HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
+    HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
+    bool ok = false;
+    comb_for_point(ctx, BASEPOINT, ctx->tab_g, &ok);
+    if (!ok) {
+      ctx->err = "basepoint failed to decode on device";
+      return DKG_E_DEVICE;
+    }
+    return DKG_OK;
+  });
+  if (rc != DKG_OK) {
+    fprintf(stderr, "dkg_ctx_create: %s\n", ctx->err.c_str());
+    dkg_ctx_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return DKG_OK;
+}
+
+void dkg_ctx_destroy(dkg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->bufs) (void)hipFree(kv.second.first);
+  if (ctx->tab_g) (void)hipFree(ctx->tab_g);
+  if (ctx->tab_h) (void)hipFree(ctx->tab_h);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* dkg_ctx_last_error(const dkg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dkg_env_check(size_t threshold, size_t nr_members) {
+  // committee.rs:73: assert!(threshold < (nr_members + 1) / 2)
+  if (nr_members == 0 || !(threshold < (nr_members + 1) / 2)) return DKG_E_ARG;
+  return DKG_OK;
+}
+
+int dkg_env_init(dkg_ctx* ctx, size_t threshold, size_t nr_members, const uint8_t* ck, size_t ck_len,
+                 uint8_t h_out[32]) {
+  int rc = dkg_env_check(threshold, nr_members);
+  if (rc != DKG_OK) {
+    if (ctx) ctx->err = "threshold must be < (nr_members + 1) / 2 (committee.rs:73)";
+    return rc;
+  }
+  return guarded(ctx, [&] {
+    // CommitmentKey::generate: h = RistrettoPoint::hash_from_bytes::<Blake2b>(ck) (commitment.rs:13-17)
+    uint8_t hash[64];
+    dkgh::blake2b(hash, 64, ck, ck_len);
+    uint32_t* in = buf<uint32_t>(ctx, "h_in", 64);
+    uint32_t* ext = buf<uint32_t>(ctx, "h_ext", PTB);
+    uint32_t* comp = buf<uint32_t>(ctx, "h_comp", 32);
+    h2d(ctx, in, hash, 64);
+    dkgk::from_uniform(in, ext, ctx->stream);
+    dkgk::encode_points(ext, 1, 1, comp, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, ctx->h, comp, 32);
+    sync(ctx);
+    bool ok = false;
+    comb_for_point(ctx, ctx->h, ctx->tab_h, &ok);
+    if (!ok) return DKG_E_DEVICE;
+    ctx->have_h = true;
+    ctx->threshold = threshold;
+    ctx->nr_members = nr_members;
+    if (h_out) memcpy(h_out, ctx->h, 32);
+    return DKG_OK;
+  });
+}
+
+int dkg_msm_batch(dkg_ctx* ctx, size_t B, size_t N, const uint8_t* scalars, const uint8_t* points, uint8_t* out) {
+  return guarded(ctx, [&] {
+    if (B == 0) return DKG_OK;
+    uint32_t* sc = upload_scalars(ctx, "msm_sc", scalars, B * N);
+    uint32_t* pc = buf<uint32_t>(ctx, "msm_pc", 32 * B * N);
+    uint32_t* pe = buf<uint32_t>(ctx, "msm_pe", PTB * B * N);
+    uint8_t* ok = buf<uint8_t>(ctx, "msm_ok", B * N);
+    h2d(ctx, pc, points, 32 * B * N);
+    dkgk::decode_points(pc, B * N, pe, B * N, ok, ctx->stream);
+    uint32_t* oe = buf<uint32_t>(ctx, "msm_oe", PTB * B);
+    uint32_t* oc = buf<uint32_t>(ctx, "msm_oc", 32 * B);
+    dkgk::msm_batch(B, N, sc, pe, B * N, oe, ctx->stream);
+    dkgk::encode_points(oe, B, B, oc, ctx->stream);
+    check_launch(ctx);
+    std::vector<uint8_t> okh(B * N);
+    d2h(ctx, okh.data(), ok, B * N);
+    d2h(ctx, out, oc, 32 * B);
+    sync(ctx);
+    for (auto v : okh)
+      if (!v) {
+        ctx->err = "msm: a point failed to decode";
+        return DKG_E_DECODE;
+      }
+    return DKG_OK;
+  });
+}
+
+int dkg_fixed_base_batch(dkg_ctx* ctx, const uint8_t base[32], size_t count, const uint8_t* scalars, uint8_t* out) {
+  return guarded(ctx, [&] {
+    if (count == 0) return DKG_OK;
+    const uint32_t* tab = ctx->tab_g;
+    if (base) {
+      uint32_t* t = buf<uint32_t>(ctx, "fb_tab", COMB_BYTES);
+      bool ok = false;
+      comb_for_point(ctx, base, t, &ok);
+      if (!ok) {
+        ctx->err = "fixed_base: base point failed to decode";
+        return DKG_E_DECODE;
+      }
+      tab = t;
+    }
+    uint32_t* sc = upload_scalars(ctx, "fb_sc", scalars, count);
+    uint32_t* oe = buf<uint32_t>(ctx, "fb_oe", PTB * count);
+    uint32_t* oc = buf<uint32_t>(ctx, "fb_oc", 32 * count);
+    dkgk::fixed_base(count, sc, tab, oe, ctx->stream);
+    dkgk::encode_points(oe, count, count, oc, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, out, oc, 32 * count);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_poly_eval_batch(dkg_ctx* ctx, size_t D, size_t N, const uint8_t* coeffs, size_t M, const uint32_t* xs,
+                        uint8_t* out) {
+  return guarded(ctx, [&] {
+    if (D == 0 || M == 0) return DKG_OK;
+    if (N == 0) return DKG_E_ARG;
+    for (size_t m = 0; m < M; m++)
+      if (xs[m] >= (1u << 24)) {
+        ctx->err = "poly_eval: evaluation points must be < 2^24";
+        return DKG_E_ARG;
+      }
+    uint32_t* c = upload_scalars(ctx, "pe_c", coeffs, D * N);
+    uint32_t* x = buf<uint32_t>(ctx, "pe_x", 4 * M);
+    uint32_t* o = buf<uint32_t>(ctx, "pe_o", 32 * D * M);
+    h2d(ctx, x, xs, 4 * M);
+    dkgk::poly_eval(D, N, c, M, x, o, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, out, o, 32 * D * M);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_points_valid_batch(dkg_ctx* ctx, size_t count, const uint8_t* points, uint8_t* ok) {
+  return guarded(ctx, [&] {
+    if (count == 0) return DKG_OK;
+    uint32_t* pc = buf<uint32_t>(ctx, "pv_c", 32 * count);
+    uint32_t* pe = buf<uint32_t>(ctx, "pv_e", PTB * count);
+    uint8_t* od = buf<uint8_t>(ctx, "pv_ok", count);
+    h2d(ctx, pc, points, 32 * count);
+    dkgk::decode_points(pc, count, pe, count, od, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, ok, od, count);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_share_gen(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint8_t* a, const uint8_t* b, uint8_t* E,
+                  uint8_t* A, uint8_t* s, uint8_t* s_prime) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (D == 0) return DKG_OK;
+    const size_t N = t + 1;
+    uint32_t* da = upload_scalars(ctx, "sg_a", a, D * N);
+    uint32_t* db = upload_scalars(ctx, "sg_b", b, D * N);
+    uint32_t* Ec = buf<uint32_t>(ctx, "sg_E", 32 * D * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "sg_A", 32 * D * N);
+    uint32_t* ds = buf<uint32_t>(ctx, "sg_s", 32 * D * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "sg_sp", 32 * D * n);
+    round1_device(ctx, D, n, t, da, db, Ec, Ac, ds, dsp);
+    if (E) d2h(ctx, E, Ec, 32 * D * N);
+    if (A) d2h(ctx, A, Ac, 32 * D * N);
+    if (s) d2h(ctx, s, ds, 32 * D * n);
+    if (s_prime) d2h(ctx, s_prime, dsp, 32 * D * n);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_verify_pairs(dkg_ctx* ctx, size_t n, size_t t, int round, size_t d0, size_t d1, const uint8_t* C,
+                     const uint8_t* s, const uint8_t* s_prime, uint8_t* decision) {
+  return guarded(ctx, [&] {
+    if ((round != 2 && round != 4) || d1 < d0 || d1 > n) return DKG_E_ARG;
+    if (round == 2) {
+      int rc = need_env(ctx);
+      if (rc) return rc;
+      if (!s_prime) return DKG_E_ARG;
+    }
+    const size_t D = d1 - d0, N = t + 1;
+    if (D == 0) return DKG_OK;
+    uint32_t* Cc = buf<uint32_t>(ctx, "vp_C", 32 * D * N);
+    h2d(ctx, Cc, C, 32 * D * N);
+    uint32_t* ds = upload_scalars(ctx, "vp_s", s, D * n);
+    uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vp_sp", s_prime, D * n) : nullptr;
+    uint8_t* dec = buf<uint8_t>(ctx, "vp_dec", D * n);
+    verify_device(ctx, n, t, round, D, d0, Cc, ds, dsp, dec);
+    d2h(ctx, decision, dec, D * n);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, const uint8_t* C, const uint8_t* s,
+                        const uint8_t* s_prime, uint8_t* decision) {
+  return guarded(ctx, [&] {
+    if ((round != 2 && round != 4) || j >= n) return DKG_E_ARG;
+    if (round == 2) {
+      int rc = need_env(ctx);
+      if (rc) return rc;
+      if (!s_prime) return DKG_E_ARG;
+    }
+    const size_t N = t + 1, npad = pad64(n);
+    uint32_t* Cc = buf<uint32_t>(ctx, "vr_C", 32 * n * N);
+    h2d(ctx, Cc, C, 32 * n * N);
+    uint32_t* Cext = buf<uint32_t>(ctx, "Cext", PTB * n * N);
+    uint8_t* pok = buf<uint8_t>(ctx, "pok", n * N);
+    uint8_t* dok = buf<uint8_t>(ctx, "dok", n);
+    uint32_t* Cpm = buf<uint32_t>(ctx, "Cpm", PTB * N * npad);
+    dkgk::decode_points(Cc, n * N, Cext, n * N, pok, ctx->stream);
+    dkgk::dealer_ok(n, N, pok, dok, ctx->stream);
+    dkgk::to_position_major(n, N, npad, Cext, Cpm, ctx->stream);
+    uint32_t* R = buf<uint32_t>(ctx, "vr_R", PTB * n);
+    dkgk::horner(n, npad, N, Cpm, (uint32_t)(j + 1), 1, R, ctx->stream);  // committee.rs:287-296, one party
+    uint32_t* ds = upload_scalars(ctx, "vr_s", s, n);
+    uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vr_sp", s_prime, n) : nullptr;
+    uint8_t* dec = buf<uint8_t>(ctx, "vr_dec", n);
+    dkgk::check(n, 1, 0, j, round, ds, dsp, R, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, decision, dec, n);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_run_device(dkg_ctx* ctx, size_t n, size_t t, const void* d_a, const void* d_b,
+                            dkg_ceremony_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out) return DKG_E_ARG;
+    const size_t N = t + 1;
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    uint32_t* Ec = buf<uint32_t>(ctx, "cer_E", 32 * n * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
+    uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
+    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, false);  // small outputs only
+    out->ms_round1 = ev_ms(ctx, 0, 1);
+    out->ms_round2 = ev_ms(ctx, 1, 2);
+    out->ms_round3 = ev_ms(ctx, 2, 3);
+    out->ms_round4 = ev_ms(ctx, 3, 4);
+    out->ms_finalise = ev_ms(ctx, 4, 5);
+    out->ms_total = ev_ms(ctx, 0, 5);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_run(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* a, const uint8_t* b, dkg_ceremony_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out) return DKG_E_ARG;
+    const size_t N = t + 1;
+    uint32_t* da = upload_scalars(ctx, "cer_a", a, n * N);
+    uint32_t* db = upload_scalars(ctx, "cer_b", b, n * N);
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    uint32_t* Ec = buf<uint32_t>(ctx, "cer_E", 32 * n * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
+    uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
+    round1_device(ctx, n, n, t, da, db, Ec, Ac, ds, dsp);
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    if (out->E) d2h(ctx, out->E, Ec, 32 * n * N);
+    if (out->A) d2h(ctx, out->A, Ac, 32 * n * N);
+    if (out->s) d2h(ctx, out->s, ds, 32 * n * n);
+    if (out->s_prime) d2h(ctx, out->s_prime, dsp, 32 * n * n);
+    receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, true);
+    out->ms_round1 = ev_ms(ctx, 0, 1);
+    out->ms_round2 = ev_ms(ctx, 1, 2);
+    out->ms_round3 = ev_ms(ctx, 2, 3);
+    out->ms_round4 = ev_ms(ctx, 3, 4);
+    out->ms_finalise = ev_ms(ctx, 4, 5);
+    out->ms_total = ev_ms(ctx, 0, 5);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_verify(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E, const uint8_t* A, const uint8_t* s,
+                        const uint8_t* s_prime, dkg_ceremony_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out) return DKG_E_ARG;
+    const size_t N = t + 1;
+    uint32_t* Ec = buf<uint32_t>(ctx, "cer_E", 32 * n * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
+    h2d(ctx, Ec, E, 32 * n * N);
+    h2d(ctx, Ac, A, 32 * n * N);
+    uint32_t* ds = upload_scalars(ctx, "cer_s", s, n * n);
+    uint32_t* dsp = upload_scalars(ctx, "cer_sp", s_prime, n * n);
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, true);
+    out->ms_round1 = 0;
+    out->ms_round2 = ev_ms(ctx, 1, 2);
+    out->ms_round3 = ev_ms(ctx, 2, 3);
+    out->ms_round4 = ev_ms(ctx, 3, 4);
+    out->ms_finalise = ev_ms(ctx, 4, 5);
+    out->ms_total = ev_ms(ctx, 0, 5);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t d1, const void* d_a,
+                              const void* d_b, void* d_dec2, void* d_dec4, void* d_A0, void* d_partial,
+                              double* ms_total) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || d1 < d0 || d1 > n) return DKG_E_ARG;
+    const size_t D = d1 - d0, N = t + 1;
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    uint32_t* Ec = buf<uint32_t>(ctx, "sh_E", 32 * D * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "sh_A", 32 * D * N);
+    uint32_t* ds = buf<uint32_t>(ctx, "sh_s", 32 * D * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "sh_sp", 32 * D * n);
+    if (D) {
+      round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+      verify_device(ctx, n, t, 2, D, d0, Ec, ds, dsp, (uint8_t*)d_dec2);
+      verify_device(ctx, n, t, 4, D, d0, Ac, ds, nullptr, (uint8_t*)d_dec4);
+      HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
+      uint8_t* ones = buf<uint8_t>(ctx, "sh_ones", D);
+      HCK(hipMemsetAsync(ones, 1, D, ctx->stream));
+      dkgk::sum_shares(D, n, ds, ones, (uint32_t*)d_partial, ctx->stream);
+    } else {
+      HCK(hipMemsetAsync(d_partial, 0, 32 * n, ctx->stream));
+    }
+    check_launch(ctx);
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    sync(ctx);
+    if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
+    return DKG_OK;
+  });
+}
+
+int dkg_dealer_coeffs(const uint8_t master[32], uint32_t ceremony, size_t d0, size_t D, size_t t, uint8_t* a,
+                      uint8_t* b) {
+  if (!master || (!a && !b)) return DKG_E_ARG;
+  const size_t N = t + 1;
+  static const char tag[] = "dkg-amd/v1/dealer";
+  std::vector<uint8_t> stream(2 * N * 64);
+  for (size_t i = 0; i < D; i++) {
+    uint8_t msg[sizeof tag - 1 + 40];
+    memcpy(msg, tag, sizeof tag - 1);
+    memcpy(msg + sizeof tag - 1, master, 32);
+    const uint32_t dealer = (uint32_t)(d0 + i);
+    for (int k = 0; k < 4; k++) {
+      msg[sizeof tag - 1 + 32 + k] = (uint8_t)(ceremony >> (8 * k));
+      msg[sizeof tag - 1 + 36 + k] = (uint8_t)(dealer >> (8 * k));
+    }
+    uint8_t seed[32];
+    dkgh::blake2b(seed, 32, msg, sizeof msg);
+    dkgh::chacha20(seed, 0, stream.data(), stream.size());
+    for (size_t k = 0; k < N; k++) {  // hiding polynomial first (committee.rs:143-146)
+      if (b) dkgh::zl_to_bytes(b + 32 * (i * N + k), dkgh::zl_from_bytes_wide(&stream[64 * k], 64));
+      if (a) dkgh::zl_to_bytes(a + 32 * (i * N + k), dkgh::zl_from_bytes_wide(&stream[64 * (N + k)], 64));
+    }
+  }
+  return DKG_OK;
+}
+
+}  // extern "C"

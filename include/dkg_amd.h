@@ -1,0 +1,141 @@
+/*
+ * dkg_amd.h — C ABI of the MI355X (gfx950) backend for the share-generation and
+ * share-verification hot path of danielSanchezQ/dkg (Pedersen-VSS DKG over Ristretto255).
+ *
+ * Encodings (identical to the reference's wire values):
+ *   scalar = 32 bytes little-endian, canonical mod l      (groups.rs:23-27)
+ *   point  = 32 bytes compressed Ristretto255             (groups.rs:72-76)
+ * Every buffer is caller-owned host memory unless a function name ends in `_device`
+ * (then the pointers are HIP device pointers).  No pointer is retained after return.
+ * One dkg_ctx drives one GPU (one process per GPU); a ctx is not re-entrant.
+ *
+ * Status codes: protocol outcomes (a rejected share, MisbehaviourHigherThreshold) are DATA,
+ * returned in decision matrices and flags; negative codes are call failures only.
+ */
+#ifndef DKG_AMD_H
+#define DKG_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DKG_OK 0
+#define DKG_E_ARG (-1)    /* where the reference panics: length mismatch, t >= (n+1)/2, index range */
+#define DKG_E_DECODE (-2) /* an input point does not decode (CompressedRistretto::decompress -> None) */
+#define DKG_E_DEVICE (-3) /* HIP runtime failure (message in dkg_ctx_last_error) */
+#define DKG_E_NOMEM (-4)
+
+/* decision matrix values ([dealer][receiver], one byte per pair) */
+#define DKG_REJECT 0
+#define DKG_ACCEPT 1
+#define DKG_SELF 2       /* i == j: a party never checks itself (qualified_set starts at 1) */
+#define DKG_SKIPPED 3    /* round 4 only: dealer not qualified, check skipped (committee.rs:522) */
+
+typedef struct dkg_ctx dkg_ctx;
+
+/* ---- context ---- */
+int dkg_ctx_create(int device, dkg_ctx **out);
+void dkg_ctx_destroy(dkg_ctx *ctx);
+const char *dkg_ctx_last_error(const dkg_ctx *ctx);
+/* Number of GPUs visible to this process (counts only; does not create a context). */
+int dkg_device_count(void);
+
+/* ---- Environment::init (committee.rs:72-83) ----
+ * Checks threshold < (nr_members + 1) / 2 (DKG_E_ARG otherwise, where the reference asserts) and
+ * derives the Pedersen commitment key h = hash_to_group::<Blake2b>(ck_bytes) (commitment.rs:13-17),
+ * caching its fixed-base table on the device.  h_out may be NULL. */
+int dkg_env_init(dkg_ctx *ctx, size_t threshold, size_t nr_members, const uint8_t *ck_bytes, size_t ck_len,
+                 uint8_t h_out[32]);
+/* Same check without a context (pure function). */
+int dkg_env_check(size_t threshold, size_t nr_members);
+
+/* ---- trait-level batches (traits.rs:142-238, groups.rs:11-90) ---- */
+/* PrimeGroupElement::vartime_multiscalar_multiplication (traits.rs:234-237), B independent MSMs of
+ * N terms: out[b] = sum_k scalars[b][k] * points[b][k].  scalars [B][N][32], points [B][N][32]. */
+int dkg_msm_batch(dkg_ctx *ctx, size_t B, size_t N, const uint8_t *scalars, const uint8_t *points, uint8_t *out);
+/* Mul<Scalar> by a fixed base (traits.rs:212): out[c] = scalars[c] * base.  base == NULL means
+ * PrimeGroupElement::generator() (groups.rs:60-62). */
+int dkg_fixed_base_batch(dkg_ctx *ctx, const uint8_t base[32], size_t count, const uint8_t *scalars, uint8_t *out);
+/* Polynomial::evaluate (polynomial.rs:68-74) of D polynomials with N coefficients each
+ * (coeffs [D][N][32]) at M small integer points xs[m] < 2^24: out [D][M][32]. */
+int dkg_poly_eval_batch(dkg_ctx *ctx, size_t D, size_t N, const uint8_t *coeffs, size_t M, const uint32_t *xs,
+                        uint8_t *out);
+/* PrimeGroupElement::from_bytes validity (groups.rs:78-81): ok[c] = 1 iff points[c] decodes. */
+int dkg_points_valid_batch(dkg_ctx *ctx, size_t count, const uint8_t *points, uint8_t *ok);
+
+/* ---- round 1: share generation (Phases<Initialise>::init, committee.rs:124-216) ----
+ * For dealers i in [0, D): coefficients a (sharing) and b (hiding), [D][t+1][32];
+ * E[i][k] = h*b[i][k] + g*a[i][k], A[i][k] = g*a[i][k] ([D][t+1][32], committee.rs:151-159);
+ * s[i][j] = f_i(j+1), s_prime[i][j] = f'_i(j+1) for receivers j in [0, n) ([D][n][32], :164-167).
+ * Requires dkg_env_init (for h).  Any output may be NULL to skip it. */
+int dkg_share_gen(dkg_ctx *ctx, size_t D, size_t n, size_t t, const uint8_t *a, const uint8_t *b, uint8_t *E,
+                  uint8_t *A, uint8_t *s, uint8_t *s_prime);
+
+/* ---- rounds 2 and 4: share checks ----
+ * round 2 (Phases<Phase1>::proceed, committee.rs:273-338): h*s' + g*s == sum_k (j+1)^k E_i[k]
+ * round 4 (Phases<Phase3>::proceed, committee.rs:520-559):          g*s == sum_k (j+1)^k A_i[k]
+ * for dealers i in [d0, d1) and ALL receivers j in [0, n).  C = E (round 2) or A (round 4) of those
+ * dealers, [d1-d0][t+1][32]; s, s_prime = the dealers' share rows [d1-d0][n][32] (s_prime unused in
+ * round 4).  decision [d1-d0][n] (DKG_ACCEPT / DKG_REJECT / DKG_SELF).  A dealer whose commitment
+ * vector does not decode is rejected by every receiver (and the call returns DKG_OK). */
+int dkg_verify_pairs(dkg_ctx *ctx, size_t n, size_t t, int round, size_t d0, size_t d1, const uint8_t *C,
+                     const uint8_t *s, const uint8_t *s_prime, uint8_t *decision);
+/* The same check seen from ONE receiver j (what one party runs in the reference): decisions of
+ * receiver j (0-based; index j+1) over all n dealers.  C [n][t+1][32], s / s_prime [n][32] = the
+ * column of shares addressed to j.  decision [n]. */
+int dkg_verify_receiver(dkg_ctx *ctx, size_t n, size_t t, int round, size_t j, const uint8_t *C, const uint8_t *s,
+                        const uint8_t *s_prime, uint8_t *decision);
+
+/* ---- whole ceremony (rounds 1-5, every party played in one process as the reference tests do,
+ * committee.rs:1518-1656) in plaintext-share mode. ---- */
+typedef struct {
+  /* host outputs; any pointer may be NULL */
+  uint8_t *E, *A;               /* [n][t+1][32] (round-1 broadcast; A = round-3 broadcast) */
+  uint8_t *s, *s_prime;         /* [n][n][32] */
+  uint8_t *dec2, *dec4;         /* [n dealer][n receiver] */
+  uint8_t *qualified;           /* [n] common qualified set after round 3 */
+  uint8_t *r2_error;            /* [n] receiver j: more than t complaints (MisbehaviourHigherThreshold) */
+  int32_t *complaints2;         /* [n] complaints raised by receiver j in round 2 */
+  uint8_t *reconstruct;         /* [n] dealers whose secret is reconstructed in finalise */
+  uint8_t *final_share;         /* [n][32] s_j = sum_{i in Q} s_ij (committee.rs:454-462) */
+  uint8_t *public_share;        /* [n][32] g * s_j (committee.rs:464-466) */
+  uint8_t mpk[32];              /* MasterPublicKey (committee.rs:726-805) */
+  int32_t n_qualified;
+  /* device times of each phase, milliseconds (HIP events) */
+  double ms_round1, ms_round2, ms_round3, ms_round4, ms_finalise, ms_total;
+} dkg_ceremony_out;
+
+/* Honest run from coefficients a, b ([n][t+1][32], host). */
+int dkg_ceremony_run(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *a, const uint8_t *b, dkg_ceremony_out *out);
+/* Receiver side (rounds 2-5) from broadcast values that may have been tampered with:
+ * E, A [n][t+1][32]; s, s_prime [n][n][32]. */
+int dkg_ceremony_verify(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *E, const uint8_t *A, const uint8_t *s,
+                        const uint8_t *s_prime, dkg_ceremony_out *out);
+/* Device-resident variant for benchmarks: d_a, d_b are device pointers to [n][t+1][32] canonical
+ * scalars; intermediates stay in HBM; only the small outputs (mpk, flags, counts, timings) are
+ * copied back into *out (its array pointers are ignored except qualified / r2_error / complaints2). */
+int dkg_ceremony_run_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, const void *d_b,
+                            dkg_ceremony_out *out);
+/* Sharded variant (one rank of a multi-GPU run): this ctx owns dealers [d0, d1) of the same
+ * ceremony.  Produces this rank's commitments E/A and decision rows; the caller all-gathers
+ * (RCCL over xGMI) the rows, A_0 values and share partial sums.  Device pointers throughout:
+ * d_a, d_b [d1-d0][t+1][32]; d_dec2, d_dec4 [d1-d0][n]; d_A0 [d1-d0][32] (compressed A_i0);
+ * d_partial [n][32] = sum over this rank's dealers of s_ij (all assumed qualified). */
+int dkg_ceremony_shard_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const void *d_a,
+                              const void *d_b, void *d_dec2, void *d_dec4, void *d_A0, void *d_partial,
+                              double *ms_total);
+
+/* ---- synthetic inputs: the seeded RNG convention ----
+ * dealer seed = BLAKE2b-256("dkg-amd/v1/dealer" || master[32] || u32le ceremony || u32le dealer);
+ * coefficients = ChaCha20Rng(seed): hiding b_0..b_t first, then sharing a_0..a_t (committee.rs:143-146),
+ * each 64 bytes wide-reduced mod l (Scalar::random).  Host computation; a, b [D][t+1][32] for
+ * dealers [d0, d0+D). */
+int dkg_dealer_coeffs(const uint8_t master[32], uint32_t ceremony, size_t d0, size_t D, size_t t, uint8_t *a,
+                      uint8_t *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

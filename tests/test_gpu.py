@@ -1,0 +1,272 @@
+"""Parity of the HIP path (through the C ABI) with the golden fixtures and the CPU oracle.
+
+Every test here runs the gfx950 kernels in dkg_amd/libdkg_amd.so; the oracle (tests/oracle_lib.py)
+and the libsodium-generated fixtures are the checkers.  Bit-exact comparison throughout: this path
+is integer arithmetic, so there is no tolerance.
+"""
+import random
+
+import pytest
+
+import dkg_amd
+from dkg_amd import ACCEPT, REJECT, SELF
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+H = bytes.fromhex
+L = 2**252 + 27742317777372353535851937790883648493
+CK = b"Example of a shared string."
+
+
+@pytest.fixture(scope="module")
+def be():
+    b = dkg_amd.Backend(0)
+    yield b
+    b.close()
+
+
+def dec_str(raw):
+    return "".join(str(x) for x in raw)
+
+
+def test_env_and_commitment_key(be, golden):
+    g = golden("kat_group.json")
+    h = be.env_init(4, 10, CK)
+    assert h.hex() == g["hash_to_group"][0]["P"]  # commitment.rs:13-17
+    with pytest.raises(dkg_amd.DkgError):
+        dkg_amd.Environment(be, 5, 10)  # BASELINE config 1: committee.rs:73 rejects t=5, n=10
+    for e in g["hash_to_group"][1:]:
+        m = H(e["msg"])
+        assert be.env_init(0, 2, m).hex() == e["P"]
+    be.env_init(4, 10, CK)
+
+
+def test_fixed_base_generator(be, golden):
+    g = golden("kat_group.json")
+    ks = [e["k"].to_bytes(32, "little") for e in g["base_multiples"]] + [H(e["k"]) for e in g["base_mul"]]
+    exp = [e["P"] for e in g["base_multiples"]] + [e["P"] for e in g["base_mul"]]
+    out = be.fixed_base_batch(b"".join(ks))
+    assert [out[32 * i:32 * i + 32].hex() for i in range(len(ks))] == exp
+
+
+def test_fixed_base_other_point(be, golden):
+    for e in golden("kat_group.json")["mul"]:
+        assert be.fixed_base_batch(H(e["k"]), base=H(e["P"])).hex() == e["kP"]
+
+
+def test_points_valid(be, golden):
+    g = golden("kat_group.json")
+    bad = b"".join(H(x) for x in g["invalid_encodings"])
+    assert set(be.points_valid(bad)) == {0}
+    good = b"".join(H(e["P"]) for e in g["base_multiples"])
+    assert set(be.points_valid(good)) == {1}
+
+
+@pytest.mark.parametrize("idx", range(10))
+def test_msm_batch(be, golden, idx):
+    c = golden("kat_group.json")["msm"][idx]
+    N = c["N"]
+    if N == 0:
+        return
+    assert be.msm_batch(H(c["scalars"]), H(c["points"]), 1, N).hex() == c["out"]
+
+
+def test_msm_batch_many(be, golden):
+    cases = [c for c in golden("kat_group.json")["msm"] if c["N"] == 32]
+    sc = b"".join(H(c["scalars"]) for c in cases) * 3
+    pt = b"".join(H(c["points"]) for c in cases) * 3
+    out = be.msm_batch(sc, pt, 3 * len(cases), 32)
+    assert [out[32 * i:32 * i + 32].hex() for i in range(3 * len(cases))] == [c["out"] for c in cases] * 3
+
+
+def test_msm_decode_error(be, golden):
+    bad = H(golden("kat_group.json")["invalid_encodings"][0])
+    with pytest.raises(dkg_amd.DkgError) as ei:
+        be.msm_batch(bytes(32), bad, 1, 1)
+    assert ei.value.code == -2
+
+
+def test_poly_eval(be, golden):
+    s = golden("kat_scalar.json")
+    kt = s["poly_tests"]
+    coeffs = b"".join(c.to_bytes(32, "little") for c in kt["coeffs"])
+    assert be.poly_eval_batch(coeffs, 1, 5, [kt["x"]]) == kt["value"].to_bytes(32, "little")
+    for e in s["poly_eval"]:
+        pts = [x for x in e["points"] if x < 2**24]
+        N = len(H(e["coeffs"])) // 32
+        out = be.poly_eval_batch(H(e["coeffs"]), 1, N, pts)
+        exp = [v for x, v in zip(e["points"], e["values"]) if x < 2**24]
+        assert [out[32 * i:32 * i + 32].hex() for i in range(len(pts))] == exp
+
+
+CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.json",
+              "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
+FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
+          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json"]
+
+
+@pytest.mark.parametrize("name", CEREMONIES)
+def test_share_gen(be, golden, name):
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(H(c["master_seed"]), c["ceremony"], 0, n, t)
+    assert a.hex() == c["a"] and b.hex() == c["b"]
+    E, A, s, sp = be.share_gen(a, b, n, n, t)
+    assert E.hex() == c["E"]
+    assert A.hex() == c["A"]
+    assert s.hex() == c["s"]
+    assert sp.hex() == c["s_prime"]
+
+
+@pytest.mark.parametrize("name", CEREMONIES + FAULTS)
+def test_verify_pairs(be, golden, name):
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    d2 = be.verify_pairs(n, t, 2, 0, n, H(c["E"]), H(c["s"]), H(c["s_prime"]))
+    assert dec_str(d2) == c["dec2"]
+    d4 = dec_str(be.verify_pairs(n, t, 4, 0, n, H(c["A"]), H(c["s"])))
+    for i in range(n * n):
+        if c["dec4"][i] != "3":
+            assert d4[i] == c["dec4"][i], (name, i // n, i % n)
+    # dealer sub-range (a sharded rank's rows)
+    d0, d1 = n // 3, n - 1
+    N = t + 1
+    part = be.verify_pairs(n, t, 2, d0, d1, H(c["E"])[32 * N * d0:32 * N * d1],
+                           H(c["s"])[32 * n * d0:32 * n * d1], H(c["s_prime"])[32 * n * d0:32 * n * d1])
+    assert dec_str(part) == c["dec2"][n * d0:n * d1]
+
+
+@pytest.mark.parametrize("name", ["ceremony_n16_t7.json", "fault_share_flip_n10_t4.json",
+                                  "fault_e_identity_n10_t4.json"])
+def test_verify_receiver(be, golden, name):
+    """One party's view (what Phases<Phase1>::proceed computes for receiver j)."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    s, sp = H(c["s"]), H(c["s_prime"])
+    for j in range(n):
+        col = b"".join(s[32 * (i * n + j):32 * (i * n + j) + 32] for i in range(n))
+        colp = b"".join(sp[32 * (i * n + j):32 * (i * n + j) + 32] for i in range(n))
+        d = be.verify_receiver(n, t, 2, j, H(c["E"]), col, colp)
+        assert dec_str(d) == "".join(c["dec2"][i * n + j] for i in range(n)), j
+
+
+def _check_ceremony(c, r, n):
+    assert r.E.hex() == c["E"] if r.E is not None and "a" in c else True
+    assert dec_str(r.dec2) == c["dec2"]
+    assert dec_str(r.dec4) == c["dec4"]
+    assert r.qualified == c["qualified"]
+    assert r.r2_error == [int(x) for x in c["r2_error"]]
+    assert r.complaints2 == c["complaints2"]
+    assert r.reconstruct == c["reconstruct"]
+    assert r.final_share.hex() == c["final_share"]
+    assert r.public_share.hex() == c["public_share"]
+    assert r.mpk.hex() == c["mpk"]
+
+
+@pytest.mark.parametrize("name", CEREMONIES)
+def test_ceremony_honest(be, golden, name):
+    """full_valid_run (committee.rs:1518-1656): every output of every party, bit for bit."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(H(c["master_seed"]), c["ceremony"], 0, n, t)
+    r = be.ceremony(a, b, n, t)
+    assert r.E.hex() == c["E"] and r.A.hex() == c["A"]
+    assert r.s.hex() == c["s"] and r.s_prime.hex() == c["s_prime"]
+    _check_ceremony(c, r, n)
+
+
+@pytest.mark.parametrize("name", FAULTS)
+def test_ceremony_faults(be, golden, name):
+    """misbehaving_parties / invalid_phase_2 / phase_4 style fault injection (committee.rs:1105-1313)."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+    _check_ceremony(c, r, n)
+
+
+def test_ceremony_n64(be, golden):
+    c = golden("ceremony_n64_t31.json")
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(H(c["master_seed"]), c["ceremony"], 0, n, t)
+    r = be.ceremony(a, b, n, t)
+    assert r.E.hex() == c["E"] and r.A.hex() == c["A"]
+    assert r.s.hex() == c["s"] and r.s_prime.hex() == c["s_prime"]
+    _check_ceremony(c, r, n)
+
+
+@pytest.mark.parametrize("name", ["spot_n256_t127.json", "spot_n1024_t511.json"])
+def test_spot_vectors(be, golden, name):
+    sp = golden(name)
+    n, t = sp["n"], sp["t"]
+    be.env_init(t, n, CK)
+    for d in sp["dealers"]:
+        i = d["dealer"]
+        a, b = dkg_amd.dealer_coefficients(H(sp["master_seed"]), 0, i, 1, t)
+        E, A, s, s_p = be.share_gen(a, b, 1, n, t)
+        assert E.hex() == d["E"] and A.hex() == d["A"]
+        for pr in d["pairs"]:
+            j = pr["receiver"]
+            assert s[32 * j:32 * j + 32].hex() == pr["s"] and s_p[32 * j:32 * j + 32].hex() == pr["s_prime"]
+        dec = be.verify_pairs(n, t, 2, i, i + 1, E, s, s_p)
+        exp = [SELF if j == i else ACCEPT for j in range(n)]
+        assert list(dec) == exp
+        # flip one share: exactly that pair is rejected (committee.rs:305)
+        j = d["pairs"][0]["receiver"]
+        bad = bytearray(s)
+        bad[32 * j] ^= 1
+        dec = be.verify_pairs(n, t, 2, i, i + 1, E, bytes(bad), s_p)
+        assert [k for k in range(n) if dec[k] == REJECT] == ([j] if j != i else [])
+
+
+def _gsum(values):
+    return sum(values) % L
+
+
+@pytest.mark.parametrize("n,t", [(256, 127), (1024, 511)])
+def test_ceremony_large_properties(be, n, t):
+    """BASELINE configs 2 and 3 at full size: size-independent properties plus oracle spot pairs."""
+    be.env_init(t, n, CK)
+    master = bytes([7]) * 32
+    a, b = dkg_amd.dealer_coefficients(master, 3, 0, n, t)
+    r = be.ceremony(a, b, n, t)
+    N = t + 1
+    # every share verifies in both rounds, nobody complains, everyone is qualified
+    assert r.dec2.count(bytes([ACCEPT])) == n * (n - 1) and r.dec4.count(bytes([ACCEPT])) == n * (n - 1)
+    assert r.qualified == [1] * n and r.complaints2 == [0] * n
+    # mpk == g * sum_i a_i0  (committee.rs:1633-1647)
+    secret = _gsum(int.from_bytes(a[32 * N * i:32 * N * i + 32], "little") for i in range(n))
+    assert r.mpk == O.base_mul(secret.to_bytes(32, "little"))
+    # final share j == sum_i s_ij and mpk == g * Lagrange(t+1 final shares)
+    fs = [int.from_bytes(r.final_share[32 * j:32 * j + 32], "little") for j in range(n)]
+    rng = random.Random(n)
+    for j in rng.sample(range(n), 3):
+        assert fs[j] == _gsum(int.from_bytes(r.s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+                              for i in range(n))
+    xs = rng.sample(range(1, n + 1), t + 1)
+    lag = 0
+    for xa in xs:
+        coef = 1
+        for xb in xs:
+            if xb != xa:
+                coef = coef * (-xb) * pow(xa - xb, -1, L) % L
+        lag = (lag + coef * fs[xa - 1]) % L
+    assert lag == secret
+    # oracle: a few (dealer, receiver) pairs recomputed the reference's way (vartime MSM)
+    for _ in range(3):
+        i, j = rng.randrange(n), rng.randrange(n)
+        if i == j:
+            continue
+        acc, _rc = O.verify_pairs(n, t, 2, r.E, be.h, r.s, r.s_prime, i, i + 1, j, j + 1)
+        assert acc[0] == 1
+    # commitments of a sampled dealer re-derived by the oracle
+    i = rng.randrange(n)
+    E, A, s, sp = O.share_gen(1, n, t, a[32 * N * i:32 * N * (i + 1)], b[32 * N * i:32 * N * (i + 1)], be.h)
+    assert E == r.E[32 * N * i:32 * N * (i + 1)] and A == r.A[32 * N * i:32 * N * (i + 1)]
+    assert s == r.s[32 * n * i:32 * n * (i + 1)] and sp == r.s_prime[32 * n * i:32 * n * (i + 1)]
