@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: verified shares/sec (whole node) for the n=1024, t=511 DKG ceremony (BASELINE.json).
+
+One step = one full plaintext-mode ceremony on synthetic seeded coefficients already resident in
+HBM: round-1 share generation (commitments E/A + all n^2 share evaluations), round-2 checks of all
+n(n-1) shares, round-3 share aggregation, round-4 checks, finalise (master public key).
+value = n(n-1) verified shares per ceremony x steps / wall time (max over ranks).
+
+N GPUs (torchrun, one process per GPU): the SAME ceremony is sharded by dealer; every rank
+generates and verifies its dealers' rows for all receivers, then RCCL all-gathers (over xGMI) the
+decision rows, the A_i0 commitments and the final-share partial sums (strong scaling).
+
+Also printed in the same JSON line: the roofline of the dominant kernel (INT32-VALU bound; see
+DESIGN.md "Measurement") and the CPU baseline: the dalek-algorithm-matched C oracle timed on a
+bounded sample of round-2 checks on this host's cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+L = 2**252 + 27742317777372353535851937790883648493
+CONFIGS = {"D": (1024, 511), "C": (256, 127), "E": (4096, 2047), "B": (64, 31)}
+
+# Peak INT32 VALU issue rate of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (full-rate
+# v_add_u32; tools/ubench/intrate2.hip, profiles/r01_ubench_*).  A field multiplication of the
+# implemented radix-2^25.5 schoolbook (fe25519.h) issues VALU_PER_FMUL VALU instructions per lane
+# (static count of the gfx950 ISA, tools/count_valu.py); work is counted in field multiplications.
+INT32_PEAK = 256 * 4 * 32 * 2.4e9
+VALU_PER_FMUL = 178.0
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def algorithmic_fmuls(n, t):
+    """Closed-form field-multiplication count of one verification round for all n dealers as
+    implemented (DESIGN.md "Work per unit"): binomial-basis Horner + stepping + fixed-base check."""
+    # mul_small_uniform(m): NAF of m -> (len-1) doublings (7M each, 8M when T needed) + nz adds (9M)
+    def naf(m):
+        pos = neg = 0
+        ln = 0
+        v = m
+        digits = []
+        while v:
+            if v & 1:
+                d = 2 - (v & 3)
+                v -= d
+            else:
+                d = 0
+            digits.append(d)
+            v >>= 1
+            ln += 1
+        return digits
+
+    binom = 0
+    cost_m = {}
+    for m in range(1, t + 1):
+        ds = naf(m)
+        c = 9 + 1 + 1  # e_{m-1} + e_m (8M + cached conversion 1M) + cached(x) for the chain
+        for i in range(len(ds) - 2, -1, -1):
+            nz = ds[i] != 0
+            c += 8 if (nz or i == 0) else 7
+            if nz:
+                c += 8
+        if len(ds) <= 1:
+            c = 9
+        cost_m[m] = c
+    for r in range(1, t + 1):
+        for m in range(1, r + 1):
+            binom += cost_m[m]
+    stepping = n * t * 9            # one 8M add + 1M cached conversion per position per receiver
+    check = n * 2 * 64 * 7 + 4      # two 64-window comb sums (7M madd) + equality, per receiver
+    per_dealer = {"binomial": binom, "stepping": stepping, "check": check}
+    return {k: v * n for k, v in per_dealer.items()}
+
+
+def cpu_baseline(n, t, seconds_target=15.0):
+    """Reference-algorithm CPU baseline: the oracle (dalek-3 u64 algorithms: radix-16 variable-base
+    mul + Pippenger w=7 MSM for N=512) verifying a bounded sample of round-2 pairs on all cores."""
+    from tests import oracle_lib as O
+    import dkg_amd
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    master = b"\x05" * 32
+    nd = 2  # sample dealers
+    a, b = dkg_amd.dealer_coefficients(master, 0, 0, nd, t)
+    h = O.call32("or_pt_hash_to_group", b"Example of a shared string.", 27)[0]
+    E, A, s, sp = O.share_gen(nd, n, t, a, b, h, cores)
+    C = E + bytes(32 * (t + 1) * (n - nd))  # only the sampled dealers' rows are read
+    S = s + bytes(32 * n * (n - nd))
+    SP = sp + bytes(32 * n * (n - nd))
+    # calibrate then run ~seconds_target of work
+    r1 = cores
+    t0 = time.perf_counter()
+    acc, _ = O.verify_pairs(n, t, 2, C, h, S, SP, 0, 1, 1, 1 + r1, cores)
+    dt = time.perf_counter() - t0
+    assert all(x == 1 for x in acc)
+    per_pair = dt / r1
+    nrecv = max(cores, min(n - 1, int(seconds_target / max(per_pair, 1e-6) / nd)))
+    nrecv = min(nrecv, n - nd)
+    t0 = time.perf_counter()
+    acc, _ = O.verify_pairs(n, t, 2, C, h, S, SP, 0, nd, nd, nd + nrecv, cores)
+    dt = time.perf_counter() - t0
+    assert all(x == 1 for x in acc)
+    pairs = nd * nrecv
+    return {"value": pairs / dt, "unit": "verified shares/sec", "cores": cores, "kind": "port",
+            "sample": f"round-2 checks (h*s'+g*s == vartime MSM over t+1={t+1} points) of {nd} dealers x "
+                      f"{nrecv} receivers at n={n}, t={t} on {cores} threads: {pairs} pairs in {dt:.1f} s; "
+                      f"excludes share generation and round 4 (so it overstates the CPU ceremony rate)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="D", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    n, t = CONFIGS[args.config]
+    ws, rank, local = dist_env()
+
+    import torch
+
+    torch.cuda.set_device(local)
+    import dkg_amd
+
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    be = dkg_amd.Backend(local)
+    h = be.env_init(t, n)
+    N = t + 1
+    master = b"\xbe" * 32
+    d0, d1 = (rank * n) // ws, ((rank + 1) * n) // ws
+    D = d1 - d0
+    a, b = dkg_amd.dealer_coefficients(master, 0, d0, D, t)
+    dev = torch.device("cuda", local)
+    ta = torch.frombuffer(bytearray(a), dtype=torch.uint8).to(dev)
+    tb = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    torch.cuda.synchronize()
+
+    if ws == 1:
+        def step():
+            return be.ceremony_device(ta.data_ptr(), tb.data_ptr(), n, t)
+    else:
+        dec2 = torch.empty(D * n, dtype=torch.uint8, device=dev)
+        dec4 = torch.empty(D * n, dtype=torch.uint8, device=dev)
+        A0 = torch.empty(D * 32, dtype=torch.uint8, device=dev)
+        part = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        D_max = -(-n // ws)
+        g_dec2 = torch.empty(ws * D_max * n, dtype=torch.uint8, device=dev)
+        g_dec4 = torch.empty(ws * D_max * n, dtype=torch.uint8, device=dev)
+        g_A0 = torch.empty(ws * D_max * 32, dtype=torch.uint8, device=dev)
+        g_part = torch.empty(ws * n * 32, dtype=torch.uint8, device=dev)
+
+        def padded(x, rows, width):
+            if x.numel() == rows * width:
+                return x
+            y = torch.zeros(rows * width, dtype=torch.uint8, device=dev)
+            y[: x.numel()] = x
+            return y
+
+        def step():
+            ms = be.ceremony_shard_device(n, t, d0, d1, ta.data_ptr(), tb.data_ptr(), dec2.data_ptr(),
+                                          dec4.data_ptr(), A0.data_ptr(), part.data_ptr())
+            # exchange step: decision rows, A_i0 and partial final shares to every rank (RCCL)
+            dist.all_gather_into_tensor(g_dec2, padded(dec2, D_max, n))
+            dist.all_gather_into_tensor(g_dec4, padded(dec4, D_max, n))
+            dist.all_gather_into_tensor(g_A0, padded(A0, D_max, 32))
+            dist.all_gather_into_tensor(g_part, part)
+            return ms
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    pairs = n * (n - 1)
+    value = pairs * args.steps / elapsed
+    out = {
+        "metric": "verified shares/sec (whole node) at n=1024,t=511; full-ceremony wall time",
+        "value": value, "unit": "verified shares/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if ws > 1 else "weak", "vs_baseline": None, "dtype": "u32 (GF(2^255-19), Z_l)",
+        "data": "synthetic: seeded ChaCha20 coefficients (SURVEY.md 8d), honest ceremony",
+        "config": {"workload": f"one DKG ceremony n={n}, t={t} (share gen + round-2/4 checks + finalise)",
+                   "n": n, "t": t, "pairs_per_step": pairs,
+                   "parallelism": f"dealer-sharded x{ws}" if ws > 1 else "single GPU"},
+    }
+    if rank == 0 and ws == 1 and res is not None:
+        out["phases_ms"] = {k: round(v, 3) for k, v in res.ms.items()}
+        out["round2_verified_shares_per_s"] = pairs / (res.ms["round2"] / 1e3)
+        work = algorithmic_fmuls(n, t)
+        ph = be.phase_times()
+        rl = {}
+        for k in ("binomial", "stepping", "check"):
+            ms = ph.get(k, 0.0)
+            if ms > 0:
+                fm = work[k]
+                rl[k] = {"ms_per_round": ms, "gfmul_per_s": fm / (ms / 1e3) / 1e9,
+                         "valu_frac": fm * VALU_PER_FMUL / (ms / 1e3) / INT32_PEAK}
+        dom = max(rl, key=lambda k: rl[k]["ms_per_round"]) if rl else None
+        if dom:
+            ach = work[dom] * VALU_PER_FMUL / (rl[dom]["ms_per_round"] / 1e3) / 1e12
+            out["roofline"] = {"bound": "valu-int32", "kernel": dom, "achieved": ach, "peak": INT32_PEAK / 1e12,
+                               "unit": "Tint32op/s", "frac": ach / (INT32_PEAK / 1e12), "traffic": None,
+                               "work": f"{work[dom]:.4g} field mults x {VALU_PER_FMUL} VALU ops per round",
+                               "all_kernels": rl}
+        if not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(n, t)
+            out["gpu_vs_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    be.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -57,6 +57,8 @@ def lib():
     L.dkg_ctx_last_error.argtypes = [p]
     L.dkg_ctx_last_error.restype = ctypes.c_char_p
     L.dkg_device_count.argtypes = []
+    L.dkg_ctx_phase_ms.argtypes = [p, ctypes.c_char_p]
+    L.dkg_ctx_phase_ms.restype = ctypes.c_double
     L.dkg_env_check.argtypes = [sz, sz]
     L.dkg_env_init.argtypes = [p, sz, sz, u8p, sz, p]
     L.dkg_msm_batch.argtypes = [p, sz, sz, u8p, u8p, p]
@@ -71,14 +73,16 @@ def lib():
     L.dkg_ceremony_run_device.argtypes = [p, sz, sz, p, p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_shard_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]
     L.dkg_dealer_coeffs.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, p, p]
+    L.dkg_scalar_sum_device.argtypes = [p, sz, sz, p, p, p]
+    L.dkg_point_sum_device.argtypes = [p, sz, p, p, p]
     _lib = L
     return L
 
 
 EXPORTED = [
-    "dkg_ctx_create", "dkg_ctx_destroy", "dkg_ctx_last_error", "dkg_device_count", "dkg_env_init",
+    "dkg_ctx_create", "dkg_ctx_destroy", "dkg_ctx_last_error", "dkg_ctx_phase_ms", "dkg_device_count", "dkg_env_init",
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
-    "dkg_dealer_coeffs",
+    "dkg_dealer_coeffs", "dkg_scalar_sum_device", "dkg_point_sum_device",
 ]

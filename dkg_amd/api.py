@@ -94,6 +94,11 @@ class Backend:
     def ctx(self):
         return self._ctx
 
+    def phase_times(self, rnd: int = 2) -> dict:
+        """Device ms of binomial / stepping / check in the last ceremony's round `rnd`."""
+        L = _lib.lib()
+        return {k: L.dkg_ctx_phase_ms(self._ctx, f"r{rnd}.{k}".encode()) for k in ("binomial", "stepping", "check")}
+
     def env_init(self, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT) -> bytes:
         out = ctypes.create_string_buffer(32)
         _check(self._ctx, _lib.lib().dkg_env_init(self._ctx, threshold, nr_members, ck_gen_bytes,

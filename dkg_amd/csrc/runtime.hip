@@ -24,6 +24,8 @@ struct dkg_ctx {
   bool have_h = false;
   size_t threshold = 0, nr_members = 0;
   hipEvent_t ev[8] = {};
+  hipEvent_t pev[4] = {};               // phase profiling inside verify_device
+  std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
 
 namespace {
@@ -131,7 +133,9 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t
   dkgk::to_position_major(D, N, npad, Cext, Cpm, ctx->stream);
   uint32_t* e0 = buf<uint32_t>(ctx, "binom0", PTB * N * npad);
   uint32_t* e1 = buf<uint32_t>(ctx, "binom1", PTB * N * npad);
+  HCK(hipEventRecord(ctx->pev[0], ctx->stream));
   uint32_t* e = dkgk::binomial(D, npad, N, Cpm, e0, e1, ctx->stream);
+  HCK(hipEventRecord(ctx->pev[1], ctx->stream));
   uint32_t* R = buf<uint32_t>(ctx, "R", PTB * D * n);
   uint32_t *sa = nullptr, *sb = nullptr;
   if (N > 256) {
@@ -139,8 +143,20 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t
     sb = buf<uint32_t>(ctx, "step_b", PTB * D * n);
   }
   dkgk::stepping(D, npad, N, e, n, R, sa, sb, ctx->stream);
+  HCK(hipEventRecord(ctx->pev[2], ctx->stream));
   dkgk::check(D, n, dealer_base, 0, round, s, sp, R, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
+  HCK(hipEventRecord(ctx->pev[3], ctx->stream));
   check_launch(ctx);
+}
+
+// After a sync: record the device time of binomial / stepping / check of the last verify_device.
+void collect_phases(dkg_ctx* ctx, int round) {
+  const char* names[3] = {"binomial", "stepping", "check"};
+  for (int i = 0; i < 3; i++) {
+    float ms = 0;
+    HCK(hipEventElapsedTime(&ms, ctx->pev[i], ctx->pev[i + 1]));
+    ctx->phase_ms["r" + std::to_string(round) + "." + names[i]] = ms;
+  }
 }
 
 double ev_ms(dkg_ctx* ctx, int a, int b) {
@@ -161,6 +177,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   d2h(ctx, h2.data(), dec2, n * n);
   HCK(hipEventRecord(ctx->ev[2], ctx->stream));
   sync(ctx);
+  collect_phases(ctx, 2);
   std::vector<uint8_t> qualified(n, 1), r2err(n, 0);
   std::vector<int32_t> complaints(n, 0);
   for (size_t i = 0; i < n; i++)
@@ -186,6 +203,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   d2h(ctx, h4.data(), dec4, n * n);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
+  collect_phases(ctx, 4);
   std::vector<uint8_t> recon(n, 0);
   for (size_t i = 0; i < n; i++)
     for (size_t j = 0; j < n; j++) {
@@ -311,6 +329,7 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
   int rc = guarded(ctx, [&] {
     HCK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (auto& e : ctx->ev) HCK(hipEventCreate(&e));
+    for (auto& e : ctx->pev) HCK(hipEventCreate(&e));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
     bool ok = false;
@@ -339,11 +358,19 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   if (ctx->tab_h) (void)hipFree(ctx->tab_h);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->pev)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
 const char* dkg_ctx_last_error(const dkg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+double dkg_ctx_phase_ms(const dkg_ctx* ctx, const char* name) {
+  if (!ctx || !name) return -1.0;
+  auto it = ctx->phase_ms.find(name);
+  return it == ctx->phase_ms.end() ? -1.0 : it->second;
+}
 
 int dkg_env_check(size_t threshold, size_t nr_members) {
   // committee.rs:73: assert!(threshold < (nr_members + 1) / 2)
@@ -647,11 +674,19 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     if (D) {
       round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
       verify_device(ctx, n, t, 2, D, d0, Ec, ds, dsp, (uint8_t*)d_dec2);
+      // Qualification of a dealer depends only on its own decision row (any REJECT disqualifies,
+      // committee.rs:370-398), so each rank decides it for its dealers with no exchange.
+      std::vector<uint8_t> rows(D * n), q(D, 1);
+      d2h(ctx, rows.data(), d_dec2, D * n);
+      sync(ctx);
+      for (size_t i = 0; i < D; i++)
+        for (size_t j = 0; j < n; j++)
+          if (rows[i * n + j] == DKG_REJECT) q[i] = 0;
       verify_device(ctx, n, t, 4, D, d0, Ac, ds, nullptr, (uint8_t*)d_dec4);
       HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
-      uint8_t* ones = buf<uint8_t>(ctx, "sh_ones", D);
-      HCK(hipMemsetAsync(ones, 1, D, ctx->stream));
-      dkgk::sum_shares(D, n, ds, ones, (uint32_t*)d_partial, ctx->stream);
+      uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
+      h2d(ctx, qm, q.data(), D);
+      dkgk::sum_shares(D, n, ds, qm, (uint32_t*)d_partial, ctx->stream);  // partial of :454-462
     } else {
       HCK(hipMemsetAsync(d_partial, 0, 32 * n, ctx->stream));
     }
@@ -659,6 +694,43 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     sync(ctx);
     if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
+    return DKG_OK;
+  });
+}
+
+int dkg_scalar_sum_device(dkg_ctx* ctx, size_t rows, size_t n, const void* d_in, const void* d_mask, void* d_out) {
+  return guarded(ctx, [&] {
+    const uint8_t* mask = (const uint8_t*)d_mask;
+    if (!mask) {
+      uint8_t* ones = buf<uint8_t>(ctx, "ss_ones", rows);
+      HCK(hipMemsetAsync(ones, 1, rows, ctx->stream));
+      mask = ones;
+    }
+    dkgk::sum_shares(rows, n, (const uint32_t*)d_in, mask, (uint32_t*)d_out, ctx->stream);
+    check_launch(ctx);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_point_sum_device(dkg_ctx* ctx, size_t count, const void* d_points, const void* d_mask, void* d_out) {
+  return guarded(ctx, [&] {
+    uint32_t* ext = buf<uint32_t>(ctx, "ps_ext", PTB * count);
+    uint8_t* ok = buf<uint8_t>(ctx, "ps_ok", count);
+    uint32_t* sum = buf<uint32_t>(ctx, "ps_sum", PTB);
+    dkgk::decode_points((const uint32_t*)d_points, count, ext, count, ok, ctx->stream);
+    dkgk::sum_points(count, ext, count, (const uint8_t*)d_mask, sum, 1, 0, ctx->stream);
+    dkgk::encode_points(sum, 1, 1, (uint32_t*)d_out, ctx->stream);
+    check_launch(ctx);
+    std::vector<uint8_t> okh(count), mh(count, 1);
+    d2h(ctx, okh.data(), ok, count);
+    if (d_mask) d2h(ctx, mh.data(), d_mask, count);
+    sync(ctx);
+    for (size_t c = 0; c < count; c++)
+      if (mh[c] && !okh[c]) {
+        ctx->err = "point_sum: a selected point does not decode";
+        return DKG_E_DECODE;
+      }
     return DKG_OK;
   });
 }

@@ -39,6 +39,9 @@ typedef struct dkg_ctx dkg_ctx;
 int dkg_ctx_create(int device, dkg_ctx **out);
 void dkg_ctx_destroy(dkg_ctx *ctx);
 const char *dkg_ctx_last_error(const dkg_ctx *ctx);
+/* Device time (ms) of one phase of the last ceremony's round-2 / round-4 checks, by name
+ * "r2.binomial", "r2.stepping", "r2.check", "r4.*" (HIP events on the ctx stream); -1 if unknown. */
+double dkg_ctx_phase_ms(const dkg_ctx *ctx, const char *name);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
 int dkg_device_count(void);
 
@@ -122,10 +125,18 @@ int dkg_ceremony_run_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, c
  * ceremony.  Produces this rank's commitments E/A and decision rows; the caller all-gathers
  * (RCCL over xGMI) the rows, A_0 values and share partial sums.  Device pointers throughout:
  * d_a, d_b [d1-d0][t+1][32]; d_dec2, d_dec4 [d1-d0][n]; d_A0 [d1-d0][32] (compressed A_i0);
- * d_partial [n][32] = sum over this rank's dealers of s_ij (all assumed qualified). */
+ * d_partial [n][32] = sum over this rank's QUALIFIED dealers of s_ij (qualification of a dealer is
+ * decided by its own round-2 row, so it needs no exchange). */
 int dkg_ceremony_shard_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const void *d_a,
                               const void *d_b, void *d_dec2, void *d_dec4, void *d_A0, void *d_partial,
                               double *ms_total);
+/* Combine step of the sharded run (device pointers):
+ * round-3 sum (committee.rs:454-462): out[j] = sum over rows r with mask[r] (NULL = all) of in[r][j]
+ * mod l; in [rows][n][32] canonical scalars (e.g. the all-gathered per-rank partials), out [n][32]. */
+int dkg_scalar_sum_device(dkg_ctx *ctx, size_t rows, size_t n, const void *d_in, const void *d_mask, void *d_out);
+/* finalise (committee.rs:790-795): out = sum of points[c] with mask[c] (NULL = all), points
+ * [count][32] compressed, out [32] compressed.  DKG_E_DECODE if a selected point does not decode. */
+int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const void *d_mask, void *d_out);
 
 /* ---- synthetic inputs: the seeded RNG convention ----
  * dealer seed = BLAKE2b-256("dkg-amd/v1/dealer" || master[32] || u32le ceremony || u32le dealer);

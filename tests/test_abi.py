@@ -1,0 +1,62 @@
+"""CPU-only checks of the boundary: the C ABI library loads and exports every symbol that
+include/dkg_amd.h declares; host-side logic (seeded coefficients, environment check, error path
+without a GPU) behaves like the reference."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import dkg_amd
+from dkg_amd import _lib
+from tests import oracle_lib as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "dkg_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dkg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    names = declared_functions()
+    assert len(names) >= 18
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(_lib.EXPORTED)
+
+
+def test_env_check_matches_reference_assert():
+    # committee.rs:73: assert!(threshold < (nr_members + 1) / 2)
+    for t, n in [(0, 1), (0, 2), (1, 3), (4, 10), (5, 11), (511, 1024), (2047, 4096)]:
+        dkg_amd.env_check(t, n)
+    for t, n in [(5, 10), (1, 2), (2, 3), (512, 1024), (0, 0)]:
+        with pytest.raises(dkg_amd.DkgError):
+            dkg_amd.env_check(t, n)
+
+
+@pytest.mark.parametrize("t", [0, 3, 31])
+def test_dealer_coefficients_match_oracle(t):
+    master = bytes(range(32))
+    a, b = dkg_amd.dealer_coefficients(master, 5, 3, 4, t)
+    N = t + 1
+    for i in range(4):
+        oa, ob = O.dealer_coeffs(O.dealer_seed(master, 5, 3 + i), t)
+        assert a[32 * N * i:32 * N * (i + 1)] == oa and b[32 * N * i:32 * N * (i + 1)] == ob
+
+
+def test_dealer_coefficients_golden(golden):
+    c = golden("ceremony_n10_t4.json")
+    a, b = dkg_amd.dealer_coefficients(bytes.fromhex(c["master_seed"]), c["ceremony"], 0, c["n"], c["t"])
+    assert a.hex() == c["a"] and b.hex() == c["b"]
+
+
+def test_no_gpu_fails_loudly():
+    """Without a visible GPU the product path raises; it never falls back to the CPU."""
+    if _lib.lib().dkg_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(dkg_amd.DkgError):
+        dkg_amd.Backend(0)
