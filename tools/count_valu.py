@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Static VALU instruction count of each group/field primitive as compiled for gfx950.
+
+Compiles tiny kernels that loop over one primitive and counts the VALU instructions of the hottest
+basic block in the ISA.  bench.py's roofline multiplies these counts by the closed-form number of
+primitive calls of the implemented schedule (the "algorithmic" work: no PMC, no guesswork).
+Usage: python tools/count_valu.py  (prints a JSON dict; copy into bench.py VALU_PER_OP).
+"""
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRIMS = {
+    "fe_mul": ("fe a, b; LD10(a.v, 0); LD10(b.v, 640);", "fe_mul(a, a, b);", "ST10(a.v);"),
+    "fe_sq": ("fe a; LD10(a.v, 0);", "fe_sq(a, a);", "ST10(a.v);"),
+    "ge_add": ("ge_p3 p; ge_cached q; LDP(p, 0); LDP(q, 2560);", "ge_add(p, p, q);", "STP(p);"),
+    "ge_add_signed": ("ge_p3 p; ge_cached q; LDP(p, 0); LDP(q, 2560); bool ng = o[9999] & 1;",
+                      "ge_add_signed(p, p, q, ng); ng = !ng;", "STP(p);"),
+    "ge_dbl_t": ("ge_p3 p; LDP(p, 0);", "ge_dbl_rt(p, p, true);", "STP(p);"),
+    "ge_dbl_not": ("ge_p3 p; LDP(p, 0);", "ge_dbl_rt(p, p, false);", "STP(p);"),
+    "ge_madd": ("ge_p3 p; ge_aff q; LDP(p, 0); LD10(q.ypx.v, 3000); LD10(q.ymx.v, 3640); LD10(q.xy2d.v, 4280);",
+                "ge_madd(p, p, q);", "STP(p);"),
+    "comb_window": ("ge_p3 p; LDP(p, 0); sc x; for (int i_ = 0; i_ < 8; i_++) x.v[i_] = o[9000 + i_];",
+                    "comb_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
+    "ge_to_cached": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached(q, p); p.X = q.T2d; p.Y = q.YpX;",
+                     "STP(p);"),
+}
+HDR = r'''
+#include "%s/dkg_amd/csrc/points.h"
+#define LD10(dst, off) for (int i_ = 0; i_ < 10; i_++) (dst)[i_] = o[(off) + i_ * 64 + threadIdx.x];
+#define ST10(src) for (int i_ = 0; i_ < 10; i_++) o[i_ * 64 + threadIdx.x] = (src)[i_];
+#define LDP(p, off) { uint32_t* w_ = (uint32_t*)&(p); for (int i_ = 0; i_ < 40; i_++) w_[i_] = o[(off) + i_ * 64 + threadIdx.x]; }
+#define STP(p) { uint32_t* w_ = (uint32_t*)&(p); for (int i_ = 0; i_ < 40; i_++) o[i_ * 64 + threadIdx.x] = w_[i_]; }
+''' % ROOT
+
+
+def main():
+    src = HDR
+    for name, (pro, body, epi) in PRIMS.items():
+        src += f'extern "C" __global__ void k_{name}(uint32_t* o, int n) {{ {pro} for (int it = 0; it < n; it++) {{ {body} }} {epi} }}\n'
+    d = tempfile.mkdtemp()
+    with open(os.path.join(d, "k.hip"), "w") as f:
+        f.write(src)
+    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-S", "--cuda-device-only", "-o",
+                           os.path.join(d, "k.s"), os.path.join(d, "k.hip")])
+    s = open(os.path.join(d, "k.s")).read()
+    out = {}
+    for name in PRIMS:
+        body = s[s.index(f"k_{name}:"):]
+        body = body[:body.index("s_endpgm")]
+        blocks = re.split(r"\n\.LBB\d+_\d+:", body)
+        best = max(blocks, key=lambda b: sum(1 for l in b.split("\n") if l.strip().startswith("v_")))
+        ins = [l.strip() for l in best.split("\n") if l.strip().startswith("v_")]
+        out[name] = {"valu": len(ins), "mad_u64": sum(1 for i in ins if i.startswith("v_mad_u64_u32"))}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
