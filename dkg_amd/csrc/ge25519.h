@@ -192,6 +192,26 @@ DKG_DEV void ge_dbl_rt(ge_p3& r, const ge_p3& p, bool with_t) {
   if (with_t) fe_mul(r.T, e, h);
 }
 
+// Doubling with the fewest simultaneously live temporaries (inputs consumed early; r may alias p).
+DKG_DEV void ge_dbl_lean(ge_p3& r, const ge_p3& p, bool with_t) {
+  fe a, b, t, h, g;
+  fe_sq(a, p.X);
+  fe_sq(b, p.Y);
+  fe_add(h, a, b);          // <= 2^27             (= -H_std)
+  fe_sub(g, a, b);          // <= 1.5*2^27         (= -G_std)
+  fe_sq(t, p.Z);
+  fe_add(t, t, t);          // 2Z^2 <= 2^27
+  fe_add(t, t, g);          // <= 2.5*2^27
+  fe_carry(t, t);           // f, tight            (= -F_std)
+  fe_add(a, p.X, p.Y);      // <= 2^27
+  fe_sq(a, a);              // (X+Y)^2
+  fe_sub(b, h, a);          // e <= 2^28           (= -E_std)
+  fe_mul(r.X, b, t);
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, t, g);
+  if (with_t) fe_mul(r.T, b, h);
+}
+
 // r = p + q (neg = false) or p - q (neg = true) with one code path: the sign only selects
 // which of (Y+X, Y-X) multiplies which, and the sign of the 2dT product.
 DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg) {

@@ -190,6 +190,83 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 }
 
 // ------------------------------------------------------------------ K3a binomial-basis Horner
+// Register-lean variants for the m-chains: the cached addend lives in LDS (lane-interleaved,
+// word w of lane l at q[w * 64 + l], conflict-free) and is read field by field when the addition
+// needs it, so a chain keeps one point + the doubling temporaries in VGPRs (<= 128: 4 waves/SIMD).
+// q points at this lane's column (base + lane); consecutive words are `stride` apart.
+__device__ __forceinline__ void lds_put_cached(uint32_t* q, const ge_cached& c, int stride = 64) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&c);
+#pragma unroll
+  for (int k = 0; k < PT_WORDS; k++) q[k * stride] = w[k];
+}
+// which: 0 = Y+X, 1 = Y-X, 2 = 2Z, 3 = 2dT
+__device__ __forceinline__ void lds_get_fe(fe& r, const uint32_t* q, int which, int stride = 64) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = q[(which * 10 + i) * stride];
+  // Opaque use of all ten limbs at once (one lgkmcnt wait for the group): stops LICM from
+  // hoisting the loads and their x19 products out of the chain loop (~140 extra VGPRs).
+  asm volatile("" : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+               "+v"(r.v[6]), "+v"(r.v[7]), "+v"(r.v[8]), "+v"(r.v[9]));
+}
+
+// r = p +/- Q with Q the cached point in LDS; `neg` must be wave-uniform.
+__device__ __forceinline__ void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
+                                           int stride = 64) {
+  fe a, b, e, h, t, qv;
+  fe_sub(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 0 : 1, stride);
+  fe_mul(a, t, qv);
+  fe_add(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 1 : 0, stride);
+  fe_mul(b, t, qv);
+  fe_sub(e, b, a);          // <= 1.5*2^27
+  fe_add(h, b, a);          // <= 2^27
+  lds_get_fe(qv, q, 3, stride);
+  fe_mul(a, p.T, qv);       // c
+  if (neg) {
+    fe_neg(a, a);
+    fe_carry(a, a);
+  }
+  lds_get_fe(qv, q, 2, stride);
+  fe_mul(b, p.Z, qv);       // d
+  fe_sub(t, b, a);          // f
+  fe_add(b, b, a);          // g
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, t, b);
+  fe_mul(r.T, e, h);
+}
+
+// y = m * y, m wave-uniform; q = this lane's column of the wave's 40 x 64-word LDS slot (clobbered).
+__device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q) {
+  uint32_t pos = 0, neg = 0;
+  int len = 0;
+  for (uint32_t v = m; v; v >>= 1, len++) {
+    if (v & 1u) {
+      if ((v & 3u) == 1u) {
+        pos |= 1u << len;
+        v -= 1;
+      } else {
+        neg |= 1u << len;
+        v += 1;
+      }
+    }
+  }
+  if (len <= 1) return;
+  {
+    ge_cached xc;
+    ge_to_cached(xc, y);
+    lds_put_cached(q, xc);
+  }
+#pragma unroll 1
+  for (int i = len - 2; i >= 0; i--) {
+    const uint32_t bit = 1u << i;
+    const bool nz = ((pos | neg) & bit) != 0;
+    ge_dbl_lean(y, y, nz || i == 0);
+    if (nz) ge_add_lds(y, y, q, (neg & bit) != 0);
+  }
+}
+
 // y = m * x for a wave-uniform small m (non-adjacent form, left to right).
 __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint32_t m) {
   uint32_t pos = 0, neg = 0;
@@ -230,29 +307,41 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t npad, size_t N, const u
 }
 
 // One Horner step in the binomial basis: e'_0 = C_k, e'_m = m (e_{m-1} + e_m), m = 1..r.
-// Lanes = dealers (so m is uniform per wave); blockIdx.x = block of POS consecutive positions.
-constexpr int BINOM_POS = 4;
-__global__ __launch_bounds__(64, 3) void k_binom_step(int r, size_t npad, size_t N, const uint32_t* __restrict__ ein,
-                                                    uint32_t* __restrict__ eout) {
+// Lanes = dealers (so m is uniform per wave: no divergence in the m-chain); one wave per
+// (position, 64 dealers); position 0 (blockIdx.x == 0) just copies the next coefficient C_k.
+__global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
+                                                    const uint32_t* __restrict__ C,
+                                                    const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout) {
+  __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
+  uint32_t* q = qs + threadIdx.x;
   const size_t d = (size_t)blockIdx.y * blockDim.x + threadIdx.x;
   const size_t S = N * npad;
-  const int lo = blockIdx.x * BINOM_POS + 1;
-  const int hi = min(r, (int)(blockIdx.x + 1) * BINOM_POS);
-  for (int m = hi; m >= lo; m--) {
-    // both operands re-read from HBM/L2 each position: keeps one point live, not two
-    ge_p3 x;
-    ge_cached cc;
-    {
-      ge_p3 cur;
-      if (m == r) ge_identity(cur);  // degree r-1 input: position r is zero
-      else pt_load(cur, ein, S, (size_t)m * npad + d);
-      ge_to_cached(cc, cur);
-    }
-    pt_load(x, ein, S, (size_t)(m - 1) * npad + d);
-    ge_add(x, x, cc);
-    mul_small_uniform(x, x, (uint32_t)m);
-    pt_store(eout, S, (size_t)m * npad + d, x);
+  const int m = blockIdx.x;
+  if (m == 0) {
+#pragma unroll 8
+    for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
+    return;
   }
+  {
+    ge_p3 cur;
+    pt_load(cur, ein, S, (size_t)m * npad + d);
+    // degree r-1 input: position r is zero.  Branch-free, opaque select (a visible branch lets the
+    // compiler specialise the identity path and doubles the register footprint).
+    uint32_t keep = (m == r) ? 0u : 0xffffffffu;
+    asm volatile("" : "+v"(keep));
+    uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
+#pragma unroll
+    for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
+    ge_cached cc;
+    ge_to_cached(cc, cur);
+    lds_put_cached(q, cc);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the second point's loads after the first is retired
+  ge_p3 x;
+  pt_load(x, ein, S, (size_t)(m - 1) * npad + d);
+  ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
+  mul_small_lds(x, (uint32_t)m, q);        // * m
+  pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
 uint32_t* binomial(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
@@ -264,12 +353,9 @@ uint32_t* binomial(size_t ndealers, size_t npad, size_t N, const uint32_t* C, ui
   uint32_t* out = e1;
   for (size_t r = 1; r <= t; r++) {
     const size_t k = t - r;
-    hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, stream, npad, N, C, k,
-                       out);
-    const unsigned nblk = (unsigned)((r + BINOM_POS - 1) / BINOM_POS);
-    // npad is a multiple of 64: one wave per (position block, 64 dealers)
-    hipLaunchKernelGGL(k_binom_step, dim3(nblk, (unsigned)(npad / 64)), dim3(64), 0, stream, (int)r, npad, N, in,
-                       out);
+    // npad is a multiple of 64: one wave per (position 0..r, 64 dealers)
+    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(r + 1), (unsigned)(npad / 64)), dim3(64), 0, stream, (int)r,
+                       (int)k, npad, N, C, in, out);
     uint32_t* tmp = in;
     in = out;
     out = tmp;
@@ -294,53 +380,56 @@ __device__ __forceinline__ void cached_identity(ge_cached& c) {
   fe_zero(c.T2d);
 }
 
-__global__ __launch_bounds__(STEP_BS, 2) void k_stepping(size_t npad, size_t N, const uint32_t* __restrict__ e,
+__global__ __launch_bounds__(STEP_BS, 4) void k_stepping(size_t npad, size_t N, const uint32_t* __restrict__ e,
                                                          size_t nrecv, size_t pos0,
                                                          const uint32_t* __restrict__ up,   // NULL: top block
                                                          uint32_t* __restrict__ down,       // NULL: block 0
                                                          uint32_t* __restrict__ R, size_t rstride) {
-  __shared__ uint32_t slot[2][STEP_BS / 64][PT_WORDS];
+  // Lane l's cached value sits in LDS column l (word k at col[k * STEP_BS]); lane l adds column
+  // l + 1.  Column 0 is never read inside the block (lane 0's value leaves through `down`), so the
+  // top lane parks the upstream value there: lane l reads column (l + 1) mod blockDim.  40 KB per
+  // 256-lane block -> 4 blocks (16 waves) per CU, and the addend never occupies VGPRs.
+  __shared__ uint32_t cols[PT_WORDS * STEP_BS];
   const size_t d = blockIdx.x;
-  const int l = threadIdx.x;
-  const int lane = l & 63, wave = l >> 6, nwaves = blockDim.x >> 6;
+  const int l = threadIdx.x, bs = blockDim.x;
   const size_t S = N * npad;
   const size_t pos = pos0 + l;
   ge_p3 D;
   if (pos < N) pt_load(D, e, S, pos * npad + d);
   else ge_identity(D);
-  const bool top_lane = (l == (int)blockDim.x - 1);
+  const bool top_lane = (l == bs - 1);
   const uint4* upd = up ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
   uint4* downd = down ? reinterpret_cast<uint4*>(down + d * nrecv * PT_WORDS) : nullptr;
+  uint32_t* mine = cols + l;
+  const uint32_t* nbr = cols + ((l + 1) % bs);
   for (size_t j = 0; j < nrecv; j++) {
-    ge_cached c0, nb;
-    ge_to_cached(c0, D);
-    uint32_t* w = reinterpret_cast<uint32_t*>(&c0);
-    uint32_t* nw = reinterpret_cast<uint32_t*>(&nb);
+    {
+      ge_cached c0;
+      ge_to_cached(c0, D);
+      if (l == 0) {
+        if (downd) {
+          const uint4* w4 = reinterpret_cast<const uint4*>(&c0);
 #pragma unroll
-    for (int k = 0; k < PT_WORDS; k++) nw[k] = __shfl_down(w[k], 1, 64);
-    if (lane == 0) {
-#pragma unroll
-      for (int k = 0; k < PT_WORDS; k++) slot[j & 1][wave][k] = w[k];
-      if (l == 0 && downd) {
-        const uint4* w4 = reinterpret_cast<const uint4*>(w);
-#pragma unroll
-        for (int k = 0; k < PT_WORDS / 4; k++) downd[j * (PT_WORDS / 4) + k] = w4[k];
+          for (int k = 0; k < PT_WORDS / 4; k++) downd[j * (PT_WORDS / 4) + k] = w4[k];
+        }
+      } else {
+        lds_put_cached(mine, c0, STEP_BS);
       }
+    }
+    if (top_lane) {
+      ge_cached u;
+      if (upd) {
+        uint4* u4 = reinterpret_cast<uint4*>(&u);
+#pragma unroll
+        for (int k = 0; k < PT_WORDS / 4; k++) u4[k] = upd[j * (PT_WORDS / 4) + k];
+      } else {
+        cached_identity(u);
+      }
+      lds_put_cached(cols, u, STEP_BS);
     }
     __syncthreads();
-    if (lane == 63) {
-      if (wave + 1 < nwaves) {
-#pragma unroll
-        for (int k = 0; k < PT_WORDS; k++) nw[k] = slot[j & 1][wave + 1][k];
-      } else if (top_lane && upd) {
-        uint4* n4 = reinterpret_cast<uint4*>(nw);
-#pragma unroll
-        for (int k = 0; k < PT_WORDS / 4; k++) n4[k] = upd[j * (PT_WORDS / 4) + k];
-      } else {
-        cached_identity(nb);
-      }
-    }
-    if (pos + 1 < N) ge_add(D, D, nb);
+    if (pos + 1 < N) ge_add_lds(D, D, nbr, false, STEP_BS);
+    __syncthreads();  // every column read before the next step overwrites it
     if (l == 0 && R) pt_store(R, rstride, d * nrecv + j, D);
   }
 }
