@@ -94,8 +94,13 @@ class Backend:
     def ctx(self):
         return self._ctx
 
+    def set_streams(self, nsub: int):
+        """Dealer-chunk streams of the round-2/4 checks (1 = serialised, phase times recorded)."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_streams(self._ctx, nsub))
+
     def phase_times(self, rnd: int = 2) -> dict:
-        """Device ms of binomial / stepping / check in the last ceremony's round `rnd`."""
+        """Device ms of binomial / stepping / check in the last ceremony's round `rnd` (only
+        recorded with set_streams(1); -1 otherwise)."""
         L = _lib.lib()
         return {k: L.dkg_ctx_phase_ms(self._ctx, f"r{rnd}.{k}".encode()) for k in ("binomial", "stepping", "check")}
 
@@ -208,6 +213,16 @@ class Backend:
                                                                 vp(d_dec2), vp(d_dec4), vp(d_A0),
                                                                 vp(d_partial), ctypes.byref(ms)))
         return ms.value
+
+    def scalar_sum_device(self, rows: int, n: int, d_in: int, d_mask: Optional[int], d_out: int):
+        """out[j] = sum over rows r with mask[r] of in[r][j] mod l (device pointers)."""
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_scalar_sum_device(self._ctx, rows, n, vp(d_in), vp(d_mask), vp(d_out)))
+
+    def point_sum_device(self, count: int, d_points: int, d_mask: Optional[int], d_out: int):
+        """out = sum of the compressed points[c] with mask[c] (device pointers)."""
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_point_sum_device(self._ctx, count, vp(d_points), vp(d_mask), vp(d_out)))
 
 
 class Environment:

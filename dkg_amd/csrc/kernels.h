@@ -26,19 +26,21 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
                hipStream_t stream);
 
 // K3a: binomial-basis Horner.  C: decoded commitments SoA [40][N][npad] (position-major,
-// dealer-minor); e0/e1 ping-pong buffers of the same shape.  Returns the buffer holding
-// e_m = Delta^m P_i(0), m = 0..t.
-uint32_t* binomial(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
+// dealer-minor); e0/e1 ping-pong buffers of the same shape.  Processes `width` (multiple of 64)
+// dealer columns starting at the given pointers (a dealer chunk: pass C + c0, e0 + c0, e1 + c0).
+// Returns the buffer holding e_m = Delta^m P_i(0), m = 0..t.
+uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
                    hipStream_t stream);
-// K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][ndealers*nrecv].
-// stream_a / stream_b: scratch for the inter-block boundary streams, each >= ndealers*nrecv*160 B
-// (unused when N <= 256).
-void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
+// K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][rstride]
+// (element i*nrecv + j).  stream_a / stream_b: scratch for the inter-block boundary streams, each
+// >= ndealers*nrecv*160 B (unused when N <= 256).
+void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream);
 // K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);
 // dealer_ok[i] == 0 forces 0; i == j (self, index i + dealer_base == j) gives 2.
+// R: SoA [40][rstride], element i*nrecv + j.
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round, const uint32_t* s,
-           const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
+           const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
            const uint8_t* dealer_ok, uint8_t* decision, hipStream_t stream);
 // per-dealer validity: dealer_ok[i] = AND of point_ok over its N commitments (dealer-major [D][N])
 void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream);

@@ -297,10 +297,10 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
   }
 }
 
-__global__ __launch_bounds__(256) void k_copy_pos(size_t npad, size_t N, const uint32_t* __restrict__ C,
+__global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, size_t N, const uint32_t* __restrict__ C,
                                                   size_t kpos, uint32_t* __restrict__ e) {
   const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= npad) return;
+  if (d >= width) return;
   const size_t S = N * npad;
 #pragma unroll 8
   for (int w = 0; w < PT_WORDS; w++) e[w * S + d] = C[w * S + kpos * npad + d];
@@ -308,15 +308,17 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t npad, size_t N, const u
 
 // One Horner step in the binomial basis: e'_0 = C_k, e'_m = m (e_{m-1} + e_m), m = 1..r.
 // Lanes = dealers (so m is uniform per wave: no divergence in the m-chain); one wave per
-// (position, 64 dealers); position 0 (blockIdx.x == 0) just copies the next coefficient C_k.
+// (position, 64 dealers); position 0 just copies the next coefficient C_k.  Grid (dealer groups,
+// r+1) with m = r - blockIdx.y: workgroups are dispatched x-fastest, so the longest NAF chains
+// (largest m) start first and the launch tail is made of the short ones.
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
-  const size_t d = (size_t)blockIdx.y * blockDim.x + threadIdx.x;
+  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t S = N * npad;
-  const int m = blockIdx.x;
+  const int m = r - (int)blockIdx.y;
   if (m == 0) {
 #pragma unroll 8
     for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
@@ -344,17 +346,17 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
   pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
-uint32_t* binomial(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
+uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
                    hipStream_t stream) {
-  (void)ndealers;
   const size_t t = N - 1;
-  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, stream, npad, N, C, t, e0);
+  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, stream, width, npad, N, C, t,
+                     e0);
   uint32_t* in = e0;
   uint32_t* out = e1;
   for (size_t r = 1; r <= t; r++) {
     const size_t k = t - r;
-    // npad is a multiple of 64: one wave per (position 0..r, 64 dealers)
-    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(r + 1), (unsigned)(npad / 64)), dim3(64), 0, stream, (int)r,
+    // width is a multiple of 64: one wave per (position 0..r, 64 dealers)
+    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64), (unsigned)(r + 1)), dim3(64), 0, stream, (int)r,
                        (int)k, npad, N, C, in, out);
     uint32_t* tmp = in;
     in = out;
@@ -434,10 +436,9 @@ __global__ __launch_bounds__(STEP_BS, 4) void k_stepping(size_t npad, size_t N, 
   }
 }
 
-void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
+void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream) {
   if (!ndealers || !nrecv) return;
-  const size_t rstride = ndealers * nrecv;
   const size_t bs = N >= STEP_BS ? STEP_BS : ((N + 63) / 64) * 64;
   const size_t nblk = (N + bs - 1) / bs;
   uint32_t* up = nullptr;
@@ -452,7 +453,8 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
 // ------------------------------------------------------------------ K3c check
 __global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round,
                                                 const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
-                                                const uint32_t* __restrict__ R, const uint32_t* __restrict__ tab_g,
+                                                const uint32_t* __restrict__ R, size_t rstride,
+                                                const uint32_t* __restrict__ tab_g,
                                                 const uint32_t* __restrict__ tab_h,
                                                 const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec) {
   extern __shared__ uint4 lds4[];
@@ -472,7 +474,7 @@ __global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, s
       sc_load(x, sp + 8 * p);
       comb_mul_add(acc, x, lds + COMB_WORDS);        // + h * s'                 (committee.rs:292-293)
     }
-    pt_load(r, R, total, p);
+    pt_load(r, R, rstride, p);
     const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
     uint8_t v = (dok[i] && eq) ? 1 : 0;
     if (i + dealer_base == j + recv_base) v = 2;
@@ -481,13 +483,13 @@ __global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, s
 }
 
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round, const uint32_t* s,
-           const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h, const uint8_t* dok,
-           uint8_t* dec, hipStream_t stream) {
+           const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
+           const uint8_t* dok, uint8_t* dec, hipStream_t stream) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
   const size_t lds = (round == 2 ? 2 : 1) * COMB_WORDS * 4;
   hipLaunchKernelGGL(k_check, dim3(comb_grid(total, 1024)), dim3(1024), lds, stream, ndealers, nrecv, dealer_base,
-                     recv_base, round, s, sp, R, tab_g, tab_h, dok, dec);
+                     recv_base, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
 }
 
 __global__ void k_dealer_ok(size_t ndealers, size_t N, const uint8_t* __restrict__ pok, uint8_t* __restrict__ ok) {

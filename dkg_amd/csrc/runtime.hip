@@ -24,7 +24,12 @@ struct dkg_ctx {
   bool have_h = false;
   size_t threshold = 0, nr_members = 0;
   hipEvent_t ev[8] = {};
-  hipEvent_t pev[4] = {};               // phase profiling inside verify_device
+  hipEvent_t pev[4] = {};               // phase profiling inside verify_device (nsub == 1)
+  static constexpr int MAX_SUB = 8;
+  int nsub = 2;                         // dealer-chunk streams of verify_device
+  hipStream_t sub[MAX_SUB] = {};
+  hipEvent_t fork = nullptr, join[MAX_SUB] = {};
+  bool timed_verify = false;
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
 
@@ -121,6 +126,11 @@ uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, si
 
 // Rounds 2 / 4 for dealers [dealer_base, dealer_base + D) against receivers 0..n-1, all on device.
 // Ccomp [D][N][8] compressed commitments; s, sp [D][n][8] canonical; dec [D][n].
+// With ctx->nsub > 1 the dealers are cut into nsub chunks (multiples of 64 columns) whose
+// binomial -> stepping -> check pipelines run on their own streams: the hundreds of short,
+// partly-filled binomial launches of one chunk then share the CUs with another chunk's work
+// instead of leaving them idle in launch tails.  nsub == 1 is the serialised schedule whose
+// per-phase device times are recorded (dkg_ctx_phase_ms).
 void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t dealer_base,
                    const uint32_t* Ccomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec) {
   const size_t N = t + 1, npad = pad64(D);
@@ -128,24 +138,50 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t
   uint8_t* pok = buf<uint8_t>(ctx, "pok", D * N);
   uint8_t* dok = buf<uint8_t>(ctx, "dok", D);
   uint32_t* Cpm = buf<uint32_t>(ctx, "Cpm", PTB * N * npad);
-  dkgk::decode_points(Ccomp, D * N, Cext, D * N, pok, ctx->stream);  // K5 (groups.rs:78-81)
-  dkgk::dealer_ok(D, N, pok, dok, ctx->stream);
-  dkgk::to_position_major(D, N, npad, Cext, Cpm, ctx->stream);
   uint32_t* e0 = buf<uint32_t>(ctx, "binom0", PTB * N * npad);
   uint32_t* e1 = buf<uint32_t>(ctx, "binom1", PTB * N * npad);
-  HCK(hipEventRecord(ctx->pev[0], ctx->stream));
-  uint32_t* e = dkgk::binomial(D, npad, N, Cpm, e0, e1, ctx->stream);
-  HCK(hipEventRecord(ctx->pev[1], ctx->stream));
   uint32_t* R = buf<uint32_t>(ctx, "R", PTB * D * n);
   uint32_t *sa = nullptr, *sb = nullptr;
   if (N > 256) {
     sa = buf<uint32_t>(ctx, "step_a", PTB * D * n);
     sb = buf<uint32_t>(ctx, "step_b", PTB * D * n);
   }
-  dkgk::stepping(D, npad, N, e, n, R, sa, sb, ctx->stream);
-  HCK(hipEventRecord(ctx->pev[2], ctx->stream));
-  dkgk::check(D, n, dealer_base, 0, round, s, sp, R, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
-  HCK(hipEventRecord(ctx->pev[3], ctx->stream));
+  const size_t rstride = D * n;
+  dkgk::decode_points(Ccomp, D * N, Cext, D * N, pok, ctx->stream);  // K5 (groups.rs:78-81)
+  dkgk::dealer_ok(D, N, pok, dok, ctx->stream);
+  dkgk::to_position_major(D, N, npad, Cext, Cpm, ctx->stream);
+  // dealer chunk [c0, c0 + w) (w a multiple of 64 except possibly at the tail) on stream st
+  auto chunk = [&](size_t c0, size_t w, hipStream_t st, bool timed) {
+    const size_t wpad = pad64(w);
+    if (timed) HCK(hipEventRecord(ctx->pev[0], st));
+    uint32_t* e = dkgk::binomial(wpad, npad, N, Cpm + c0, e0 + c0, e1 + c0, st);
+    if (timed) HCK(hipEventRecord(ctx->pev[1], st));
+    dkgk::stepping(w, npad, N, e, n, R + c0 * n, rstride, sa ? sa + c0 * n * 40 : nullptr,
+                   sb ? sb + c0 * n * 40 : nullptr, st);
+    if (timed) HCK(hipEventRecord(ctx->pev[2], st));
+    dkgk::check(w, n, dealer_base + c0, 0, round, s + c0 * n * 8, sp ? sp + c0 * n * 8 : nullptr, R + c0 * n,
+                rstride, ctx->tab_g, ctx->tab_h, dok + c0, dec + c0 * n, st);
+    if (timed) HCK(hipEventRecord(ctx->pev[3], st));
+  };
+  const size_t nsub = std::min<size_t>(ctx->nsub, npad / 64);
+  if (nsub <= 1) {
+    chunk(0, D, ctx->stream, true);
+    ctx->timed_verify = true;
+  } else {
+    const size_t groups = npad / 64;
+    HCK(hipEventRecord(ctx->fork, ctx->stream));
+    size_t c0 = 0;
+    for (size_t c = 0; c < nsub; c++) {
+      const size_t g1 = groups * (c + 1) / nsub;
+      const size_t c1 = std::min(D, g1 * 64);
+      HCK(hipStreamWaitEvent(ctx->sub[c], ctx->fork, 0));
+      chunk(c0, c1 - c0, ctx->sub[c], false);
+      HCK(hipEventRecord(ctx->join[c], ctx->sub[c]));
+      HCK(hipStreamWaitEvent(ctx->stream, ctx->join[c], 0));
+      c0 = c1;
+    }
+    ctx->timed_verify = false;
+  }
   check_launch(ctx);
 }
 
@@ -153,9 +189,14 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t
 void collect_phases(dkg_ctx* ctx, int round) {
   const char* names[3] = {"binomial", "stepping", "check"};
   for (int i = 0; i < 3; i++) {
+    const std::string key = "r" + std::to_string(round) + "." + names[i];
+    if (!ctx->timed_verify) {  // overlapped chunks: phases have no separate device time
+      ctx->phase_ms.erase(key);
+      continue;
+    }
     float ms = 0;
     HCK(hipEventElapsedTime(&ms, ctx->pev[i], ctx->pev[i + 1]));
-    ctx->phase_ms["r" + std::to_string(round) + "." + names[i]] = ms;
+    ctx->phase_ms[key] = ms;
   }
 }
 
@@ -330,6 +371,9 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     HCK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (auto& e : ctx->ev) HCK(hipEventCreate(&e));
     for (auto& e : ctx->pev) HCK(hipEventCreate(&e));
+    for (auto& st : ctx->sub) HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HCK(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
+    for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
     bool ok = false;
@@ -360,6 +404,11 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->pev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->join)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+  for (auto& st : ctx->sub)
+    if (st) (void)hipStreamDestroy(st);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -370,6 +419,12 @@ double dkg_ctx_phase_ms(const dkg_ctx* ctx, const char* name) {
   if (!ctx || !name) return -1.0;
   auto it = ctx->phase_ms.find(name);
   return it == ctx->phase_ms.end() ? -1.0 : it->second;
+}
+
+int dkg_ctx_set_streams(dkg_ctx* ctx, int nsub) {
+  if (!ctx || nsub < 1 || nsub > dkg_ctx::MAX_SUB) return DKG_E_ARG;
+  ctx->nsub = nsub;
+  return DKG_OK;
 }
 
 int dkg_env_check(size_t threshold, size_t nr_members) {
@@ -569,7 +624,7 @@ int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, c
     uint32_t* ds = upload_scalars(ctx, "vr_s", s, n);
     uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vr_sp", s_prime, n) : nullptr;
     uint8_t* dec = buf<uint8_t>(ctx, "vr_dec", n);
-    dkgk::check(n, 1, 0, j, round, ds, dsp, R, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
+    dkgk::check(n, 1, 0, j, round, ds, dsp, R, n, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
     check_launch(ctx);
     d2h(ctx, decision, dec, n);
     sync(ctx);

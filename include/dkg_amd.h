@@ -42,6 +42,10 @@ const char *dkg_ctx_last_error(const dkg_ctx *ctx);
 /* Device time (ms) of one phase of the last ceremony's round-2 / round-4 checks, by name
  * "r2.binomial", "r2.stepping", "r2.check", "r4.*" (HIP events on the ctx stream); -1 if unknown. */
 double dkg_ctx_phase_ms(const dkg_ctx *ctx, const char *name);
+/* Scheduling of the round-2/4 checks: the dealers are cut into nsub chunks (1..8, default 2)
+ * whose pipelines run on their own HIP streams and overlap on the GPU.  nsub = 1 serialises
+ * them and is the only mode that records dkg_ctx_phase_ms.  Results do not depend on nsub. */
+int dkg_ctx_set_streams(dkg_ctx *ctx, int nsub);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
 int dkg_device_count(void);
 

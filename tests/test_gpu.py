@@ -270,3 +270,84 @@ def test_ceremony_large_properties(be, n, t):
     E, A, s, sp = O.share_gen(1, n, t, a[32 * N * i:32 * N * (i + 1)], b[32 * N * i:32 * N * (i + 1)], be.h)
     assert E == r.E[32 * N * i:32 * N * (i + 1)] and A == r.A[32 * N * i:32 * N * (i + 1)]
     assert s == r.s[32 * n * i:32 * n * (i + 1)] and sp == r.s_prime[32 * n * i:32 * n * (i + 1)]
+
+
+@pytest.mark.parametrize("round_", [2, 4])
+def test_chunked_streams_identical(be, round_):
+    """Dealer chunks on 1..8 HIP streams (dkg_ctx_set_streams) give identical decisions, with a
+    ragged dealer count (200, not a multiple of 64), flipped shares and one undecodable dealer."""
+    n, t = 200, 99
+    N = t + 1
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([9]) * 32, 1, 0, n, t)
+    E, A, s, sp = be.share_gen(a, b, n, n, t)
+    C = bytearray(E if round_ == 2 else A)
+    s = bytearray(s)
+    rng = random.Random(round_)
+    flips = {(rng.randrange(n), rng.randrange(n)) for _ in range(40)}
+    for i, j in flips:
+        s[32 * (i * n + j) + 5] ^= 0x10
+    bad_dealer = 137
+    C[32 * (N * bad_dealer + 3) + 31] |= 0x80  # bit 255 set: does not decode (groups.rs:78-81)
+    exp = bytearray(ACCEPT for _ in range(n * n))
+    for i, j in flips:
+        exp[i * n + j] = REJECT
+    for j in range(n):
+        exp[bad_dealer * n + j] = REJECT
+    for i in range(n):
+        exp[i * n + i] = SELF
+    try:
+        for nsub in (1, 3, 8):
+            be.set_streams(nsub)
+            d = be.verify_pairs(n, t, round_, 0, n, bytes(C), bytes(s), sp if round_ == 2 else None)
+            assert bytes(d) == bytes(exp), nsub
+    finally:
+        be.set_streams(2)
+
+
+@pytest.mark.parametrize("name,ws", [("ceremony_n16_t7.json", 2), ("ceremony_n64_t31.json", 3),
+                                     ("ceremony_n11_t5.json", 4)])
+def test_sharded_ceremony_matches_golden(be, golden, name, ws):
+    """dkg_ceremony_shard_device for every rank of a ws-way dealer split (played in one process),
+    the host-side exchange (concatenation = what the all-gathers deliver) and the device combine
+    reproduce the single-GPU golden ceremony bit for bit."""
+    import numpy as np
+    import torch
+
+    from dkg_amd.distributed import combine_decisions, dealer_range
+
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    dev = torch.device("cuda", 0)
+    a, b = dkg_amd.dealer_coefficients(H(c["master_seed"]), c["ceremony"], 0, n, t)
+    dec2, dec4, A0, parts = [], [], [], []
+    for r in range(ws):
+        d0, d1 = dealer_range(r, ws, n)
+        D = d1 - d0
+        ta = torch.frombuffer(bytearray(a[32 * N * d0:32 * N * d1] or b"\0"), dtype=torch.uint8).to(dev)
+        tb = torch.frombuffer(bytearray(b[32 * N * d0:32 * N * d1] or b"\0"), dtype=torch.uint8).to(dev)
+        o2 = torch.zeros(max(D * n, 1), dtype=torch.uint8, device=dev)
+        o4 = torch.zeros_like(o2)
+        oA = torch.zeros(max(D * 32, 1), dtype=torch.uint8, device=dev)
+        op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+        be.ceremony_shard_device(n, t, d0, d1, ta.data_ptr(), tb.data_ptr(), o2.data_ptr(), o4.data_ptr(),
+                                 oA.data_ptr(), op.data_ptr())
+        dec2.append(o2[:D * n])
+        dec4.append(o4[:D * n])
+        A0.append(oA[:D * 32])
+        parts.append(op)
+    g2, g4, gA0, gp = (torch.cat(x) for x in (dec2, dec4, A0, parts))
+    assert dec_str(bytes(g2.cpu().numpy())) == c["dec2"]
+    assert bytes(gA0.cpu().numpy()) == b"".join(H(c["A"])[32 * N * i:32 * N * i + 32] for i in range(n))
+    d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
+    assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
+    assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
+    fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
+    assert bytes(fs.cpu().numpy()).hex() == c["final_share"]
+    mask = torch.from_numpy(np.ascontiguousarray(d.honest)).to(dev)
+    mpk = torch.empty(32, dtype=torch.uint8, device=dev)
+    be.point_sum_device(n, gA0.data_ptr(), mask.data_ptr(), mpk.data_ptr())
+    assert bytes(mpk.cpu().numpy()).hex() == c["mpk"]
