@@ -1,37 +1,46 @@
-"""Per-launch efficiency of the binomial step kernel from a rocprofv3 kernel-trace database."""
-import glob
-import sqlite3
+"""Per-launch efficiency of the binomial step kernel from a rocprofv3 kernel-trace CSV
+(tools/profile.sh output).  usage: python3 tools/prof_binom.py gpurun_out/prof_<tag> [t n]"""
+import csv
+import os
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
-db = glob.glob(sys.argv[1] + "/**/*.db", recursive=True)[0]
-t = int(sys.argv[2]) if len(sys.argv) > 2 else 511
-n = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
-c = sqlite3.connect(db)
-rows = c.execute("select grid_x, grid_y, workgroup_x, duration, start from kernels where name like '%binom%' "
-                 "order by start").fetchall()
-V = bench.VALU
-cost = {}
-for m in range(1, t + 1):
-    ds = bench._naf(m)
-    cc = V["ge_to_cached"] + V["ge_add"]
-    if len(ds) > 1:
-        cc += V["ge_to_cached"]
-        for i in range(len(ds) - 2, -1, -1):
-            nz = ds[i] != 0
-            cc += V["ge_dbl_t"] if (nz or i == 0) else V["ge_dbl_not"]
-            if nz:
-                cc += V["ge_add_signed"]
-    cost[m] = cc
-seg = rows[:t]
-for r in [1, 2, 4, 8, 16, 32, 64, 128, 192, 256, 320, 384, 448, 511]:
-    if r > len(seg):
-        break
-    gx, gy, wx, dur, st = seg[r - 1]
-    work = sum(cost[m] for m in range(1, r + 1)) * n
-    print(f"r={r:4d} grid={gx}x{gy} dur={dur / 1e3:8.1f}us  eff={work / (dur * 1e-9) / bench.INT32_PEAK * 100:5.1f}%")
-tot = sum(r[3] for r in seg)
-gaps = sum(seg[i + 1][4] - (seg[i][4] + seg[i][3]) for i in range(len(seg) - 1))
-print("total binom kernel time %.1f ms, gaps %.1f ms" % (tot / 1e6, gaps / 1e6))
+
+def main(d, t=511, n=1024):
+    rows = [r for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv")))
+            if "binom" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    V = bench.VALU
+    cost = {}
+    for m in range(1, t + 1):
+        ds = bench._naf(m)
+        cc = V["ge_to_cached"] + V["ge_add"]
+        if len(ds) > 1:
+            cc += V["ge_to_cached"]
+            for i in range(len(ds) - 2, -1, -1):
+                nz = ds[i] != 0
+                cc += V["ge_dbl_t"] if (nz or i == 0) else V["ge_dbl_not"]
+                if nz:
+                    cc += V["ge_add_signed"]
+        cost[m] = cc
+    seg = rows[:t]
+    tot = totw = 0
+    for i, r in enumerate(seg):
+        rr = i + 1
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        w = sum(cost[m] for m in range(1, rr + 1)) * n
+        tot += dur
+        totw += w
+        if rr in (1, 2, 4, 8, 16, 32, 64, 128, 192, 255, 256, 257, 300, 384, 448, 500, 511):
+            print(f"r={rr:4d} grid={r['Grid_Size_X']}x{r['Grid_Size_Y']} dur={dur / 1e3:8.1f}us "
+                  f"eff={w / (dur * 1e-9) / bench.INT32_PEAK * 100:5.1f}%")
+    print("total %.1f ms eff %.1f%%" % (tot / 1e6, totw / (tot * 1e-9) / bench.INT32_PEAK * 100))
+    gaps = sum(int(seg[i + 1]["Start_Timestamp"]) - int(seg[i]["End_Timestamp"]) for i in range(len(seg) - 1))
+    print("gaps between launches %.2f ms" % (gaps / 1e6))
+
+
+if __name__ == "__main__":
+    a = sys.argv[1:]
+    main(a[0], *(int(x) for x in a[1:]))
