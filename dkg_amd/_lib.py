@@ -58,6 +58,7 @@ def lib():
     L.dkg_ctx_last_error.restype = ctypes.c_char_p
     L.dkg_device_count.argtypes = []
     L.dkg_ctx_set_streams.argtypes = [p, ctypes.c_int]
+    L.dkg_ctx_set_overlap.argtypes = [p, ctypes.c_int]
     L.dkg_ctx_phase_ms.argtypes = [p, ctypes.c_char_p]
     L.dkg_ctx_phase_ms.restype = ctypes.c_double
     L.dkg_env_check.argtypes = [sz, sz]
@@ -81,7 +82,8 @@ def lib():
 
 
 EXPORTED = [
-    "dkg_ctx_create", "dkg_ctx_destroy", "dkg_ctx_last_error", "dkg_ctx_phase_ms", "dkg_ctx_set_streams", "dkg_device_count", "dkg_env_init",
+    "dkg_ctx_create", "dkg_ctx_destroy", "dkg_ctx_last_error", "dkg_ctx_phase_ms", "dkg_ctx_set_streams", "dkg_ctx_set_overlap",
+    "dkg_device_count", "dkg_env_init",
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",

@@ -33,7 +33,7 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
                    hipStream_t stream);
 // K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][rstride]
 // (element i*nrecv + j).  stream_a / stream_b: scratch for the inter-block boundary streams, each
-// >= ndealers*nrecv*160 B (unused when N <= 256).
+// >= ndealers*nrecv*160 B (unused when N <= 512).
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream);
 // K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);

@@ -367,12 +367,13 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
 
 // ------------------------------------------------------------------ K3b stepping
 // D_m <- D_m + D_{m+1} (m = 0..t-1) once per receiver; D_0 after step j is P_i(j+1).
-// Positions are cut into blocks of STEP_BS (one lane each, registers only).  D_m depends only on
-// D_{m+1}, so block b never waits on block b-1: blocks run as separate launches from the top
-// block down, and each launch streams its lowest position's per-step value (cached form,
-// [dealer][step][40]) to the launch below.  Inside a block the neighbour value crosses lanes by
-// shuffle and waves by a double-buffered LDS slot; one workgroup per dealer.
-constexpr int STEP_BS = 256;
+// Positions are cut into blocks of BS lanes (one position per lane, registers only).  D_m depends
+// only on D_{m+1}, so block b never waits on block b-1: blocks run as separate launches from the
+// top block down, and each launch streams its lowest position's per-step value (cached form,
+// [dealer][step][40]) to the launch below.  Inside a block the neighbour value crosses lanes
+// through LDS; one workgroup per dealer.  BS = 512 (80 KB of LDS, 2 workgroups = 16 waves per CU)
+// keeps t = 511 in ONE launch: each launch is a chain of n dependent additions per lane, so fewer,
+// wider blocks shorten the serial part when few dealers are resident (a small multi-GPU shard).
 
 __device__ __forceinline__ void cached_identity(ge_cached& c) {
   fe_one(c.YpX);
@@ -382,16 +383,17 @@ __device__ __forceinline__ void cached_identity(ge_cached& c) {
   fe_zero(c.T2d);
 }
 
-__global__ __launch_bounds__(STEP_BS, 4) void k_stepping(size_t npad, size_t N, const uint32_t* __restrict__ e,
-                                                         size_t nrecv, size_t pos0,
-                                                         const uint32_t* __restrict__ up,   // NULL: top block
-                                                         uint32_t* __restrict__ down,       // NULL: block 0
-                                                         uint32_t* __restrict__ R, size_t rstride) {
-  // Lane l's cached value sits in LDS column l (word k at col[k * STEP_BS]); lane l adds column
-  // l + 1.  Column 0 is never read inside the block (lane 0's value leaves through `down`), so the
-  // top lane parks the upstream value there: lane l reads column (l + 1) mod blockDim.  40 KB per
-  // 256-lane block -> 4 blocks (16 waves) per CU, and the addend never occupies VGPRs.
-  __shared__ uint32_t cols[PT_WORDS * STEP_BS];
+template <int BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_stepping(size_t npad, size_t N, const uint32_t* __restrict__ e,
+                                                                size_t nrecv, size_t pos0,
+                                                                const uint32_t* __restrict__ up,   // NULL: top block
+                                                                uint32_t* __restrict__ down,       // NULL: block 0
+                                                                uint32_t* __restrict__ R, size_t rstride) {
+  // Lane l's cached value sits in LDS column l (word k at col[k * BS]); lane l adds column l + 1.
+  // Column 0 is never read inside the block (lane 0's value leaves through `down`), so the top lane
+  // parks the upstream value there: lane l reads column (l + 1) mod blockDim.  160 B per lane, and
+  // the addend never occupies VGPRs.
+  __shared__ uint32_t cols[PT_WORDS * BS];
   const size_t d = blockIdx.x;
   const int l = threadIdx.x, bs = blockDim.x;
   const size_t S = N * npad;
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(STEP_BS, 4) void k_stepping(size_t npad, size_t N, 
           for (int k = 0; k < PT_WORDS / 4; k++) downd[j * (PT_WORDS / 4) + k] = w4[k];
         }
       } else {
-        lds_put_cached(mine, c0, STEP_BS);
+        lds_put_cached(mine, c0, BS);
       }
     }
     if (top_lane) {
@@ -427,10 +429,10 @@ __global__ __launch_bounds__(STEP_BS, 4) void k_stepping(size_t npad, size_t N, 
       } else {
         cached_identity(u);
       }
-      lds_put_cached(cols, u, STEP_BS);
+      lds_put_cached(cols, u, BS);
     }
     __syncthreads();
-    if (pos + 1 < N) ge_add_lds(D, D, nbr, false, STEP_BS);
+    if (pos + 1 < N) ge_add_lds(D, D, nbr, false, BS);
     __syncthreads();  // every column read before the next step overwrites it
     if (l == 0 && R) pt_store(R, rstride, d * nrecv + j, D);
   }
@@ -439,13 +441,18 @@ __global__ __launch_bounds__(STEP_BS, 4) void k_stepping(size_t npad, size_t N, 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream) {
   if (!ndealers || !nrecv) return;
-  const size_t bs = N >= STEP_BS ? STEP_BS : ((N + 63) / 64) * 64;
+  const bool wide = N > 256;
+  const size_t bs = wide ? 512 : ((N + 63) / 64) * 64;
   const size_t nblk = (N + bs - 1) / bs;
   uint32_t* up = nullptr;
   for (size_t b = nblk; b-- > 0;) {
     uint32_t* down = b ? ((nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
-    hipLaunchKernelGGL(k_stepping, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream, npad, N, e, nrecv,
-                       b * bs, up, down, b ? nullptr : R, rstride);
+    if (wide)
+      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream, npad, N, e, nrecv,
+                         b * bs, up, down, b ? nullptr : R, rstride);
+    else
+      hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream, npad, N, e, nrecv,
+                         b * bs, up, down, b ? nullptr : R, rstride);
     up = down;
   }
 }

@@ -29,7 +29,8 @@ struct dkg_ctx {
   int nsub = 2;                         // dealer-chunk streams of verify_device
   hipStream_t sub[MAX_SUB] = {};
   hipEvent_t fork = nullptr, join[MAX_SUB] = {};
-  bool timed_verify = false;
+  bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
+  std::string timed_tag;                // set while pev[] hold a serialised verify_device's phases
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
 
@@ -60,7 +61,7 @@ T* buf(dkg_ctx* ctx, const char* name, size_t bytes) {
   auto it = ctx->bufs.find(name);
   if (it != ctx->bufs.end() && it->second.second >= bytes) return reinterpret_cast<T*>(it->second.first);
   if (it != ctx->bufs.end()) {
-    HCK(hipStreamSynchronize(ctx->stream));
+    HCK(hipDeviceSynchronize());  // the old buffer may still be read on any of the ctx's streams
     HCK(hipFree(it->second.first));
     ctx->bufs.erase(it);
   }
@@ -124,79 +125,144 @@ uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, si
   return red;
 }
 
-// Rounds 2 / 4 for dealers [dealer_base, dealer_base + D) against receivers 0..n-1, all on device.
-// Ccomp [D][N][8] compressed commitments; s, sp [D][n][8] canonical; dec [D][n].
-// With ctx->nsub > 1 the dealers are cut into nsub chunks (multiples of 64 columns) whose
-// binomial -> stepping -> check pipelines run on their own streams: the hundreds of short,
-// partly-filled binomial launches of one chunk then share the CUs with another chunk's work
-// instead of leaving them idle in launch tails.  nsub == 1 is the serialised schedule whose
-// per-phase device times are recorded (dkg_ctx_phase_ms).
-void verify_device(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t dealer_base,
-                   const uint32_t* Ccomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec) {
-  const size_t N = t + 1, npad = pad64(D);
-  uint32_t* Cext = buf<uint32_t>(ctx, "Cext", PTB * D * N);
-  uint8_t* pok = buf<uint8_t>(ctx, "pok", D * N);
-  uint8_t* dok = buf<uint8_t>(ctx, "dok", D);
-  uint32_t* Cpm = buf<uint32_t>(ctx, "Cpm", PTB * N * npad);
-  uint32_t* e0 = buf<uint32_t>(ctx, "binom0", PTB * N * npad);
-  uint32_t* e1 = buf<uint32_t>(ctx, "binom1", PTB * N * npad);
-  uint32_t* R = buf<uint32_t>(ctx, "R", PTB * D * n);
-  uint32_t *sa = nullptr, *sb = nullptr;
-  if (N > 256) {
-    sa = buf<uint32_t>(ctx, "step_a", PTB * D * n);
-    sb = buf<uint32_t>(ctx, "step_b", PTB * D * n);
+// After a sync: record the device time of binomial / stepping / check of the last verify_device
+// when it ran serialised and timed (names "<tag>.binomial" etc.; tag r2, r4 or r24 = fused).
+void collect_phases(dkg_ctx* ctx) {
+  if (ctx->timed_tag.empty()) return;
+  const char* names[3] = {"binomial", "stepping", "check"};
+  for (int i = 0; i < 3; i++) {
+    float ms = 0;
+    HCK(hipEventElapsedTime(&ms, ctx->pev[i], ctx->pev[i + 1]));
+    ctx->phase_ms[ctx->timed_tag + "." + names[i]] = ms;
   }
-  const size_t rstride = D * n;
-  dkgk::decode_points(Ccomp, D * N, Cext, D * N, pok, ctx->stream);  // K5 (groups.rs:78-81)
-  dkgk::dealer_ok(D, N, pok, dok, ctx->stream);
-  dkgk::to_position_major(D, N, npad, Cext, Cpm, ctx->stream);
-  // dealer chunk [c0, c0 + w) (w a multiple of 64 except possibly at the tail) on stream st
-  auto chunk = [&](size_t c0, size_t w, hipStream_t st, bool timed) {
-    const size_t wpad = pad64(w);
-    if (timed) HCK(hipEventRecord(ctx->pev[0], st));
-    uint32_t* e = dkgk::binomial(wpad, npad, N, Cpm + c0, e0 + c0, e1 + c0, st);
-    if (timed) HCK(hipEventRecord(ctx->pev[1], st));
+  ctx->timed_tag.clear();
+}
+
+// One block of rows to verify: `D` dealers [dealer_base, dealer_base + D) against receivers
+// 0..n-1 in `round` (2: h*s' + g*s == sum_k j^k E_i[k]; 4: g*s == sum_k j^k A_i[k]).
+// Ccomp [D][N][8] compressed commitments; s, sp [D][n][8] canonical; dec [D][n].
+struct VerifySeg {
+  int round;
+  size_t D, dealer_base;
+  const uint32_t* Ccomp;
+  const uint32_t* s;
+  const uint32_t* sp;
+  uint8_t* dec;
+};
+
+// All segments on device, as ONE pipeline over their concatenated "virtual dealers" (a dealer's E
+// row and its A row are two independent polynomials in the exponent: the binomial-basis Horner and
+// the stepping never look at which one a column is).  Fusing round 2 with round 4 doubles the
+// independent work inside each of the t dependent binomial launches and halves the launch count;
+// only the checks differ per segment.  Work is ordered after what is queued on ctx->stream and
+// completes on it.  With ctx->nsub > 1 the virtual dealers are cut into nsub chunks (multiples of
+// 64 columns) whose binomial -> stepping -> check pipelines run on their own streams, so one
+// chunk's partly-filled binomial launches share the CUs with another chunk's work.  nsub == 1 with
+// `timed` records per-phase device times (dkg_ctx_phase_ms, under `tag`).
+void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int nseg, bool timed,
+                   const char* tag) {
+  const size_t N = t + 1;
+  size_t V = 0;
+  for (int k = 0; k < nseg; k++) V += segs[k].D;
+  if (!V) return;
+  const size_t npad = pad64(V);
+  hipStream_t home = ctx->stream;
+  uint32_t* Cext = buf<uint32_t>(ctx, "v.Cext", PTB * V * N);
+  uint8_t* pok = buf<uint8_t>(ctx, "v.pok", V * N);
+  uint8_t* dok = buf<uint8_t>(ctx, "v.dok", V);
+  uint32_t* Cpm = buf<uint32_t>(ctx, "v.Cpm", PTB * N * npad);
+  uint32_t* e0 = buf<uint32_t>(ctx, "v.binom0", PTB * N * npad);
+  uint32_t* e1 = buf<uint32_t>(ctx, "v.binom1", PTB * N * npad);
+  uint32_t* R = buf<uint32_t>(ctx, "v.R", PTB * V * n);
+  uint32_t *sa = nullptr, *sb = nullptr;
+  if (N > 512) {
+    sa = buf<uint32_t>(ctx, "v.step_a", PTB * V * n);
+    sb = buf<uint32_t>(ctx, "v.step_b", PTB * V * n);
+  }
+  const size_t rstride = V * n;
+  std::vector<size_t> v0(nseg + 1, 0);
+  for (int k = 0; k < nseg; k++) {
+    v0[k + 1] = v0[k] + segs[k].D;
+    // K5 (groups.rs:78-81): virtual dealer v's commitments are elements v*N .. v*N + t
+    dkgk::decode_points(segs[k].Ccomp, segs[k].D * N, Cext + v0[k] * N, V * N, pok + v0[k] * N, home);
+  }
+  dkgk::dealer_ok(V, N, pok, dok, home);
+  dkgk::to_position_major(V, N, npad, Cext, Cpm, home);
+  // checks of virtual dealers [c0, c1) on stream st, split at segment boundaries
+  auto checks = [&](size_t c0, size_t c1, hipStream_t st) {
+    for (int k = 0; k < nseg; k++) {
+      const size_t a = std::max(c0, v0[k]), b = std::min(c1, v0[k + 1]);
+      if (a >= b) continue;
+      const VerifySeg& g = segs[k];
+      const size_t l0 = a - v0[k];
+      dkgk::check(b - a, n, g.dealer_base + l0, 0, g.round, g.s + l0 * n * 8,
+                  g.round == 2 ? g.sp + l0 * n * 8 : nullptr, R + a * n, rstride, ctx->tab_g, ctx->tab_h, dok + a,
+                  g.dec + l0 * n, st);
+    }
+  };
+  auto chunk = [&](size_t c0, size_t w, hipStream_t st, bool tm) {
+    if (tm) HCK(hipEventRecord(ctx->pev[0], st));
+    uint32_t* e = dkgk::binomial(pad64(w), npad, N, Cpm + c0, e0 + c0, e1 + c0, st);
+    if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::stepping(w, npad, N, e, n, R + c0 * n, rstride, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st);
-    if (timed) HCK(hipEventRecord(ctx->pev[2], st));
-    dkgk::check(w, n, dealer_base + c0, 0, round, s + c0 * n * 8, sp ? sp + c0 * n * 8 : nullptr, R + c0 * n,
-                rstride, ctx->tab_g, ctx->tab_h, dok + c0, dec + c0 * n, st);
-    if (timed) HCK(hipEventRecord(ctx->pev[3], st));
+    if (tm) HCK(hipEventRecord(ctx->pev[2], st));
+    checks(c0, c0 + w, st);
+    if (tm) HCK(hipEventRecord(ctx->pev[3], st));
   };
   const size_t nsub = std::min<size_t>(ctx->nsub, npad / 64);
+  ctx->timed_tag.clear();
   if (nsub <= 1) {
-    chunk(0, D, ctx->stream, true);
-    ctx->timed_verify = true;
+    chunk(0, V, home, timed);
+    if (timed) ctx->timed_tag = tag;
   } else {
     const size_t groups = npad / 64;
-    HCK(hipEventRecord(ctx->fork, ctx->stream));
+    HCK(hipEventRecord(ctx->fork, home));
     size_t c0 = 0;
     for (size_t c = 0; c < nsub; c++) {
       const size_t g1 = groups * (c + 1) / nsub;
-      const size_t c1 = std::min(D, g1 * 64);
+      const size_t c1 = std::min(V, g1 * 64);
       HCK(hipStreamWaitEvent(ctx->sub[c], ctx->fork, 0));
       chunk(c0, c1 - c0, ctx->sub[c], false);
       HCK(hipEventRecord(ctx->join[c], ctx->sub[c]));
-      HCK(hipStreamWaitEvent(ctx->stream, ctx->join[c], 0));
+      HCK(hipStreamWaitEvent(home, ctx->join[c], 0));
       c0 = c1;
     }
-    ctx->timed_verify = false;
   }
   check_launch(ctx);
 }
 
-// After a sync: record the device time of binomial / stepping / check of the last verify_device.
-void collect_phases(dkg_ctx* ctx, int round) {
-  const char* names[3] = {"binomial", "stepping", "check"};
-  for (int i = 0; i < 3; i++) {
-    const std::string key = "r" + std::to_string(round) + "." + names[i];
-    if (!ctx->timed_verify) {  // overlapped chunks: phases have no separate device time
-      ctx->phase_ms.erase(key);
-      continue;
-    }
-    float ms = 0;
-    HCK(hipEventElapsedTime(&ms, ctx->pev[i], ctx->pev[i + 1]));
-    ctx->phase_ms[key] = ms;
+void verify_one(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t dealer_base, const uint32_t* Ccomp,
+                const uint32_t* s, const uint32_t* sp, uint8_t* dec, bool timed) {
+  VerifySeg g{round, D, dealer_base, Ccomp, s, sp, dec};
+  verify_device(ctx, n, t, &g, 1, timed, round == 2 ? "r2" : "r4");
+}
+
+// Rounds 2 and 4 of one set of dealers.  ctx->overlap (default): one fused pipeline over both
+// commitment vectors -- the round-4 inputs (A_i, s_ij) are fixed in round 1 and only the SKIPPED
+// mask applied afterwards depends on round 2, so every output is identical to protocol order.
+// Otherwise round 2, then (after `between`, e.g. round 3) round 4, each timed when nsub == 1.
+// `after2` (may be null) is recorded on ctx->stream once the round-2 decisions are complete.
+template <typename F>
+void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
+                   const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
+                   hipEvent_t after2, F&& between) {
+  if (ctx->overlap) {
+    VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2}, {4, D, dealer_base, Acomp, s, nullptr, dec4}};
+    verify_device(ctx, n, t, g, 2, true, "r24");
+    if (after2) HCK(hipEventRecord(after2, ctx->stream));
+    sync(ctx);
+    collect_phases(ctx);
+    between();
+  } else {
+    verify_one(ctx, n, t, 2, D, dealer_base, Ecomp, s, sp, dec2, true);
+    if (after2) HCK(hipEventRecord(after2, ctx->stream));
+    sync(ctx);
+    collect_phases(ctx);
+    between();
+    verify_one(ctx, n, t, 4, D, dealer_base, Acomp, s, nullptr, dec4, true);
+    sync(ctx);
+    collect_phases(ctx);
   }
 }
 
@@ -212,39 +278,35 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   const size_t N = t + 1;
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
-  // ---- round 2 (committee.rs:260-366)
-  verify_device(ctx, n, t, 2, n, 0, Ecomp, s, sp, dec2);
-  std::vector<uint8_t> h2(n * n);
-  d2h(ctx, h2.data(), dec2, n * n);
-  HCK(hipEventRecord(ctx->ev[2], ctx->stream));
-  sync(ctx);
-  collect_phases(ctx, 2);
+  // ---- rounds 2 and 4 (committee.rs:260-366, :508-580), fused or in protocol order (verify_rounds)
+  std::vector<uint8_t> h2(n * n), h4(n * n);
   std::vector<uint8_t> qualified(n, 1), r2err(n, 0);
   std::vector<int32_t> complaints(n, 0);
-  for (size_t i = 0; i < n; i++)
-    for (size_t j = 0; j < n; j++)
-      if (h2[i * n + j] == DKG_REJECT) {
-        complaints[j]++;     // receiver j accuses dealer i (committee.rs:311-316)
-        qualified[i] = 0;    // a valid complaint disqualifies i for everyone (:370-398)
-      }
-  for (size_t j = 0; j < n; j++) r2err[j] = complaints[j] > (int32_t)t;  // :340-347
-  // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
-  uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
-  h2d(ctx, qmask, qualified.data(), n);
   uint32_t* fs = buf<uint32_t>(ctx, "final_share", 32 * n);
-  dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
-  uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
-  dkgk::fixed_base(n, fs, ctx->tab_g, pub, ctx->stream);
   uint32_t* pubc = buf<uint32_t>(ctx, "pub_comp", 32 * n);
-  dkgk::encode_points(pub, n, n, pubc, ctx->stream);
-  HCK(hipEventRecord(ctx->ev[3], ctx->stream));
-  // ---- round 4 (committee.rs:508-580)
-  verify_device(ctx, n, t, 4, n, 0, Acomp, s, nullptr, dec4);
-  std::vector<uint8_t> h4(n * n);
+  auto round3 = [&] {
+    d2h(ctx, h2.data(), dec2, n * n);
+    sync(ctx);
+    for (size_t i = 0; i < n; i++)
+      for (size_t j = 0; j < n; j++)
+        if (h2[i * n + j] == DKG_REJECT) {
+          complaints[j]++;     // receiver j accuses dealer i (committee.rs:311-316)
+          qualified[i] = 0;    // a valid complaint disqualifies i for everyone (:370-398)
+        }
+    for (size_t j = 0; j < n; j++) r2err[j] = complaints[j] > (int32_t)t;  // :340-347
+    // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
+    uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
+    h2d(ctx, qmask, qualified.data(), n);
+    dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
+    uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
+    dkgk::fixed_base(n, fs, ctx->tab_g, pub, ctx->stream);
+    dkgk::encode_points(pub, n, n, pubc, ctx->stream);
+    HCK(hipEventRecord(ctx->ev[3], ctx->stream));
+  };
+  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3);
   d2h(ctx, h4.data(), dec4, n * n);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
-  collect_phases(ctx, 4);
   std::vector<uint8_t> recon(n, 0);
   for (size_t i = 0; i < n; i++)
     for (size_t j = 0; j < n; j++) {
@@ -396,7 +458,7 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
 void dkg_ctx_destroy(dkg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) (void)hipDeviceSynchronize();
   for (auto& kv : ctx->bufs) (void)hipFree(kv.second.first);
   if (ctx->tab_g) (void)hipFree(ctx->tab_g);
   if (ctx->tab_h) (void)hipFree(ctx->tab_h);
@@ -424,6 +486,12 @@ double dkg_ctx_phase_ms(const dkg_ctx* ctx, const char* name) {
 int dkg_ctx_set_streams(dkg_ctx* ctx, int nsub) {
   if (!ctx || nsub < 1 || nsub > dkg_ctx::MAX_SUB) return DKG_E_ARG;
   ctx->nsub = nsub;
+  return DKG_OK;
+}
+
+int dkg_ctx_set_overlap(dkg_ctx* ctx, int on) {
+  if (!ctx) return DKG_E_ARG;
+  ctx->overlap = on != 0;
   return DKG_OK;
 }
 
@@ -593,7 +661,7 @@ int dkg_verify_pairs(dkg_ctx* ctx, size_t n, size_t t, int round, size_t d0, siz
     uint32_t* ds = upload_scalars(ctx, "vp_s", s, D * n);
     uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vp_sp", s_prime, D * n) : nullptr;
     uint8_t* dec = buf<uint8_t>(ctx, "vp_dec", D * n);
-    verify_device(ctx, n, t, round, D, d0, Cc, ds, dsp, dec);
+    verify_one(ctx, n, t, round, D, d0, Cc, ds, dsp, dec, false);
     d2h(ctx, decision, dec, D * n);
     sync(ctx);
     return DKG_OK;
@@ -728,16 +796,16 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     uint32_t* dsp = buf<uint32_t>(ctx, "sh_sp", 32 * D * n);
     if (D) {
       round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
-      verify_device(ctx, n, t, 2, D, d0, Ec, ds, dsp, (uint8_t*)d_dec2);
       // Qualification of a dealer depends only on its own decision row (any REJECT disqualifies,
       // committee.rs:370-398), so each rank decides it for its dealers with no exchange.
       std::vector<uint8_t> rows(D * n), q(D, 1);
-      d2h(ctx, rows.data(), d_dec2, D * n);
-      sync(ctx);
-      for (size_t i = 0; i < D; i++)
-        for (size_t j = 0; j < n; j++)
-          if (rows[i * n + j] == DKG_REJECT) q[i] = 0;
-      verify_device(ctx, n, t, 4, D, d0, Ac, ds, nullptr, (uint8_t*)d_dec4);
+      verify_rounds(ctx, n, t, D, d0, Ec, Ac, ds, dsp, (uint8_t*)d_dec2, (uint8_t*)d_dec4, nullptr, [&] {
+        d2h(ctx, rows.data(), d_dec2, D * n);
+        sync(ctx);
+        for (size_t i = 0; i < D; i++)
+          for (size_t j = 0; j < n; j++)
+            if (rows[i * n + j] == DKG_REJECT) q[i] = 0;
+      });
       HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
       uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
       h2d(ctx, qm, q.data(), D);

@@ -40,12 +40,20 @@ int dkg_ctx_create(int device, dkg_ctx **out);
 void dkg_ctx_destroy(dkg_ctx *ctx);
 const char *dkg_ctx_last_error(const dkg_ctx *ctx);
 /* Device time (ms) of one phase of the last ceremony's round-2 / round-4 checks, by name
- * "r2.binomial", "r2.stepping", "r2.check", "r4.*" (HIP events on the ctx stream); -1 if unknown. */
+ * "r2.binomial", "r2.stepping", "r2.check", "r4.*", or "r24.*" for the fused rounds (HIP events
+ * on the ctx stream, recorded only with dkg_ctx_set_streams(ctx, 1)); -1 if unknown. */
 double dkg_ctx_phase_ms(const dkg_ctx *ctx, const char *name);
 /* Scheduling of the round-2/4 checks: the dealers are cut into nsub chunks (1..8, default 2)
  * whose pipelines run on their own HIP streams and overlap on the GPU.  nsub = 1 serialises
  * them and is the only mode that records dkg_ctx_phase_ms.  Results do not depend on nsub. */
 int dkg_ctx_set_streams(dkg_ctx *ctx, int nsub);
+/* on != 0 (default): the ceremony drivers verify round 2 (committee.rs:273-338) and round 4
+ * (committee.rs:520-559) as ONE fused pipeline over both commitment vectors.  The round-4 inputs
+ * (A_i, s_ij) are fixed in round 1 and only the SKIPPED mask of disqualified dealers depends on
+ * round 2 (it is applied afterwards), so every output is identical to protocol order; ms_round2
+ * then covers both rounds' checks and ms_round4 only the copy-back.  on == 0: protocol order.
+ * Phase times (dkg_ctx_phase_ms, nsub == 1) are recorded under "r24.*" when fused. */
+int dkg_ctx_set_overlap(dkg_ctx *ctx, int on);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
 int dkg_device_count(void);
 

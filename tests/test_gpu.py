@@ -180,13 +180,19 @@ def test_ceremony_honest(be, golden, name):
     _check_ceremony(c, r, n)
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("name", FAULTS)
-def test_ceremony_faults(be, golden, name):
-    """misbehaving_parties / invalid_phase_2 / phase_4 style fault injection (committee.rs:1105-1313)."""
+def test_ceremony_faults(be, golden, name, overlap):
+    """misbehaving_parties / invalid_phase_2 / phase_4 style fault injection (committee.rs:1105-1313),
+    with the round-4 checks overlapped with rounds 2-3 (default) and in protocol order."""
     c = golden(name)
     n, t = c["n"], c["t"]
     be.env_init(t, n, CK)
-    r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+    be.set_overlap(overlap)
+    try:
+        r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+    finally:
+        be.set_overlap(True)
     _check_ceremony(c, r, n)
 
 
