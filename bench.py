@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 
 L = 2**252 + 27742317777372353535851937790883648493
 CONFIGS = {"D": (1024, 511), "C": (256, 127), "E": (4096, 2047), "B": (64, 31)}
+BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t=31 ceremonies
 
 # Peak INT32 VALU issue rate of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one wave64
 # instruction per 2 cycles per SIMD; full-rate v_add_u32 reaches it: tools/ubench/intrate2.hip).
@@ -119,18 +120,87 @@ def cpu_baseline(n, t, seconds_target=15.0):
                       f"overstates the CPU ceremony rate)"}
 
 
+def bench_batch(args, ws, rank, local):
+    """BASELINE config 5: B independent ceremonies per step (replicas only: with N GPUs each rank
+    runs its own B ceremonies, no collective -- weak scaling).  Coefficients are generated on the
+    GPU (dkg_dealer_coeffs_device) and stay in HBM; one step = rounds 1-5 of all B ceremonies."""
+    import torch
+
+    import dkg_amd
+
+    B, n, t = BATCH[args.config]
+    N = t + 1
+    torch.cuda.set_device(local)
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    be = dkg_amd.Backend(local)
+    be.set_streams(args.streams)
+    be.set_overlap(not args.no_overlap)
+    be.env_init(t, n)
+    dev = torch.device("cuda", local)
+    ta = torch.empty(B * n * N * 32, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    be.dealer_coefficients_device(b"\xb5" * 32, rank * B, B, 0, n, t, ta.data_ptr(), tb.data_ptr())
+
+    def step():
+        return dkg_amd.ceremony_batch_device(be, B, n, t, ta.data_ptr(), tb.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    assert all(q == n for q in res.n_qualified), "an honest ceremony disqualified a dealer"
+    pairs = B * n * (n - 1) * ws
+    out = {"metric": f"verified shares/sec (whole node), {B} independent n={n},t={t} ceremonies per GPU "
+                     f"(BASELINE config 5)",
+           "value": pairs * args.steps / elapsed, "unit": "verified shares/s", "n_gpus": ws, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u32 (GF(2^255-19), Z_l)",
+           "data": "synthetic: seeded ChaCha20 coefficients generated on the GPU, honest ceremonies",
+           "config": {"workload": f"{B} ceremonies n={n}, t={t} per GPU (share gen + round-2/4 checks + "
+                                  f"finalise of each)", "ceremonies_per_gpu": B, "n": n, "t": t,
+                      "pairs_per_step": pairs, "parallelism": f"replicas x{ws}" if ws > 1 else "single GPU"},
+           "ceremonies_per_s": B * ws * args.steps / elapsed,
+           "phases_ms": {k: round(v, 3) for k, v in res.ms.items()}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    be.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="D", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="D", choices=sorted(CONFIGS) + sorted(BATCH))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="dealer-chunk streams of the round-2/4 checks")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     args = ap.parse_args()
-    n, t = CONFIGS[args.config]
     ws, rank, local = dist_env()
+    if args.config in BATCH:
+        return bench_batch(args, ws, rank, local)
+    n, t = CONFIGS[args.config]
 
     import torch
 

@@ -42,6 +42,17 @@ class CeremonyOut(ctypes.Structure):
     ]
 
 
+class BatchOut(ctypes.Structure):
+    _fields_ = [
+        ("mpk", ctypes.c_void_p), ("n_qualified", ctypes.c_void_p), ("qualified", ctypes.c_void_p),
+        ("r2_error", ctypes.c_void_p), ("complaints2", ctypes.c_void_p), ("reconstruct", ctypes.c_void_p),
+        ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
+        ("dec2", ctypes.c_void_p), ("dec4", ctypes.c_void_p),
+        ("ms_round1", ctypes.c_double), ("ms_checks", ctypes.c_double), ("ms_round3", ctypes.c_double),
+        ("ms_finalise", ctypes.c_double), ("ms_total", ctypes.c_double),
+    ]
+
+
 def lib():
     """Load libdkg_amd.so (raises if it is absent: the HIP path is mandatory)."""
     global _lib
@@ -74,6 +85,9 @@ def lib():
     L.dkg_ceremony_verify.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_run_device.argtypes = [p, sz, sz, p, p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_shard_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]
+    L.dkg_ceremony_batch_device.argtypes = [p, sz, sz, sz, p, p, ctypes.POINTER(BatchOut)]
+    L.dkg_ceremony_batch_verify.argtypes = [p, sz, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(BatchOut)]
+    L.dkg_dealer_coeffs_device.argtypes = [p, u8p, ctypes.c_uint32, sz, sz, sz, sz, p, p]
     L.dkg_dealer_coeffs.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, p, p]
     L.dkg_scalar_sum_device.argtypes = [p, sz, sz, p, p, p]
     L.dkg_point_sum_device.argtypes = [p, sz, p, p, p]
@@ -87,5 +101,6 @@ EXPORTED = [
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
-    "dkg_dealer_coeffs", "dkg_scalar_sum_device", "dkg_point_sum_device",
+    "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
+    "dkg_scalar_sum_device", "dkg_point_sum_device",
 ]

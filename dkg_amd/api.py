@@ -17,7 +17,7 @@ from dataclasses import dataclass
 from typing import List, Optional
 
 from . import _lib
-from ._lib import CeremonyOut, DkgError
+from ._lib import BatchOut, CeremonyOut, DkgError
 
 CK_DEFAULT = b"Example of a shared string."
 
@@ -213,6 +213,13 @@ class Backend:
                                                               ctypes.c_void_p(d_b), ctypes.byref(o)))
         return self._result(n, t, o, bufs, False)
 
+    def dealer_coefficients_device(self, master: bytes, ceremony0: int, B: int, d0: int, D: int, t: int,
+                                   d_a: int, d_b: int):
+        """dkg_dealer_coeffs on the GPU for B ceremonies: rows [B*D][t+1][32] at device pointers."""
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_dealer_coeffs_device(self._ctx, master, ceremony0, B, d0, D, t, vp(d_a),
+                                                               vp(d_b)))
+
     def ceremony_shard_device(self, n, t, d0, d1, d_a, d_b, d_dec2, d_dec4, d_A0, d_partial) -> float:
         ms = ctypes.c_double()
         vp = ctypes.c_void_p
@@ -230,6 +237,86 @@ class Backend:
         """out = sum of the compressed points[c] with mask[c] (device pointers)."""
         vp = ctypes.c_void_p
         _check(self._ctx, _lib.lib().dkg_point_sum_device(self._ctx, count, vp(d_points), vp(d_mask), vp(d_out)))
+
+
+@dataclass
+class BatchResult:
+    """Outputs of B independent ceremonies (row c*n + i = party i of ceremony c)."""
+    B: int
+    n: int
+    t: int
+    mpk: List[bytes]
+    n_qualified: List[int]
+    qualified: bytes
+    r2_error: bytes
+    complaints2: List[int]
+    reconstruct: bytes
+    final_share: Optional[bytes]
+    public_share: Optional[bytes]
+    dec2: Optional[bytes]
+    dec4: Optional[bytes]
+    ms: dict
+
+    def ceremony(self, c: int) -> dict:
+        """The outputs of ceremony c in the layout of a single CeremonyResult."""
+        n = self.n
+        r = slice(c * n, (c + 1) * n)
+        d = {"mpk": self.mpk[c], "n_qualified": self.n_qualified[c], "qualified": list(self.qualified[r]),
+             "r2_error": list(self.r2_error[r]), "complaints2": self.complaints2[r],
+             "reconstruct": list(self.reconstruct[r])}
+        for k in ("final_share", "public_share"):
+            v = getattr(self, k)
+            d[k] = v[32 * n * c:32 * n * (c + 1)] if v is not None else None
+        for k in ("dec2", "dec4"):
+            v = getattr(self, k)
+            d[k] = v[n * n * c:n * n * (c + 1)] if v is not None else None
+        return d
+
+
+def _batch_out(B, n, big):
+    import struct  # noqa: F401
+    V = B * n
+    sizes = {"mpk": 32 * B, "n_qualified": 4 * B, "qualified": V, "r2_error": V, "complaints2": 4 * V,
+             "reconstruct": V}
+    if big:
+        sizes.update({"final_share": 32 * V, "public_share": 32 * V, "dec2": V * n, "dec4": V * n})
+    o = BatchOut()
+    bufs = {}
+    for k, v in sizes.items():
+        bufs[k] = ctypes.create_string_buffer(max(v, 1))
+        setattr(o, k, ctypes.cast(bufs[k], ctypes.c_void_p))
+    return o, bufs
+
+
+def _batch_result(B, n, t, o, bufs):
+    import struct
+    V = B * n
+    g = lambda k, size: bufs[k].raw[:size] if k in bufs else None  # noqa: E731
+    return BatchResult(
+        B=B, n=n, t=t, mpk=[bufs["mpk"].raw[32 * c:32 * c + 32] for c in range(B)],
+        n_qualified=list(struct.unpack(f"<{B}i", bufs["n_qualified"].raw[:4 * B])),
+        qualified=g("qualified", V), r2_error=g("r2_error", V),
+        complaints2=list(struct.unpack(f"<{V}i", bufs["complaints2"].raw[:4 * V])),
+        reconstruct=g("reconstruct", V), final_share=g("final_share", 32 * V), public_share=g("public_share", 32 * V),
+        dec2=g("dec2", V * n), dec4=g("dec4", V * n),
+        ms={"round1": o.ms_round1, "checks": o.ms_checks, "round3": o.ms_round3, "finalise": o.ms_finalise,
+            "total": o.ms_total})
+
+
+def ceremony_batch_device(be: "Backend", B: int, n: int, t: int, d_a: int, d_b: int, big: bool = False) -> BatchResult:
+    """B honest ceremonies from device coefficients [B*n][t+1][32] (dkg_ceremony_batch_device)."""
+    o, bufs = _batch_out(B, n, big)
+    _check(be.ctx, _lib.lib().dkg_ceremony_batch_device(be.ctx, B, n, t, ctypes.c_void_p(d_a), ctypes.c_void_p(d_b),
+                                                          ctypes.byref(o)))
+    return _batch_result(B, n, t, o, bufs)
+
+
+def ceremony_batch_verify(be: "Backend", B: int, n: int, t: int, E: bytes, A: bytes, s: bytes,
+                          s_prime: bytes) -> BatchResult:
+    """Receiver side of B ceremonies from (possibly tampered) broadcast values (dkg_ceremony_batch_verify)."""
+    o, bufs = _batch_out(B, n, True)
+    _check(be.ctx, _lib.lib().dkg_ceremony_batch_verify(be.ctx, B, n, t, E, A, s, s_prime, ctypes.byref(o)))
+    return _batch_result(B, n, t, o, bufs)
 
 
 class Environment:

@@ -37,19 +37,27 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream);
 // K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);
-// dealer_ok[i] == 0 forces 0; i == j (self, index i + dealer_base == j) gives 2.
+// dealer_ok[i] == 0 forces 0; self ((i + dealer_base) mod nmod == j + recv_base, nmod = parties per
+// ceremony, so batched ceremonies stacked dealer-wise work too) gives 2.
 // R: SoA [40][rstride], element i*nrecv + j.
-void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round, const uint32_t* s,
-           const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
-           const uint8_t* dealer_ok, uint8_t* decision, hipStream_t stream);
+void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
+           const uint32_t* s, const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g,
+           const uint32_t* tab_h, const uint8_t* dealer_ok, uint8_t* decision, hipStream_t stream);
 // per-dealer validity: dealer_ok[i] = AND of point_ok over its N commitments (dealer-major [D][N])
 void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream);
 // Horner in the exponent for receivers x0 .. x0+nrecv-1 (1-based indices): R [40][ndealers*nrecv]
 void horner(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t x0, size_t nrecv, uint32_t* R,
             hipStream_t stream);
-// out (one SoA point, stride 1) = sum of mask[e] * P_e (mask may be NULL)
-void sum_points(size_t count, const uint32_t* pts, size_t stride, const uint8_t* mask, uint32_t* out, size_t ostride, size_t col,
-                hipStream_t stream);
+// out column col + g (SoA, stride ostride) = sum over e in [g*count, (g+1)*count) of mask[e] * P_e
+// (mask may be NULL), for each group g < groups.
+void sum_points(size_t count, const uint32_t* pts, size_t stride, const uint8_t* mask, uint32_t* out, size_t ostride,
+                size_t col, hipStream_t stream, size_t groups = 1);
+// out[e] = a[e] + b[e] for SoA point vectors of the same stride (out may alias a)
+void add_points(size_t count, const uint32_t* a, const uint32_t* b, size_t stride, uint32_t* out, hipStream_t stream);
+// Decision-matrix summaries for `groups` stacked ceremonies of n parties (dec [groups*n][n]):
+// row_reject[i] = any REJECT in row i; complaints[g][j] = REJECTs by receiver j in group g.
+void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
+                      hipStream_t stream);
 // hash_to_group tail: from_uniform_bytes(64 bytes as 16 LE words) -> SoA point (stride 1)
 void from_uniform(const uint32_t* in16, uint32_t* out, hipStream_t stream);
 
@@ -66,7 +74,12 @@ void to_position_major(size_t D, size_t N, size_t npad, const uint32_t* in, uint
 // Scalar reduction of 256-bit inputs to canonical (from_bits semantics, groups.rs:29-36).
 void reduce_scalars(size_t count, const uint32_t* in, uint32_t* out, hipStream_t stream);
 // Modular sum over dealers with mask: out[j] = sum_i mask[i] * s[i][j]  (round-3 final share)
-void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out,
-                hipStream_t stream);
+void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out, hipStream_t stream,
+                size_t groups = 1);
+// On-device synthetic coefficients (seedgen.hip): rows r in [0, rows) are dealer d0 + r % D of
+// ceremony c0 + r / D; a, b [rows][N][8] canonical, identical to the host dkg_dealer_coeffs.
+// master: 8 words on the device; seeds: scratch [rows][8].
+void dealer_coeffs(size_t rows, size_t D, size_t d0, uint32_t c0, const uint32_t* master, size_t N, uint32_t* seeds,
+                   uint32_t* a, uint32_t* b, hipStream_t stream);
 
 }  // namespace dkgk

@@ -136,13 +136,14 @@ void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* 
 }
 
 // ------------------------------------------------------------------ K1 share evaluation
-// Horner at x = j+1: identical field value to the power-sum of polynomial.rs:68-74.
-__global__ __launch_bounds__(256) void k_share_eval(size_t n, size_t N, const uint32_t* __restrict__ a,
+// Horner at x = j+1: identical field value to the power-sum of polynomial.rs:68-74.  One thread per
+// (dealer i, receiver j), flattened (the dealer count of a batch of ceremonies exceeds grid.y).
+__global__ __launch_bounds__(256) void k_share_eval(size_t D, size_t n, size_t N, const uint32_t* __restrict__ a,
                                                     const uint32_t* __restrict__ b, uint32_t* __restrict__ s,
                                                     uint32_t* __restrict__ sp) {
-  const size_t i = blockIdx.y;
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= D * n) return;
+  const size_t i = e / n, j = e % n;
   const uint32_t x = (uint32_t)(j + 1);
   const uint32_t* ai = a + 8 * i * N;
   const uint32_t* bi = b + 8 * i * N;
@@ -155,23 +156,23 @@ __global__ __launch_bounds__(256) void k_share_eval(size_t n, size_t N, const ui
     sc_load(c, bi + 8 * k);
     sc_mul_small_add(fb, fb, x, c);
   }
-  st_words8(s + 8 * (i * n + j), fa.v);
-  st_words8(sp + 8 * (i * n + j), fb.v);
+  st_words8(s + 8 * e, fa.v);
+  st_words8(sp + 8 * e, fb.v);
 }
 
 void share_eval(size_t D, size_t n, size_t N, const uint32_t* a, const uint32_t* b, uint32_t* s, uint32_t* sp,
                 hipStream_t stream) {
   if (!D || !n) return;
-  hipLaunchKernelGGL(k_share_eval, dim3((unsigned)((n + 255) / 256), (unsigned)D), dim3(256), 0, stream, n, N,
-                     a, b, s, sp);
+  hipLaunchKernelGGL(k_share_eval, dim3((unsigned)((D * n + 255) / 256)), dim3(256), 0, stream, D, n, N, a, b, s,
+                     sp);
 }
 
 __global__ __launch_bounds__(256) void k_poly_eval(size_t D, size_t N, const uint32_t* __restrict__ coeffs,
                                                    size_t M, const uint32_t* __restrict__ xs,
                                                    uint32_t* __restrict__ out) {
-  const size_t i = blockIdx.y;
-  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= D * M) return;
+  const size_t i = e / M, m = e % M;
   const uint32_t* ci = coeffs + 8 * i * N;
   sc f, c;
   sc_load(f, ci + 8 * (N - 1));
@@ -179,14 +180,14 @@ __global__ __launch_bounds__(256) void k_poly_eval(size_t D, size_t N, const uin
     sc_load(c, ci + 8 * k);
     sc_mul_small_add(f, f, xs[m], c);
   }
-  st_words8(out + 8 * (i * M + m), f.v);
+  st_words8(out + 8 * e, f.v);
 }
 
 void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint32_t* xs, uint32_t* out,
                hipStream_t stream) {
   if (!D || !M) return;
-  hipLaunchKernelGGL(k_poly_eval, dim3((unsigned)((M + 255) / 256), (unsigned)D), dim3(256), 0, stream, D, N,
-                     coeffs, M, xs, out);
+  hipLaunchKernelGGL(k_poly_eval, dim3((unsigned)((D * M + 255) / 256)), dim3(256), 0, stream, D, N, coeffs, M, xs,
+                     out);
 }
 
 // ------------------------------------------------------------------ K3a binomial-basis Horner
@@ -458,7 +459,8 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
 }
 
 // ------------------------------------------------------------------ K3c check
-__global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round,
+__global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base,
+                                                uint32_t nmod, int round,
                                                 const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
                                                 const uint32_t* __restrict__ R, size_t rstride,
                                                 const uint32_t* __restrict__ tab_g,
@@ -484,19 +486,19 @@ __global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, s
     pt_load(r, R, rstride, p);
     const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
     uint8_t v = (dok[i] && eq) ? 1 : 0;
-    if (i + dealer_base == j + recv_base) v = 2;
+    if ((uint32_t)((i + dealer_base) % nmod) == (uint32_t)(j + recv_base)) v = 2;  // self (batched: per ceremony)
     dec[p] = v;
   }
 }
 
-void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, int round, const uint32_t* s,
-           const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
-           const uint8_t* dok, uint8_t* dec, hipStream_t stream) {
+void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
+           const uint32_t* s, const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g,
+           const uint32_t* tab_h, const uint8_t* dok, uint8_t* dec, hipStream_t stream) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
   const size_t lds = (round == 2 ? 2 : 1) * COMB_WORDS * 4;
   hipLaunchKernelGGL(k_check, dim3(comb_grid(total, 1024)), dim3(1024), lds, stream, ndealers, nrecv, dealer_base,
-                     recv_base, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
+                     recv_base, (uint32_t)nmod, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
 }
 
 __global__ void k_dealer_ok(size_t ndealers, size_t N, const uint8_t* __restrict__ pok, uint8_t* __restrict__ ok) {
@@ -541,14 +543,16 @@ void horner(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t 
                      C, x0, nrecv, R);
 }
 
-// Sum of the masked points of an SoA vector (one workgroup, tree reduction): out = sum mask[e] P_e.
+// Sums of the masked points of an SoA vector, one workgroup (tree reduction) per group g:
+// out column col + g = sum over e in [g*count, (g+1)*count) of mask[e] P_e.
 __global__ __launch_bounds__(256) void k_sum_points(size_t count, const uint32_t* __restrict__ pts, size_t stride,
                                                     const uint8_t* __restrict__ mask, uint32_t* __restrict__ out,
                                                     size_t ostride, size_t col) {
   __shared__ uint32_t red[256][PT_WORDS];
   ge_p3 acc;
   ge_identity(acc);
-  for (size_t e = threadIdx.x; e < count; e += blockDim.x) {
+  const size_t g = blockIdx.x;
+  for (size_t e = g * count + threadIdx.x; e < (g + 1) * count; e += blockDim.x) {
     if (mask && !mask[e]) continue;
     ge_p3 p;
     pt_load(p, pts, stride, e);
@@ -576,12 +580,36 @@ __global__ __launch_bounds__(256) void k_sum_points(size_t count, const uint32_t
     __syncthreads();
   }
   if (threadIdx.x == 0)
-    for (int w = 0; w < PT_WORDS; w++) out[w * ostride + col] = red[0][w];
+    for (int w = 0; w < PT_WORDS; w++) out[w * ostride + col + g] = red[0][w];
 }
 
 void sum_points(size_t count, const uint32_t* pts, size_t stride, const uint8_t* mask, uint32_t* out,
-                size_t ostride, size_t col, hipStream_t stream) {
-  hipLaunchKernelGGL(k_sum_points, dim3(1), dim3(256), 0, stream, count, pts, stride, mask, out, ostride, col);
+                size_t ostride, size_t col, hipStream_t stream, size_t groups) {
+  if (!groups) return;
+  hipLaunchKernelGGL(k_sum_points, dim3((unsigned)groups), dim3(256), 0, stream, count, pts, stride, mask, out,
+                     ostride, col);
+}
+
+// out[e] = a[e] + b[e] (SoA points, same stride), e < count.
+__global__ __launch_bounds__(256) void k_add_points(size_t count, const uint32_t* __restrict__ a,
+                                                    const uint32_t* __restrict__ b, size_t stride,
+                                                    uint32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  ge_p3 x, y;
+  pt_load(x, a, stride, e);
+  pt_load(y, b, stride, e);
+  ge_cached yc;
+  ge_to_cached(yc, y);
+  ge_add(x, x, yc);
+  pt_store(out, stride, e, x);
+}
+
+void add_points(size_t count, const uint32_t* a, const uint32_t* b, size_t stride, uint32_t* out,
+                hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_add_points, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, a, b, stride,
+                     out);
 }
 
 // RistrettoPoint::from_uniform_bytes of 64 hash bytes (hash_to_group, groups.rs:68-70) -> SoA point.
@@ -729,10 +757,15 @@ void reduce_scalars(size_t count, const uint32_t* in, uint32_t* out, hipStream_t
   hipLaunchKernelGGL(k_reduce_scalars, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, in, out);
 }
 
+// Group g (blockIdx.y) of D dealers: out[g][j] = sum over dealers i of group g with mask of s[g][i][j].
 __global__ void k_sum_shares(size_t D, size_t n, const uint32_t* __restrict__ s, const uint8_t* __restrict__ mask,
                              uint32_t* __restrict__ out) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
+  const size_t g = blockIdx.y;
+  s += g * D * n * 8;
+  mask += g * D;
+  out += g * n * 8;
   sc acc, x;
   sc_zero(acc);
   for (size_t i = 0; i < D; i++) {
@@ -743,9 +776,46 @@ __global__ void k_sum_shares(size_t D, size_t n, const uint32_t* __restrict__ s,
   st_words8(out + 8 * j, acc.v);
 }
 
-void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out, hipStream_t stream) {
+void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out, hipStream_t stream,
+                size_t groups) {
   if (!n) return;
-  hipLaunchKernelGGL(k_sum_shares, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, D, n, s, mask, out);
+  for (size_t g0 = 0; g0 < groups; g0 += 65535) {  // grid.y limit
+    const size_t gc = groups - g0 < 65535 ? groups - g0 : 65535;
+    hipLaunchKernelGGL(k_sum_shares, dim3((unsigned)((n + 255) / 256), (unsigned)gc), dim3(256), 0, stream, D, n,
+                       s + g0 * D * n * 8, mask + g0 * D, out + g0 * n * 8);
+  }
+}
+
+// Row / column summaries of a decision matrix [rows][n] (rows = groups x n dealers of batched
+// ceremonies): row_reject[i] = some receiver rejected dealer i; complaints[g][j] = number of
+// dealers of group g rejected by receiver j (committee.rs:311-316, 340-347).
+__global__ void k_row_reject(size_t rows, size_t n, const uint8_t* __restrict__ dec, uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  uint8_t r = 0;
+  for (size_t j = 0; j < n; j++) r |= dec[i * n + j] == 0;
+  out[i] = r;
+}
+
+__global__ void k_col_complaints(size_t groups, size_t n, const uint8_t* __restrict__ dec, int32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = g * n + j
+  if (e >= groups * n) return;
+  const size_t g = e / n, j = e % n;
+  int32_t c = 0;
+  for (size_t i = 0; i < n; i++) c += dec[(g * n + i) * n + j] == 0;
+  out[e] = c;
+}
+
+void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
+                      hipStream_t stream) {
+  const size_t rows = groups * n;
+  if (!rows) return;
+  if (row_reject)
+    hipLaunchKernelGGL(k_row_reject, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, rows, n, dec,
+                       row_reject);
+  if (complaints)
+    hipLaunchKernelGGL(k_col_complaints, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, groups, n, dec,
+                       complaints);
 }
 
 }  // namespace dkgk

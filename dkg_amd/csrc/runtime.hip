@@ -195,7 +195,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       if (a >= b) continue;
       const VerifySeg& g = segs[k];
       const size_t l0 = a - v0[k];
-      dkgk::check(b - a, n, g.dealer_base + l0, 0, g.round, g.s + l0 * n * 8,
+      dkgk::check(b - a, n, g.dealer_base + l0, 0, n, g.round, g.s + l0 * n * 8,
                   g.round == 2 ? g.sp + l0 * n * 8 : nullptr, R + a * n, rstride, ctx->tab_g, ctx->tab_h, dok + a,
                   g.dec + l0 * n, st);
     }
@@ -272,6 +272,38 @@ double ev_ms(dkg_ctx* ctx, int a, int b) {
   return ms;
 }
 
+// Lagrange reconstruction (polynomial.rs:172-184 at 0; the reference interpolates the disclosed
+// shares, committee.rs:748-789) of the secret of every dealer i with recon[i], from the shares of
+// the first t+1 parties outside the reconstructable set.  hs: the ceremony's shares [n][n][32].
+std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, const uint8_t* hs) {
+  std::vector<size_t> xs;
+  for (size_t j = 0; j < n && xs.size() < t + 1; j++)
+    if (!recon[j]) xs.push_back(j);
+  std::vector<dkgh::Zl> lambda(xs.size());
+  for (size_t a = 0; a < xs.size(); a++) {
+    dkgh::Zl num = dkgh::zl_from_u64(1), den = dkgh::zl_from_u64(1);
+    for (size_t b = 0; b < xs.size(); b++) {
+      if (a == b) continue;
+      num = dkgh::zl_mul(num, dkgh::zl_sub(dkgh::zl_from_u64(0), dkgh::zl_from_u64(xs[b] + 1)));
+      den = dkgh::zl_mul(den, dkgh::zl_sub(dkgh::zl_from_u64(xs[a] + 1), dkgh::zl_from_u64(xs[b] + 1)));
+    }
+    lambda[a] = dkgh::zl_mul(num, dkgh::zl_inv(den));
+  }
+  std::vector<uint8_t> secrets;
+  for (size_t i = 0; i < n; i++) {
+    if (!recon[i]) continue;
+    dkgh::Zl acc = dkgh::zl_from_u64(0);
+    for (size_t a = 0; a < xs.size(); a++) {
+      dkgh::Zl y = dkgh::zl_from_bytes_wide(&hs[32 * (i * n + xs[a])], 32);
+      acc = dkgh::zl_add(acc, dkgh::zl_mul(lambda[a], y));
+    }
+    uint8_t b[32];
+    dkgh::zl_to_bytes(b, acc);
+    secrets.insert(secrets.end(), b, b + 32);
+  }
+  return secrets;
+}
+
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
 void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
                       const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big) {
@@ -331,36 +363,10 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   uint32_t* parts = buf<uint32_t>(ctx, "mpk_parts", PTB * 2);
   dkgk::sum_points(n, A0, n, hmask, parts, 2, 0, ctx->stream);
   if (nrecon) {
-    // Lagrange reconstruction from t+1 shares of parties outside the reconstructable set
-    // (polynomial.rs:172-184 at 0; the reference interpolates the disclosed shares, :748-789).
-    std::vector<size_t> xs;
-    for (size_t j = 0; j < n && xs.size() < t + 1; j++)
-      if (!recon[j]) xs.push_back(j);
-    std::vector<dkgh::Zl> lambda(xs.size());
-    for (size_t a = 0; a < xs.size(); a++) {
-      dkgh::Zl num = dkgh::zl_from_u64(1), den = dkgh::zl_from_u64(1);
-      for (size_t b = 0; b < xs.size(); b++) {
-        if (a == b) continue;
-        num = dkgh::zl_mul(num, dkgh::zl_sub(dkgh::zl_from_u64(0), dkgh::zl_from_u64(xs[b] + 1)));
-        den = dkgh::zl_mul(den, dkgh::zl_sub(dkgh::zl_from_u64(xs[a] + 1), dkgh::zl_from_u64(xs[b] + 1)));
-      }
-      lambda[a] = dkgh::zl_mul(num, dkgh::zl_inv(den));
-    }
     std::vector<uint8_t> hs(32 * n * n);
     d2h(ctx, hs.data(), s, 32 * n * n);
     sync(ctx);
-    std::vector<uint8_t> secrets;
-    for (size_t i = 0; i < n; i++) {
-      if (!recon[i]) continue;
-      dkgh::Zl acc = dkgh::zl_from_u64(0);
-      for (size_t a = 0; a < xs.size(); a++) {
-        dkgh::Zl y = dkgh::zl_from_bytes_wide(&hs[32 * (i * n + xs[a])], 32);
-        acc = dkgh::zl_add(acc, dkgh::zl_mul(lambda[a], y));
-      }
-      uint8_t b[32];
-      dkgh::zl_to_bytes(b, acc);
-      secrets.insert(secrets.end(), b, b + 32);
-    }
+    std::vector<uint8_t> secrets = lagrange_secrets(n, t, recon.data(), hs.data());
     uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
     h2d(ctx, sec, secrets.data(), secrets.size());
     uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
@@ -404,6 +410,127 @@ void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a
   dkgk::encode_points(Aext, D * N, D * N, Acomp, ctx->stream);
   dkgk::share_eval(D, n, N, a, b, s, sp, ctx->stream);                            // K1 (:164-167)
   check_launch(ctx);
+}
+
+// ---- batches of independent ceremonies (BASELINE config 5: many small key ceremonies)
+// B ceremonies of n parties are stacked dealer-wise: dealer c*n + i is party i of ceremony c, and
+// its share row addresses that ceremony's n receivers.  The verification pipeline is the same as
+// for one ceremony (2*B*n virtual dealers in the fused pipeline); the per-ceremony combine steps
+// (qualification, complaints, round-3 sums, mpk) are grouped kernels.  Every output equals what B
+// separate ceremonies produce.
+void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
+                     const uint32_t* s, const uint32_t* sp, dkg_batch_out* out) {
+  const size_t N = t + 1, V = B * n;
+  uint8_t* dec2 = buf<uint8_t>(ctx, "b.dec2", V * n);
+  uint8_t* dec4 = buf<uint8_t>(ctx, "b.dec4", V * n);
+  uint8_t* rej = buf<uint8_t>(ctx, "b.rej", V);
+  int32_t* cnt = buf<int32_t>(ctx, "b.cnt", 4 * V);
+  uint8_t* qmask = buf<uint8_t>(ctx, "b.qmask", V);
+  uint32_t* fs = buf<uint32_t>(ctx, "b.final", 32 * V);
+  uint32_t* pub = buf<uint32_t>(ctx, "b.pub_ext", PTB * V);
+  uint32_t* pubc = buf<uint32_t>(ctx, "b.pub_comp", 32 * V);
+  std::vector<uint8_t> qualified(V), r2err(V), recon(V, 0), honest(V);
+  std::vector<int32_t> complaints(V);
+  auto round3 = [&] {
+    // round-2 outcome per ceremony (committee.rs:311-316, 340-347, 370-398)
+    dkgk::decision_summary(B, n, dec2, rej, cnt, ctx->stream);
+    d2h(ctx, qualified.data(), rej, V);
+    d2h(ctx, complaints.data(), cnt, 4 * V);
+    sync(ctx);
+    for (size_t i = 0; i < V; i++) {
+      qualified[i] = !qualified[i];
+      r2err[i] = complaints[i] > (int32_t)t;
+    }
+    // round 3 (committee.rs:433-476) per ceremony
+    h2d(ctx, qmask, qualified.data(), V);
+    dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
+    dkgk::fixed_base(V, fs, ctx->tab_g, pub, ctx->stream);
+    dkgk::encode_points(pub, V, V, pubc, ctx->stream);
+    HCK(hipEventRecord(ctx->ev[3], ctx->stream));
+  };
+  verify_rounds(ctx, n, t, V, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3);
+  // round-4 outcome: a qualified dealer rejected by someone is reconstructed (committee.rs:660-670)
+  std::vector<uint8_t> rej4(V);
+  dkgk::decision_summary(B, n, dec4, rej, nullptr, ctx->stream);
+  d2h(ctx, rej4.data(), rej, V);
+  HCK(hipEventRecord(ctx->ev[4], ctx->stream));
+  sync(ctx);
+  std::vector<size_t> recon_cer;
+  for (size_t c = 0; c < B; c++) {
+    bool any = false;
+    for (size_t i = c * n; i < (c + 1) * n; i++) {
+      recon[i] = qualified[i] && rej4[i];
+      honest[i] = qualified[i] && !recon[i];
+      any |= recon[i] != 0;
+    }
+    if (any) recon_cer.push_back(c);
+  }
+  // finalise (committee.rs:726-805): mpk_c = sum of honest A_i0 (+ g * reconstructed secrets)
+  uint32_t* A0c = buf<uint32_t>(ctx, "b.A0c", 32 * V);
+  HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, V, hipMemcpyDeviceToDevice, ctx->stream));
+  uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
+  uint8_t* a0ok = buf<uint8_t>(ctx, "b.A0ok", V);
+  dkgk::decode_points(A0c, V, A0, V, a0ok, ctx->stream);
+  uint8_t* hmask = buf<uint8_t>(ctx, "b.hmask", V);
+  h2d(ctx, hmask, honest.data(), V);
+  uint32_t* mpk_ext = buf<uint32_t>(ctx, "b.mpk_ext", PTB * B);
+  dkgk::sum_points(n, A0, V, hmask, mpk_ext, B, 0, ctx->stream, B);
+  if (!recon_cer.empty()) {
+    uint32_t* extra = buf<uint32_t>(ctx, "b.mpk_extra", PTB * B);
+    std::vector<uint8_t> hs(32 * n * n);
+    for (size_t c : recon_cer) {
+      d2h(ctx, hs.data(), s + c * n * n * 8, 32 * n * n);
+      sync(ctx);
+      std::vector<uint8_t> secrets = lagrange_secrets(n, t, &recon[c * n], hs.data());
+      const size_t nr = secrets.size() / 32;
+      uint32_t* sec = buf<uint32_t>(ctx, "b.recon_sec", 32 * nr);
+      h2d(ctx, sec, secrets.data(), secrets.size());
+      uint32_t* gsec = buf<uint32_t>(ctx, "b.recon_ext", PTB * nr);
+      dkgk::fixed_base(nr, sec, ctx->tab_g, gsec, ctx->stream);
+      dkgk::sum_points(nr, gsec, nr, nullptr, extra, B, c, ctx->stream);
+      dkgk::add_points(1, mpk_ext + c, extra + c, B, mpk_ext + c, ctx->stream);
+      sync(ctx);  // sec / gsec are reused by the next ceremony
+    }
+  }
+  uint32_t* mpk_c = buf<uint32_t>(ctx, "b.mpk_comp", 32 * B);
+  dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
+  check_launch(ctx);
+  if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
+  if (out->final_share) d2h(ctx, out->final_share, fs, 32 * V);
+  if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * V);
+  std::vector<uint8_t> h4;
+  if (out->dec2) d2h(ctx, out->dec2, dec2, V * n);
+  if (out->dec4) {
+    h4.resize(V * n);
+    d2h(ctx, h4.data(), dec4, V * n);
+  }
+  HCK(hipEventRecord(ctx->ev[5], ctx->stream));
+  sync(ctx);
+  if (out->dec4) {
+    for (size_t i = 0; i < V; i++)
+      if (!qualified[i])
+        for (size_t j = 0; j < n; j++)
+          if (j != i % n) h4[i * n + j] = DKG_SKIPPED;  // committee.rs:522
+    memcpy(out->dec4, h4.data(), V * n);
+  }
+  if (out->qualified) memcpy(out->qualified, qualified.data(), V);
+  if (out->r2_error) memcpy(out->r2_error, r2err.data(), V);
+  if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * V);
+  if (out->reconstruct) memcpy(out->reconstruct, recon.data(), V);
+  if (out->n_qualified)
+    for (size_t c = 0; c < B; c++) {
+      int32_t q = 0;
+      for (size_t i = c * n; i < (c + 1) * n; i++) q += qualified[i];
+      out->n_qualified[c] = q;
+    }
+}
+
+void batch_times(dkg_ctx* ctx, dkg_batch_out* out, bool round1) {
+  out->ms_round1 = round1 ? ev_ms(ctx, 0, 1) : 0.0;
+  out->ms_checks = ev_ms(ctx, 1, 2);
+  out->ms_round3 = ev_ms(ctx, 2, 3);
+  out->ms_finalise = ev_ms(ctx, 3, 5);
+  out->ms_total = ev_ms(ctx, 0, 5);
 }
 
 int need_env(dkg_ctx* ctx) {
@@ -692,7 +819,7 @@ int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, c
     uint32_t* ds = upload_scalars(ctx, "vr_s", s, n);
     uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vr_sp", s_prime, n) : nullptr;
     uint8_t* dec = buf<uint8_t>(ctx, "vr_dec", n);
-    dkgk::check(n, 1, 0, j, round, ds, dsp, R, n, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
+    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, n, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
     check_launch(ctx);
     d2h(ctx, decision, dec, n);
     sync(ctx);
@@ -854,6 +981,65 @@ int dkg_point_sum_device(dkg_ctx* ctx, size_t count, const void* d_points, const
         ctx->err = "point_sum: a selected point does not decode";
         return DKG_E_DECODE;
       }
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_batch_device(dkg_ctx* ctx, size_t B, size_t n, size_t t, const void* d_a, const void* d_b,
+                              dkg_batch_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out) return DKG_E_ARG;
+    if (B == 0) return DKG_OK;
+    const size_t N = t + 1, V = B * n;
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    uint32_t* Ec = buf<uint32_t>(ctx, "bat_E", 32 * V * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "bat_A", 32 * V * N);
+    uint32_t* ds = buf<uint32_t>(ctx, "bat_s", 32 * V * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "bat_sp", 32 * V * n);
+    round1_device(ctx, V, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    batch_receivers(ctx, B, n, t, Ec, Ac, ds, dsp, out);
+    batch_times(ctx, out, true);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_batch_verify(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint8_t* E, const uint8_t* A,
+                              const uint8_t* s, const uint8_t* s_prime, dkg_batch_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out || !E || !A || !s || !s_prime) return DKG_E_ARG;
+    if (B == 0) return DKG_OK;
+    const size_t N = t + 1, V = B * n;
+    uint32_t* Ec = buf<uint32_t>(ctx, "bat_E", 32 * V * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "bat_A", 32 * V * N);
+    h2d(ctx, Ec, E, 32 * V * N);
+    h2d(ctx, Ac, A, 32 * V * N);
+    uint32_t* ds = upload_scalars(ctx, "bat_s", s, V * n);
+    uint32_t* dsp = upload_scalars(ctx, "bat_sp", s_prime, V * n);
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    batch_receivers(ctx, B, n, t, Ec, Ac, ds, dsp, out);
+    batch_times(ctx, out, false);
+    return DKG_OK;
+  });
+}
+
+int dkg_dealer_coeffs_device(dkg_ctx* ctx, const uint8_t master[32], uint32_t ceremony0, size_t B, size_t d0,
+                             size_t D, size_t t, void* d_a, void* d_b) {
+  return guarded(ctx, [&] {
+    if (!master || !d_a || !d_b) return DKG_E_ARG;
+    const size_t rows = B * D;
+    if (!rows) return DKG_OK;
+    uint32_t* m = buf<uint32_t>(ctx, "sg_master", 32);
+    uint32_t* seeds = buf<uint32_t>(ctx, "sg_seeds", 32 * rows);
+    h2d(ctx, m, master, 32);
+    dkgk::dealer_coeffs(rows, D, d0, ceremony0, m, t + 1, seeds, (uint32_t*)d_a, (uint32_t*)d_b, ctx->stream);
+    check_launch(ctx);
+    sync(ctx);
     return DKG_OK;
   });
 }

@@ -150,6 +150,35 @@ int dkg_scalar_sum_device(dkg_ctx *ctx, size_t rows, size_t n, const void *d_in,
  * [count][32] compressed, out [32] compressed.  DKG_E_DECODE if a selected point does not decode. */
 int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const void *d_mask, void *d_out);
 
+/* ---- batches of independent ceremonies (BASELINE config 5: e.g. 10,000 ceremonies of n = 64) ----
+ * B ceremonies with the same (n, t) and commitment key, each played as dkg_ceremony_run plays one
+ * (full_valid_run, committee.rs:1518-1656): rounds 1-5 for every party of every ceremony.
+ * Ceremony c's dealers are rows c*n .. c*n + n-1 of every [B*n]-row array; every output equals
+ * what B separate single-ceremony calls return (the work of all B shares each kernel launch). */
+typedef struct {
+  /* host outputs; any pointer may be NULL */
+  uint8_t *mpk;                 /* [B][32] MasterPublicKey per ceremony (committee.rs:726-805) */
+  int32_t *n_qualified;         /* [B] */
+  uint8_t *qualified;           /* [B][n] */
+  uint8_t *r2_error;            /* [B][n] receiver saw more than t complaints */
+  int32_t *complaints2;         /* [B][n] complaints raised by each receiver in round 2 */
+  uint8_t *reconstruct;         /* [B][n] */
+  uint8_t *final_share;         /* [B][n][32] */
+  uint8_t *public_share;        /* [B][n][32] */
+  uint8_t *dec2, *dec4;         /* [B][n dealer][n receiver] decision matrices (dec4 with SKIPPED) */
+  /* device times, milliseconds (HIP events): round 1, the fused round-2/4 checks, round 3,
+   * finalise (mpk incl. the round-4 combine), total */
+  double ms_round1, ms_checks, ms_round3, ms_finalise, ms_total;
+} dkg_batch_out;
+
+/* Honest batch from device-resident coefficients d_a, d_b [B*n][t+1][32] (canonical scalars). */
+int dkg_ceremony_batch_device(dkg_ctx *ctx, size_t B, size_t n, size_t t, const void *d_a, const void *d_b,
+                              dkg_batch_out *out);
+/* Receiver side of a batch from host broadcast values that may have been tampered with:
+ * E, A [B*n][t+1][32]; s, s_prime [B*n][n][32] (row c*n + i = dealer i of ceremony c). */
+int dkg_ceremony_batch_verify(dkg_ctx *ctx, size_t B, size_t n, size_t t, const uint8_t *E, const uint8_t *A,
+                              const uint8_t *s, const uint8_t *s_prime, dkg_batch_out *out);
+
 /* ---- synthetic inputs: the seeded RNG convention ----
  * dealer seed = BLAKE2b-256("dkg-amd/v1/dealer" || master[32] || u32le ceremony || u32le dealer);
  * coefficients = ChaCha20Rng(seed): hiding b_0..b_t first, then sharing a_0..a_t (committee.rs:143-146),
@@ -157,6 +186,12 @@ int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const
  * dealers [d0, d0+D). */
 int dkg_dealer_coeffs(const uint8_t master[32], uint32_t ceremony, size_t d0, size_t D, size_t t, uint8_t *a,
                       uint8_t *b);
+/* The same convention on the GPU, for B ceremonies at once: row r in [0, B*D)
+ * holds dealer d0 + r % D of ceremony ceremony0 + r / D; d_a, d_b are device buffers
+ * [B*D][t+1][32].  Bit-identical to dkg_dealer_coeffs; keeps n = 4096 or 10,000-ceremony inputs
+ * off the PCIe bus. */
+int dkg_dealer_coeffs_device(dkg_ctx *ctx, const uint8_t master[32], uint32_t ceremony0, size_t B, size_t d0,
+                             size_t D, size_t t, void *d_a, void *d_b);
 
 #ifdef __cplusplus
 }

@@ -357,3 +357,83 @@ def test_sharded_ceremony_matches_golden(be, golden, name, ws):
     mpk = torch.empty(32, dtype=torch.uint8, device=dev)
     be.point_sum_device(n, gA0.data_ptr(), mask.data_ptr(), mpk.data_ptr())
     assert bytes(mpk.cpu().numpy()).hex() == c["mpk"]
+
+
+def _check_batch_member(c, d, n):
+    """One ceremony of a BatchResult against its golden file (same fields as _check_ceremony)."""
+    assert dec_str(d["dec2"]) == c["dec2"]
+    assert dec_str(d["dec4"]) == c["dec4"]
+    assert d["qualified"] == c["qualified"]
+    assert d["r2_error"] == [int(x) for x in c["r2_error"]]
+    assert d["complaints2"] == c["complaints2"]
+    assert d["reconstruct"] == c["reconstruct"]
+    assert d["final_share"].hex() == c["final_share"]
+    assert d["public_share"].hex() == c["public_share"]
+    assert d["mpk"].hex() == c["mpk"]
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_batch_verify_goldens(be, golden, overlap):
+    """BASELINE config 5 path: five n=10, t=4 ceremonies (one honest, four with the fault injections
+    of committee.rs:1105-1313) verified as ONE batch give each golden ceremony's outputs bit for bit."""
+    names = ["ceremony_n10_t4.json"] + FAULTS
+    cs = [golden(x) for x in names]
+    n, t = 10, 4
+    assert all((c["n"], c["t"]) == (n, t) for c in cs)
+    be.env_init(t, n, CK)
+    E = b"".join(H(c["E"]) for c in cs)
+    A = b"".join(H(c["A"]) for c in cs)
+    s = b"".join(H(c["s"]) for c in cs)
+    sp = b"".join(H(c["s_prime"]) for c in cs)
+    be.set_overlap(overlap)
+    try:
+        r = dkg_amd.ceremony_batch_verify(be, len(cs), n, t, E, A, s, sp)
+    finally:
+        be.set_overlap(True)
+    for k, c in enumerate(cs):
+        _check_batch_member(c, r.ceremony(k), n)
+
+
+def test_batch_device_matches_single(be, golden):
+    """Honest batch from device coefficients (dkg_ceremony_batch_device) = the golden n=16 ceremony
+    plus independent ceremonies each re-run alone through dkg_ceremony_run."""
+    import torch
+
+    c0 = golden("ceremony_n16_t7.json")
+    n, t = c0["n"], c0["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    seeds = [(H(c0["master_seed"]), c0["ceremony"])] + [(bytes([7 + k]) * 32, 100 + k) for k in range(4)]
+    coeffs = [dkg_amd.dealer_coefficients(m, cid, 0, n, t) for m, cid in seeds]
+    dev = torch.device("cuda", 0)
+    ta = torch.frombuffer(bytearray(b"".join(a for a, _ in coeffs)), dtype=torch.uint8).to(dev)
+    tb = torch.frombuffer(bytearray(b"".join(b for _, b in coeffs)), dtype=torch.uint8).to(dev)
+    r = dkg_amd.ceremony_batch_device(be, len(seeds), n, t, ta.data_ptr(), tb.data_ptr(), big=True)
+    _check_batch_member(c0, r.ceremony(0), n)
+    for k, (a, b) in enumerate(coeffs[1:], start=1):
+        single = be.ceremony(a, b, n, t)
+        d = r.ceremony(k)
+        assert d["mpk"] == single.mpk and d["final_share"] == single.final_share
+        assert d["public_share"] == single.public_share and d["dec2"] == single.dec2 and d["dec4"] == single.dec4
+        assert d["qualified"] == single.qualified and d["n_qualified"] == n
+        secret = sum(int.from_bytes(a[32 * N * i:32 * N * i + 32], "little") for i in range(n)) % L
+        assert d["mpk"] == O.base_mul(secret.to_bytes(32, "little"))
+    assert r.ms["total"] > 0
+
+
+@pytest.mark.parametrize("c0,B,d0,D,t", [(0, 1, 0, 10, 4), (5, 3, 2, 7, 31), (9, 2, 0, 3, 0), (1, 1, 100, 5, 511)])
+def test_dealer_coefficients_device(be, c0, B, d0, D, t):
+    """On-device seeded coefficients are bit-identical to the host convention."""
+    import torch
+
+    N = t + 1
+    master = bytes(range(32))
+    dev = torch.device("cuda", 0)
+    ta = torch.zeros(B * D * N * 32, dtype=torch.uint8, device=dev)
+    tb = torch.zeros_like(ta)
+    be.dealer_coefficients_device(master, c0, B, d0, D, t, ta.data_ptr(), tb.data_ptr())
+    ga, gb = bytes(ta.cpu().numpy()), bytes(tb.cpu().numpy())
+    for c in range(B):
+        a, b = dkg_amd.dealer_coefficients(master, c0 + c, d0, D, t)
+        assert ga[32 * N * D * c:32 * N * D * (c + 1)] == a
+        assert gb[32 * N * D * c:32 * N * D * (c + 1)] == b
