@@ -10,6 +10,12 @@ namespace dkgk {
 // K5: 32-byte encodings [count][8 words] -> extended SoA [40][stride]; ok[e] = 1 if valid.
 void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t stride, uint8_t* ok,
                    hipStream_t stream);
+// K5 straight into the binomial's position-major layout: D dealers x N commitments ([D][N][8],
+// dealer-major) -> [40][N][npad] at out (pass table + first dealer column); ok [D*N] dealer-major.
+void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
+                           hipStream_t stream);
+// identity points in dealer columns [V, npad) of a position-major table [40][N][npad]
+void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream);
 // extended SoA -> encodings [count][8]
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream);
 // comb table of the decoded point ext[.., e0] into tab (30 x 512 words)

@@ -14,9 +14,13 @@ namespace dkgk {
 constexpr int COMB_WORDS = AFF_WORDS * COMB_ENTRIES;  // 15360 words = 61440 B per base
 
 // ------------------------------------------------------------------ K5 decode / encode
+// pm_N != 0: element e = i * pm_N + k (dealer-major input) is stored at k * pm_npad + i, i.e.
+// straight into the position-major layout of the binomial (the decode is compute-bound, so the
+// scattered 40 stores per point cost nothing next to its exponentiation, and no transpose pass or
+// second copy of the points is needed).
 __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ comp, size_t count,
                                                 uint32_t* __restrict__ ext, size_t stride,
-                                                uint8_t* __restrict__ ok) {
+                                                uint8_t* __restrict__ ok, size_t pm_N, size_t pm_npad) {
   size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
   uint32_t w[8];
@@ -24,8 +28,20 @@ __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ com
   ge_p3 p;
   bool v = ristretto_decode(p, w);
   if (!v) ge_identity(p);
-  pt_store(ext, stride, e, p);
+  const size_t idx = pm_N ? (e % pm_N) * pm_npad + e / pm_N : e;
+  pt_store(ext, stride, idx, p);
   ok[e] = v ? 1 : 0;
+}
+
+// Identity points in dealer columns [V, npad) of a position-major table [40][N][npad].
+__global__ void k_fill_identity(size_t N, size_t npad, size_t V, uint32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = k * (npad - V) + c
+  const size_t w = npad - V;
+  if (e >= N * w) return;
+  const size_t k = e / w, c = e % w;
+  ge_p3 id;
+  ge_identity(id);
+  pt_store(out, N * npad, k * npad + V + c, id);
 }
 
 __global__ __launch_bounds__(256) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
@@ -43,7 +59,21 @@ void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t str
                    hipStream_t stream) {
   if (!count) return;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count,
-                     ext, stride, ok);
+                     ext, stride, ok, (size_t)0, (size_t)0);
+}
+
+void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
+                           hipStream_t stream) {
+  const size_t count = D * N;
+  if (!count) return;
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count, out,
+                     N * npad, ok, N, npad);
+}
+
+void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream) {
+  const size_t tot = N * (npad - V);
+  if (!tot) return;
+  hipLaunchKernelGGL(k_fill_identity, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, N, npad, V, out);
 }
 
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream) {
@@ -384,41 +414,49 @@ __device__ __forceinline__ void cached_identity(ge_cached& c) {
   fe_zero(c.T2d);
 }
 
-template <int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_stepping(size_t npad, size_t N, const uint32_t* __restrict__ e,
-                                                                size_t nrecv, size_t pos0,
-                                                                const uint32_t* __restrict__ up,   // NULL: top block
-                                                                uint32_t* __restrict__ down,       // NULL: block 0
-                                                                uint32_t* __restrict__ R, size_t rstride) {
-  // Lane l's cached value sits in LDS column l (word k at col[k * BS]); lane l adds column l + 1.
-  // Column 0 is never read inside the block (lane 0's value leaves through `down`), so the top lane
-  // parks the upstream value there: lane l reads column (l + 1) mod blockDim.  160 B per lane, and
-  // the addend never occupies VGPRs.
-  __shared__ uint32_t cols[PT_WORDS * BS];
-  const size_t d = blockIdx.x;
+// One launch covers position block [pos0, pos0 + P) of every dealer.  Lanes are cut into segments
+// of P lanes, one dealer each (P = N when the whole table fits one block: a t = 31 table packs 8
+// dealers into a 256-lane workgroup instead of idling half of a 64-lane one).
+template <int MAXBS>
+__global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_stepping(
+    size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ e, size_t nrecv, size_t pos0, int P,
+    const uint32_t* __restrict__ up,  // NULL: top block
+    uint32_t* __restrict__ down,      // NULL: block 0
+    uint32_t* __restrict__ R, size_t rstride) {
+  // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
+  // segment position q adds column q + 1 of its segment.  Column q = 0 is never read inside a
+  // segment (its value leaves through `down` / R), so the segment's top lane parks the upstream
+  // value there: position q reads segment column (q + 1) mod P.  160 B of LDS per lane (a
+  // compile-time stride keeps the address arithmetic out of the VGPR budget); the addend never
+  // occupies VGPRs.
+  __shared__ uint32_t cols[PT_WORDS * MAXBS];
   const int l = threadIdx.x, bs = blockDim.x;
+  const int seg = l / P, q = l - seg * P;
+  const size_t d = (size_t)blockIdx.x * (bs / P) + seg;
+  const bool live = seg < bs / P && d < ndealers;
   const size_t S = N * npad;
-  const size_t pos = pos0 + l;
+  const size_t pos = pos0 + q;
   ge_p3 D;
-  if (pos < N) pt_load(D, e, S, pos * npad + d);
+  if (live && pos < N) pt_load(D, e, S, pos * npad + d);
   else ge_identity(D);
-  const bool top_lane = (l == bs - 1);
-  const uint4* upd = up ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
-  uint4* downd = down ? reinterpret_cast<uint4*>(down + d * nrecv * PT_WORDS) : nullptr;
+  const bool top_lane = live && (q == P - 1);
+  const uint4* upd = (up && live) ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
+  uint4* downd = (down && live) ? reinterpret_cast<uint4*>(down + d * nrecv * PT_WORDS) : nullptr;
   uint32_t* mine = cols + l;
-  const uint32_t* nbr = cols + ((l + 1) % bs);
+  uint32_t* base = cols + seg * P;
+  const uint32_t* nbr = base + ((q + 1) % P);
   for (size_t j = 0; j < nrecv; j++) {
     {
       ge_cached c0;
       ge_to_cached(c0, D);
-      if (l == 0) {
+      if (q == 0) {
         if (downd) {
           const uint4* w4 = reinterpret_cast<const uint4*>(&c0);
 #pragma unroll
           for (int k = 0; k < PT_WORDS / 4; k++) downd[j * (PT_WORDS / 4) + k] = w4[k];
         }
       } else {
-        lds_put_cached(mine, c0, BS);
+        lds_put_cached(mine, c0, MAXBS);
       }
     }
     if (top_lane) {
@@ -430,32 +468,34 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       } else {
         cached_identity(u);
       }
-      lds_put_cached(cols, u, BS);
+      lds_put_cached(base, u, MAXBS);
     }
     __syncthreads();
-    if (pos + 1 < N) ge_add_lds(D, D, nbr, false, BS);
+    if (live && pos + 1 < N) ge_add_lds(D, D, nbr, false, MAXBS);
     __syncthreads();  // every column read before the next step overwrites it
-    if (l == 0 && R) pt_store(R, rstride, d * nrecv + j, D);
+    if (live && q == 0 && R) pt_store(R, rstride, d * nrecv + j, D);
   }
 }
 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream) {
   if (!ndealers || !nrecv) return;
-  const bool wide = N > 256;
-  const size_t bs = wide ? 512 : ((N + 63) / 64) * 64;
-  const size_t nblk = (N + bs - 1) / bs;
-  uint32_t* up = nullptr;
-  for (size_t b = nblk; b-- > 0;) {
-    uint32_t* down = b ? ((nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
-    if (wide)
-      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream, npad, N, e, nrecv,
-                         b * bs, up, down, b ? nullptr : R, rstride);
-    else
-      hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream, npad, N, e, nrecv,
-                         b * bs, up, down, b ? nullptr : R, rstride);
-    up = down;
+  if (N > 256) {  // 512-lane blocks, one dealer per workgroup, top block first
+    const size_t bs = 512, nblk = (N + bs - 1) / bs;
+    uint32_t* up = nullptr;
+    for (size_t b = nblk; b-- > 0;) {
+      uint32_t* down = b ? ((nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
+      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream,
+                         ndealers, npad, N, e, nrecv, b * bs, (int)bs, up, down, b ? nullptr : R, rstride);
+      up = down;
+    }
+    return;
   }
+  // whole table in one segment of N lanes; floor(256 / N) dealers per 256-lane workgroup
+  const size_t P = N, per = 256 / P, bs = ((per * P + 63) / 64) * 64;
+  const size_t grid = (ndealers + per - 1) / per;
+  hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid), dim3((unsigned)bs), 0, stream, ndealers,
+                     npad, N, e, nrecv, (size_t)0, (int)P, (const uint32_t*)nullptr, (uint32_t*)nullptr, R, rstride);
 }
 
 // ------------------------------------------------------------------ K3c check

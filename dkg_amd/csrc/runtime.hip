@@ -167,7 +167,6 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   if (!V) return;
   const size_t npad = pad64(V);
   hipStream_t home = ctx->stream;
-  uint32_t* Cext = buf<uint32_t>(ctx, "v.Cext", PTB * V * N);
   uint8_t* pok = buf<uint8_t>(ctx, "v.pok", V * N);
   uint8_t* dok = buf<uint8_t>(ctx, "v.dok", V);
   uint32_t* Cpm = buf<uint32_t>(ctx, "v.Cpm", PTB * N * npad);
@@ -183,11 +182,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   std::vector<size_t> v0(nseg + 1, 0);
   for (int k = 0; k < nseg; k++) {
     v0[k + 1] = v0[k] + segs[k].D;
-    // K5 (groups.rs:78-81): virtual dealer v's commitments are elements v*N .. v*N + t
-    dkgk::decode_points(segs[k].Ccomp, segs[k].D * N, Cext + v0[k] * N, V * N, pok + v0[k] * N, home);
+    // K5 (groups.rs:78-81) into the position-major table: virtual dealer v is column v
+    dkgk::decode_position_major(segs[k].Ccomp, segs[k].D, N, npad, Cpm + v0[k], pok + v0[k] * N, home);
   }
+  dkgk::fill_identity_columns(N, npad, V, Cpm, home);
   dkgk::dealer_ok(V, N, pok, dok, home);
-  dkgk::to_position_major(V, N, npad, Cext, Cpm, home);
   // checks of virtual dealers [c0, c1) on stream st, split at segment boundaries
   auto checks = [&](size_t c0, size_t c1, hipStream_t st) {
     for (int k = 0; k < nseg; k++) {
