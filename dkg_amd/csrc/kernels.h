@@ -11,9 +11,18 @@ namespace dkgk {
 void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t stride, uint8_t* ok,
                    hipStream_t stream);
 // K5 straight into the binomial's position-major layout: D dealers x N commitments ([D][N][8],
-// dealer-major) -> [40][N][npad] at out (pass table + first dealer column); ok [D*N] dealer-major.
+// dealer-major) -> [40][N][npad].  nseg segments are interleaved in 64-column groups: dealer i of
+// segment seg lands in column (i / 64) * 64 * nseg + seg * 64 + i % 64; ok[column * N + k].
 void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
-                           hipStream_t stream);
+                           hipStream_t stream, int nseg = 1, int seg = 0);
+// every column of a position-major table [40][S] set to the identity
+void fill_identity(size_t S, uint32_t* out, hipStream_t stream);
+// fused round-2/4 check over interleaved E/A columns (see k_check_both): dealers
+// [dealer0, dealer0 + ndealers) of this call, s / sp / dec2 / dec4 indexed dealer * nrecv + j from
+// their bases, self = (dealer + dealer_base) mod nmod == j.
+void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
+                const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
+                const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream);
 // identity points in dealer columns [V, npad) of a position-major table [40][N][npad]
 void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream);
 // extended SoA -> encodings [count][8]

@@ -18,9 +18,12 @@ constexpr int COMB_WORDS = AFF_WORDS * COMB_ENTRIES;  // 15360 words = 61440 B p
 // straight into the position-major layout of the binomial (the decode is compute-bound, so the
 // scattered 40 stores per point cost nothing next to its exponentiation, and no transpose pass or
 // second copy of the points is needed).
+// With interleaved segments (nseg > 1) dealer i of segment seg goes to column
+// (i / 64) * 64 * nseg + seg * 64 + i % 64, and ok[] is indexed by column * pm_N + k.
 __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ comp, size_t count,
                                                 uint32_t* __restrict__ ext, size_t stride,
-                                                uint8_t* __restrict__ ok, size_t pm_N, size_t pm_npad) {
+                                                uint8_t* __restrict__ ok, size_t pm_N, size_t pm_npad,
+                                                uint32_t nseg, uint32_t seg) {
   size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
   uint32_t w[8];
@@ -28,9 +31,15 @@ __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ com
   ge_p3 p;
   bool v = ristretto_decode(p, w);
   if (!v) ge_identity(p);
-  const size_t idx = pm_N ? (e % pm_N) * pm_npad + e / pm_N : e;
+  size_t idx = e, oidx = e;
+  if (pm_N) {
+    const size_t i = e / pm_N, k = e % pm_N;
+    const size_t col = (i / 64) * 64 * nseg + seg * 64 + i % 64;
+    idx = k * pm_npad + col;
+    oidx = col * pm_N + k;
+  }
   pt_store(ext, stride, idx, p);
-  ok[e] = v ? 1 : 0;
+  ok[oidx] = v ? 1 : 0;
 }
 
 // Identity points in dealer columns [V, npad) of a position-major table [40][N][npad].
@@ -59,15 +68,15 @@ void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t str
                    hipStream_t stream) {
   if (!count) return;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count,
-                     ext, stride, ok, (size_t)0, (size_t)0);
+                     ext, stride, ok, (size_t)0, (size_t)0, 1u, 0u);
 }
 
 void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
-                           hipStream_t stream) {
+                           hipStream_t stream, int nseg, int seg) {
   const size_t count = D * N;
   if (!count) return;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count, out,
-                     N * npad, ok, N, npad);
+                     N * npad, ok, N, npad, (uint32_t)nseg, (uint32_t)seg);
 }
 
 void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream) {
@@ -539,6 +548,68 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
   const size_t lds = (round == 2 ? 2 : 1) * COMB_WORDS * 4;
   hipLaunchKernelGGL(k_check, dim3(comb_grid(total, 1024)), dim3(1024), lds, stream, ndealers, nrecv, dealer_base,
                      recv_base, (uint32_t)nmod, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
+}
+
+// Fused round-2 + round-4 check of dealers [dealer0, dealer0 + ndealers) (local indices) whose E and A
+// difference tables sit in interleaved columns: dealer i's E row is column (i / 64) * 128 + i % 64
+// and its A row the column 64 after it.  g*s_ij is computed ONCE: compared with R_A (round 4,
+// committee.rs:537-541), then h*s'_ij is added and the sum compared with R_E (round 2,
+// committee.rs:292-305) -- the same group elements the two rounds compute separately.
+__global__ __launch_bounds__(1024) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
+                                                     uint32_t nmod, const uint32_t* __restrict__ s,
+                                                     const uint32_t* __restrict__ sp, const uint32_t* __restrict__ R,
+                                                     size_t rstride, const uint32_t* __restrict__ tab_g,
+                                                     const uint32_t* __restrict__ tab_h,
+                                                     const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
+                                                     uint8_t* __restrict__ dec4) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  lds_fill(lds, tab_g, COMB_WORDS);
+  lds_fill(lds + COMB_WORDS, tab_h, COMB_WORDS);
+  __syncthreads();
+  const size_t total = ndealers * nrecv;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = dealer0 + p / nrecv, j = p % nrecv;
+    const size_t cE = (i / 64) * 128 + i % 64, cA = cE + 64;
+    const size_t q = i * nrecv + j;  // share / decision index
+    const bool self = (uint32_t)((i + dealer_base) % nmod) == (uint32_t)j;
+    ge_p3 acc, r;
+    ge_identity(acc);
+    sc x;
+    sc_load(x, s + 8 * q);
+    comb_mul_add(acc, x, lds);                       // G::generator() * s   (committee.rs:294, :537)
+    pt_load(r, R, rstride, cA * nrecv + j);
+    bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
+    dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);
+    sc_load(x, sp + 8 * q);
+    comb_mul_add(acc, x, lds + COMB_WORDS);          // + h * s'              (committee.rs:292-293)
+    pt_load(r, R, rstride, cE * nrecv + j);
+    eq = ristretto_eq(acc, r);                       // round 2 (:305)
+    dec2[q] = self ? 2 : ((dok[cE] && eq) ? 1 : 0);
+  }
+}
+
+void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
+                const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
+                const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream) {
+  const size_t total = ndealers * nrecv;
+  if (!total) return;
+  hipLaunchKernelGGL(k_check_both, dim3(comb_grid(total, 1024)), dim3(1024), 2 * COMB_WORDS * 4, stream, ndealers,
+                     nrecv, dealer0, dealer_base, (uint32_t)nmod, s, sp, R, rstride, tab_g, tab_h, dok, dec2, dec4);
+}
+
+// Identity in every column of a position-major table [40][S] (S = N * npad words apart).
+__global__ void k_fill_all_identity(size_t S, uint32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S) return;
+  ge_p3 id;
+  ge_identity(id);
+  pt_store(out, S, e, id);
+}
+
+void fill_identity(size_t S, uint32_t* out, hipStream_t stream) {
+  if (!S) return;
+  hipLaunchKernelGGL(k_fill_all_identity, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, S, out);
 }
 
 __global__ void k_dealer_ok(size_t ndealers, size_t N, const uint8_t* __restrict__ pok, uint8_t* __restrict__ ok) {

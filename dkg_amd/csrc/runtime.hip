@@ -150,82 +150,91 @@ struct VerifySeg {
   uint8_t* dec;
 };
 
-// All segments on device, as ONE pipeline over their concatenated "virtual dealers" (a dealer's E
-// row and its A row are two independent polynomials in the exponent: the binomial-basis Horner and
-// the stepping never look at which one a column is).  Fusing round 2 with round 4 doubles the
-// independent work inside each of the t dependent binomial launches and halves the launch count;
-// only the checks differ per segment.  Work is ordered after what is queued on ctx->stream and
-// completes on it.  With ctx->nsub > 1 the virtual dealers are cut into nsub chunks (multiples of
-// 64 columns) whose binomial -> stepping -> check pipelines run on their own streams, so one
-// chunk's partly-filled binomial launches share the CUs with another chunk's work.  nsub == 1 with
-// `timed` records per-phase device times (dkg_ctx_phase_ms, under `tag`).
+// One or two segments on device, as ONE pipeline over "virtual dealers" (table columns).  With two
+// segments (round 2 on E and round 4 on A of the SAME dealers) a dealer's E row and A row are two
+// independent polynomials in the exponent: the binomial-basis Horner and the stepping never look
+// at which one a column is, so both run in the same launches (twice the independent work inside
+// each of the t dependent binomial launches, half the launches).  Columns are interleaved in
+// 64-dealer groups (E of dealers 64q.., then A of the same dealers) so that a chunk holds both rows
+// of its dealers and one fused check computes g*s_ij once for both rounds.  Work is ordered after
+// what is queued on ctx->stream and completes on it.  With ctx->nsub > 1 the dealer groups are cut
+// into nsub chunks whose binomial -> stepping -> check pipelines run on their own streams, so one
+// chunk's partly-filled binomial launches share the CUs with another chunk's work.  nsub == 1
+// with `timed` records per-phase device times (dkg_ctx_phase_ms, under `tag`).
 void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int nseg, bool timed,
                    const char* tag) {
-  const size_t N = t + 1;
-  size_t V = 0;
-  for (int k = 0; k < nseg; k++) V += segs[k].D;
-  if (!V) return;
-  const size_t npad = pad64(V);
+  const size_t N = t + 1, D = segs[0].D;
+  if (!D) return;
+  if (nseg == 2 && (segs[1].D != D || segs[1].dealer_base != segs[0].dealer_base || segs[1].s != segs[0].s ||
+                    segs[0].round != 2 || segs[1].round != 4)) {
+    ctx->err = "verify_device: fused segments must be round 2 then round 4 of the same dealers";
+    throw Fail{DKG_E_ARG};
+  }
+  const size_t groups = (D + 63) / 64, gw = 64 * nseg;  // columns per dealer group
+  const size_t npad = groups * gw;
   hipStream_t home = ctx->stream;
-  uint8_t* pok = buf<uint8_t>(ctx, "v.pok", V * N);
-  uint8_t* dok = buf<uint8_t>(ctx, "v.dok", V);
+  uint8_t* pok = buf<uint8_t>(ctx, "v.pok", npad * N);
+  uint8_t* dok = buf<uint8_t>(ctx, "v.dok", npad);
   uint32_t* Cpm = buf<uint32_t>(ctx, "v.Cpm", PTB * N * npad);
   uint32_t* e0 = buf<uint32_t>(ctx, "v.binom0", PTB * N * npad);
   uint32_t* e1 = buf<uint32_t>(ctx, "v.binom1", PTB * N * npad);
-  uint32_t* R = buf<uint32_t>(ctx, "v.R", PTB * V * n);
+  uint32_t* R = buf<uint32_t>(ctx, "v.R", PTB * npad * n);
   uint32_t *sa = nullptr, *sb = nullptr;
   if (N > 512) {
-    sa = buf<uint32_t>(ctx, "v.step_a", PTB * V * n);
-    sb = buf<uint32_t>(ctx, "v.step_b", PTB * V * n);
+    sa = buf<uint32_t>(ctx, "v.step_a", PTB * npad * n);
+    sb = buf<uint32_t>(ctx, "v.step_b", PTB * npad * n);
   }
-  const size_t rstride = V * n;
-  std::vector<size_t> v0(nseg + 1, 0);
-  for (int k = 0; k < nseg; k++) {
-    v0[k + 1] = v0[k] + segs[k].D;
-    // K5 (groups.rs:78-81) into the position-major table: virtual dealer v is column v
-    dkgk::decode_position_major(segs[k].Ccomp, segs[k].D, N, npad, Cpm + v0[k], pok + v0[k] * N, home);
-  }
-  dkgk::fill_identity_columns(N, npad, V, Cpm, home);
-  dkgk::dealer_ok(V, N, pok, dok, home);
-  // checks of virtual dealers [c0, c1) on stream st, split at segment boundaries
-  auto checks = [&](size_t c0, size_t c1, hipStream_t st) {
-    for (int k = 0; k < nseg; k++) {
-      const size_t a = std::max(c0, v0[k]), b = std::min(c1, v0[k + 1]);
-      if (a >= b) continue;
-      const VerifySeg& g = segs[k];
-      const size_t l0 = a - v0[k];
-      dkgk::check(b - a, n, g.dealer_base + l0, 0, n, g.round, g.s + l0 * n * 8,
-                  g.round == 2 ? g.sp + l0 * n * 8 : nullptr, R + a * n, rstride, ctx->tab_g, ctx->tab_h, dok + a,
-                  g.dec + l0 * n, st);
+  const size_t rstride = npad * n;
+  if (npad != D * nseg) dkgk::fill_identity(N * npad, Cpm, home);  // padding columns
+  HCK(hipMemsetAsync(pok, 1, npad * N, home));
+  for (int k = 0; k < nseg; k++)  // K5 (groups.rs:78-81) into the position-major table
+    dkgk::decode_position_major(segs[k].Ccomp, D, N, npad, Cpm, pok, home, nseg, k);
+  dkgk::dealer_ok(npad, N, pok, dok, home);
+  // checks of dealers [d0, d1) on stream st
+  auto checks = [&](size_t d0, size_t d1, hipStream_t st) {
+    if (d1 <= d0) return;
+    const VerifySeg& g = segs[0];
+    if (nseg == 2) {
+      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, n, g.s, g.sp, R, rstride, ctx->tab_g, ctx->tab_h, dok,
+                       g.dec, segs[1].dec, st);
+    } else {
+      dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, n, g.round, g.s + d0 * n * 8,
+                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n, rstride, ctx->tab_g, ctx->tab_h,
+                  dok + d0, g.dec + d0 * n, st);
     }
   };
-  auto chunk = [&](size_t c0, size_t w, hipStream_t st, bool tm) {
+  // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
+  auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
+    const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    uint32_t* e = dkgk::binomial(pad64(w), npad, N, Cpm + c0, e0 + c0, e1 + c0, st);
+    uint32_t* e = dkgk::binomial(w, npad, N, Cpm + c0, e0 + c0, e1 + c0, st);
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::stepping(w, npad, N, e, n, R + c0 * n, rstride, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
-    checks(c0, c0 + w, st);
+    checks(g0 * 64, std::min(D, g1 * 64), st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));
   };
-  const size_t nsub = std::min<size_t>(ctx->nsub, npad / 64);
+  // Chunk streams only pay when the binomial saturates the GPU: chunk c+1's triangle then fills
+  // the CUs that chunk c's launch tails leave idle.  A small shard (few dealers, e.g. one rank of
+  // 8) is latency-bound -- every step is one dependent NAF chain long whatever its width -- so all
+  // its columns go through one launch per step (average waves per step < 4 per SIMD -> nsub = 1).
+  const bool saturating = (npad / 64) * (N / 2) >= 4 * 1024;
+  const size_t nsub = saturating ? std::min<size_t>(ctx->nsub, groups) : 1;
   ctx->timed_tag.clear();
   if (nsub <= 1) {
-    chunk(0, V, home, timed);
+    chunk(0, groups, home, timed);
     if (timed) ctx->timed_tag = tag;
   } else {
-    const size_t groups = npad / 64;
     HCK(hipEventRecord(ctx->fork, home));
-    size_t c0 = 0;
+    size_t g0 = 0;
     for (size_t c = 0; c < nsub; c++) {
       const size_t g1 = groups * (c + 1) / nsub;
-      const size_t c1 = std::min(V, g1 * 64);
       HCK(hipStreamWaitEvent(ctx->sub[c], ctx->fork, 0));
-      chunk(c0, c1 - c0, ctx->sub[c], false);
+      chunk(g0, g1, ctx->sub[c], false);
       HCK(hipEventRecord(ctx->join[c], ctx->sub[c]));
       HCK(hipStreamWaitEvent(home, ctx->join[c], 0));
-      c0 = c1;
+      g0 = g1;
     }
   }
   check_launch(ctx);

@@ -55,8 +55,10 @@ def main():
             ms.append((time.perf_counter() - t0) * 1e3)
         assert bool((o2.view(D, n) != 0).all()), "an honest shard rejected a share"
         res[ws] = round(min(ms), 2)
+        ph = be.phase_times("r24" if not args.no_overlap else "r4")
         print(json.dumps({"n": n, "t": t, "ws": ws, "dealers": D, "ms_wall": res[ws],
-                          "overlap": not args.no_overlap, "streams": args.streams}), flush=True)
+                          "overlap": not args.no_overlap, "streams": args.streams,
+                          "phases_ms_if_serialised": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     base = res.get(1)
     if base:
         print(json.dumps({"speedup_vs_1": {k: round(base / v, 2) for k, v in res.items()}}))
