@@ -14,7 +14,7 @@ DKG_E_ARG = -1
 DKG_E_DECODE = -2
 DKG_E_DEVICE = -3
 DKG_E_NOMEM = -4
-REJECT, ACCEPT, SELF, SKIPPED = 0, 1, 2, 3
+REJECT, ACCEPT, SELF, SKIPPED, MISSING = 0, 1, 2, 3, 4
 
 _lib = None
 
@@ -88,6 +88,13 @@ def lib():
     L.dkg_ceremony_batch_device.argtypes = [p, sz, sz, sz, p, p, ctypes.POINTER(BatchOut)]
     L.dkg_ceremony_batch_verify.argtypes = [p, sz, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(BatchOut)]
     L.dkg_dealer_coeffs_device.argtypes = [p, u8p, ctypes.c_uint32, sz, sz, sz, sz, p, p]
+    L.dkg_member_keys.argtypes = [p, u8p, ctypes.c_uint32, sz, p, p]
+    L.dkg_enc_randomness.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, sz, p]
+    L.dkg_enc_randomness_device.argtypes = [p, u8p, ctypes.c_uint32, sz, sz, sz, sz, sz, p]
+    L.dkg_encrypt_shares.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, p, p]
+    L.dkg_decrypt_shares.argtypes = [p, sz, sz, u8p, u8p, u8p, p, p, p]
+    L.dkg_ceremony_run_full_device.argtypes = [p, sz, sz, p, p, p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
+    L.dkg_ceremony_verify_full.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
     L.dkg_dealer_coeffs.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, p, p]
     L.dkg_scalar_sum_device.argtypes = [p, sz, sz, p, p, p]
     L.dkg_point_sum_device.argtypes = [p, sz, p, p, p]
@@ -101,6 +108,8 @@ EXPORTED = [
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
-    "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
+    "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_member_keys", "dkg_enc_randomness",
+    "dkg_enc_randomness_device", "dkg_encrypt_shares", "dkg_decrypt_shares", "dkg_ceremony_run_full_device",
+    "dkg_ceremony_verify_full", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
     "dkg_scalar_sum_device", "dkg_point_sum_device",
 ]

@@ -46,6 +46,15 @@ def dealer_coefficients(master: bytes, ceremony: int, d0: int, D: int, t: int):
     return a.raw, b.raw
 
 
+def enc_randomness(master: bytes, ceremony: int, d0: int, D: int, n: int, t: int) -> bytes:
+    """Encryption randomness [D][n][2][32] continuing each dealer's seeded stream (committee.rs:171-172)."""
+    r = ctypes.create_string_buffer(max(64 * D * n, 1))
+    rc = _lib.lib().dkg_enc_randomness(master, ceremony, d0, D, n, t, r)
+    if rc != _lib.DKG_OK:
+        raise DkgError(rc, "enc_randomness")
+    return r.raw[:64 * D * n]
+
+
 @dataclass
 class CeremonyResult:
     n: int
@@ -212,6 +221,44 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_ceremony_run_device(self._ctx, n, t, ctypes.c_void_p(d_a),
                                                               ctypes.c_void_p(d_b), ctypes.byref(o)))
         return self._result(n, t, o, bufs, False)
+
+    # ---- full (encrypted-share) mode
+    def member_keys(self, master: bytes, ceremony: int, n: int):
+        """Seeded member communication keys, sorted by public key (party q+1 owns sk[q]): (sk, pk)."""
+        sk, pk = ctypes.create_string_buffer(32 * n), ctypes.create_string_buffer(32 * n)
+        _check(self._ctx, _lib.lib().dkg_member_keys(self._ctx, master, ceremony, n, sk, pk))
+        return sk.raw, pk.raw
+
+    def encrypt_shares(self, pk: bytes, s: bytes, s_prime: bytes, r: bytes, D: int, n: int):
+        e1, ct = ctypes.create_string_buffer(64 * D * n), ctypes.create_string_buffer(64 * D * n)
+        _check(self._ctx, _lib.lib().dkg_encrypt_shares(self._ctx, D, n, pk, s, s_prime, r, e1, ct))
+        return e1.raw, ct.raw
+
+    def decrypt_shares(self, sk: bytes, e1: bytes, ct: bytes, D: int, n: int):
+        s, sp, ok = (ctypes.create_string_buffer(32 * D * n), ctypes.create_string_buffer(32 * D * n),
+                     ctypes.create_string_buffer(2 * D * n))
+        _check(self._ctx, _lib.lib().dkg_decrypt_shares(self._ctx, D, n, sk, e1, ct, s, sp, ok))
+        return s.raw, sp.raw, ok.raw
+
+    def enc_randomness_device(self, master: bytes, ceremony0: int, B: int, d0: int, D: int, n: int, t: int, d_r: int):
+        _check(self._ctx, _lib.lib().dkg_enc_randomness_device(self._ctx, master, ceremony0, B, d0, D, n, t,
+                                                                ctypes.c_void_p(d_r)))
+
+    def ceremony_full_device(self, d_a: int, d_b: int, d_r: int, sk: bytes, pk: bytes, n: int, t: int):
+        o, bufs = self._ceremony_out(n, t, False)
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_ceremony_run_full_device(self._ctx, n, t, vp(d_a), vp(d_b), vp(d_r), sk, pk,
+                                                                   ctypes.byref(o)))
+        return self._result(n, t, o, bufs, False)
+
+    def ceremony_verify_full(self, E: bytes, A: bytes, e1: bytes, ct: bytes, sk: bytes, n: int, t: int):
+        o, bufs = self._ceremony_out(n, t, True)
+        for k in ("E", "A"):
+            setattr(o, k, None)
+        _check(self._ctx, _lib.lib().dkg_ceremony_verify_full(self._ctx, n, t, E, A, e1, ct, sk, ctypes.byref(o)))
+        r = self._result(n, t, o, bufs, True)
+        r.E, r.A = E, A
+        return r
 
     def dealer_coefficients_device(self, master: bytes, ceremony0: int, B: int, d0: int, D: int, t: int,
                                    d_a: int, d_b: int):

@@ -1,0 +1,184 @@
+// Full (encrypted-share) mode on gfx950: the reference's hybrid ElGamal + ChaCha20 transport of the
+// round-1 shares (committee.rs:164-172 encrypt, :282-286 decrypt; elgamal.rs:134-193,
+// procedure_keys.rs:88-105).  Per (dealer i, recipient q) two ciphertexts: w = 0 carries the
+// randomness s'_iq, w = 1 the share s_iq.
+//   encrypt: e1 = g r, K = pk_q r, e2 = m XOR ChaCha20_IETF(key = B(K)[0..32], nonce = B(K)[32..44])
+//   decrypt: K = sk_q e1, m = e2 XOR the same keystream, Scalar::from_bytes = from_bits
+// with B = Blake2b-512 of K's 32-byte encoding.  The work is split into stages so that no kernel
+// carries the register footprint of two different group algorithms:
+//   enc_mul  : two fixed-base combs per item -- g (shared) and pk_q: the recipient's key is the same
+//              for all n dealers, so it gets its own LDS-resident comb table (64 mixed additions,
+//              no doublings) instead of a 253-doubling variable-base multiplication;
+//   dec_mul  : sk_q * e1 with sk_q uniform across the wave (lanes = dealers of one recipient), a
+//              branch-uniform NAF double-and-add with the addend parked in LDS;
+//   encode / decode : the K5 kernels;  sym_xor : Blake2b + one ChaCha20 block + XOR (+ reduce).
+#include "kernels.h"
+#include "points.h"
+#include "sym.h"
+
+namespace dkgk {
+
+constexpr int HY_COMB_WORDS = AFF_WORDS * COMB_ENTRIES;
+
+// grid (ceil(2D / 1024), n): recipient q = blockIdx.y; both comb tables in LDS (120 KB).
+__global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
+                                                  const uint32_t* __restrict__ tab_g,
+                                                  const uint32_t* __restrict__ tabs_pk, uint32_t* __restrict__ R_ext,
+                                                  uint32_t* __restrict__ K_ext) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  const size_t q = blockIdx.y;
+  {
+    const uint4* sg = reinterpret_cast<const uint4*>(tab_g);
+    const uint4* sp = reinterpret_cast<const uint4*>(tabs_pk + q * HY_COMB_WORDS);
+    for (int i = threadIdx.x; i < HY_COMB_WORDS / 4; i += blockDim.x) {
+      lds4[i] = sg[i];
+      lds4[HY_COMB_WORDS / 4 + i] = sp[i];
+    }
+  }
+  __syncthreads();
+  const size_t item = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // i * 2 + w
+  if (item >= 2 * D) return;
+  const size_t i = item >> 1, w = item & 1;
+  const size_t idx = (i * n + q) * 2 + w;
+  const size_t count = 2 * D * n;
+  sc x;
+  sc_load(x, r + 8 * idx);
+  ge_p3 acc;
+  ge_identity(acc);
+  comb_mul_add(acc, x, lds);                   // e1 = G::generator() * r      (elgamal.rs:141)
+  pt_store(R_ext, count, idx, acc);
+  ge_identity(acc);
+  comb_mul_add(acc, x, lds + HY_COMB_WORDS);   // symmetric key = pk * r       (elgamal.rs:138-140)
+  pt_store(K_ext, count, idx, acc);
+}
+
+void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_g, const uint32_t* tabs_pk, uint32_t* R_ext,
+             uint32_t* K_ext, hipStream_t stream) {
+  if (!D || !n) return;
+  hipLaunchKernelGGL(k_enc_mul, dim3((unsigned)((2 * D + 1023) / 1024), (unsigned)n), dim3(1024),
+                     2 * HY_COMB_WORDS * 4, stream, D, n, r, tab_g, tabs_pk, R_ext, K_ext);
+}
+
+// grid (ceil(D / 64), n, 2): recipient q = blockIdx.y, w = blockIdx.z; lanes = dealers.
+// K = sk_q * R: left-to-right NAF of the (wave-uniform) 253-bit scalar; R's cached form in LDS.
+__global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uint32_t* __restrict__ sk,
+                                                   const uint32_t* __restrict__ R_ext, uint32_t* __restrict__ K_ext) {
+  __shared__ uint32_t qs[PT_WORDS * 64];
+  uint32_t* qcol = qs + threadIdx.x;
+  const size_t q = blockIdx.y, w = blockIdx.z;
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const bool live = i < D;
+  const size_t count = 2 * D * n;
+  const size_t idx = ((live ? i : 0) * n + q) * 2 + w;
+  // NAF of sk_q (canonical, < 2^253), computed once per wave into LDS: digits[b] in {0, 1, -1};
+  // reading a wave-uniform LDS byte per bit keeps the recoding out of the VGPR budget of the chain
+  __shared__ int8_t digits[288];
+  __shared__ int top_s;
+  if (threadIdx.x == 0) {
+    uint32_t k[9];
+    for (int j = 0; j < 8; j++) k[j] = sk[8 * q + j];
+    k[8] = 0;
+    int top = -1;
+    for (int b = 0; b < 287; b++) {
+      int8_t d = 0;
+      if ((k[b >> 5] >> (b & 31)) & 1u) {
+        if ((k[(b + 1) >> 5] >> ((b + 1) & 31)) & 1u) {  // ...11: digit -1, k += 2^b (carry upwards)
+          d = -1;
+          uint32_t add = 1u << (b & 31);
+          for (int wi = b >> 5; wi < 9; wi++) {
+            const uint32_t old = k[wi];
+            k[wi] = old + add;
+            if (k[wi] >= old) break;
+            add = 1u;
+          }
+        } else {  // ...01: digit +1, k -= 2^b
+          d = 1;
+          k[b >> 5] &= ~(1u << (b & 31));
+        }
+        top = b;
+      }
+      digits[b] = d;
+    }
+    top_s = top;
+  }
+  __syncthreads();
+  const int top = __builtin_amdgcn_readfirstlane(top_s);
+  ge_p3 x;
+  if (live) pt_load(x, R_ext, count, idx);
+  else ge_identity(x);
+  if (top < 0) {  // sk = 0: K = identity
+    ge_identity(x);
+  } else {
+    {
+      ge_cached xc;
+      ge_to_cached(xc, x);
+      lds_put_cached(qcol, xc);
+    }
+    // leading digit is +1 (NAF top digit of a positive number); x already holds 1 * R
+#pragma unroll 1
+    for (int b = top - 1; b >= 0; b--) {
+      const int d = __builtin_amdgcn_readfirstlane((int)digits[b]);
+      ge_dbl_lean(x, x, d != 0 || b == 0);
+      if (d != 0) ge_add_lds(x, x, qcol, d < 0);
+    }
+  }
+  if (live) pt_store(K_ext, count, idx, x);
+}
+
+void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream) {
+  if (!D || !n) return;
+  hipLaunchKernelGGL(k_dec_mul, dim3((unsigned)((D + 63) / 64), (unsigned)n, 2u), dim3(64), 0, stream, D, n, sk,
+                     R_ext, K_ext);
+}
+
+// SymmetricKey::process (elgamal.rs:172-193) on 32-byte messages: one Blake2b-512 of the key's
+// encoding, one ChaCha20 block (counter 0), XOR.
+__global__ __launch_bounds__(256) void k_sym_xor(size_t D, size_t n, const uint32_t* __restrict__ Kc, int decrypt,
+                                                 uint32_t* __restrict__ ct, uint32_t* __restrict__ s,
+                                                 uint32_t* __restrict__ sp) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 2 * D * n) return;
+  const size_t pair = idx >> 1, w = idx & 1;
+  uint64_t m[16];
+#pragma unroll
+  for (int j = 0; j < 4; j++) m[j] = (uint64_t)Kc[8 * idx + 2 * j] | ((uint64_t)Kc[8 * idx + 2 * j + 1] << 32);
+#pragma unroll
+  for (int j = 4; j < 16; j++) m[j] = 0;
+  uint64_t h[8];
+  sym::blake2b_1block(h, m, 32, 64);
+  uint32_t key[8], nonce[3];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    key[2 * j] = (uint32_t)h[j];
+    key[2 * j + 1] = (uint32_t)(h[j] >> 32);
+  }
+  nonce[0] = (uint32_t)h[4];
+  nonce[1] = (uint32_t)(h[4] >> 32);
+  nonce[2] = (uint32_t)h[5];
+  uint32_t ks[16];
+  sym::chacha20_ietf_block(ks, key, 0u, nonce);
+  uint32_t* msg = w ? s + 8 * pair : sp + 8 * pair;
+  if (!decrypt) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) ct[8 * idx + j] = msg[j] ^ ks[j];
+  } else {
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = ct[8 * idx + j] ^ ks[j];
+    v[7] &= 0x7fffffffu;  // Scalar::from_bytes = from_bits (groups.rs:29-36); reduced mod l on device
+    sc r;
+    sc_reduce256(r, v);
+    st_words8(msg, r.v);
+  }
+}
+
+void sym_xor(size_t D, size_t n, const uint32_t* Kc, bool decrypt, uint32_t* ct, uint32_t* s, uint32_t* sp,
+             hipStream_t stream) {
+  const size_t tot = 2 * D * n;
+  if (!tot) return;
+  hipLaunchKernelGGL(k_sym_xor, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, D, n, Kc, decrypt ? 1 : 0,
+                     ct, s, sp);
+}
+
+}  // namespace dkgk

@@ -27,8 +27,8 @@ void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_bas
 void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream);
 // extended SoA -> encodings [count][8]
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream);
-// comb table of the decoded point ext[.., e0] into tab (30 x 512 words)
-void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream);
+// comb tables of the decoded points ext[.., e0 + c], c < count, into tab + c * 15360 (30 x 512 words each)
+void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count = 1);
 
 // K2: A_k = g a_k, E_k = A_k + h b_k for D*N coefficients (scalars [D*N][8]); outputs SoA [40][DN].
 void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g,
@@ -58,6 +58,8 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
            const uint32_t* s, const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g,
            const uint32_t* tab_h, const uint8_t* dealer_ok, uint8_t* decision, hipStream_t stream);
+// dok[column of dealer i of segment seg] &= extra[i] (verify_device's interleaved column layout)
+void and_dealer_mask(size_t D, int nseg, int seg, const uint8_t* extra, uint8_t* dok, hipStream_t stream);
 // per-dealer validity: dealer_ok[i] = AND of point_ok over its N commitments (dealer-major [D][N])
 void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream);
 // Horner in the exponent for receivers x0 .. x0+nrecv-1 (1-based indices): R [40][ndealers*nrecv]
@@ -96,5 +98,23 @@ void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint
 // master: 8 words on the device; seeds: scratch [rows][8].
 void dealer_coeffs(size_t rows, size_t D, size_t d0, uint32_t c0, const uint32_t* master, size_t N, uint32_t* seeds,
                    uint32_t* a, uint32_t* b, hipStream_t stream);
+
+// ---- full (encrypted-share) mode, hybrid.hip (elgamal.rs:134-193) ----
+// Items are (dealer i, recipient q, w) at index (i * n + q) * 2 + w; w = 0 is the randomness (s')
+// ciphertext, w = 1 the share (s) ciphertext (committee.rs:171-172 order).
+// R = g r, K = pk_q r for every item (r [items][8]); tabs_pk: one comb table per recipient.
+void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_g, const uint32_t* tabs_pk, uint32_t* R_ext,
+             uint32_t* K_ext, hipStream_t stream);
+// K = sk_q * R for every item, R decoded SoA [40][items] (sk [n][8], wave-uniform per recipient)
+void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream);
+// SymmetricKey::process: keystream from Blake2b-512(Kc) (Kc [items][8] encodings).
+// encrypt: ct[item] = (w ? s : sp)[i*n+q] ^ ks.  decrypt: (w ? s : sp)[i*n+q] = reduce(from_bits(ct[item] ^ ks)).
+void sym_xor(size_t D, size_t n, const uint32_t* Kc, bool decrypt, uint32_t* ct, uint32_t* s, uint32_t* sp,
+             hipStream_t stream);
+// per-row dealer seeds [rows][8] (row r = dealer d0 + r % D of ceremony c0 + r / D; seedgen.hip)
+void dealer_seeds(size_t rows, size_t D, size_t d0, uint32_t c0, const uint32_t* master, uint32_t* seeds,
+                  hipStream_t stream);
+// encryption randomness rows (seedgen.hip): r [rows][n][2][8] = wide(block 2N + 2q + w) of each dealer stream
+void enc_randomness(size_t rows, size_t n, size_t N, const uint32_t* seeds, uint32_t* r, hipStream_t stream);
 
 }  // namespace dkgk

@@ -93,11 +93,14 @@ void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* c
 
 // ------------------------------------------------------------------ comb tables
 // Thread w (0..63) builds window w: B_w = 16^w B, entries d B_w (d = 1..8) in affine Niels form.
+// Workgroup g builds the table of point e0 + g into tab + g * COMB_WORDS (one table per
+// workgroup, so a batch of bases -- e.g. every member's communication key -- is one launch).
 __global__ __launch_bounds__(64) void k_build_comb(const uint32_t* __restrict__ ext, size_t stride, size_t e0,
                                                    uint32_t* __restrict__ tab) {
   const int w = threadIdx.x;
+  tab += (size_t)blockIdx.x * COMB_WORDS;
   ge_p3 b;
-  pt_load(b, ext, stride, e0);
+  pt_load(b, ext, stride, e0 + blockIdx.x);
   for (int i = 0; i < 4 * w; i++) ge_dbl<true>(b, b);
   ge_cached bc;
   ge_to_cached(bc, b);
@@ -126,8 +129,9 @@ __global__ __launch_bounds__(64) void k_build_comb(const uint32_t* __restrict__ 
   }
 }
 
-void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream) {
-  hipLaunchKernelGGL(k_build_comb, dim3(1), dim3(64), 0, stream, ext, stride, e0, tab);
+void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_build_comb, dim3((unsigned)count), dim3(64), 0, stream, ext, stride, e0, tab);
 }
 
 __device__ __forceinline__ void lds_fill(uint32_t* lds, const uint32_t* __restrict__ g, int words) {
@@ -230,53 +234,6 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 }
 
 // ------------------------------------------------------------------ K3a binomial-basis Horner
-// Register-lean variants for the m-chains: the cached addend lives in LDS (lane-interleaved,
-// word w of lane l at q[w * 64 + l], conflict-free) and is read field by field when the addition
-// needs it, so a chain keeps one point + the doubling temporaries in VGPRs (<= 128: 4 waves/SIMD).
-// q points at this lane's column (base + lane); consecutive words are `stride` apart.
-__device__ __forceinline__ void lds_put_cached(uint32_t* q, const ge_cached& c, int stride = 64) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(&c);
-#pragma unroll
-  for (int k = 0; k < PT_WORDS; k++) q[k * stride] = w[k];
-}
-// which: 0 = Y+X, 1 = Y-X, 2 = 2Z, 3 = 2dT
-__device__ __forceinline__ void lds_get_fe(fe& r, const uint32_t* q, int which, int stride = 64) {
-#pragma unroll
-  for (int i = 0; i < 10; i++) r.v[i] = q[(which * 10 + i) * stride];
-  // Opaque use of all ten limbs at once (one lgkmcnt wait for the group): stops LICM from
-  // hoisting the loads and their x19 products out of the chain loop (~140 extra VGPRs).
-  asm volatile("" : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
-               "+v"(r.v[6]), "+v"(r.v[7]), "+v"(r.v[8]), "+v"(r.v[9]));
-}
-
-// r = p +/- Q with Q the cached point in LDS; `neg` must be wave-uniform.
-__device__ __forceinline__ void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
-                                           int stride = 64) {
-  fe a, b, e, h, t, qv;
-  fe_sub(t, p.Y, p.X);
-  lds_get_fe(qv, q, neg ? 0 : 1, stride);
-  fe_mul(a, t, qv);
-  fe_add(t, p.Y, p.X);
-  lds_get_fe(qv, q, neg ? 1 : 0, stride);
-  fe_mul(b, t, qv);
-  fe_sub(e, b, a);          // <= 1.5*2^27
-  fe_add(h, b, a);          // <= 2^27
-  lds_get_fe(qv, q, 3, stride);
-  fe_mul(a, p.T, qv);       // c
-  if (neg) {
-    fe_neg(a, a);
-    fe_carry(a, a);
-  }
-  lds_get_fe(qv, q, 2, stride);
-  fe_mul(b, p.Z, qv);       // d
-  fe_sub(t, b, a);          // f
-  fe_add(b, b, a);          // g
-  fe_mul(r.X, e, t);
-  fe_mul(r.Y, b, h);
-  fe_mul(r.Z, t, b);
-  fe_mul(r.T, e, h);
-}
-
 // y = m * y, m wave-uniform; q = this lane's column of the wave's 40 x 64-word LDS slot (clobbered).
 __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q) {
   uint32_t pos = 0, neg = 0;
@@ -534,7 +491,9 @@ __global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, s
     }
     pt_load(r, R, rstride, p);
     const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
-    uint8_t v = (dok[i] && eq) ? 1 : 0;
+    // a dealer whose broadcast does not decode is missing data: disqualified without a complaint in
+    // round 2 (committee.rs:331-335), an accusation in round 4 (:549-555)
+    uint8_t v = dok[i] ? (eq ? 1 : 0) : (round == 2 ? 4 : 0);
     if ((uint32_t)((i + dealer_base) % nmod) == (uint32_t)(j + recv_base)) v = 2;  // self (batched: per ceremony)
     dec[p] = v;
   }
@@ -580,12 +539,12 @@ __global__ __launch_bounds__(1024) void k_check_both(size_t ndealers, size_t nre
     comb_mul_add(acc, x, lds);                       // G::generator() * s   (committee.rs:294, :537)
     pt_load(r, R, rstride, cA * nrecv + j);
     bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
-    dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);
+    dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
     sc_load(x, sp + 8 * q);
     comb_mul_add(acc, x, lds + COMB_WORDS);          // + h * s'              (committee.rs:292-293)
     pt_load(r, R, rstride, cE * nrecv + j);
     eq = ristretto_eq(acc, r);                       // round 2 (:305)
-    dec2[q] = self ? 2 : ((dok[cE] && eq) ? 1 : 0);
+    dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)
   }
 }
 
@@ -618,6 +577,21 @@ __global__ void k_dealer_ok(size_t ndealers, size_t N, const uint8_t* __restrict
   uint8_t v = 1;
   for (size_t k = 0; k < N; k++) v &= pok[i * N + k];
   ok[i] = v;
+}
+
+// dok[column of dealer i in segment seg] &= extra[i] (interleaved column layout of verify_device)
+__global__ void k_and_dealer_mask(size_t D, uint32_t nseg, uint32_t seg, const uint8_t* __restrict__ extra,
+                                  uint8_t* __restrict__ dok) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= D) return;
+  const size_t col = (i / 64) * 64 * nseg + seg * 64 + i % 64;
+  dok[col] &= extra[i];
+}
+
+void and_dealer_mask(size_t D, int nseg, int seg, const uint8_t* extra, uint8_t* dok, hipStream_t stream) {
+  if (!D) return;
+  hipLaunchKernelGGL(k_and_dealer_mask, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, D, (uint32_t)nseg,
+                     (uint32_t)seg, extra, dok);
 }
 
 void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream) {
@@ -898,13 +872,14 @@ void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint
 }
 
 // Row / column summaries of a decision matrix [rows][n] (rows = groups x n dealers of batched
-// ceremonies): row_reject[i] = some receiver rejected dealer i; complaints[g][j] = number of
-// dealers of group g rejected by receiver j (committee.rs:311-316, 340-347).
+// ceremonies): row_reject[i] = some receiver rejected dealer i or its data is missing (it is not
+// qualified); complaints[g][j] = number of dealers of group g rejected (REJECT only, MISSING is no
+// complaint) by receiver j (committee.rs:311-316, 331-335, 340-347).
 __global__ void k_row_reject(size_t rows, size_t n, const uint8_t* __restrict__ dec, uint8_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows) return;
   uint8_t r = 0;
-  for (size_t j = 0; j < n; j++) r |= dec[i * n + j] == 0;
+  for (size_t j = 0; j < n; j++) r |= dec[i * n + j] == 0 || dec[i * n + j] == 4;  // REJECT or MISSING
   out[i] = r;
 }
 

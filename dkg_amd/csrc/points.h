@@ -91,3 +91,52 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
     ge_madd(acc, acc, r);
   }
 }
+
+// Register-lean variants for the m-chains: the cached addend lives in LDS (lane-interleaved,
+// word w of lane l at q[w * 64 + l], conflict-free) and is read field by field when the addition
+// needs it, so a chain keeps one point + the doubling temporaries in VGPRs (<= 128: 4 waves/SIMD).
+// q points at this lane's column (base + lane); consecutive words are `stride` apart.
+DKG_DEV void lds_put_cached(uint32_t* q, const ge_cached& c, int stride = 64) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&c);
+#pragma unroll
+  for (int k = 0; k < PT_WORDS; k++) q[k * stride] = w[k];
+}
+// which: 0 = Y+X, 1 = Y-X, 2 = 2Z, 3 = 2dT
+DKG_DEV void lds_get_fe(fe& r, const uint32_t* q, int which, int stride = 64) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = q[(which * 10 + i) * stride];
+  // Opaque use of all ten limbs at once (one lgkmcnt wait for the group): stops LICM from
+  // hoisting the loads and their x19 products out of the chain loop (~140 extra VGPRs).
+  asm volatile("" : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+               "+v"(r.v[6]), "+v"(r.v[7]), "+v"(r.v[8]), "+v"(r.v[9]));
+}
+
+// r = p +/- Q with Q the cached point in LDS; `neg` must be wave-uniform.
+DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
+                                           int stride = 64) {
+  fe a, b, e, h, t, qv;
+  fe_sub(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 0 : 1, stride);
+  fe_mul(a, t, qv);
+  fe_add(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 1 : 0, stride);
+  fe_mul(b, t, qv);
+  fe_sub(e, b, a);          // <= 1.5*2^27
+  fe_add(h, b, a);          // <= 2^27
+  lds_get_fe(qv, q, 3, stride);
+  fe_mul(a, p.T, qv);       // c
+  if (neg) {
+    fe_neg(a, a);
+    fe_carry(a, a);
+  }
+  lds_get_fe(qv, q, 2, stride);
+  fe_mul(b, p.Z, qv);       // d
+  fe_sub(t, b, a);          // f
+  fe_add(b, b, a);          // g
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, t, b);
+  fe_mul(r.T, e, h);
+}
+
+

@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -148,6 +149,7 @@ struct VerifySeg {
   const uint32_t* s;
   const uint32_t* sp;
   uint8_t* dec;
+  const uint8_t* extra_ok = nullptr;  // [D] device: 0 = the dealer's other broadcast data is missing
 };
 
 // One or two segments on device, as ONE pipeline over "virtual dealers" (table columns).  With two
@@ -190,6 +192,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   for (int k = 0; k < nseg; k++)  // K5 (groups.rs:78-81) into the position-major table
     dkgk::decode_position_major(segs[k].Ccomp, D, N, npad, Cpm, pok, home, nseg, k);
   dkgk::dealer_ok(npad, N, pok, dok, home);
+  for (int k = 0; k < nseg; k++)
+    if (segs[k].extra_ok) dkgk::and_dealer_mask(D, nseg, k, segs[k].extra_ok, dok, home);
   // checks of dealers [d0, d1) on stream st
   auto checks = [&](size_t d0, size_t d1, hipStream_t st) {
     if (d1 <= d0) return;
@@ -251,19 +255,22 @@ void verify_one(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t de
 // mask applied afterwards depends on round 2, so every output is identical to protocol order.
 // Otherwise round 2, then (after `between`, e.g. round 3) round 4, each timed when nsub == 1.
 // `after2` (may be null) is recorded on ctx->stream once the round-2 decisions are complete.
+// e_ok (may be null): per-dealer device mask, 0 = the dealer's round-1 ciphertexts are missing data
+// (full mode), folded into the round-2 decisions like an undecodable commitment.
 template <typename F>
 void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
                    const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
-                   hipEvent_t after2, F&& between) {
+                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr) {
   if (ctx->overlap) {
-    VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2}, {4, D, dealer_base, Acomp, s, nullptr, dec4}};
+    VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok}, {4, D, dealer_base, Acomp, s, nullptr, dec4}};
     verify_device(ctx, n, t, g, 2, true, "r24");
     if (after2) HCK(hipEventRecord(after2, ctx->stream));
     sync(ctx);
     collect_phases(ctx);
     between();
   } else {
-    verify_one(ctx, n, t, 2, D, dealer_base, Ecomp, s, sp, dec2, true);
+    VerifySeg g2{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok};
+    verify_device(ctx, n, t, &g2, 1, true, "r2");
     if (after2) HCK(hipEventRecord(after2, ctx->stream));
     sync(ctx);
     collect_phases(ctx);
@@ -314,7 +321,8 @@ std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, 
 
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
 void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
-                      const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big) {
+                      const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
+                      const uint8_t* e_ok = nullptr) {
   const size_t N = t + 1;
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
@@ -332,6 +340,8 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
         if (h2[i * n + j] == DKG_REJECT) {
           complaints[j]++;     // receiver j accuses dealer i (committee.rs:311-316)
           qualified[i] = 0;    // a valid complaint disqualifies i for everyone (:370-398)
+        } else if (h2[i * n + j] == DKG_MISSING) {
+          qualified[i] = 0;    // no (decodable) broadcast: disqualified, no complaint (:331-335)
         }
     for (size_t j = 0; j < n; j++) r2err[j] = complaints[j] > (int32_t)t;  // :340-347
     // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
@@ -343,7 +353,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     dkgk::encode_points(pub, n, n, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
-  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3);
+  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok);
   d2h(ctx, h4.data(), dec4, n * n);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
@@ -539,6 +549,44 @@ void batch_times(dkg_ctx* ctx, dkg_batch_out* out, bool round1) {
   out->ms_round3 = ev_ms(ctx, 2, 3);
   out->ms_finalise = ev_ms(ctx, 3, 5);
   out->ms_total = ev_ms(ctx, 0, 5);
+}
+
+// ---- full (encrypted-share) mode: hybrid.hip (elgamal.rs:134-193, committee.rs:164-172, 282-286)
+// Items (dealer i, recipient q, w) at (i * n + q) * 2 + w: w = 0 the randomness s', w = 1 the share s.
+void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const uint32_t* s, const uint32_t* sp,
+                    const uint32_t* r, uint32_t* e1, uint32_t* ct) {
+  const size_t items = 2 * D * n;
+  hipStream_t st = ctx->stream;
+  uint32_t* pk_ext = buf<uint32_t>(ctx, "hy.pk_ext", PTB * n);
+  uint8_t* pk_ok = buf<uint8_t>(ctx, "hy.pk_ok", n);
+  dkgk::decode_points(pkc, n, pk_ext, n, pk_ok, st);
+  uint32_t* tabs = buf<uint32_t>(ctx, "hy.tabs", COMB_BYTES * n);
+  dkgk::build_comb(pk_ext, n, 0, tabs, st, n);  // one comb per recipient key: r * pk_q is fixed-base
+  uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
+  uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
+  uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
+  dkgk::enc_mul(D, n, r, ctx->tab_g, tabs, R, K, st);
+  dkgk::encode_points(R, items, items, e1, st);
+  dkgk::encode_points(K, items, items, Kc, st);
+  dkgk::sym_xor(D, n, Kc, false, ct, const_cast<uint32_t*>(s), const_cast<uint32_t*>(sp), st);
+  check_launch(ctx);
+}
+
+// Receivers' side: item_ok[item] = e1 decodes; dealer_ok_out[i] = all of dealer i's items decode (a
+// broadcast that does not deserialize is missing data, committee.rs:331-335).
+void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const uint32_t* e1, const uint32_t* ct,
+                    uint32_t* s, uint32_t* sp, uint8_t* item_ok, uint8_t* dealer_ok_out) {
+  const size_t items = 2 * D * n;
+  hipStream_t st = ctx->stream;
+  uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
+  uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
+  uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
+  dkgk::decode_points(e1, items, R, items, item_ok, st);
+  dkgk::dec_mul(D, n, sk, R, K, st);
+  dkgk::encode_points(K, items, items, Kc, st);
+  dkgk::sym_xor(D, n, Kc, true, const_cast<uint32_t*>(ct), s, sp, st);
+  if (dealer_ok_out) dkgk::dealer_ok(D, 2 * n, item_ok, dealer_ok_out, st);
+  check_launch(ctx);
 }
 
 int need_env(dkg_ctx* ctx) {
@@ -939,7 +987,7 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
         sync(ctx);
         for (size_t i = 0; i < D; i++)
           for (size_t j = 0; j < n; j++)
-            if (rows[i * n + j] == DKG_REJECT) q[i] = 0;
+            if (rows[i * n + j] == DKG_REJECT || rows[i * n + j] == DKG_MISSING) q[i] = 0;
       });
       HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
       uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
@@ -1048,6 +1096,212 @@ int dkg_dealer_coeffs_device(dkg_ctx* ctx, const uint8_t master[32], uint32_t ce
     dkgk::dealer_coeffs(rows, D, d0, ceremony0, m, t + 1, seeds, (uint32_t*)d_a, (uint32_t*)d_b, ctx->stream);
     check_launch(ctx);
     sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_member_keys(dkg_ctx* ctx, const uint8_t master[32], uint32_t ceremony, size_t n, uint8_t* sk_out,
+                    uint8_t* pk_out) {
+  return guarded(ctx, [&] {
+    if (!master || !sk_out || !pk_out) return DKG_E_ARG;
+    if (!n) return DKG_OK;
+    static const char tag[] = "dkg-amd/v1/member";
+    std::vector<uint8_t> sk(32 * n), pk(32 * n);
+    for (size_t j = 0; j < n; j++) {  // MemberCommunicationKey::new (procedure_keys.rs:72-76), seeded
+      uint8_t msg[sizeof tag - 1 + 40], seed[32], st[64];
+      memcpy(msg, tag, sizeof tag - 1);
+      memcpy(msg + sizeof tag - 1, master, 32);
+      for (int k = 0; k < 4; k++) {
+        msg[sizeof tag - 1 + 32 + k] = (uint8_t)(ceremony >> (8 * k));
+        msg[sizeof tag - 1 + 36 + k] = (uint8_t)((uint32_t)j >> (8 * k));
+      }
+      dkgh::blake2b(seed, 32, msg, sizeof msg);
+      dkgh::chacha20(seed, 0, st, 64);
+      dkgh::zl_to_bytes(&sk[32 * j], dkgh::zl_from_bytes_wide(st, 64));
+    }
+    uint32_t* dsk = buf<uint32_t>(ctx, "mk_sk", 32 * n);
+    uint32_t* dpe = buf<uint32_t>(ctx, "mk_pk_ext", PTB * n);
+    uint32_t* dpc = buf<uint32_t>(ctx, "mk_pk", 32 * n);
+    h2d(ctx, dsk, sk.data(), 32 * n);
+    dkgk::fixed_base(n, dsk, ctx->tab_g, dpe, ctx->stream);  // to_public (procedure_keys.rs:78-82)
+    dkgk::encode_points(dpe, n, n, dpc, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, pk.data(), dpc, 32 * n);
+    sync(ctx);
+    // committee.rs:134-135: ordered_pks.sort() by the byte order of procedure_keys.rs:26-40
+    std::vector<size_t> order(n);
+    for (size_t j = 0; j < n; j++) order[j] = j;
+    std::sort(order.begin(), order.end(),
+              [&](size_t a, size_t b) { return memcmp(&pk[32 * a], &pk[32 * b], 32) < 0; });
+    for (size_t q = 0; q < n; q++) {
+      memcpy(sk_out + 32 * q, &sk[32 * order[q]], 32);
+      memcpy(pk_out + 32 * q, &pk[32 * order[q]], 32);
+    }
+    return DKG_OK;
+  });
+}
+
+int dkg_enc_randomness(const uint8_t master[32], uint32_t ceremony, size_t d0, size_t D, size_t n, size_t t,
+                       uint8_t* r) {
+  if (!master || !r) return DKG_E_ARG;
+  static const char tag[] = "dkg-amd/v1/dealer";
+  std::vector<uint8_t> stream(2 * n * 64);
+  for (size_t i = 0; i < D; i++) {
+    uint8_t msg[sizeof tag - 1 + 40], seed[32];
+    memcpy(msg, tag, sizeof tag - 1);
+    memcpy(msg + sizeof tag - 1, master, 32);
+    const uint32_t dealer = (uint32_t)(d0 + i);
+    for (int k = 0; k < 4; k++) {
+      msg[sizeof tag - 1 + 32 + k] = (uint8_t)(ceremony >> (8 * k));
+      msg[sizeof tag - 1 + 36 + k] = (uint8_t)(dealer >> (8 * k));
+    }
+    dkgh::blake2b(seed, 32, msg, sizeof msg);
+    dkgh::chacha20(seed, 2 * (t + 1), stream.data(), stream.size());  // after the 2(t+1) coefficients
+    for (size_t q = 0; q < 2 * n; q++)
+      dkgh::zl_to_bytes(r + 32 * (i * 2 * n + q), dkgh::zl_from_bytes_wide(&stream[64 * q], 64));
+  }
+  return DKG_OK;
+}
+
+int dkg_enc_randomness_device(dkg_ctx* ctx, const uint8_t master[32], uint32_t ceremony0, size_t B, size_t d0,
+                              size_t D, size_t n, size_t t, void* d_r) {
+  return guarded(ctx, [&] {
+    if (!master || !d_r) return DKG_E_ARG;
+    const size_t rows = B * D;
+    if (!rows || !n) return DKG_OK;
+    uint32_t* m = buf<uint32_t>(ctx, "sg_master", 32);
+    uint32_t* seeds = buf<uint32_t>(ctx, "sg_seeds", 32 * rows);
+    h2d(ctx, m, master, 32);
+    dkgk::dealer_seeds(rows, D, d0, ceremony0, m, seeds, ctx->stream);
+    dkgk::enc_randomness(rows, n, t + 1, seeds, (uint32_t*)d_r, ctx->stream);
+    check_launch(ctx);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_encrypt_shares(dkg_ctx* ctx, size_t D, size_t n, const uint8_t* pk, const uint8_t* s, const uint8_t* s_prime,
+                       const uint8_t* r, uint8_t* e1, uint8_t* ct) {
+  return guarded(ctx, [&] {
+    if (!pk || !s || !s_prime || !r || !e1 || !ct) return DKG_E_ARG;
+    if (!D || !n) return DKG_OK;
+    const size_t items = 2 * D * n;
+    uint32_t* dpk = buf<uint32_t>(ctx, "hx_pk", 32 * n);
+    h2d(ctx, dpk, pk, 32 * n);
+    std::vector<uint8_t> ok(n);
+    uint32_t* ds = upload_scalars(ctx, "hx_s", s, D * n);
+    uint32_t* dsp = upload_scalars(ctx, "hx_sp", s_prime, D * n);
+    uint32_t* dr = upload_scalars(ctx, "hx_r", r, items);
+    uint32_t* de1 = buf<uint32_t>(ctx, "hx_e1", 32 * items);
+    uint32_t* dct = buf<uint32_t>(ctx, "hx_ct", 32 * items);
+    encrypt_device(ctx, D, n, dpk, ds, dsp, dr, de1, dct);
+    d2h(ctx, ok.data(), buf<uint8_t>(ctx, "hy.pk_ok", n), n);
+    d2h(ctx, e1, de1, 32 * items);
+    d2h(ctx, ct, dct, 32 * items);
+    sync(ctx);
+    for (auto v : ok)
+      if (!v) {
+        ctx->err = "encrypt_shares: a recipient public key does not decode";
+        return DKG_E_DECODE;
+      }
+    return DKG_OK;
+  });
+}
+
+int dkg_decrypt_shares(dkg_ctx* ctx, size_t D, size_t n, const uint8_t* sk, const uint8_t* e1, const uint8_t* ct,
+                       uint8_t* s, uint8_t* s_prime, uint8_t* ok) {
+  return guarded(ctx, [&] {
+    if (!sk || !e1 || !ct || !s || !s_prime) return DKG_E_ARG;
+    if (!D || !n) return DKG_OK;
+    const size_t items = 2 * D * n;
+    uint32_t* dsk = upload_scalars(ctx, "hx_sk", sk, n);
+    uint32_t* de1 = buf<uint32_t>(ctx, "hx_e1", 32 * items);
+    uint32_t* dct = buf<uint32_t>(ctx, "hx_ct", 32 * items);
+    h2d(ctx, de1, e1, 32 * items);
+    h2d(ctx, dct, ct, 32 * items);
+    uint32_t* ds = buf<uint32_t>(ctx, "hx_s", 32 * D * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "hx_sp", 32 * D * n);
+    uint8_t* iok = buf<uint8_t>(ctx, "hx_ok", items);
+    decrypt_device(ctx, D, n, dsk, de1, dct, ds, dsp, iok, nullptr);
+    d2h(ctx, s, ds, 32 * D * n);
+    d2h(ctx, s_prime, dsp, 32 * D * n);
+    if (ok) d2h(ctx, ok, iok, items);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+// Full-mode ceremony: round 1 with the shares hybrid-encrypted to the sorted member keys, the
+// receivers decrypting them in round 2 (timed inside ms_round1 / ms_round2), then rounds 2-5 on
+// the decrypted shares exactly as in plaintext mode.
+int dkg_ceremony_run_full_device(dkg_ctx* ctx, size_t n, size_t t, const void* d_a, const void* d_b, const void* d_r,
+                                 const uint8_t* sk, const uint8_t* pk, dkg_ceremony_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out || !sk || !pk || !d_r) return DKG_E_ARG;
+    const size_t N = t + 1, items = 2 * n * n;
+    uint32_t* dsk = upload_scalars(ctx, "fm_sk", sk, n);
+    uint32_t* dpk = buf<uint32_t>(ctx, "fm_pk", 32 * n);
+    h2d(ctx, dpk, pk, 32 * n);
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    uint32_t* Ec = buf<uint32_t>(ctx, "cer_E", 32 * n * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
+    uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
+    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    uint32_t* e1 = buf<uint32_t>(ctx, "fm_e1", 32 * items);
+    uint32_t* ct = buf<uint32_t>(ctx, "fm_ct", 32 * items);
+    encrypt_device(ctx, n, n, dpk, ds, dsp, (const uint32_t*)d_r, e1, ct);  // committee.rs:169-172
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    uint32_t* rs = buf<uint32_t>(ctx, "fm_s", 32 * n * n);
+    uint32_t* rsp = buf<uint32_t>(ctx, "fm_sp", 32 * n * n);
+    uint8_t* iok = buf<uint8_t>(ctx, "fm_iok", items);
+    uint8_t* eok = buf<uint8_t>(ctx, "fm_eok", n);
+    decrypt_device(ctx, n, n, dsk, e1, ct, rs, rsp, iok, eok);  // committee.rs:282-286
+    receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, false, eok);
+    out->ms_round1 = ev_ms(ctx, 0, 1);
+    out->ms_round2 = ev_ms(ctx, 1, 2);
+    out->ms_round3 = ev_ms(ctx, 2, 3);
+    out->ms_round4 = ev_ms(ctx, 3, 4);
+    out->ms_finalise = ev_ms(ctx, 4, 5);
+    out->ms_total = ev_ms(ctx, 0, 5);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_verify_full(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E, const uint8_t* A, const uint8_t* e1,
+                             const uint8_t* ct, const uint8_t* sk, dkg_ceremony_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out || !E || !A || !e1 || !ct || !sk) return DKG_E_ARG;
+    const size_t N = t + 1, items = 2 * n * n;
+    uint32_t* Ec = buf<uint32_t>(ctx, "cer_E", 32 * n * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
+    h2d(ctx, Ec, E, 32 * n * N);
+    h2d(ctx, Ac, A, 32 * n * N);
+    uint32_t* dsk = upload_scalars(ctx, "fm_sk", sk, n);
+    uint32_t* de1 = buf<uint32_t>(ctx, "fm_e1", 32 * items);
+    uint32_t* dct = buf<uint32_t>(ctx, "fm_ct", 32 * items);
+    h2d(ctx, de1, e1, 32 * items);
+    h2d(ctx, dct, ct, 32 * items);
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    uint32_t* rs = buf<uint32_t>(ctx, "fm_s", 32 * n * n);
+    uint32_t* rsp = buf<uint32_t>(ctx, "fm_sp", 32 * n * n);
+    uint8_t* iok = buf<uint8_t>(ctx, "fm_iok", items);
+    uint8_t* eok = buf<uint8_t>(ctx, "fm_eok", n);
+    decrypt_device(ctx, n, n, dsk, de1, dct, rs, rsp, iok, eok);
+    if (out->s) d2h(ctx, out->s, rs, 32 * n * n);
+    if (out->s_prime) d2h(ctx, out->s_prime, rsp, 32 * n * n);
+    receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, true, eok);
+    out->ms_round1 = 0;
+    out->ms_round2 = ev_ms(ctx, 1, 2);
+    out->ms_round3 = ev_ms(ctx, 2, 3);
+    out->ms_round4 = ev_ms(ctx, 3, 4);
+    out->ms_finalise = ev_ms(ctx, 4, 5);
+    out->ms_total = ev_ms(ctx, 0, 5);
     return DKG_OK;
   });
 }

@@ -16,7 +16,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import ACCEPT, REJECT, SKIPPED  # noqa: F401  (ACCEPT re-exported for callers)
+from ._lib import ACCEPT, MISSING, REJECT, SKIPPED  # noqa: F401  (ACCEPT re-exported for callers)
 
 
 def dealer_range(rank: int, world_size: int, n: int):
@@ -48,7 +48,8 @@ def combine_decisions(dec2: np.ndarray, dec4: np.ndarray, n: int, t: int) -> Dec
     dec2 = np.asarray(dec2, dtype=np.uint8).reshape(n, n)
     dec4 = np.array(dec4, dtype=np.uint8).reshape(n, n)
     rej2 = dec2 == REJECT
-    qualified = (~rej2.any(axis=1)).astype(np.uint8)
+    # MISSING (undecodable broadcast) disqualifies without a complaint (committee.rs:331-335)
+    qualified = (~(rej2 | (dec2 == MISSING)).any(axis=1)).astype(np.uint8)
     complaints = rej2.sum(axis=0).astype(np.int32)
     r2_error = (complaints > t).astype(np.uint8)
     off = ~np.eye(n, dtype=bool)

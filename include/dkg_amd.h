@@ -32,6 +32,9 @@ extern "C" {
 #define DKG_ACCEPT 1
 #define DKG_SELF 2       /* i == j: a party never checks itself (qualified_set starts at 1) */
 #define DKG_SKIPPED 3    /* round 4 only: dealer not qualified, check skipped (committee.rs:522) */
+#define DKG_MISSING 4    /* round 2 only: the dealer's broadcast does not decode (no data): it is
+                          * disqualified WITHOUT a complaint (committee.rs:331-335); in round 4 the
+                          * same case is an accusation (:549-555) and reads DKG_REJECT */
 
 typedef struct dkg_ctx dkg_ctx;
 
@@ -94,7 +97,8 @@ int dkg_share_gen(dkg_ctx *ctx, size_t D, size_t n, size_t t, const uint8_t *a, 
  * for dealers i in [d0, d1) and ALL receivers j in [0, n).  C = E (round 2) or A (round 4) of those
  * dealers, [d1-d0][t+1][32]; s, s_prime = the dealers' share rows [d1-d0][n][32] (s_prime unused in
  * round 4).  decision [d1-d0][n] (DKG_ACCEPT / DKG_REJECT / DKG_SELF).  A dealer whose commitment
- * vector does not decode is rejected by every receiver (and the call returns DKG_OK). */
+ * vector does not decode reads DKG_MISSING for every receiver in round 2 (disqualified without a
+ * complaint, committee.rs:331-335) and DKG_REJECT in round 4 (:549-555); the call returns DKG_OK. */
 int dkg_verify_pairs(dkg_ctx *ctx, size_t n, size_t t, int round, size_t d0, size_t d1, const uint8_t *C,
                      const uint8_t *s, const uint8_t *s_prime, uint8_t *decision);
 /* The same check seen from ONE receiver j (what one party runs in the reference): decisions of
@@ -178,6 +182,46 @@ int dkg_ceremony_batch_device(dkg_ctx *ctx, size_t B, size_t n, size_t t, const 
  * E, A [B*n][t+1][32]; s, s_prime [B*n][n][32] (row c*n + i = dealer i of ceremony c). */
 int dkg_ceremony_batch_verify(dkg_ctx *ctx, size_t B, size_t n, size_t t, const uint8_t *E, const uint8_t *A,
                               const uint8_t *s, const uint8_t *s_prime, dkg_batch_out *out);
+
+/* ---- full (encrypted-share) mode: the round-1 shares travel hybrid-encrypted
+ * (committee.rs:164-172) under the members' communication keys and each receiver decrypts its own
+ * (committee.rs:282-286).  Hybrid scheme (elgamal.rs:134-193): e1 = g*r, K = pk*r,
+ * e2 = m XOR ChaCha20(key = Blake2b-512(K)[0..32], nonce = [32..44]); decryption K = sk*e1;
+ * decrypted scalars are from_bits (groups.rs:29-36), reduced mod l on the device.
+ * Ciphertext arrays are [D dealer][n recipient][2][32] with [..][0] = the randomness s' and
+ * [..][1] = the share s (the reference encrypts the randomness first, committee.rs:171-172). ---- */
+/* Seeded MemberCommunicationKey for n members (procedure_keys.rs:72-82):
+ * sk_j = wide(ChaCha20Rng(BLAKE2b-256("dkg-amd/v1/member" || master || u32le ceremony || u32le j))),
+ * pk_j = g*sk_j; returned SORTED by public-key bytes (committee.rs:134-135, procedure_keys.rs:26-40):
+ * the party of index q+1 owns sk[q].  sk, pk [n][32]. */
+int dkg_member_keys(dkg_ctx *ctx, const uint8_t master[32], uint32_t ceremony, size_t n, uint8_t *sk, uint8_t *pk);
+/* Encryption randomness of dealers [d0, d0+D) for n recipients, continuing each dealer's seeded
+ * stream after its 2(t+1) coefficient draws: r [D][n][2][32] (host), and the device variant for B
+ * ceremonies (rows as dkg_dealer_coeffs_device). */
+int dkg_enc_randomness(const uint8_t master[32], uint32_t ceremony, size_t d0, size_t D, size_t n, size_t t,
+                       uint8_t *r);
+int dkg_enc_randomness_device(dkg_ctx *ctx, const uint8_t master[32], uint32_t ceremony0, size_t B, size_t d0,
+                              size_t D, size_t n, size_t t, void *d_r);
+/* Hybrid-encrypt the share rows of D dealers (s, s_prime [D][n][32]) to the n recipients' keys
+ * pk [n][32] with randomness r [D][n][2][32]: e1, ct [D][n][2][32].  DKG_E_DECODE if a key does
+ * not decode. */
+int dkg_encrypt_shares(dkg_ctx *ctx, size_t D, size_t n, const uint8_t *pk, const uint8_t *s, const uint8_t *s_prime,
+                       const uint8_t *r, uint8_t *e1, uint8_t *ct);
+/* Receivers' decryption with their secret keys sk [n][32]: s, s_prime [D][n][32];
+ * ok [D][n][2] (may be NULL) = e1 decoded (a ciphertext that does not decode is missing data). */
+int dkg_decrypt_shares(dkg_ctx *ctx, size_t D, size_t n, const uint8_t *sk, const uint8_t *e1, const uint8_t *ct,
+                       uint8_t *s, uint8_t *s_prime, uint8_t *ok);
+/* Whole ceremony in full mode from device coefficients d_a, d_b [n][t+1][32] and encryption
+ * randomness d_r [n][n][2][32]; sk, pk = dkg_member_keys output (host).  Encryption is timed in
+ * ms_round1, decryption in ms_round2. */
+int dkg_ceremony_run_full_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, const void *d_b, const void *d_r,
+                                 const uint8_t *sk, const uint8_t *pk, dkg_ceremony_out *out);
+/* Receiver side of a full-mode ceremony from (possibly tampered) broadcast values: E, A
+ * [n][t+1][32], e1, ct [n][n][2][32], the members' sorted secret keys sk [n][32].  A dealer with a
+ * ciphertext that does not decode is missing data (DKG_MISSING in round 2).  out->s / s_prime
+ * receive the decrypted shares. */
+int dkg_ceremony_verify_full(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *E, const uint8_t *A, const uint8_t *e1,
+                             const uint8_t *ct, const uint8_t *sk, dkg_ceremony_out *out);
 
 /* ---- synthetic inputs: the seeded RNG convention ----
  * dealer seed = BLAKE2b-256("dkg-amd/v1/dealer" || master[32] || u32le ceremony || u32le dealer);

@@ -107,8 +107,8 @@ int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8
       *out = 2;
       continue;
     }
-    if (bad[ii]) {
-      *out = 0;
+    if (bad[ii]) { /* no decodable broadcast: round 2 MISSING (committee.rs:331-335), round 4 REJECT (:549-555) */
+      *out = round == 2 ? 4 : 0;
       continue;
     }
     /* committee.rs:287-290 / 532-535: index_pow = from_u64(me).exp_iter().take(t+1) */

@@ -71,10 +71,21 @@ void or_share_gen(size_t D, size_t n, size_t t, const uint8_t *a, const uint8_t 
  * dealers [d0,d1) x receivers [r0,r1), computed as the reference does: lhs = h*s' + g*s (or g*s),
  * rhs = vartime MSM(j^0..j^t, C_i). C: [n][t+1][32]; s, sp: [n dealer][n receiver][32].
  * accept: byte matrix [d1-d0][r1-r0]; 1 = equal, 0 = reject, 2 = self (i == j, not checked).
- * Returns -1 if a commitment fails to decode (its dealer's row is then all 0). */
+ * Returns -1 if a commitment fails to decode: its dealer is missing data, so its row reads 4
+ * (DKG_MISSING: disqualified without a complaint, committee.rs:331-335) in round 2 and 0 in round 4. */
 int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8_t h[32],
                     const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
                     uint8_t *accept, int nthreads);
+/* ---- full (encrypted-share) mode: hybrid.c (elgamal.rs, procedure_keys.rs) ---- */
+void or_chacha20_ietf_xor(uint8_t *out, const uint8_t *in, size_t len, const uint8_t key[32],
+                          const uint8_t nonce[12]);
+/* e1 = G r, e2 = msg XOR ChaCha20(Blake2b-512(pk r)) (elgamal.rs:134-145, 172-193); -1 if pk is invalid */
+int or_hybrid_encrypt(uint8_t e1[32], uint8_t *e2, const uint8_t pk[32], const uint8_t r[32], const uint8_t *msg,
+                      size_t len);
+/* msg = e2 XOR ChaCha20(Blake2b-512(e1 sk)) (elgamal.rs:161-170); -1 if e1 does not decode */
+int or_hybrid_decrypt(uint8_t *msg, const uint8_t sk[32], const uint8_t e1[32], const uint8_t *e2, size_t len);
+void or_member_sk(uint8_t sk[32], const uint8_t master[32], uint32_t ceremony, uint32_t member);
+void or_enc_randomness(uint8_t *r, const uint8_t seed[32], size_t t, size_t n);
 /* Lagrange interpolation at x (polynomial.rs:162-184). */
 void or_lagrange(uint8_t out[32], const uint8_t x[32], const uint8_t *ys, const uint8_t *xs, size_t m);
 

@@ -35,6 +35,12 @@ def lib():
         _lib.or_chacha20_stream.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, sz]
         _lib.or_pt_hash_to_group.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
         _lib.or_sc_from_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+        cp = ctypes.c_char_p
+        _lib.or_chacha20_ietf_xor.argtypes = [cp, cp, sz, cp, cp]
+        _lib.or_hybrid_encrypt.argtypes = [cp, cp, cp, cp, cp, sz]
+        _lib.or_hybrid_decrypt.argtypes = [cp, cp, cp, cp, sz]
+        _lib.or_member_sk.argtypes = [cp, cp, ctypes.c_uint32, ctypes.c_uint32]
+        _lib.or_enc_randomness.argtypes = [cp, cp, sz, sz]
     return _lib
 
 
@@ -87,3 +93,27 @@ def verify_pairs(n, t, rnd, C, h, s, sp, d0, d1, r0, r1, nthreads=0):
     acc = _b((d1 - d0) * (r1 - r0))
     rc = lib().or_verify_pairs(n, t, rnd, C, h, s, sp or b"", d0, d1, r0, r1, acc, nthreads)
     return acc.raw, rc
+
+
+def hybrid_encrypt(pk: bytes, r: bytes, msg: bytes):
+    e1, e2 = _b(32), _b(len(msg))
+    rc = lib().or_hybrid_encrypt(e1, e2, pk, r, msg, len(msg))
+    return (e1.raw, e2.raw) if rc == 0 else None
+
+
+def hybrid_decrypt(sk: bytes, e1: bytes, e2: bytes):
+    m = _b(len(e2))
+    rc = lib().or_hybrid_decrypt(m, sk, e1, e2, len(e2))
+    return m.raw if rc == 0 else None
+
+
+def member_sk(master: bytes, ceremony: int, member: int):
+    out = _b(32)
+    lib().or_member_sk(out, master, ceremony, member)
+    return out.raw
+
+
+def enc_randomness(seed: bytes, t: int, n: int):
+    out = _b(64 * n)
+    lib().or_enc_randomness(out, seed, t, n)
+    return out.raw

@@ -60,3 +60,11 @@ def test_no_gpu_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(dkg_amd.DkgError):
         dkg_amd.Backend(0)
+
+
+@pytest.mark.parametrize("name", ["full_n4_t1.json", "full_n10_t4.json"])
+def test_enc_randomness_golden(golden, name):
+    """Host encryption randomness (committee.rs:171-172 draw order) against the libsodium fixture."""
+    c = golden(name)
+    r = dkg_amd.enc_randomness(bytes.fromhex(c["master_seed"]), c["ceremony"], 0, c["n"], c["n"], c["t"])
+    assert r.hex() == c["enc_r"]

@@ -9,7 +9,7 @@ import random
 import pytest
 
 import dkg_amd
-from dkg_amd import ACCEPT, REJECT, SELF
+from dkg_amd import ACCEPT, MISSING, REJECT, SELF
 from tests import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
@@ -298,8 +298,8 @@ def test_chunked_streams_identical(be, round_):
     exp = bytearray(ACCEPT for _ in range(n * n))
     for i, j in flips:
         exp[i * n + j] = REJECT
-    for j in range(n):
-        exp[bad_dealer * n + j] = REJECT
+    for j in range(n):  # no decodable broadcast: MISSING in round 2 (no complaint), REJECT in round 4
+        exp[bad_dealer * n + j] = MISSING if round_ == 2 else REJECT
     for i in range(n):
         exp[i * n + i] = SELF
     try:
@@ -437,3 +437,124 @@ def test_dealer_coefficients_device(be, c0, B, d0, D, t):
         a, b = dkg_amd.dealer_coefficients(master, c0 + c, d0, D, t)
         assert ga[32 * N * D * c:32 * N * D * (c + 1)] == a
         assert gb[32 * N * D * c:32 * N * D * (c + 1)] == b
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_ceremony_undecodable_broadcast(be, golden, overlap):
+    """A dealer whose round-1 broadcast does not decode (CompressedRistretto::decompress -> None,
+    groups.rs:78-81) is missing data: disqualified by everyone WITHOUT a complaint
+    (committee.rs:331-335), so complaints / r2 errors stay as in the honest run; its round-4 row is
+    SKIPPED and it drops out of the final shares and the master key."""
+    c = golden("ceremony_n10_t4.json")
+    n, t = c["n"], c["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    bad = 3
+    E = bytearray(H(c["E"]))
+    E[32 * (N * bad + 2) + 31] |= 0x80  # bit 255 set: not a canonical encoding
+    be.set_overlap(overlap)
+    try:
+        r = be.ceremony_verify(bytes(E), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+    finally:
+        be.set_overlap(True)
+    assert [r.dec2[bad * n + j] for j in range(n)] == [SELF if j == bad else MISSING for j in range(n)]
+    assert r.complaints2 == c["complaints2"] == [0] * n and r.r2_error == [0] * n
+    assert r.qualified == [0 if i == bad else 1 for i in range(n)]
+    assert [r.dec4[bad * n + j] for j in range(n)] == [SELF if j == bad else 3 for j in range(n)]
+    s = H(c["s"])
+    a = H(c["a"])
+    fs = b"".join((sum(int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+                       for i in range(n) if i != bad) % L).to_bytes(32, "little") for j in range(n))
+    assert r.final_share == fs
+    secret = sum(int.from_bytes(a[32 * N * i:32 * N * i + 32], "little") for i in range(n) if i != bad) % L
+    assert r.mpk == O.base_mul(secret.to_bytes(32, "little"))
+
+
+# ---------------- full (encrypted-share) mode: elgamal.rs / procedure_keys.rs ----------------
+FULL = ["full_n4_t1.json", "full_n10_t4.json", "full_faults_n10_t4.json"]
+
+
+def test_member_keys_golden(be, golden):
+    """Seeded member keys sorted by public key (committee.rs:134-135) as in the fixtures."""
+    for name in ("full_n4_t1.json", "full_n10_t4.json"):
+        c = golden(name)
+        sk, pk = be.member_keys(H(c["master_seed"]), c["ceremony"], c["n"])
+        assert sk.hex() == c["member_sk"] and pk.hex() == c["member_pk"]
+
+
+def test_hybrid_kat_device(be, golden):
+    """Device encryption / decryption of the libsodium hybrid vectors (elgamal.rs:134-193): each KAT
+    is a 1-dealer x 1-recipient batch whose two ciphertexts carry msg (w = 0) and msg reversed (w = 1)."""
+    k = golden("kat_hybrid.json")
+    for c in k["hybrid"]:
+        msg = H(c["msg"])
+        if int.from_bytes(msg, "little") >= L:
+            continue  # the share arrays hold canonical scalars
+        r = H(c["r"]) * 2
+        e1, ct = be.encrypt_shares(H(c["pk"]), msg, msg, r, 1, 1)
+        assert e1[:32].hex() == c["e1"] and ct[:32].hex() == c["e2"]
+        assert e1[32:] == e1[:32] and ct[32:] == ct[:32]
+        s, sp, ok = be.decrypt_shares(H(c["sk"]), e1, ct, 1, 1)
+        assert s == msg and sp == msg and ok == b"\x01\x01"
+
+
+@pytest.mark.parametrize("name", FULL)
+def test_full_mode_verify_golden(be, golden, name):
+    """Receivers decrypt the (possibly tampered) golden ciphertexts on the GPU and run rounds 2-5:
+    every output bit for bit, including the complaints raised by tampered ciphertexts."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    r = be.ceremony_verify_full(H(c["E"]), H(c["A"]), H(c["e1"]), H(c["ct"]), H(c["member_sk"]), n, t)
+    assert r.s.hex() == c["s"] and r.s_prime.hex() == c["s_prime"]
+    _check_ceremony(c, r, n)
+
+
+@pytest.mark.parametrize("name", ["full_n4_t1.json", "full_n10_t4.json"])
+def test_full_mode_device_ceremony(be, golden, name):
+    """Whole full-mode ceremony on the device from seeded coefficients, encryption randomness and
+    member keys; the ciphertexts the device produced decrypt (on the oracle) to the golden shares."""
+    import torch
+
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    master = H(c["master_seed"])
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(32 * n * N, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    tr = torch.empty(64 * n * n, dtype=torch.uint8, device=dev)
+    be.dealer_coefficients_device(master, c["ceremony"], 1, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    be.enc_randomness_device(master, c["ceremony"], 1, 0, n, n, t, tr.data_ptr())
+    assert bytes(tr.cpu().numpy()).hex() == c["enc_r"]
+    sk, pk = be.member_keys(master, c["ceremony"], n)
+    r = be.ceremony_full_device(ta.data_ptr(), tb.data_ptr(), tr.data_ptr(), sk, pk, n, t)
+    assert r.mpk.hex() == c["mpk"] and r.qualified == c["qualified"] and r.n_qualified == n
+    # the host-buffer encryption entry point reproduces the golden wire ciphertexts
+    e1, ct = be.encrypt_shares(pk, H(c["s"]), H(c["s_prime"]), H(c["enc_r"]), n, n)
+    assert e1.hex() == c["e1"] and ct.hex() == c["ct"]
+
+
+def test_full_mode_oracle_random(be):
+    """Random keys / messages / randomness: device encryption equals the CPU oracle's, and device
+    decryption inverts it (a wrong key does not)."""
+    rng = random.Random(11)
+    D, n = 3, 5
+    sks = [rng.randrange(1, L).to_bytes(32, "little") for _ in range(n)]
+    pks = [O.base_mul(k) for k in sks]
+    s = b"".join(rng.randrange(L).to_bytes(32, "little") for _ in range(D * n))
+    sp = b"".join(rng.randrange(L).to_bytes(32, "little") for _ in range(D * n))
+    r = b"".join(rng.randrange(L).to_bytes(32, "little") for _ in range(2 * D * n))
+    e1, ct = be.encrypt_shares(b"".join(pks), s, sp, r, D, n)
+    for i in range(D):
+        for q in range(n):
+            for w, msg in ((0, sp), (1, s)):
+                k = 2 * (i * n + q) + w
+                oe1, oct_ = O.hybrid_encrypt(pks[q], r[32 * k:32 * k + 32], msg[32 * (i * n + q):32 * (i * n + q) + 32])
+                assert (oe1, oct_) == (e1[32 * k:32 * k + 32], ct[32 * k:32 * k + 32])
+    ds, dsp, ok = be.decrypt_shares(b"".join(sks), e1, ct, D, n)
+    assert ds == s and dsp == sp and set(ok) == {1}
+    wrong = b"".join(sks[1:] + sks[:1])
+    ds2, _, _ = be.decrypt_shares(wrong, e1, ct, D, n)
+    assert ds2 != s

@@ -165,3 +165,57 @@ def test_spot_n256(golden):
             pw = b"".join(pow(j + 1, k, 2**252 + 27742317777372353535851937790883648493).to_bytes(32, "little")
                           for k in range(t + 1))
             assert O.msm(pw, H(d["E"])).hex() == pr["rhs2"]
+
+
+# ---------------- full (encrypted-share) mode: elgamal.rs / procedure_keys.rs ----------------
+FULL = ["full_n4_t1.json", "full_n10_t4.json", "full_faults_n10_t4.json"]
+
+
+def test_hybrid_kat(golden):
+    """Oracle hybrid encryption (elgamal.rs:134-193) against the libsodium vectors."""
+    k = golden("kat_hybrid.json")
+    for c in k["hybrid"]:
+        e1, e2 = O.hybrid_encrypt(H(c["pk"]), H(c["r"]), H(c["msg"]))
+        assert (e1.hex(), e2.hex()) == (c["e1"], c["e2"])
+        assert O.hybrid_decrypt(H(c["sk"]), e1, e2).hex() == c["msg"]
+        assert O.call32("or_pt_mul", H(c["pk"]), H(c["r"]))[0].hex() == c["K"]
+    assert O.member_sk(bytes(32), 0, 0).hex() == k["member_sk0"]
+
+
+def _member_keys(master, ceremony, n):
+    sks = [O.member_sk(master, ceremony, j) for j in range(n)]
+    pks = [O.base_mul(sk) for sk in sks]
+    order = sorted(range(n), key=lambda j: pks[j])  # procedure_keys.rs:26-40, committee.rs:134-135
+    return [sks[j] for j in order], [pks[j] for j in order]
+
+
+@pytest.mark.parametrize("name", FULL)
+def test_full_mode_ceremony(golden, name):
+    """Full mode end to end on the oracle: sorted member keys, the draw order of the encryption
+    randomness, every ciphertext of the honest pairs, decryption of the (possibly tampered) wire
+    ciphertexts, and the round-2/4 decisions on the decrypted shares."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    master = H(c["master_seed"])
+    sks, pks = _member_keys(master, c["ceremony"], n)
+    assert b"".join(sks).hex() == c["member_sk"] and b"".join(pks).hex() == c["member_pk"]
+    r = b"".join(O.enc_randomness(O.dealer_seed(master, c["ceremony"], i), t, n) for i in range(n))
+    assert r.hex() == c["enc_r"]
+    a = b"".join(O.dealer_coeffs(O.dealer_seed(master, c["ceremony"], i), t)[0] for i in range(n))
+    b = b"".join(O.dealer_coeffs(O.dealer_seed(master, c["ceremony"], i), t)[1] for i in range(n))
+    E, A, s, sp = O.share_gen(n, n, t, a, b, H(c["h"]))
+    e1w, ctw = H(c["e1"]), H(c["ct"])
+    tampered = {(f["dealer"] - 1, f["receiver"] - 1) for f in c["faults"]}
+    dec_s, dec_sp = bytearray(32 * n * n), bytearray(32 * n * n)
+    for i in range(n):
+        for q in range(n):
+            for w, msg in ((0, sp), (1, s)):  # randomness ciphertext first (committee.rs:171-172)
+                k = 2 * (i * n + q) + w
+                if (i, q) not in tampered:
+                    e1, e2 = O.hybrid_encrypt(pks[q], r[32 * k:32 * k + 32], msg[32 * (i * n + q):32 * (i * n + q) + 32])
+                    assert (e1, e2) == (e1w[32 * k:32 * k + 32], ctw[32 * k:32 * k + 32]), (i, q, w)
+                m = O.hybrid_decrypt(sks[q], e1w[32 * k:32 * k + 32], ctw[32 * k:32 * k + 32])
+                red = O.call32("or_sc_reduce", bytes(m[:31]) + bytes([m[31] & 0x7f]))[0]  # from_bits, reduced
+                (dec_sp if w == 0 else dec_s)[32 * (i * n + q):32 * (i * n + q) + 32] = red
+    assert bytes(dec_s).hex() == c["s"] and bytes(dec_sp).hex() == c["s_prime"]
+    assert _decisions(c, 2)[0] == bytes(int(x) for x in c["dec2"])

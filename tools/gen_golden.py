@@ -143,7 +143,7 @@ def lagrange_at_zero(ys, xs):
 
 
 # ---------------- the ceremony (plaintext-share mode) ----------------
-def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True):
+def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transport=None):
     """Returns a dict of inputs/outputs.  faults: list of dicts
        {"kind": "E_identity", "dealer": i} (committee.rs:1127-1128 style),
        {"kind": "share_flip", "dealer": i, "receiver": j}   s_ij += 1,
@@ -169,6 +169,9 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True):
     Aw = [list(x) for x in Apub]
     Sw = [list(s) for s in S]
     SPw = [list(s) for s in SP]
+    extra = {}
+    if transport is not None:  # full mode: shares travel hybrid-encrypted (committee.rs:169-172, 282-286)
+        Sw, SPw, extra = transport(S, SP)
     for f in faults:
         i = f["dealer"] - 1
         if f["kind"] == "E_identity":
@@ -239,11 +242,137 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True):
         "public_share": "".join(hx(p) for p in public_share),
         "mpk": hx(mpk),
     }
+    out.update(extra)
     if with_coeffs:
         out["a"] = "".join(hx(scb(x)) for row in A for x in row)
         out["b"] = "".join(hx(scb(x)) for row in B for x in row)
         out["dealer_seeds"] = [hx(dealer_seed(master, ceremony_id, i)) for i in range(n)]
     return out
+
+
+# ---------------- full (encrypted-share) mode: elgamal.rs hybrid encryption ----------------
+def member_seed(master, ceremony, member):
+    return hashlib.blake2b(b"dkg-amd/v1/member" + master + ceremony.to_bytes(4, "little")
+                           + member.to_bytes(4, "little"), digest_size=32).digest()
+
+
+def member_keys(master, ceremony_id, n):
+    """MemberCommunicationKey::new per member (procedure_keys.rs:72-76) from the seeded convention,
+    returned SORTED by public-key bytes (procedure_keys.rs:26-40 Ord; committee.rs:134-135): the
+    party of index q+1 is the q-th smallest key."""
+    sks = [wide_reduce(chacha_stream(member_seed(master, ceremony_id, j), 64)) for j in range(n)]
+    pks = [gmul_base(sk) for sk in sks]
+    order = sorted(range(n), key=lambda j: pks[j])
+    return [sks[j] for j in order], [pks[j] for j in order]
+
+
+def enc_randomness(seed, t, n):
+    """Scalar::random draws after the two polynomials (committee.rs:171-172, elgamal.rs:137):
+    recipient q takes block 2(t+1) + 2q for the randomness ciphertext, the next for the share."""
+    N = t + 1
+    st = chacha_stream(seed, (2 * N + 2 * n) * 64)
+    return [[wide_reduce(st[64 * (2 * N + 2 * q + w):64 * (2 * N + 2 * q + w + 1)]) for w in range(2)]
+            for q in range(n)]
+
+
+def sym_keystream(K, nbytes):
+    """SymmetricKey::initialise_encryption (elgamal.rs:175-181): Blake2b-512 of the group element,
+    key = h[0..32], nonce = h[32..44], ChaCha20 (IETF, counter 0)."""
+    hh = hashlib.blake2b(K, digest_size=64).digest()
+    o = buf(nbytes)
+    SO.crypto_stream_chacha20_ietf(o, ctypes.c_ulonglong(nbytes), hh[32:44], hh[:32])
+    return o.raw
+
+
+def hybrid_encrypt(pk, r, msg):
+    """PublicKey::hybrid_encrypt (elgamal.rs:134-145): e1 = g r, e2 = msg XOR keystream(pk r)."""
+    ks = sym_keystream(gmul(pk, r), len(msg))
+    return gmul_base(r), bytes(x ^ y for x, y in zip(msg, ks))
+
+
+def hybrid_decrypt(sk, e1, e2):
+    """SecretKey::hybrid_decrypt (elgamal.rs:161-170): keystream(e1 sk) XOR e2."""
+    ks = sym_keystream(gmul(e1, sk), len(e2))
+    return bytes(x ^ y for x, y in zip(e2, ks))
+
+
+def from_bits(b32):
+    """Scalar::from_bytes = from_bits (groups.rs:29-36): bit 255 cleared; the device reduces mod l."""
+    return int.from_bytes(b32, "little") & ((1 << 255) - 1)
+
+
+def full_ceremony(n, t, master, ceremony_id=0, faults=None):
+    """The same ceremony with the shares hybrid-encrypted to the recipients' communication keys
+    (committee.rs:164-172) and decrypted by each receiver (committee.rs:282-286,
+    procedure_keys.rs:88-105).  Extra faults act on the ciphertexts:
+       {"kind": "ct_flip", "dealer": i, "receiver": j, "which": w, "byte": b}  e2 byte b ^= 1,
+       {"kind": "e1_generator", "dealer": i, "receiver": j, "which": w}          e1 := g
+    with w = 0 (randomness / s' ciphertext) or 1 (share / s ciphertext)."""
+    faults = faults or []
+    sks, pks = member_keys(master, ceremony_id, n)
+    ct_faults = [f for f in faults if f["kind"] in ("ct_flip", "e1_generator")]
+    plain_faults = [f for f in faults if f["kind"] in ("share_flip", "rand_flip")]  # before encryption
+
+    def transport(S, SP):
+        S = [list(r) for r in S]
+        SP = [list(r) for r in SP]
+        for f in plain_faults:
+            i, j = f["dealer"] - 1, f["receiver"] - 1
+            if f["kind"] == "share_flip":
+                S[i][j] = (S[i][j] + 1) % L
+            else:
+                SP[i][j] = (SP[i][j] + 1) % L
+        E1 = []
+        Sd = [[0] * n for _ in range(n)]
+        SPd = [[0] * n for _ in range(n)]
+        for i in range(n):
+            R = enc_randomness(dealer_seed(master, ceremony_id, i), t, n)
+            for q in range(n):
+                pair = []
+                for w, msg in ((0, SP[i][q]), (1, S[i][q])):   # randomness first (committee.rs:171-172)
+                    e1, e2 = hybrid_encrypt(pks[q], R[q][w], scb(msg))
+                    for f in ct_faults:
+                        if (f["dealer"] - 1, f["receiver"] - 1, f["which"]) == (i, q, w):
+                            if f["kind"] == "ct_flip":
+                                e2 = e2[:f["byte"]] + bytes([e2[f["byte"]] ^ 1]) + e2[f["byte"] + 1:]
+                            else:
+                                e1 = gmul_base(1)
+                    pair.append((e1, e2))
+                    dm = from_bits(hybrid_decrypt(sks[q], e1, e2)) % L
+                    if w == 0:
+                        SPd[i][q] = dm
+                    else:
+                        Sd[i][q] = dm
+                E1.append(pair)
+        extra = {"mode": "full", "member_sk": "".join(hx(scb(x)) for x in sks),
+                 "member_pk": "".join(hx(p) for p in pks),
+                 "e1": "".join(hx(e1) for pair in E1 for e1, _ in pair),
+                 "ct": "".join(hx(e2) for pair in E1 for _, e2 in pair),
+                 "enc_r": "".join(hx(scb(x)) for i in range(n)
+                                  for rr in enc_randomness(dealer_seed(master, ceremony_id, i), t, n) for x in rr)}
+        return Sd, SPd, extra
+
+    other = [f for f in faults if f not in ct_faults and f not in plain_faults]
+    out = ceremony(n, t, master, ceremony_id, faults=other, transport=transport)
+    out["faults"] = faults
+    return out
+
+
+def kat_hybrid(rng):
+    """elgamal.rs hybrid encryption vectors: (pk, r, msg) -> (e1, e2), and back with sk."""
+    cases = []
+    for k in range(6):
+        sk = rng.randrange(1, L)
+        pk = gmul_base(sk)
+        r = rng.randrange(1, L)
+        msg = scb(rng.randrange(L)) if k < 5 else bytes(range(32))
+        e1, e2 = hybrid_encrypt(pk, r, msg)
+        assert hybrid_decrypt(sk, e1, e2) == msg
+        cases.append({"sk": hx(scb(sk)), "pk": hx(pk), "r": hx(scb(r)), "msg": hx(msg), "e1": hx(e1),
+                      "e2": hx(e2), "K": hx(gmul(pk, r))})
+    seed = member_seed(bytes(32), 0, 0)
+    return {"hybrid": cases, "member_seed0": hx(seed),
+            "member_sk0": hx(scb(wide_reduce(chacha_stream(seed, 64))))}
 
 
 def kat_group(rng):
@@ -378,6 +507,13 @@ def main():
     }
     for name, fs in faults.items():
         files[f"fault_{name}_n10_t4.json"] = ceremony(10, 4, m, ceremony_id=1, faults=fs)
+    files["kat_hybrid.json"] = kat_hybrid(random.Random(7))
+    files["full_n4_t1.json"] = full_ceremony(4, 1, m, ceremony_id=3)
+    files["full_n10_t4.json"] = full_ceremony(10, 4, m, ceremony_id=4)
+    files["full_faults_n10_t4.json"] = full_ceremony(10, 4, m, ceremony_id=4, faults=[
+        {"kind": "ct_flip", "dealer": 3, "receiver": 5, "which": 1, "byte": 7},
+        {"kind": "e1_generator", "dealer": 6, "receiver": 2, "which": 0},
+        {"kind": "share_flip", "dealer": 9, "receiver": 1}])
     files["spot_n256_t127.json"] = spot(256, 127, m, [0, 200], [1, 17, 255])
     files["spot_n1024_t511.json"] = spot(1024, 511, m, [513], [0, 1023])
     for name, obj in files.items():
