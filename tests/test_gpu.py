@@ -558,3 +558,35 @@ def test_full_mode_oracle_random(be):
     wrong = b"".join(sks[1:] + sks[:1])
     ds2, _, _ = be.decrypt_shares(wrong, e1, ct, D, n)
     assert ds2 != s
+
+
+def test_ceremony_n4096_device(be):
+    """BASELINE config 4 (n = 4096, t = 2047) end to end on one GPU from device-generated
+    coefficients: every share of both rounds verifies and mpk == g * sum_i a_i0 (committee.rs:
+    1633-1647); then rank 0 of the 8-way dealer split (dkg_ceremony_shard_device) accepts its rows."""
+    import torch
+
+    n, t = 4096, 2047
+    N = t + 1
+    be.env_init(t, n, CK)
+    master = bytes([4]) * 32
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(32 * n * N, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    be.dealer_coefficients_device(master, 0, 1, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    r = be.ceremony_device(ta.data_ptr(), tb.data_ptr(), n, t)
+    assert r.qualified == [1] * n and r.complaints2 == [0] * n and r.n_qualified == n
+    a0 = ta.view(n, N, 32)[:, 0, :].cpu().numpy()
+    secret = sum(int.from_bytes(bytes(a0[i]), "little") for i in range(n)) % L
+    assert r.mpk == O.base_mul(secret.to_bytes(32, "little"))
+    D = n // 8
+    o2 = torch.empty(D * n, dtype=torch.uint8, device=dev)
+    o4 = torch.empty_like(o2)
+    oA = torch.empty(D * 32, dtype=torch.uint8, device=dev)
+    op = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    be.ceremony_shard_device(n, t, 0, D, ta.data_ptr(), tb.data_ptr(), o2.data_ptr(), o4.data_ptr(), oA.data_ptr(),
+                             op.data_ptr())
+    m2, m4 = o2.view(D, n).cpu().numpy(), o4.view(D, n).cpu().numpy()
+    for i in range(D):
+        assert m2[i, i] == SELF and m4[i, i] == SELF
+    assert (m2 != 0).all() and (m4 != 0).all() and int((m2 == ACCEPT).sum()) == D * (n - 1)
