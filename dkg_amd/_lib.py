@@ -95,6 +95,9 @@ def lib():
     L.dkg_decrypt_shares.argtypes = [p, sz, sz, u8p, u8p, u8p, p, p, p]
     L.dkg_ceremony_run_full_device.argtypes = [p, sz, sz, p, p, p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_verify_full.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
+    L.dkg_misbehaviour_prove.argtypes = [p, sz, u8p, u8p, u8p, p]
+    L.dkg_complaint1_verify.argtypes = [p, sz, sz, p, u8p, u8p, u8p, u8p, p]
+    L.dkg_complaint3_verify.argtypes = [p, sz, sz, p, u8p, u8p, u8p, u8p, p]
     L.dkg_dealer_coeffs.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, p, p]
     L.dkg_scalar_sum_device.argtypes = [p, sz, sz, p, p, p]
     L.dkg_point_sum_device.argtypes = [p, sz, p, p, p]
@@ -110,6 +113,6 @@ EXPORTED = [
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
     "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_member_keys", "dkg_enc_randomness",
     "dkg_enc_randomness_device", "dkg_encrypt_shares", "dkg_decrypt_shares", "dkg_ceremony_run_full_device",
-    "dkg_ceremony_verify_full", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
+    "dkg_ceremony_verify_full", "dkg_misbehaviour_prove", "dkg_complaint1_verify", "dkg_complaint3_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
     "dkg_scalar_sum_device", "dkg_point_sum_device",
 ]

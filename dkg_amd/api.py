@@ -260,6 +260,28 @@ class Backend:
         r.E, r.A = E, A
         return r
 
+    # ---- complaint proofs (broadcast.rs)
+    def misbehaviour_prove(self, sk: bytes, enc: bytes, w: bytes) -> bytes:
+        """ProofOfMisbehaviour::generate for B = len(sk) // 32 complaints: proofs [B][192]."""
+        B = len(sk) // 32
+        out = ctypes.create_string_buffer(max(192 * B, 1))
+        _check(self._ctx, _lib.lib().dkg_misbehaviour_prove(self._ctx, B, sk, enc, w, out))
+        return out.raw[:192 * B]
+
+    def complaint1_verify(self, t: int, accusers: List[int], pk: bytes, enc: bytes, E: bytes, proofs: bytes):
+        B = len(accusers)
+        acc = (ctypes.c_uint32 * max(B, 1))(*accusers)
+        res = (ctypes.c_int32 * max(B, 1))()
+        _check(self._ctx, _lib.lib().dkg_complaint1_verify(self._ctx, B, t, acc, pk, enc, E, proofs, res))
+        return list(res)[:B]
+
+    def complaint3_verify(self, t: int, accusers: List[int], share: bytes, randomness: bytes, E: bytes, A: bytes):
+        B = len(accusers)
+        acc = (ctypes.c_uint32 * max(B, 1))(*accusers)
+        res = (ctypes.c_int32 * max(B, 1))()
+        _check(self._ctx, _lib.lib().dkg_complaint3_verify(self._ctx, B, t, acc, share, randomness, E, A, res))
+        return list(res)[:B]
+
     def dealer_coefficients_device(self, master: bytes, ceremony0: int, B: int, d0: int, D: int, t: int,
                                    d_a: int, d_b: int):
         """dkg_dealer_coeffs on the GPU for B ceremonies: rows [B*D][t+1][32] at device pointers."""

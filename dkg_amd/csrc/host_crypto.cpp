@@ -104,6 +104,37 @@ void chacha20(const uint8_t key[32], uint64_t block, uint8_t* out, size_t len) {
   }
 }
 
+void chacha20_ietf_xor(uint8_t* out, const uint8_t* in, size_t len, const uint8_t key[32], const uint8_t nonce[12]) {
+  auto rd = [](const uint8_t* p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+  };
+  auto rotl = [](uint32_t x, int n) { return (x << n) | (x >> (32 - n)); };
+  uint32_t counter = 0;
+  while (len) {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 8; i++) s[4 + i] = rd(key + 4 * i);
+    s[12] = counter++;
+    for (int i = 0; i < 3; i++) s[13 + i] = rd(nonce + 4 * i);
+    uint32_t x[16];
+    memcpy(x, s, sizeof s);
+    auto QR = [&](int a, int b, int c, int d) {
+      x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 16);
+      x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 12);
+      x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 8);
+      x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 7);
+    };
+    for (int r = 0; r < 10; r++) {
+      QR(0, 4, 8, 12); QR(1, 5, 9, 13); QR(2, 6, 10, 14); QR(3, 7, 11, 15);
+      QR(0, 5, 10, 15); QR(1, 6, 11, 12); QR(2, 7, 8, 13); QR(3, 4, 9, 14);
+    }
+    size_t n = len < 64 ? len : 64;
+    for (size_t i = 0; i < n; i++) out[i] = in[i] ^ (uint8_t)((x[i / 4] + s[i / 4]) >> (8 * (i % 4)));
+    out += n;
+    in += n;
+    len -= n;
+  }
+}
+
 // ---- Z_l: fold 32 bits at a time from the top with 2^252 = -delta (mod l) ----
 namespace {
 typedef unsigned __int128 u128;

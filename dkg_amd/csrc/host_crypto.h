@@ -10,6 +10,9 @@ namespace dkgh {
 void blake2b(uint8_t* out, size_t outlen, const uint8_t* in, size_t inlen);
 // ChaCha20 keystream (key = seed, 64-bit block counter from `block`, zero stream id)
 void chacha20(const uint8_t key[32], uint64_t block, uint8_t* out, size_t len);
+// RFC 8439 ChaCha20 (96-bit nonce, 32-bit counter from 0) XOR -- chacha20 0.7 `ChaCha20`, used by
+// SymmetricKey::process (elgamal.rs:172-193) on the (cold) complaint-proof path
+void chacha20_ietf_xor(uint8_t* out, const uint8_t* in, size_t len, const uint8_t key[32], const uint8_t nonce[12]);
 
 struct Zl {  // canonical element of Z_l, little-endian 64-bit limbs
   uint64_t w[4];

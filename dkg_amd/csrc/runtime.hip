@@ -589,6 +589,71 @@ void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const 
   check_launch(ctx);
 }
 
+// ---- complaint proofs (dl_equality/zkp.rs, broadcast.rs:50-135, 181-283)
+// Cold path (one proof per complaint): the group work goes to the GPU as batched MSMs (k_msm), the
+// Fiat-Shamir hashes, ChaCha20 and scalar arithmetic run on the host.
+// B MSMs of N terms: scalars / points host [B][N][32] -> out [B][32]; ok[b] = every point decodes.
+void msm_host(dkg_ctx* ctx, size_t B, size_t N, const uint8_t* scalars, const uint8_t* points, uint8_t* out,
+              std::vector<uint8_t>& ok) {
+  ok.assign(B, 1);
+  if (!B) return;
+  uint32_t* sc = upload_scalars(ctx, "cp_sc", scalars, B * N);
+  uint32_t* pc = buf<uint32_t>(ctx, "cp_pc", 32 * B * N);
+  uint32_t* pe = buf<uint32_t>(ctx, "cp_pe", PTB * B * N);
+  uint8_t* pok = buf<uint8_t>(ctx, "cp_ok", B * N);
+  h2d(ctx, pc, points, 32 * B * N);
+  dkgk::decode_points(pc, B * N, pe, B * N, pok, ctx->stream);
+  uint32_t* oe = buf<uint32_t>(ctx, "cp_oe", PTB * B);
+  uint32_t* oc = buf<uint32_t>(ctx, "cp_oc", 32 * B);
+  dkgk::msm_batch(B, N, sc, pe, B * N, oe, ctx->stream);
+  dkgk::encode_points(oe, B, B, oc, ctx->stream);
+  check_launch(ctx);
+  std::vector<uint8_t> okh(B * N);
+  d2h(ctx, okh.data(), pok, B * N);
+  d2h(ctx, out, oc, 32 * B);
+  sync(ctx);
+  for (size_t b = 0; b < B; b++)
+    for (size_t k = 0; k < N; k++) ok[b] &= okh[b * N + k];
+}
+
+dkgh::Zl zl32(const uint8_t* p) { return dkgh::zl_from_bytes_wide(p, 32); }
+void put32(std::vector<uint8_t>& v, const uint8_t* p) { v.insert(v.end(), p, p + 32); }
+void putzl(std::vector<uint8_t>& v, const dkgh::Zl& z) {
+  uint8_t b[32];
+  dkgh::zl_to_bytes(b, z);
+  put32(v, b);
+}
+
+// Scalar::hash_from_bytes::<Blake2b> (groups.rs:50-52) of ChallengeContext b1||b2||p1||p2||a1||a2
+// (challenge_context.rs:14-41)
+dkgh::Zl dleq_challenge(const uint8_t* b1, const uint8_t* b2, const uint8_t* p1, const uint8_t* p2, const uint8_t* a1,
+                        const uint8_t* a2) {
+  uint8_t buf_[192], h[64];
+  const uint8_t* parts[6] = {b1, b2, p1, p2, a1, a2};
+  for (int i = 0; i < 6; i++) memcpy(buf_ + 32 * i, parts[i], 32);
+  dkgh::blake2b(h, 64, buf_, 192);
+  return dkgh::zl_from_bytes_wide(h, 64);
+}
+
+// SymmetricKey::process + Scalar::from_bytes (from_bits, reduced) of a 32-byte ciphertext
+dkgh::Zl sym_scalar(const uint8_t K[32], const uint8_t ct[32]) {
+  uint8_t h[64], m[32];
+  dkgh::blake2b(h, 64, K, 32);
+  dkgh::chacha20_ietf_xor(m, ct, 32, h, h + 32);
+  m[31] &= 0x7f;
+  return zl32(m);
+}
+
+std::vector<uint8_t> index_powers(uint32_t j, size_t N) {  // from_u64(j).exp_iter().take(N)
+  std::vector<uint8_t> out;
+  dkgh::Zl x = dkgh::zl_from_u64(j), p = dkgh::zl_from_u64(1);
+  for (size_t k = 0; k < N; k++) {
+    putzl(out, p);
+    p = dkgh::zl_mul(p, x);
+  }
+  return out;
+}
+
 int need_env(dkg_ctx* ctx) {
   if (!ctx->have_h) {
     ctx->err = "dkg_env_init has not been called (commitment key unknown)";
@@ -1302,6 +1367,140 @@ int dkg_ceremony_verify_full(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E,
     out->ms_round4 = ev_ms(ctx, 3, 4);
     out->ms_finalise = ev_ms(ctx, 4, 5);
     out->ms_total = ev_ms(ctx, 0, 5);
+    return DKG_OK;
+  });
+}
+
+int dkg_misbehaviour_prove(dkg_ctx* ctx, size_t B, const uint8_t* sk, const uint8_t* enc, const uint8_t* w,
+                           uint8_t* proofs) {
+  return guarded(ctx, [&] {
+    if (!sk || !enc || !w || !proofs) return DKG_E_ARG;
+    if (!B) return DKG_OK;
+    // per complaint 7 single-term products: K_share, K_rand, pk, and the two DLEQ announcements
+    std::vector<uint8_t> sc, pt, out(32 * 7 * B);
+    for (size_t b = 0; b < B; b++) {
+      const uint8_t *e1r = enc + 128 * b, *e1s = e1r + 64, *x = sk + 32 * b, *w1 = w + 64 * b, *w2 = w1 + 32;
+      const uint8_t* P[7] = {e1s, e1r, BASEPOINT, BASEPOINT, e1s, BASEPOINT, e1r};
+      const uint8_t* S[7] = {x, x, x, w1, w1, w2, w2};
+      for (int k = 0; k < 7; k++) {
+        put32(pt, P[k]);
+        put32(sc, S[k]);
+      }
+    }
+    std::vector<uint8_t> ok;
+    msm_host(ctx, 7 * B, 1, sc.data(), pt.data(), out.data(), ok);
+    for (size_t b = 0; b < B; b++) {
+      for (int k = 0; k < 7; k++)
+        if (!ok[7 * b + k]) {
+          ctx->err = "misbehaviour_prove: a ciphertext point does not decode";
+          return DKG_E_DECODE;
+        }
+      const uint8_t *o = &out[32 * 7 * b], *e1r = enc + 128 * b, *e1s = e1r + 64;
+      const uint8_t *Ks = o, *Kr = o + 32, *pk = o + 64;
+      uint8_t* p = proofs + 192 * b;
+      memcpy(p, Ks, 32);       // share_key      (broadcast.rs:197-199, recover_symmetric_key)
+      memcpy(p + 32, Kr, 32);  // randomness_key (:200-202)
+      const dkgh::Zl x = zl32(sk + 32 * b);
+      // CorrectHybridDecrKeyZkp = DLEQ(g, e1, pk, K; sk) (correct_hybrid_decryption_key/zkp.rs:27-47)
+      dkgh::Zl c1 = dleq_challenge(BASEPOINT, e1s, pk, Ks, o + 96, o + 128);
+      dkgh::Zl r1 = dkgh::zl_add(dkgh::zl_mul(c1, x), zl32(w + 64 * b));
+      dkgh::Zl c2 = dleq_challenge(BASEPOINT, e1r, pk, Kr, o + 160, o + 192);
+      dkgh::Zl r2 = dkgh::zl_add(dkgh::zl_mul(c2, x), zl32(w + 64 * b + 32));
+      dkgh::zl_to_bytes(p + 64, c1);
+      dkgh::zl_to_bytes(p + 96, r1);
+      dkgh::zl_to_bytes(p + 128, c2);
+      dkgh::zl_to_bytes(p + 160, r2);
+    }
+    return DKG_OK;
+  });
+}
+
+int dkg_complaint1_verify(dkg_ctx* ctx, size_t B, size_t t, const uint32_t* accuser, const uint8_t* pk,
+                          const uint8_t* enc, const uint8_t* E, const uint8_t* proofs, int32_t* result) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (!accuser || !pk || !enc || !E || !proofs || !result) return DKG_E_ARG;
+    if (!B) return DKG_OK;
+    const size_t N = t + 1;
+    // phase A, 6 two-term MSMs per complaint: both DLEQ announcements of both proofs
+    // (dl_equality/zkp.rs:60-63) and the two h/g combinations of the decrypted scalars
+    std::vector<uint8_t> sc, pt, outA(32 * 6 * B), sb, pb, outB(32 * B);
+    for (size_t b = 0; b < B; b++) {
+      const uint8_t *e1r = enc + 128 * b, *ctr = e1r + 32, *e1s = e1r + 64, *cts = e1r + 96;
+      const uint8_t *P = proofs + 192 * b, *Ks = P, *Kr = P + 32, *pkb = pk + 32 * b;
+      const dkgh::Zl zero = dkgh::zl_from_u64(0);
+      const dkgh::Zl nc1 = dkgh::zl_sub(zero, zl32(P + 64)), nc2 = dkgh::zl_sub(zero, zl32(P + 128));
+      const dkgh::Zl p1 = sym_scalar(Ks, cts), p2 = sym_scalar(Kr, ctr);  // share, randomness
+      put32(sc, P + 96); putzl(sc, nc1); put32(pt, BASEPOINT); put32(pt, pkb);   // a1 = g r1 - pk c1
+      put32(sc, P + 96); putzl(sc, nc1); put32(pt, e1s); put32(pt, Ks);          // a2 = e1 r1 - K c1
+      put32(sc, P + 160); putzl(sc, nc2); put32(pt, BASEPOINT); put32(pt, pkb);
+      put32(sc, P + 160); putzl(sc, nc2); put32(pt, e1r); put32(pt, Kr);
+      putzl(sc, p1); putzl(sc, p2); put32(pt, ctx->h); put32(pt, BASEPOINT);  // quirk: h*share + g*rand
+      putzl(sc, p2); putzl(sc, p1); put32(pt, ctx->h); put32(pt, BASEPOINT);  // accusation: h*rand + g*share
+      std::vector<uint8_t> pw = index_powers(accuser[b], N);
+      sb.insert(sb.end(), pw.begin(), pw.end());
+      pb.insert(pb.end(), E + 32 * N * b, E + 32 * N * (b + 1));
+    }
+    std::vector<uint8_t> okA, okB;
+    msm_host(ctx, 6 * B, 2, sc.data(), pt.data(), outA.data(), okA);
+    msm_host(ctx, B, N, sb.data(), pb.data(), outB.data(), okB);  // sum_k j^k E_k
+    for (size_t b = 0; b < B; b++) {
+      bool ok = okB[b];
+      for (int k = 0; k < 6; k++) ok = ok && okA[6 * b + k];
+      if (!ok) {
+        result[b] = -1;
+        continue;
+      }
+      const uint8_t *e1r = enc + 128 * b, *e1s = e1r + 64, *P = proofs + 192 * b, *o = &outA[32 * 6 * b];
+      uint8_t c[32];
+      dkgh::zl_to_bytes(c, dleq_challenge(BASEPOINT, e1s, pk + 32 * b, P, o, o + 32));
+      const bool v1 = memcmp(c, P + 64, 32) == 0;
+      dkgh::zl_to_bytes(c, dleq_challenge(BASEPOINT, e1r, pk + 32 * b, P + 32, o + 64, o + 96));
+      const bool v2 = memcmp(c, P + 128, 32) == 0;
+      const uint8_t* rhs = &outB[32 * b];
+      if (!v1 || !v2) result[b] = 1;                            // InvalidProofOfMisbehaviour
+      else if (memcmp(o + 128, rhs, 32) == 0) result[b] = 1;   // ProofOfMisbehaviour::verify quirk (:271-283)
+      else if (memcmp(o + 160, rhs, 32) == 0) result[b] = 2;   // FalseClaimedInequality (broadcast.rs:94-96)
+      else result[b] = 0;
+    }
+    return DKG_OK;
+  });
+}
+
+int dkg_complaint3_verify(dkg_ctx* ctx, size_t B, size_t t, const uint32_t* accuser, const uint8_t* share,
+                          const uint8_t* randomness, const uint8_t* E, const uint8_t* A, int32_t* result) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (!accuser || !share || !randomness || !E || !A || !result) return DKG_E_ARG;
+    if (!B) return DKG_OK;
+    const size_t N = t + 1;
+    std::vector<uint8_t> sc, pt, outA(32 * 2 * B), sb, pb, outB(32 * 2 * B);
+    const uint8_t zero[32] = {0};
+    for (size_t b = 0; b < B; b++) {
+      put32(sc, share + 32 * b); put32(sc, randomness + 32 * b); put32(pt, BASEPOINT); put32(pt, ctx->h);
+      put32(sc, share + 32 * b); put32(sc, zero); put32(pt, BASEPOINT); put32(pt, BASEPOINT);
+      std::vector<uint8_t> pw = index_powers(accuser[b], N);
+      for (int r = 0; r < 2; r++) {
+        sb.insert(sb.end(), pw.begin(), pw.end());
+        const uint8_t* C = r == 0 ? E : A;
+        pb.insert(pb.end(), C + 32 * N * b, C + 32 * N * (b + 1));
+      }
+    }
+    std::vector<uint8_t> okA, okB;
+    msm_host(ctx, 2 * B, 2, sc.data(), pt.data(), outA.data(), okA);
+    msm_host(ctx, 2 * B, N, sb.data(), pb.data(), outB.data(), okB);
+    for (size_t b = 0; b < B; b++) {
+      if (!(okA[2 * b] && okA[2 * b + 1] && okB[2 * b] && okB[2 * b + 1])) {
+        result[b] = -1;
+        continue;
+      }
+      const uint8_t *pass = &outA[64 * b], *fail = pass + 32, *rE = &outB[64 * b], *rA = rE + 32;
+      if (memcmp(pass, rE, 32) != 0) result[b] = 3;       // FalseClaimedEquality (broadcast.rs:129-130)
+      else if (memcmp(fail, rA, 32) == 0) result[b] = 2;  // FalseClaimedInequality (:131-132)
+      else result[b] = 0;
+    }
     return DKG_OK;
   });
 }

@@ -223,6 +223,28 @@ int dkg_ceremony_run_full_device(dkg_ctx *ctx, size_t n, size_t t, const void *d
 int dkg_ceremony_verify_full(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *E, const uint8_t *A, const uint8_t *e1,
                              const uint8_t *ct, const uint8_t *sk, dkg_ceremony_out *out);
 
+/* ---- complaint proofs: dl_equality/zkp.rs, broadcast.rs ----
+ * enc [B][128] = one dealer->accuser ciphertext pair: e1_rand || ct_rand || e1_share || ct_share.
+ * proof [192] = ProofOfMisbehaviour (broadcast.rs:181-186): share_key || randomness_key || c1 || r1
+ * || c2 || r2, the two CorrectHybridDecrKeyZkp = DLEQ(g, e1, pk, K) proofs (challenge, response).
+ * Verdicts (int32): 0 Ok (a valid complaint), 1 InvalidProofOfMisbehaviour, 2 FalseClaimedInequality,
+ * 3 FalseClaimedEquality, -1 an input point does not decode. */
+/* ProofOfMisbehaviour::generate (broadcast.rs:189-226) for B complaints by accusers with secret keys
+ * sk [B][32]; nonces w [B][2][32]: w[0] for the share's proof (drawn first), w[1] the randomness's. */
+int dkg_misbehaviour_prove(dkg_ctx *ctx, size_t B, const uint8_t *sk, const uint8_t *enc, const uint8_t *w,
+                           uint8_t *proofs);
+/* MisbehavingPartiesRound1::verify (broadcast.rs:50-99), including ProofOfMisbehaviour::verify
+ * (:228-283) with its swapped-role check h*share + g*randomness (:271-274), reproduced as is:
+ * accuser[b] = 1-based index, pk [B][32] the accuser's communication key, E [B][t+1][32] the
+ * accused dealer's committed coefficients.  Requires dkg_env_init (h). */
+int dkg_complaint1_verify(dkg_ctx *ctx, size_t B, size_t t, const uint32_t *accuser, const uint8_t *pk,
+                          const uint8_t *enc, const uint8_t *E, const uint8_t *proofs, int32_t *result);
+/* MisbehavingPartiesRound3::verify (broadcast.rs:105-135): the disclosed decrypted share and
+ * randomness [B][32] must pass against E (else FalseClaimedEquality) and fail against A (else
+ * FalseClaimedInequality). */
+int dkg_complaint3_verify(dkg_ctx *ctx, size_t B, size_t t, const uint32_t *accuser, const uint8_t *share,
+                          const uint8_t *randomness, const uint8_t *E, const uint8_t *A, int32_t *result);
+
 /* ---- synthetic inputs: the seeded RNG convention ----
  * dealer seed = BLAKE2b-256("dkg-amd/v1/dealer" || master[32] || u32le ceremony || u32le dealer);
  * coefficients = ChaCha20Rng(seed): hiding b_0..b_t first, then sharing a_0..a_t (committee.rs:143-146),

@@ -86,6 +86,18 @@ int or_hybrid_encrypt(uint8_t e1[32], uint8_t *e2, const uint8_t pk[32], const u
 int or_hybrid_decrypt(uint8_t *msg, const uint8_t sk[32], const uint8_t e1[32], const uint8_t *e2, size_t len);
 void or_member_sk(uint8_t sk[32], const uint8_t master[32], uint32_t ceremony, uint32_t member);
 void or_enc_randomness(uint8_t *r, const uint8_t seed[32], size_t t, size_t n);
+/* ---- complaint proofs (hybrid.c; dl_equality/zkp.rs, broadcast.rs) ---- */
+void or_hash_to_scalar(uint8_t out[32], const uint8_t *in, size_t len); /* groups.rs:50-52 */
+int or_dleq_prove(uint8_t c[32], uint8_t r[32], const uint8_t b1[32], const uint8_t b2[32], const uint8_t p1[32],
+                  const uint8_t p2[32], const uint8_t dlog[32], const uint8_t w[32]);
+int or_dleq_verify(const uint8_t b1[32], const uint8_t b2[32], const uint8_t p1[32], const uint8_t p2[32],
+                   const uint8_t c[32], const uint8_t r[32]);
+/* enc = e1_rand || ct_rand || e1_share || ct_share; proof = share_key || randomness_key || c1 || r1 || c2 || r2 */
+int or_misbehaviour_prove(uint8_t proof[192], const uint8_t sk[32], const uint8_t enc[128], const uint8_t w[64]);
+int or_complaint1_verify(const uint8_t h[32], size_t t, uint32_t accuser, const uint8_t pk[32], const uint8_t enc[128],
+                         const uint8_t *E, const uint8_t proof[192]);
+int or_complaint3_verify(const uint8_t h[32], size_t t, uint32_t accuser, const uint8_t share[32],
+                         const uint8_t randomness[32], const uint8_t *E, const uint8_t *A);
 /* Lagrange interpolation at x (polynomial.rs:162-184). */
 void or_lagrange(uint8_t out[32], const uint8_t x[32], const uint8_t *ys, const uint8_t *xs, size_t m);
 

@@ -41,6 +41,9 @@ def lib():
         _lib.or_hybrid_decrypt.argtypes = [cp, cp, cp, cp, sz]
         _lib.or_member_sk.argtypes = [cp, cp, ctypes.c_uint32, ctypes.c_uint32]
         _lib.or_enc_randomness.argtypes = [cp, cp, sz, sz]
+        _lib.or_misbehaviour_prove.argtypes = [cp, cp, cp, cp]
+        _lib.or_complaint1_verify.argtypes = [cp, sz, ctypes.c_uint32, cp, cp, cp, cp]
+        _lib.or_complaint3_verify.argtypes = [cp, sz, ctypes.c_uint32, cp, cp, cp, cp]
     return _lib
 
 
@@ -117,3 +120,17 @@ def enc_randomness(seed: bytes, t: int, n: int):
     out = _b(64 * n)
     lib().or_enc_randomness(out, seed, t, n)
     return out.raw
+
+
+def misbehaviour_prove(sk: bytes, enc: bytes, w: bytes):
+    out = _b(192)
+    rc = lib().or_misbehaviour_prove(out, sk, enc, w)
+    return out.raw if rc == 0 else None
+
+
+def complaint1_verify(h, t, accuser, pk, enc, E, proof):
+    return lib().or_complaint1_verify(h, t, accuser, pk, enc, E, proof)
+
+
+def complaint3_verify(h, t, accuser, share, randomness, E, A):
+    return lib().or_complaint3_verify(h, t, accuser, share, randomness, E, A)

@@ -560,6 +560,41 @@ def test_full_mode_oracle_random(be):
     assert ds2 != s
 
 
+def test_complaint_proofs_device(be, golden):
+    """SURVEY 8 f2 through the ABI, all complaints of a kind in one batched call: proofs of
+    misbehaviour byte for byte (broadcast.rs:189-226), round-1 verdicts incl. the swapped-role quirk
+    (:50-99, 271-274) and round-3 verdicts incl. forged claims (:105-135), as in the fixtures."""
+    from tests.test_oracle import VERDICT, _complaint_inputs
+    c = golden("complaints_n10_t4.json")
+    full = golden(c["source"])
+    assert full["h"] == be.env_init(full["t"], full["n"], CK).hex()
+    rows = [_complaint_inputs(c, full, x) for x in c["round1"]]
+    sk, pk, enc, E, proof = (b"".join(r[k] for r in rows) for k in range(5))
+    w = b"".join(H(v) for x in c["round1"] for v in x["w"])
+    got = be.misbehaviour_prove(sk, enc, w)
+    for b, x in enumerate(c["round1"]):
+        if x["verdict"] != "InvalidProofOfMisbehaviour":
+            assert got[192 * b:192 * b + 192] == proof[192 * b:192 * b + 192], x
+    res = be.complaint1_verify(full["t"], [x["accuser"] for x in c["round1"]], pk, enc, E, proof)
+    assert res == [VERDICT[x["verdict"]] for x in c["round1"]]
+    # an undecodable key in the proof is a decode failure, not a verdict
+    bad = bytearray(proof[:192])
+    bad[0:32] = b"\xff" * 32
+    assert be.complaint1_verify(full["t"], [c["round1"][0]["accuser"]], pk[:32], enc[:128], E[:32 * (full["t"] + 1)],
+                                bytes(bad)) == [-1]
+    p3 = golden(c["round3_source"])
+    N = p3["t"] + 1
+    assert p3["h"] == be.env_init(p3["t"], p3["n"], CK).hex()
+    r3 = c["round3"]
+    Eb, Ab = H(p3["E"]), H(p3["A"])
+    Es = b"".join(Eb[32 * N * (x["accused"] - 1):32 * N * x["accused"]] for x in r3)
+    As = b"".join(Ab[32 * N * (x["accused"] - 1):32 * N * x["accused"]] for x in r3)
+    res = be.complaint3_verify(p3["t"], [x["accuser"] for x in r3], b"".join(H(x["share"]) for x in r3),
+                               b"".join(H(x["randomness"]) for x in r3), Es, As)
+    assert res == [VERDICT[x["verdict"]] for x in r3]
+    assert be.misbehaviour_prove(b"", b"", b"") == b""
+
+
 def test_ceremony_n4096_device(be):
     """BASELINE config 4 (n = 4096, t = 2047) end to end on one GPU from device-generated
     coefficients: every share of both rounds verifies and mpk == g * sum_i a_i0 (committee.rs:

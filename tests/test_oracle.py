@@ -219,3 +219,42 @@ def test_full_mode_ceremony(golden, name):
                 (dec_sp if w == 0 else dec_s)[32 * (i * n + q):32 * (i * n + q) + 32] = red
     assert bytes(dec_s).hex() == c["s"] and bytes(dec_sp).hex() == c["s_prime"]
     assert _decisions(c, 2)[0] == bytes(int(x) for x in c["dec2"])
+
+
+# ---------------- complaint proofs: dl_equality/zkp.rs, broadcast.rs ----------------
+VERDICT = {"Ok": 0, "InvalidProofOfMisbehaviour": 1, "FalseClaimedInequality": 2, "FalseClaimedEquality": 3}
+
+
+def _complaint_inputs(c, full, x):
+    n, t = full["n"], full["t"]
+    N = t + 1
+    q, i = x["accuser"] - 1, x["accused"] - 1
+    k = 2 * (i * n + q)
+    e1, ct = H(full["e1"]), H(full["ct"])
+    enc = e1[32 * k:32 * k + 32] + ct[32 * k:32 * k + 32] + e1[32 * k + 32:32 * k + 64] + ct[32 * k + 32:32 * k + 64]
+    pf = x["proof"]
+    proof = b"".join(H(pf[f]) for f in ("share_key", "randomness_key", "c1", "r1", "c2", "r2"))
+    return (H(full["member_sk"])[32 * q:32 * q + 32], H(full["member_pk"])[32 * q:32 * q + 32], enc,
+            H(full["E"])[32 * N * i:32 * N * (i + 1)], proof)
+
+
+def test_complaint_proofs_oracle(golden):
+    """ProofOfMisbehaviour::generate / MisbehavingPartiesRound1::verify (broadcast.rs:50-99, 181-283,
+    incl. the swapped-role quirk of :271-274) and MisbehavingPartiesRound3::verify (:105-135) on the
+    oracle against the libsodium fixtures: proofs byte for byte, verdicts including forged claims."""
+    c = golden("complaints_n10_t4.json")
+    full = golden(c["source"])
+    t = full["t"]
+    for x in c["round1"]:
+        sk, pk, enc, E, proof = _complaint_inputs(c, full, x)
+        w = b"".join(H(v) for v in x["w"])
+        if x["verdict"] != "InvalidProofOfMisbehaviour":
+            assert O.misbehaviour_prove(sk, enc, w) == proof
+        assert O.complaint1_verify(H(full["h"]), t, x["accuser"], pk, enc, E, proof) == VERDICT[x["verdict"]]
+    p3 = golden(c["round3_source"])
+    n, N = p3["n"], p3["t"] + 1
+    for x in c["round3"]:
+        i = x["accused"] - 1
+        rc = O.complaint3_verify(H(p3["h"]), p3["t"], x["accuser"], H(x["share"]), H(x["randomness"]),
+                                 H(p3["E"])[32 * N * i:32 * N * (i + 1)], H(p3["A"])[32 * N * i:32 * N * (i + 1)])
+        assert rc == VERDICT[x["verdict"]], x

@@ -375,6 +375,155 @@ def kat_hybrid(rng):
             "member_sk0": hx(scb(wide_reduce(chacha_stream(seed, 64))))}
 
 
+# ---------------- complaint proofs: dl_equality/zkp.rs, broadcast.rs ----------------
+def hash_to_scalar(data):
+    """Scalar::hash_from_bytes::<Blake2b> (groups.rs:50-52): wide reduction of Blake2b-512."""
+    return wide_reduce(hashlib.blake2b(data, digest_size=64).digest())
+
+
+def dleq_prove(b1, b2, p1, p2, dlog, w):
+    """DleqZkp::generate (dl_equality/zkp.rs:29-49, challenge_context.rs:14-41)."""
+    a1, a2 = gmul(b1, w), gmul(b2, w)
+    c = hash_to_scalar(b1 + b2 + p1 + p2 + a1 + a2)
+    return c, (c * dlog + w) % L
+
+
+def dleq_verify(b1, b2, p1, p2, c, r):
+    """DleqZkp::verify (dl_equality/zkp.rs:52-74)."""
+    a1 = gadd(gmul(b1, r), gneg(gmul(p1, c)))
+    a2 = gadd(gmul(b2, r), gneg(gmul(p2, c)))
+    return hash_to_scalar(b1 + b2 + p1 + p2 + a1 + a2) == c
+
+
+def sym_process(K, data):
+    ks = sym_keystream(K, len(data))
+    return bytes(x ^ y for x, y in zip(data, ks))
+
+
+def misbehaviour_prove(sk, enc, w):
+    """ProofOfMisbehaviour::generate (broadcast.rs:189-226): enc = ((e1_rand, ct_rand), (e1_share,
+    ct_share)); the share's decryption proof draws its nonce first (w[0]), the randomness's second."""
+    (e1r, _), (e1s, _) = enc
+    pk = gmul_base(sk)
+    Ks, Kr = gmul(e1s, sk), gmul(e1r, sk)          # recover_symmetric_key (elgamal.rs:154-159)
+    g = gmul_base(1)
+    c1, r1 = dleq_prove(g, e1s, pk, Ks, sk, w[0])  # CorrectHybridDecrKeyZkp (correct_hybrid.../zkp.rs:27-47)
+    c2, r2 = dleq_prove(g, e1r, pk, Kr, sk, w[1])
+    return {"share_key": hx(Ks), "randomness_key": hx(Kr), "c1": hx(scb(c1)), "r1": hx(scb(r1)),
+            "c2": hx(scb(c2)), "r2": hx(scb(r2))}
+
+
+def msm_index(j, coeffs, t):
+    return msm([pow(j, k, L) for k in range(t + 1)], coeffs)
+
+
+def complaint1_verify(h, t, j, pk, enc, E, proof):
+    """MisbehavingPartiesRound1::verify (broadcast.rs:50-99) incl. ProofOfMisbehaviour::verify
+    (:228-283) with its swapped roles (h * share_plaintext + g * randomness_plaintext, :271-274).
+    Returns "Ok" or the reference's error name."""
+    (e1r, ctr), (e1s, cts) = enc
+    g = gmul_base(1)
+    Ks, Kr = H(proof["share_key"]), H(proof["randomness_key"])
+    ok1 = dleq_verify(g, e1s, pk, Ks, int.from_bytes(H(proof["c1"]), "little"), int.from_bytes(H(proof["r1"]), "little"))
+    ok2 = dleq_verify(g, e1r, pk, Kr, int.from_bytes(H(proof["c2"]), "little"), int.from_bytes(H(proof["r2"]), "little"))
+    if not (ok1 and ok2):
+        return "InvalidProofOfMisbehaviour"
+    p1 = from_bits(sym_process(Ks, cts)) % L
+    p2 = from_bits(sym_process(Kr, ctr)) % L
+    rhs = msm_index(j, E, t)
+    if gadd(gmul(h, p1), gmul_base(p2)) == rhs:   # quirk: roles swapped w.r.t. committee.rs:292-294
+        return "InvalidProofOfMisbehaviour"
+    if gadd(gmul(h, p2), gmul_base(p1)) == rhs:   # the accusation itself (broadcast.rs:76-96)
+        return "FalseClaimedInequality"
+    return "Ok"
+
+
+def complaint3_verify(h, t, j, share, rand, E, A):
+    """MisbehavingPartiesRound3::verify (broadcast.rs:105-135)."""
+    if gadd(gmul_base(share), gmul(h, rand)) != msm_index(j, E, t):
+        return "FalseClaimedEquality"
+    if gmul_base(share) == msm_index(j, A, t):
+        return "FalseClaimedInequality"
+    return "Ok"
+
+
+def H(x):
+    return bytes.fromhex(x)
+
+
+def complaints_golden(full):
+    """Proofs and verdicts for every round-2 complaint of a full-mode fault ceremony (and forged
+    variants), plus round-3 complaints; nonces from the accuser's member stream (blocks 1 + 2c, 2 + 2c
+    for its c-th complaint -- the synthetic convention of this build)."""
+    c = full
+    n, t = c["n"], c["t"]
+    h = H(c["h"])
+    sks = [int.from_bytes(H(c["member_sk"])[32 * q:32 * q + 32], "little") for q in range(n)]
+    pks = [H(c["member_pk"])[32 * q:32 * q + 32] for q in range(n)]
+    master = H(c["master_seed"])
+    E = [[H(c["E"])[32 * ((t + 1) * i + k):32 * ((t + 1) * i + k + 1)] for k in range(t + 1)] for i in range(n)]
+    e1 = H(c["e1"])
+    ct = H(c["ct"])
+
+    def enc(i, q):
+        k = 2 * (i * n + q)
+        return ((e1[32 * k:32 * k + 32], ct[32 * k:32 * k + 32]), (e1[32 * k + 32:32 * k + 64], ct[32 * k + 32:32 * k + 64]))
+
+    out = []
+    for q in range(n):
+        accused = [i for i in range(n) if i != q and c["dec2"][i * n + q] == "0"]
+        # accuser q's member seed order: the member index before sorting is not needed: the nonce
+        # stream is keyed by the SORTED index q (this build's convention)
+        st = chacha_stream(member_seed(master, c["ceremony"], 1000 + q), 64 * (1 + 2 * max(1, len(accused)) + 2))
+        for ci, i in enumerate(accused):
+            w = [wide_reduce(st[64 * (1 + 2 * ci + k):64 * (2 + 2 * ci + k)]) for k in range(2)]
+            proof = misbehaviour_prove(sks[q], enc(i, q), w)
+            verdict = complaint1_verify(h, t, q + 1, pks[q], enc(i, q), E[i], proof)
+            assert verdict == "Ok", (q, i, verdict)
+            out.append({"accuser": q + 1, "accused": i + 1, "w": [hx(scb(x)) for x in w], "proof": proof,
+                        "verdict": verdict})
+    # forged complaints: an honest pair (proof valid, inequality false) and a tampered proof
+    qs, ivs = 0, 1
+    st = chacha_stream(member_seed(master, c["ceremony"], 2000), 128)
+    w = [wide_reduce(st[:64]), wide_reduce(st[64:])]
+    proof = misbehaviour_prove(sks[qs], enc(ivs, qs), w)
+    out.append({"accuser": qs + 1, "accused": ivs + 1, "w": [hx(scb(x)) for x in w], "proof": proof,
+                "verdict": complaint1_verify(h, t, qs + 1, pks[qs], enc(ivs, qs), E[ivs], proof)})
+    bad = dict(proof)
+    bad["r1"] = hx(scb(int.from_bytes(H(proof["r1"]), "little") + 1))
+    out.append({"accuser": qs + 1, "accused": ivs + 1, "w": [hx(scb(x)) for x in w], "proof": bad,
+                "verdict": complaint1_verify(h, t, qs + 1, pks[qs], enc(ivs, qs), E[ivs], bad)})
+    return out
+
+
+def complaints3_golden(c):
+    """Round-3 complaints of a plaintext ceremony (MisbehavingPartiesRound3, broadcast.rs:105-135):
+    every receiver's complaint against each accused dealer, plus a forged one."""
+    n, t = c["n"], c["t"]
+    h = H(c["h"])
+    E = [[H(c["E"])[32 * ((t + 1) * i + k):32 * ((t + 1) * i + k + 1)] for k in range(t + 1)] for i in range(n)]
+    A = [[H(c["A"])[32 * ((t + 1) * i + k):32 * ((t + 1) * i + k + 1)] for k in range(t + 1)] for i in range(n)]
+    s, sp = H(c["s"]), H(c["s_prime"])
+    out = []
+    for i in range(n):
+        for j in range(n):
+            if i == j or c["dec4"][i * n + j] != "0":
+                continue
+            sh, ra = int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little"), \
+                int.from_bytes(sp[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+            out.append({"accuser": j + 1, "accused": i + 1, "share": hx(scb(sh)), "randomness": hx(scb(ra)),
+                        "verdict": complaint3_verify(h, t, j + 1, sh, ra, E[i], A[i])})
+    # forged: an honest dealer's pair (FalseClaimedInequality) and a wrong share (FalseClaimedEquality)
+    i, j = 1, 2
+    sh = int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+    ra = int.from_bytes(sp[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+    out.append({"accuser": j + 1, "accused": i + 1, "share": hx(scb(sh)), "randomness": hx(scb(ra)),
+                "verdict": complaint3_verify(h, t, j + 1, sh, ra, E[i], A[i])})
+    out.append({"accuser": j + 1, "accused": i + 1, "share": hx(scb(sh + 1)), "randomness": hx(scb(ra)),
+                "verdict": complaint3_verify(h, t, j + 1, sh + 1, ra, E[i], A[i])})
+    return out
+
+
 def kat_group(rng):
     out = {}
     out["base_multiples"] = [{"k": k, "P": hx(gmul_base(k))} for k in range(0, 17)]
@@ -514,6 +663,11 @@ def main():
         {"kind": "ct_flip", "dealer": 3, "receiver": 5, "which": 1, "byte": 7},
         {"kind": "e1_generator", "dealer": 6, "receiver": 2, "which": 0},
         {"kind": "share_flip", "dealer": 9, "receiver": 1}])
+    ff = files["full_faults_n10_t4.json"]
+    files["complaints_n10_t4.json"] = {
+        "source": "full_faults_n10_t4.json", "round1": complaints_golden(ff),
+        "round3_source": "fault_a_generator_n10_t4.json",
+        "round3": complaints3_golden(files["fault_a_generator_n10_t4.json"])}
     files["spot_n256_t127.json"] = spot(256, 127, m, [0, 200], [1, 17, 255])
     files["spot_n1024_t511.json"] = spot(1024, 511, m, [513], [0, 1023])
     for name, obj in files.items():
