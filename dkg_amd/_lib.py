@@ -85,6 +85,8 @@ def lib():
     L.dkg_ceremony_verify.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_run_device.argtypes = [p, sz, sz, p, p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_shard_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]
+    L.dkg_ceremony_shard_verify_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, p, p,
+                                                    ctypes.POINTER(ctypes.c_double)]
     L.dkg_ceremony_batch_device.argtypes = [p, sz, sz, sz, p, p, ctypes.POINTER(BatchOut)]
     L.dkg_ceremony_batch_verify.argtypes = [p, sz, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(BatchOut)]
     L.dkg_dealer_coeffs_device.argtypes = [p, u8p, ctypes.c_uint32, sz, sz, sz, sz, p, p]
@@ -111,6 +113,7 @@ EXPORTED = [
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
+    "dkg_ceremony_shard_verify_device",
     "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_member_keys", "dkg_enc_randomness",
     "dkg_enc_randomness_device", "dkg_encrypt_shares", "dkg_decrypt_shares", "dkg_ceremony_run_full_device",
     "dkg_ceremony_verify_full", "dkg_misbehaviour_prove", "dkg_complaint1_verify", "dkg_complaint3_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",

@@ -297,6 +297,16 @@ class Backend:
                                                                 vp(d_partial), ctypes.byref(ms)))
         return ms.value
 
+    def ceremony_shard_verify_device(self, n, t, d0, d1, d_E, d_A, d_s, d_sp, d_dec2, d_dec4, d_A0,
+                                     d_partial) -> float:
+        """Rounds 2-5 of this rank's dealers [d0, d1) on received broadcasts (device pointers)."""
+        ms = ctypes.c_double()
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_ceremony_shard_verify_device(
+            self._ctx, n, t, d0, d1, vp(d_E), vp(d_A), vp(d_s), vp(d_sp), vp(d_dec2), vp(d_dec4), vp(d_A0),
+            vp(d_partial), ctypes.byref(ms)))
+        return ms.value
+
     def scalar_sum_device(self, rows: int, n: int, d_in: int, d_mask: Optional[int], d_out: int):
         """out[j] = sum over rows r with mask[r] of in[r][j] mod l (device pointers)."""
         vp = ctypes.c_void_p

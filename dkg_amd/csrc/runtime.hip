@@ -290,10 +290,9 @@ double ev_ms(dkg_ctx* ctx, int a, int b) {
 // Lagrange reconstruction (polynomial.rs:172-184 at 0; the reference interpolates the disclosed
 // shares, committee.rs:748-789) of the secret of every dealer i with recon[i], from the shares of
 // the first t+1 parties outside the reconstructable set.  hs: the ceremony's shares [n][n][32].
-std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, const uint8_t* hs) {
-  std::vector<size_t> xs;
-  for (size_t j = 0; j < n && xs.size() < t + 1; j++)
-    if (!recon[j]) xs.push_back(j);
+// lagrange_interpolation at zero (polynomial.rs:162-184) of `rows` share vectors: row r holds the
+// evaluations at x = j + 1 at byte offset 32 * (r * stride + j); the abscissae used are xs (0-based j).
+std::vector<uint8_t> lagrange_at_zero(const std::vector<size_t>& xs, const uint8_t* ys, size_t rows, size_t stride) {
   std::vector<dkgh::Zl> lambda(xs.size());
   for (size_t a = 0; a < xs.size(); a++) {
     dkgh::Zl num = dkgh::zl_from_u64(1), den = dkgh::zl_from_u64(1);
@@ -305,11 +304,10 @@ std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, 
     lambda[a] = dkgh::zl_mul(num, dkgh::zl_inv(den));
   }
   std::vector<uint8_t> secrets;
-  for (size_t i = 0; i < n; i++) {
-    if (!recon[i]) continue;
+  for (size_t r = 0; r < rows; r++) {
     dkgh::Zl acc = dkgh::zl_from_u64(0);
     for (size_t a = 0; a < xs.size(); a++) {
-      dkgh::Zl y = dkgh::zl_from_bytes_wide(&hs[32 * (i * n + xs[a])], 32);
+      dkgh::Zl y = dkgh::zl_from_bytes_wide(&ys[32 * (r * stride + xs[a])], 32);
       acc = dkgh::zl_add(acc, dkgh::zl_mul(lambda[a], y));
     }
     uint8_t b[32];
@@ -317,6 +315,20 @@ std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, 
     secrets.insert(secrets.end(), b, b + 32);
   }
   return secrets;
+}
+
+// Secrets of the reconstructed dealers from the shares disclosed by the first t+1 parties that are
+// not themselves reconstructed (hs = all shares [n][n][32]).  Shares of a qualified dealer passed
+// every round-2 check, so any t+1 of them interpolate to the same a_i0 (the reference's choice of
+// disclosing parties, committee.rs:755-773, gives the same value).
+std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, const uint8_t* hs) {
+  std::vector<size_t> xs;
+  for (size_t j = 0; j < n && xs.size() < t + 1; j++)
+    if (!recon[j]) xs.push_back(j);
+  std::vector<uint8_t> rows;
+  for (size_t i = 0; i < n; i++)
+    if (recon[i]) rows.insert(rows.end(), hs + 32 * n * i, hs + 32 * n * (i + 1));
+  return lagrange_at_zero(xs, rows.data(), rows.size() / (32 * n), n);
 }
 
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
@@ -1029,6 +1041,69 @@ int dkg_ceremony_verify(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E, cons
   });
 }
 
+}  // extern "C"
+
+// Rounds 2-5 of one rank of a dealer-sharded ceremony on its dealers [d0, d0+D): E/A compressed
+// [D][N][32], s/sp canonical [D][n][32] on the device -> decision rows, master-key terms, partial
+// final shares (layouts of dkg_ceremony_shard_device).
+void shard_rows(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t D, const uint32_t* Ec, const uint32_t* Ac,
+                const uint32_t* ds, const uint32_t* dsp, void* d_dec2, void* d_dec4, void* d_A0, void* d_partial) {
+  const size_t N = t + 1;
+  if (!D) {
+    HCK(hipMemsetAsync(d_partial, 0, 32 * n, ctx->stream));
+    return;
+  }
+  // Qualification of a dealer depends only on its own decision row (any REJECT disqualifies,
+  // committee.rs:370-398; missing data disqualifies, :331-335), so each rank decides it for its
+  // dealers with no exchange.
+  std::vector<uint8_t> rows(D * n), q(D, 1);
+  verify_rounds(ctx, n, t, D, d0, Ec, Ac, ds, dsp, (uint8_t*)d_dec2, (uint8_t*)d_dec4, nullptr, [&] {
+    d2h(ctx, rows.data(), d_dec2, D * n);
+    sync(ctx);
+    for (size_t i = 0; i < D; i++)
+      for (size_t j = 0; j < n; j++)
+        if (rows[i * n + j] == DKG_REJECT || rows[i * n + j] == DKG_MISSING) q[i] = 0;
+  });
+  HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
+  // Round-4 accusations against a qualified dealer put it in the reconstructable set
+  // (committee.rs:660-670) -- again a function of its own row.  Its mpk term becomes g * a_i0
+  // recovered by Lagrange interpolation of its shares (finalise, :747-783); the shares of this
+  // rank's dealers are on this GPU, so the term is computed here and sent in place of A_i0.
+  std::vector<uint8_t> r4(D * n);
+  d2h(ctx, r4.data(), d_dec4, D * n);
+  sync(ctx);
+  std::vector<size_t> recon;
+  for (size_t i = 0; i < D; i++) {
+    bool acc = false;
+    for (size_t j = 0; j < n; j++) acc |= j != d0 + i && r4[i * n + j] == DKG_REJECT;
+    if (q[i] && acc) recon.push_back(i);
+  }
+  if (!recon.empty()) {
+    const size_t R = recon.size();
+    std::vector<uint8_t> hs(32 * n * R);
+    for (size_t r = 0; r < R; r++) d2h(ctx, &hs[32 * n * r], ds + 8 * n * recon[r], 32 * n);
+    sync(ctx);
+    // the first t+1 parties' shares: a qualified dealer's shares all passed round 2, so any t+1
+    // of them interpolate to the same a_i0 as the single-GPU driver's choice
+    std::vector<size_t> xs(N);
+    for (size_t j = 0; j < N; j++) xs[j] = j;
+    std::vector<uint8_t> secrets = lagrange_at_zero(xs, hs.data(), R, n);
+    uint32_t* sec = buf<uint32_t>(ctx, "sh_rsec", 32 * R);
+    uint32_t* gsec = buf<uint32_t>(ctx, "sh_rext", PTB * R);
+    uint32_t* gc = buf<uint32_t>(ctx, "sh_rcomp", 32 * R);
+    h2d(ctx, sec, secrets.data(), secrets.size());
+    dkgk::fixed_base(R, sec, ctx->tab_g, gsec, ctx->stream);
+    dkgk::encode_points(gsec, R, R, gc, ctx->stream);
+    for (size_t r = 0; r < R; r++)
+      HCK(hipMemcpyAsync((uint8_t*)d_A0 + 32 * recon[r], gc + 8 * r, 32, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
+  h2d(ctx, qm, q.data(), D);
+  dkgk::sum_shares(D, n, ds, qm, (uint32_t*)d_partial, ctx->stream);  // partial of :454-462
+}
+
+extern "C" {
+
 int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t d1, const void* d_a,
                               const void* d_b, void* d_dec2, void* d_dec4, void* d_A0, void* d_partial,
                               double* ms_total) {
@@ -1042,25 +1117,34 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     uint32_t* Ac = buf<uint32_t>(ctx, "sh_A", 32 * D * N);
     uint32_t* ds = buf<uint32_t>(ctx, "sh_s", 32 * D * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "sh_sp", 32 * D * n);
+    if (D) round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    shard_rows(ctx, n, t, d0, D, Ec, Ac, ds, dsp, d_dec2, d_dec4, d_A0, d_partial);
+    check_launch(ctx);
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    sync(ctx);
+    if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_shard_verify_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t d1, const void* d_E,
+                                     const void* d_A, const void* d_s, const void* d_s_prime, void* d_dec2,
+                                     void* d_dec4, void* d_A0, void* d_partial, double* ms_total) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || d1 < d0 || d1 > n) return DKG_E_ARG;
+    const size_t D = d1 - d0;
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    // received shares: Scalar::from_bytes semantics (bit 255 cleared, reduced), as upload_scalars
+    uint32_t* ds = buf<uint32_t>(ctx, "shv_s", 32 * D * n);
+    uint32_t* dsp = buf<uint32_t>(ctx, "shv_sp", 32 * D * n);
     if (D) {
-      round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
-      // Qualification of a dealer depends only on its own decision row (any REJECT disqualifies,
-      // committee.rs:370-398), so each rank decides it for its dealers with no exchange.
-      std::vector<uint8_t> rows(D * n), q(D, 1);
-      verify_rounds(ctx, n, t, D, d0, Ec, Ac, ds, dsp, (uint8_t*)d_dec2, (uint8_t*)d_dec4, nullptr, [&] {
-        d2h(ctx, rows.data(), d_dec2, D * n);
-        sync(ctx);
-        for (size_t i = 0; i < D; i++)
-          for (size_t j = 0; j < n; j++)
-            if (rows[i * n + j] == DKG_REJECT || rows[i * n + j] == DKG_MISSING) q[i] = 0;
-      });
-      HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
-      uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
-      h2d(ctx, qm, q.data(), D);
-      dkgk::sum_shares(D, n, ds, qm, (uint32_t*)d_partial, ctx->stream);  // partial of :454-462
-    } else {
-      HCK(hipMemsetAsync(d_partial, 0, 32 * n, ctx->stream));
+      dkgk::reduce_scalars(D * n, (const uint32_t*)d_s, ds, ctx->stream);
+      dkgk::reduce_scalars(D * n, (const uint32_t*)d_s_prime, dsp, ctx->stream);
     }
+    shard_rows(ctx, n, t, d0, D, (const uint32_t*)d_E, (const uint32_t*)d_A, ds, dsp, d_dec2, d_dec4, d_A0,
+               d_partial);
     check_launch(ctx);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     sync(ctx);

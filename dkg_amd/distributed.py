@@ -6,7 +6,8 @@ every party learns every complaint (committee.rs:311-331, 370-398) and the round
 (committee.rs:454-467, 790-795) -- is a set of all-gathers (RCCL over xGMI with the "nccl" backend,
 gloo in the CPU tests) of:
   * the round-2 / round-4 decision rows,
-  * the compressed A_i0 of every dealer,
+  * every dealer's compressed master-key term (A_i0, or g * a_i0 recovered by Lagrange
+    interpolation on the owning rank for dealers accused in round 4),
   * each rank's partial final shares (sum over its qualified dealers of s_ij).
 combine_decisions() then derives, identically on every rank, what receivers_rounds() in runtime.hip
 derives on one GPU: qualified set, complaints, r2 errors, round-4 SKIPPED marks, reconstruction set.
@@ -114,10 +115,22 @@ class ShardedCeremony:
     def run(self, d_a: int, d_b: int, finalise: bool = True) -> ShardResult:
         """Share gen + rounds 2/4 for this rank's dealers (device pointers d_a, d_b to its [D][t+1][32]
         coefficients), exchange, combine.  With finalise, also the round-3 final shares (sum of the
-        gathered partials) and the master public key (sum of the honest A_i0), both on the GPU."""
-        n, t = self.n, self.t
-        ms = self.be.ceremony_shard_device(n, t, self.d0, self.d1, d_a, d_b, self.dec2.data_ptr(),
+        gathered partials) and the master public key (sum of the qualified dealers' terms), both on
+        the GPU."""
+        ms = self.be.ceremony_shard_device(self.n, self.t, self.d0, self.d1, d_a, d_b, self.dec2.data_ptr(),
                                            self.dec4.data_ptr(), self.A0.data_ptr(), self.part.data_ptr())
+        return self._finish(ms, finalise)
+
+    def run_verify(self, d_E: int, d_A: int, d_s: int, d_sp: int, finalise: bool = True) -> ShardResult:
+        """Rounds 2-5 on received broadcasts: this rank's dealers' commitments d_E, d_A [D][t+1][32]
+        (compressed, as broadcast in phases 1 and 3) and their shares d_s, d_sp [D][n][32]."""
+        ms = self.be.ceremony_shard_verify_device(self.n, self.t, self.d0, self.d1, d_E, d_A, d_s, d_sp,
+                                                  self.dec2.data_ptr(), self.dec4.data_ptr(),
+                                                  self.A0.data_ptr(), self.part.data_ptr())
+        return self._finish(ms, finalise)
+
+    def _finish(self, ms: float, finalise: bool) -> ShardResult:
+        n, t = self.n, self.t
         dec2, dec4, A0, parts = self.exchange()
         dec = combine_decisions(dec2.cpu().numpy(), dec4.cpu().numpy(), n, t)
         fs = mpk = None
@@ -126,9 +139,9 @@ class ShardedCeremony:
             fs_t = torch.empty(n * 32, dtype=torch.uint8, device=self.dev)
             self.be.scalar_sum_device(self.ws, n, parts.data_ptr(), None, fs_t.data_ptr())
             fs = bytes(fs_t.cpu().numpy())
-            if dec.reconstruct.any():
-                raise NotImplementedError("sharded finalise with reconstruction (SURVEY.md §8 f4)")
-            mask = torch.from_numpy(dec.honest).to(self.dev)
+            # the gathered terms are A_i0 for honest dealers and g * a_i0 (reconstructed on the
+            # owning rank) for the reconstructable set, so the sum runs over the qualified set
+            mask = torch.from_numpy(dec.qualified).to(self.dev)
             mpk_t = torch.empty(32, dtype=torch.uint8, device=self.dev)
             self.be.point_sum_device(n, A0.data_ptr(), mask.data_ptr(), mpk_t.data_ptr())
             mpk = bytes(mpk_t.cpu().numpy())

@@ -140,12 +140,23 @@ int dkg_ceremony_run_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, c
 /* Sharded variant (one rank of a multi-GPU run): this ctx owns dealers [d0, d1) of the same
  * ceremony.  Produces this rank's commitments E/A and decision rows; the caller all-gathers
  * (RCCL over xGMI) the rows, A_0 values and share partial sums.  Device pointers throughout:
- * d_a, d_b [d1-d0][t+1][32]; d_dec2, d_dec4 [d1-d0][n]; d_A0 [d1-d0][32] (compressed A_i0);
+ * d_a, d_b [d1-d0][t+1][32]; d_dec2, d_dec4 [d1-d0][n]; d_A0 [d1-d0][32] = each dealer's
+ * compressed master-key term: A_i0, or g * a_i0 recovered by Lagrange interpolation of its shares
+ * when round-4 accusations put a qualified dealer in the reconstructable set (committee.rs:747-783;
+ * both are decided by the dealer's own rows, so mpk = sum of the terms of qualified dealers);
  * d_partial [n][32] = sum over this rank's QUALIFIED dealers of s_ij (qualification of a dealer is
  * decided by its own round-2 row, so it needs no exchange). */
 int dkg_ceremony_shard_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const void *d_a,
                               const void *d_b, void *d_dec2, void *d_dec4, void *d_A0, void *d_partial,
                               double *ms_total);
+/* Sharded verification of received broadcasts (the rank's dealers' rows of MembersFetchedState1 /
+ * Phase1 / Phase3, committee.rs:260-366, 508-580, 726-805): d_E, d_A [d1-d0][t+1][32] compressed
+ * commitments as broadcast, d_s, d_s_prime [d1-d0][n][32] the shares (Scalar::from_bytes
+ * semantics).  Outputs as dkg_ceremony_shard_device; an undecodable E row is DKG_MISSING in round 2
+ * (disqualified, no complaint), an undecodable A row an accusation in round 4. */
+int dkg_ceremony_shard_verify_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const void *d_E,
+                                     const void *d_A, const void *d_s, const void *d_s_prime, void *d_dec2,
+                                     void *d_dec4, void *d_A0, void *d_partial, double *ms_total);
 /* Combine step of the sharded run (device pointers):
  * round-3 sum (committee.rs:454-462): out[j] = sum over rows r with mask[r] (NULL = all) of in[r][j]
  * mod l; in [rows][n][32] canonical scalars (e.g. the all-gathered per-rank partials), out [n][32]. */

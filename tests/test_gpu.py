@@ -353,9 +353,62 @@ def test_sharded_ceremony_matches_golden(be, golden, name, ws):
     fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
     assert bytes(fs.cpu().numpy()).hex() == c["final_share"]
-    mask = torch.from_numpy(np.ascontiguousarray(d.honest)).to(dev)
+    mask = torch.from_numpy(np.ascontiguousarray(d.qualified)).to(dev)
     mpk = torch.empty(32, dtype=torch.uint8, device=dev)
     be.point_sum_device(n, gA0.data_ptr(), mask.data_ptr(), mpk.data_ptr())
+    assert bytes(mpk.cpu().numpy()).hex() == c["mpk"]
+
+
+@pytest.mark.parametrize("ws", [1, 2, 3])
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n16_t7.json"])
+def test_sharded_verify_faults(be, golden, name, ws):
+    """dkg_ceremony_shard_verify_device on the fixtures' broadcasts (faulty commitments / shares):
+    every rank's rows, the host exchange and combine, and the device finalise -- including a dealer
+    reconstructed on its owning rank (fault_a_generator: committee.rs:660-670, 747-783) -- give the
+    single-GPU golden decisions, final shares and mpk bit for bit."""
+    import numpy as np
+    import torch
+
+    from dkg_amd.distributed import combine_decisions, dealer_range
+
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    dev = torch.device("cuda", 0)
+    E, A, s, sp = (H(c[k]) for k in ("E", "A", "s", "s_prime"))
+
+    def put(x):
+        return torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)
+
+    dec2, dec4, terms, parts = [], [], [], []
+    for r in range(ws):
+        d0, d1 = dealer_range(r, ws, n)
+        D = d1 - d0
+        tE, tA = put(E[32 * N * d0:32 * N * d1]), put(A[32 * N * d0:32 * N * d1])
+        ts, tsp = put(s[32 * n * d0:32 * n * d1]), put(sp[32 * n * d0:32 * n * d1])
+        o2 = torch.zeros(max(D * n, 1), dtype=torch.uint8, device=dev)
+        o4 = torch.zeros_like(o2)
+        oA = torch.zeros(max(D * 32, 1), dtype=torch.uint8, device=dev)
+        op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+        be.ceremony_shard_verify_device(n, t, d0, d1, tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr(),
+                                        o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+        dec2.append(o2[:D * n])
+        dec4.append(o4[:D * n])
+        terms.append(oA[:D * 32])
+        parts.append(op)
+    g2, g4, gT, gp = (torch.cat(x) for x in (dec2, dec4, terms, parts))
+    assert dec_str(bytes(g2.cpu().numpy())) == c["dec2"]
+    d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
+    assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
+    assert d.complaints2.tolist() == c["complaints2"]
+    assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
+    fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
+    assert bytes(fs.cpu().numpy()).hex() == c["final_share"]
+    mask = torch.from_numpy(np.ascontiguousarray(d.qualified)).to(dev)
+    mpk = torch.empty(32, dtype=torch.uint8, device=dev)
+    be.point_sum_device(n, gT.data_ptr(), mask.data_ptr(), mpk.data_ptr())
     assert bytes(mpk.cpu().numpy()).hex() == c["mpk"]
 
 
