@@ -32,7 +32,7 @@ class CeremonyOut(ctypes.Structure):
         ("E", ctypes.c_void_p), ("A", ctypes.c_void_p),
         ("s", ctypes.c_void_p), ("s_prime", ctypes.c_void_p),
         ("dec2", ctypes.c_void_p), ("dec4", ctypes.c_void_p),
-        ("qualified", ctypes.c_void_p), ("r2_error", ctypes.c_void_p),
+        ("qualified", ctypes.c_void_p), ("r2_error", ctypes.c_void_p), ("r4_error", ctypes.c_void_p),
         ("complaints2", ctypes.c_void_p), ("reconstruct", ctypes.c_void_p),
         ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
         ("mpk", ctypes.c_uint8 * 32),
@@ -45,8 +45,8 @@ class CeremonyOut(ctypes.Structure):
 class BatchOut(ctypes.Structure):
     _fields_ = [
         ("mpk", ctypes.c_void_p), ("n_qualified", ctypes.c_void_p), ("qualified", ctypes.c_void_p),
-        ("r2_error", ctypes.c_void_p), ("complaints2", ctypes.c_void_p), ("reconstruct", ctypes.c_void_p),
-        ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
+        ("r2_error", ctypes.c_void_p), ("r4_error", ctypes.c_void_p), ("complaints2", ctypes.c_void_p),
+        ("reconstruct", ctypes.c_void_p), ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
         ("dec2", ctypes.c_void_p), ("dec4", ctypes.c_void_p),
         ("ms_round1", ctypes.c_double), ("ms_checks", ctypes.c_double), ("ms_round3", ctypes.c_double),
         ("ms_finalise", ctypes.c_double), ("ms_total", ctypes.c_double),

@@ -62,6 +62,7 @@ class CeremonyResult:
     mpk: bytes
     qualified: List[int]
     r2_error: List[int]
+    r4_error: List[int]
     complaints2: List[int]
     reconstruct: List[int]
     n_qualified: int
@@ -178,7 +179,7 @@ class Backend:
         N = t + 1
         bufs = {}
         o = CeremonyOut()
-        sizes = {"qualified": n, "r2_error": n, "complaints2": 4 * n, "reconstruct": n}
+        sizes = {"qualified": n, "r2_error": n, "r4_error": n, "complaints2": 4 * n, "reconstruct": n}
         if big:
             sizes.update({"E": 32 * n * N, "A": 32 * n * N, "s": 32 * n * n, "s_prime": 32 * n * n,
                           "dec2": n * n, "dec4": n * n, "final_share": 32 * n, "public_share": 32 * n})
@@ -191,7 +192,7 @@ class Backend:
         import struct
         r = CeremonyResult(
             n=n, t=t, mpk=bytes(o.mpk), qualified=list(bufs["qualified"].raw[:n]),
-            r2_error=list(bufs["r2_error"].raw[:n]),
+            r2_error=list(bufs["r2_error"].raw[:n]), r4_error=list(bufs["r4_error"].raw[:n]),
             complaints2=list(struct.unpack(f"<{n}i", bufs["complaints2"].raw[: 4 * n])),
             reconstruct=list(bufs["reconstruct"].raw[:n]), n_qualified=o.n_qualified,
             ms={"round1": o.ms_round1, "round2": o.ms_round2, "round3": o.ms_round3, "round4": o.ms_round4,
@@ -328,6 +329,7 @@ class BatchResult:
     n_qualified: List[int]
     qualified: bytes
     r2_error: bytes
+    r4_error: bytes
     complaints2: List[int]
     reconstruct: bytes
     final_share: Optional[bytes]
@@ -341,7 +343,8 @@ class BatchResult:
         n = self.n
         r = slice(c * n, (c + 1) * n)
         d = {"mpk": self.mpk[c], "n_qualified": self.n_qualified[c], "qualified": list(self.qualified[r]),
-             "r2_error": list(self.r2_error[r]), "complaints2": self.complaints2[r],
+             "r2_error": list(self.r2_error[r]), "r4_error": list(self.r4_error[r]),
+             "complaints2": self.complaints2[r],
              "reconstruct": list(self.reconstruct[r])}
         for k in ("final_share", "public_share"):
             v = getattr(self, k)
@@ -355,7 +358,8 @@ class BatchResult:
 def _batch_out(B, n, big):
     import struct  # noqa: F401
     V = B * n
-    sizes = {"mpk": 32 * B, "n_qualified": 4 * B, "qualified": V, "r2_error": V, "complaints2": 4 * V,
+    sizes = {"mpk": 32 * B, "n_qualified": 4 * B, "qualified": V, "r2_error": V, "r4_error": V,
+             "complaints2": 4 * V,
              "reconstruct": V}
     if big:
         sizes.update({"final_share": 32 * V, "public_share": 32 * V, "dec2": V * n, "dec4": V * n})
@@ -374,7 +378,7 @@ def _batch_result(B, n, t, o, bufs):
     return BatchResult(
         B=B, n=n, t=t, mpk=[bufs["mpk"].raw[32 * c:32 * c + 32] for c in range(B)],
         n_qualified=list(struct.unpack(f"<{B}i", bufs["n_qualified"].raw[:4 * B])),
-        qualified=g("qualified", V), r2_error=g("r2_error", V),
+        qualified=g("qualified", V), r2_error=g("r2_error", V), r4_error=g("r4_error", V),
         complaints2=list(struct.unpack(f"<{V}i", bufs["complaints2"].raw[:4 * V])),
         reconstruct=g("reconstruct", V), final_share=g("final_share", 32 * V), public_share=g("public_share", 32 * V),
         dec2=g("dec2", V * n), dec4=g("dec4", V * n),

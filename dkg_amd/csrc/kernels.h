@@ -73,6 +73,9 @@ void sum_points(size_t count, const uint32_t* pts, size_t stride, const uint8_t*
 void add_points(size_t count, const uint32_t* a, const uint32_t* b, size_t stride, uint32_t* out, hipStream_t stream);
 // Decision-matrix summaries for `groups` stacked ceremonies of n parties (dec [groups*n][n]):
 // row_reject[i] = any REJECT in row i; complaints[g][j] = REJECTs by receiver j in group g.
+// out[g*n+j] = 1 + #{qualified i : dec[g][i][j] == ACCEPT} < t + 1 (round-4 MisbehaviourHigherThreshold)
+void r4_error(size_t groups, size_t n, size_t t, const uint8_t* dec, const uint8_t* qmask, uint8_t* out,
+              hipStream_t stream);
 void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
                       hipStream_t stream);
 // hash_to_group tail: from_uniform_bytes(64 bytes as 16 LE words) -> SoA point (stride 1)

@@ -892,6 +892,26 @@ __global__ void k_col_complaints(size_t groups, size_t n, const uint8_t* __restr
   out[e] = c;
 }
 
+// Round-4 error of receiver j (committee.rs:515-516, 567-569): itself plus the qualified dealers
+// whose check it accepted are fewer than t+1.
+__global__ void k_r4_error(size_t groups, size_t n, size_t t, const uint8_t* __restrict__ dec,
+                           const uint8_t* __restrict__ qmask, uint8_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = g * n + j
+  if (e >= groups * n) return;
+  const size_t g = e / n, j = e % n;
+  size_t honest = 1;
+  for (size_t i = 0; i < n; i++) honest += qmask[g * n + i] && dec[(g * n + i) * n + j] == 1;  // ACCEPT
+  out[e] = honest < t + 1;
+}
+
+void r4_error(size_t groups, size_t n, size_t t, const uint8_t* dec, const uint8_t* qmask, uint8_t* out,
+              hipStream_t stream) {
+  const size_t rows = groups * n;
+  if (!rows) return;
+  hipLaunchKernelGGL(k_r4_error, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, groups, n, t, dec, qmask,
+                     out);
+}
+
 void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
                       hipStream_t stream) {
   const size_t rows = groups * n;

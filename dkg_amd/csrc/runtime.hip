@@ -317,14 +317,16 @@ std::vector<uint8_t> lagrange_at_zero(const std::vector<size_t>& xs, const uint8
   return secrets;
 }
 
-// Secrets of the reconstructed dealers from the shares disclosed by the first t+1 parties that are
-// not themselves reconstructed (hs = all shares [n][n][32]).  Shares of a qualified dealer passed
-// every round-2 check, so any t+1 of them interpolate to the same a_i0 (the reference's choice of
-// disclosing parties, committee.rs:755-773, gives the same value).
+// Secrets of the reconstructed dealers from the shares of parties 1..t+1 (hs = all shares
+// [n][n][32]).  Shares of a qualified dealer passed every round-2 check, so any t+1 of them
+// interpolate to the same a_i0: the reference's choice at a finalising party -- its own share plus
+// those disclosed by the final parties, committee.rs:755-773 -- gives the same value whenever it
+// has t+1 of them.  (With exactly t points the reference interpolates anyway -- :776-778 compares
+// against `threshold`, not t+1 -- and that party's mpk is wrong; this per-party quirk is not
+// reproduced: DESIGN.md section 2.)
 std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, const uint8_t* hs) {
   std::vector<size_t> xs;
-  for (size_t j = 0; j < n && xs.size() < t + 1; j++)
-    if (!recon[j]) xs.push_back(j);
+  for (size_t j = 0; j < t + 1; j++) xs.push_back(j);
   std::vector<uint8_t> rows;
   for (size_t i = 0; i < n; i++)
     if (recon[i]) rows.insert(rows.end(), hs + 32 * n * i, hs + 32 * n * (i + 1));
@@ -370,11 +372,13 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
   std::vector<uint8_t> recon(n, 0);
+  std::vector<size_t> honest4(n, 1);  // round-4 honest count of receiver j, itself included (:515-516)
   for (size_t i = 0; i < n; i++)
     for (size_t j = 0; j < n; j++) {
       if (i == j) continue;
       if (!qualified[i]) h4[i * n + j] = DKG_SKIPPED;  // disqualified dealers are skipped (:522)
       else if (h4[i * n + j] == DKG_REJECT) recon[i] = 1;  // -> reconstructable set (:660-670)
+      else if (h4[i * n + j] == DKG_ACCEPT) honest4[j]++;
     }
   // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
   std::vector<uint8_t> honest_mask(n);
@@ -415,6 +419,8 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   // ---- outputs
   if (out->qualified) memcpy(out->qualified, qualified.data(), n);
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), n);
+  if (out->r4_error)
+    for (size_t j = 0; j < n; j++) out->r4_error[j] = honest4[j] < t + 1;  // :567-569
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * n);
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
   int32_t nq = 0;
@@ -526,6 +532,11 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
   check_launch(ctx);
   if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
+  if (out->r4_error) {  // qmask (the qualified set) is on the device since round 3
+    uint8_t* r4e = buf<uint8_t>(ctx, "b.r4err", V);
+    dkgk::r4_error(B, n, t, dec4, qmask, r4e, ctx->stream);
+    d2h(ctx, out->r4_error, r4e, V);
+  }
   if (out->final_share) d2h(ctx, out->final_share, fs, 32 * V);
   if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * V);
   std::vector<uint8_t> h4;

@@ -17,7 +17,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import ACCEPT, MISSING, REJECT, SKIPPED  # noqa: F401  (ACCEPT re-exported for callers)
+from ._lib import ACCEPT, MISSING, REJECT, SKIPPED
 
 
 def dealer_range(rank: int, world_size: int, n: int):
@@ -37,6 +37,7 @@ class Decisions:
     complaints2: np.ndarray   # [n] int32, complaints raised by receiver j
     r2_error: np.ndarray      # [n] uint8, receiver j saw more than t complaints
     reconstruct: np.ndarray   # [n] uint8, qualified dealers accused in round 4
+    r4_error: np.ndarray      # [n] uint8, receiver j saw fewer than t+1 honest dealers in round 4
     honest: np.ndarray        # [n] uint8, qualified and not reconstructed (their A_i0 enter mpk)
 
 
@@ -58,7 +59,10 @@ def combine_decisions(dec2: np.ndarray, dec4: np.ndarray, n: int, t: int) -> Dec
     dec4[skip] = SKIPPED
     recon = ((dec4 == REJECT) & off & (qualified == 1)[:, None]).any(axis=1).astype(np.uint8)
     honest = (qualified & (1 - recon)).astype(np.uint8)
-    return Decisions(dec2, dec4, qualified, complaints, r2_error, recon, honest)
+    # receiver j counts itself plus the qualified dealers it accepted in round 4 (:515-516, 567-569)
+    honest4 = 1 + ((dec4 == ACCEPT) & off & (qualified == 1)[:, None]).sum(axis=0)
+    r4_error = (honest4 < t + 1).astype(np.uint8)
+    return Decisions(dec2, dec4, qualified, complaints, r2_error, recon, r4_error, honest)
 
 
 @dataclass

@@ -116,6 +116,8 @@ typedef struct {
   uint8_t *dec2, *dec4;         /* [n dealer][n receiver] */
   uint8_t *qualified;           /* [n] common qualified set after round 3 */
   uint8_t *r2_error;            /* [n] receiver j: more than t complaints (MisbehaviourHigherThreshold) */
+  uint8_t *r4_error;            /* [n] receiver j: fewer than t+1 honest dealers (itself included) in
+                                   round 4, MisbehaviourHigherThreshold (committee.rs:567-569) */
   int32_t *complaints2;         /* [n] complaints raised by receiver j in round 2 */
   uint8_t *reconstruct;         /* [n] dealers whose secret is reconstructed in finalise */
   uint8_t *final_share;         /* [n][32] s_j = sum_{i in Q} s_ij (committee.rs:454-462) */
@@ -134,7 +136,7 @@ int dkg_ceremony_verify(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *E, cons
                         const uint8_t *s_prime, dkg_ceremony_out *out);
 /* Device-resident variant for benchmarks: d_a, d_b are device pointers to [n][t+1][32] canonical
  * scalars; intermediates stay in HBM; only the small outputs (mpk, flags, counts, timings) are
- * copied back into *out (its array pointers are ignored except qualified / r2_error / complaints2). */
+ * copied back into *out (its array pointers are ignored except qualified / r2_error / r4_error / complaints2). */
 int dkg_ceremony_run_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, const void *d_b,
                             dkg_ceremony_out *out);
 /* Sharded variant (one rank of a multi-GPU run): this ctx owns dealers [d0, d1) of the same
@@ -176,6 +178,7 @@ typedef struct {
   int32_t *n_qualified;         /* [B] */
   uint8_t *qualified;           /* [B][n] */
   uint8_t *r2_error;            /* [B][n] receiver saw more than t complaints */
+  uint8_t *r4_error;            /* [B][n] receiver saw fewer than t+1 honest dealers in round 4 */
   int32_t *complaints2;         /* [B][n] complaints raised by each receiver in round 2 */
   uint8_t *reconstruct;         /* [B][n] */
   uint8_t *final_share;         /* [B][n][32] */

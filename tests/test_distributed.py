@@ -16,7 +16,8 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 L = 2**252 + 27742317777372353535851937790883648493
 NAMES = ["ceremony_n11_t5.json", "fault_share_flip_n10_t4.json", "fault_a_generator_n10_t4.json",
-         "fault_over_threshold_n10_t4.json", "fault_e_identity_n10_t4.json", "ceremony_n3_t1.json"]
+         "fault_over_threshold_n10_t4.json", "fault_e_identity_n10_t4.json", "ceremony_n3_t1.json",
+         "fault_a_many_n10_t4.json"]
 
 
 def _free_port():
@@ -67,6 +68,7 @@ def _rank_main(rank, ws, port, names, errq):
             assert d.complaints2.tolist() == c["complaints2"], name
             assert d.r2_error.tolist() == [int(x) for x in c["r2_error"]], name
             assert d.reconstruct.tolist() == c["reconstruct"], name
+            assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]], name
             assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"], name
             parts = gpart.numpy().reshape(ws, n, 32)
             fs = b"".join((sum(int.from_bytes(bytes(parts[r, j]), "little") for r in range(ws)) % L)
@@ -112,4 +114,5 @@ def test_combine_single_process(golden):
         d = combine_decisions(dec2, dec4, n, t)
         assert d.qualified.tolist() == c["qualified"]
         assert d.reconstruct.tolist() == c["reconstruct"]
+        assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
         assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]

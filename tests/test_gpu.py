@@ -103,7 +103,7 @@ def test_poly_eval(be, golden):
 CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.json",
               "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
 FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
-          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json"]
+          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json"]
 
 
 @pytest.mark.parametrize("name", CEREMONIES)
@@ -162,6 +162,7 @@ def _check_ceremony(c, r, n):
     assert r.r2_error == [int(x) for x in c["r2_error"]]
     assert r.complaints2 == c["complaints2"]
     assert r.reconstruct == c["reconstruct"]
+    assert r.r4_error == [int(x) for x in c["r4_error"]]
     assert r.final_share.hex() == c["final_share"]
     assert r.public_share.hex() == c["public_share"]
     assert r.mpk.hex() == c["mpk"]
@@ -349,6 +350,7 @@ def test_sharded_ceremony_matches_golden(be, golden, name, ws):
     assert bytes(gA0.cpu().numpy()) == b"".join(H(c["A"])[32 * N * i:32 * N * i + 32] for i in range(n))
     d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
     assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
+    assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
     assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
     fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
@@ -401,6 +403,7 @@ def test_sharded_verify_faults(be, golden, name, ws):
     assert dec_str(bytes(g2.cpu().numpy())) == c["dec2"]
     d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
     assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
+    assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
     assert d.complaints2.tolist() == c["complaints2"]
     assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
     fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
@@ -420,6 +423,7 @@ def _check_batch_member(c, d, n):
     assert d["r2_error"] == [int(x) for x in c["r2_error"]]
     assert d["complaints2"] == c["complaints2"]
     assert d["reconstruct"] == c["reconstruct"]
+    assert d["r4_error"] == [int(x) for x in c["r4_error"]]
     assert d["final_share"].hex() == c["final_share"]
     assert d["public_share"].hex() == c["public_share"]
     assert d["mpk"].hex() == c["mpk"]

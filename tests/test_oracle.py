@@ -108,7 +108,7 @@ def test_dealer_rng(golden):
 CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.json",
               "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
 FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
-          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json"]
+          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json"]
 
 
 @pytest.mark.parametrize("name", CEREMONIES)

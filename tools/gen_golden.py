@@ -213,12 +213,16 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
             lhs = gmul_base(Sw[i][j])                                  # :537
             rhs = msm(pw, Aw[i])                                       # :538-539
             dec4[i][j] = int(lhs == rhs)                               # :541
+    # fewer than t+1 honest dealers (self included) in receiver j's round 4 (committee.rs:515-516, 567-569)
+    r4_error = [1 + sum(1 for i in range(n) if i != j and qualified[i] and dec4[i][j] == 1) < t + 1
+                for j in range(n)]
     # round 5 / finalise (committee.rs:625-805): accused-and-valid dealers are reconstructed
     recon = [int(qualified[i] and any(dec4[i][j] == 0 for j in range(n) if j != i)) for i in range(n)]
     mpk = ID
     for i in range(n):
         if recon[i]:
-            xs = [j + 1 for j in range(n) if j != i and not recon[j]][: t + 1]
+            # a qualified dealer's shares all passed round 2: any t+1 of them give its secret
+            xs = [j + 1 for j in range(n) if j != i][: t + 1]
             ys = [Sw[i][x - 1] for x in xs]
             secret = lagrange_at_zero(ys, xs)                          # :784-788
             assert secret == A[i][0]
@@ -236,7 +240,7 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
         "s_prime": "".join(hx(scb(x)) for row in SPw for x in row),
         "dec2": "".join(str(d) for row in dec2 for d in row),
         "dec4": "".join(str(d) for row in dec4 for d in row),
-        "complaints2": complaints2, "r2_error": r2_error, "qualified": qualified,
+        "complaints2": complaints2, "r2_error": r2_error, "r4_error": r4_error, "qualified": qualified,
         "reconstruct": recon,
         "final_share": "".join(hx(scb(x)) for x in final_share),
         "public_share": "".join(hx(p) for p in public_share),
@@ -653,6 +657,7 @@ def main():
                        {"kind": "rand_flip", "dealer": 7, "receiver": 9}],
         "a_generator": [{"kind": "A_generator", "dealer": 6}],
         "over_threshold": [{"kind": "E_identity", "dealer": d} for d in (1, 2, 4, 8, 9)],
+        "a_many": [{"kind": "A_generator", "dealer": d} for d in (1, 3, 5, 6, 8, 10)],
     }
     for name, fs in faults.items():
         files[f"fault_{name}_n10_t4.json"] = ceremony(10, 4, m, ceremony_id=1, faults=fs)
