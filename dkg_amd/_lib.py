@@ -36,7 +36,7 @@ class CeremonyOut(ctypes.Structure):
         ("complaints2", ctypes.c_void_p), ("reconstruct", ctypes.c_void_p),
         ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
         ("mpk", ctypes.c_uint8 * 32),
-        ("n_qualified", ctypes.c_int32),
+        ("n_qualified", ctypes.c_int32), ("phase4_error", ctypes.c_int32),
         ("ms_round1", ctypes.c_double), ("ms_round2", ctypes.c_double), ("ms_round3", ctypes.c_double),
         ("ms_round4", ctypes.c_double), ("ms_finalise", ctypes.c_double), ("ms_total", ctypes.c_double),
     ]
@@ -44,7 +44,8 @@ class CeremonyOut(ctypes.Structure):
 
 class BatchOut(ctypes.Structure):
     _fields_ = [
-        ("mpk", ctypes.c_void_p), ("n_qualified", ctypes.c_void_p), ("qualified", ctypes.c_void_p),
+        ("mpk", ctypes.c_void_p), ("n_qualified", ctypes.c_void_p), ("phase4_error", ctypes.c_void_p),
+        ("qualified", ctypes.c_void_p),
         ("r2_error", ctypes.c_void_p), ("r4_error", ctypes.c_void_p), ("complaints2", ctypes.c_void_p),
         ("reconstruct", ctypes.c_void_p), ("final_share", ctypes.c_void_p), ("public_share", ctypes.c_void_p),
         ("dec2", ctypes.c_void_p), ("dec4", ctypes.c_void_p),
@@ -83,6 +84,7 @@ def lib():
     L.dkg_verify_receiver.argtypes = [p, sz, sz, ctypes.c_int, sz, u8p, u8p, p, p]
     L.dkg_ceremony_run.argtypes = [p, sz, sz, u8p, u8p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_verify.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
+    L.dkg_ceremony_verify_fetched.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, u8p, u8p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_run_device.argtypes = [p, sz, sz, p, p, ctypes.POINTER(CeremonyOut)]
     L.dkg_ceremony_shard_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]
     L.dkg_ceremony_shard_verify_device.argtypes = [p, sz, sz, sz, sz, p, p, p, p, p, p, p, p,
@@ -112,7 +114,7 @@ EXPORTED = [
     "dkg_device_count", "dkg_env_init",
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
-    "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
+    "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_verify_fetched", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
     "dkg_ceremony_shard_verify_device",
     "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_member_keys", "dkg_enc_randomness",
     "dkg_enc_randomness_device", "dkg_encrypt_shares", "dkg_decrypt_shares", "dkg_ceremony_run_full_device",

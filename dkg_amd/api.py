@@ -66,6 +66,7 @@ class CeremonyResult:
     complaints2: List[int]
     reconstruct: List[int]
     n_qualified: int
+    phase4_error: int
     ms: dict
     E: Optional[bytes] = None
     A: Optional[bytes] = None
@@ -195,6 +196,7 @@ class Backend:
             r2_error=list(bufs["r2_error"].raw[:n]), r4_error=list(bufs["r4_error"].raw[:n]),
             complaints2=list(struct.unpack(f"<{n}i", bufs["complaints2"].raw[: 4 * n])),
             reconstruct=list(bufs["reconstruct"].raw[:n]), n_qualified=o.n_qualified,
+            phase4_error=o.phase4_error,
             ms={"round1": o.ms_round1, "round2": o.ms_round2, "round3": o.ms_round3, "round4": o.ms_round4,
                 "finalise": o.ms_finalise, "total": o.ms_total})
         if big:
@@ -212,6 +214,20 @@ class Backend:
         for k in ("E", "A", "s", "s_prime"):
             setattr(o, k, None)
         _check(self._ctx, _lib.lib().dkg_ceremony_verify(self._ctx, n, t, E, A, s, s_prime, ctypes.byref(o)))
+        r = self._result(n, t, o, bufs, True)
+        r.E, r.A, r.s, r.s_prime = E, A, s, s_prime
+        return r
+
+    def ceremony_verify_fetched(self, E: bytes, A: bytes, s: bytes, s_prime: bytes, fetched1: bytes,
+                                fetched3: bytes, n: int, t: int) -> CeremonyResult:
+        """ceremony_verify after the broadcast intake (MembersFetchedState1/3::from_broadcast):
+        fetched1[i] / fetched3[i] = 0 for a dealer whose phase-1 / phase-3 broadcast is absent or
+        malformed (see dkg_amd.broadcast)."""
+        o, bufs = self._ceremony_out(n, t, True)
+        for k in ("E", "A", "s", "s_prime"):
+            setattr(o, k, None)
+        _check(self._ctx, _lib.lib().dkg_ceremony_verify_fetched(self._ctx, n, t, E, A, s, s_prime, fetched1,
+                                                                 fetched3, ctypes.byref(o)))
         r = self._result(n, t, o, bufs, True)
         r.E, r.A, r.s, r.s_prime = E, A, s, s_prime
         return r
@@ -327,6 +343,7 @@ class BatchResult:
     t: int
     mpk: List[bytes]
     n_qualified: List[int]
+    phase4_error: bytes
     qualified: bytes
     r2_error: bytes
     r4_error: bytes
@@ -342,7 +359,8 @@ class BatchResult:
         """The outputs of ceremony c in the layout of a single CeremonyResult."""
         n = self.n
         r = slice(c * n, (c + 1) * n)
-        d = {"mpk": self.mpk[c], "n_qualified": self.n_qualified[c], "qualified": list(self.qualified[r]),
+        d = {"mpk": self.mpk[c], "n_qualified": self.n_qualified[c], "phase4_error": self.phase4_error[c],
+             "qualified": list(self.qualified[r]),
              "r2_error": list(self.r2_error[r]), "r4_error": list(self.r4_error[r]),
              "complaints2": self.complaints2[r],
              "reconstruct": list(self.reconstruct[r])}
@@ -358,7 +376,7 @@ class BatchResult:
 def _batch_out(B, n, big):
     import struct  # noqa: F401
     V = B * n
-    sizes = {"mpk": 32 * B, "n_qualified": 4 * B, "qualified": V, "r2_error": V, "r4_error": V,
+    sizes = {"mpk": 32 * B, "n_qualified": 4 * B, "phase4_error": B, "qualified": V, "r2_error": V, "r4_error": V,
              "complaints2": 4 * V,
              "reconstruct": V}
     if big:
@@ -378,6 +396,7 @@ def _batch_result(B, n, t, o, bufs):
     return BatchResult(
         B=B, n=n, t=t, mpk=[bufs["mpk"].raw[32 * c:32 * c + 32] for c in range(B)],
         n_qualified=list(struct.unpack(f"<{B}i", bufs["n_qualified"].raw[:4 * B])),
+        phase4_error=g("phase4_error", B),
         qualified=g("qualified", V), r2_error=g("r2_error", V), r4_error=g("r4_error", V),
         complaints2=list(struct.unpack(f"<{V}i", bufs["complaints2"].raw[:4 * V])),
         reconstruct=g("reconstruct", V), final_share=g("final_share", 32 * V), public_share=g("public_share", 32 * V),

@@ -245,8 +245,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
 }
 
 void verify_one(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t dealer_base, const uint32_t* Ccomp,
-                const uint32_t* s, const uint32_t* sp, uint8_t* dec, bool timed) {
-  VerifySeg g{round, D, dealer_base, Ccomp, s, sp, dec};
+                const uint32_t* s, const uint32_t* sp, uint8_t* dec, bool timed, const uint8_t* extra_ok = nullptr) {
+  VerifySeg g{round, D, dealer_base, Ccomp, s, sp, dec, extra_ok};
   verify_device(ctx, n, t, &g, 1, timed, round == 2 ? "r2" : "r4");
 }
 
@@ -255,14 +255,15 @@ void verify_one(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t de
 // mask applied afterwards depends on round 2, so every output is identical to protocol order.
 // Otherwise round 2, then (after `between`, e.g. round 3) round 4, each timed when nsub == 1.
 // `after2` (may be null) is recorded on ctx->stream once the round-2 decisions are complete.
-// e_ok (may be null): per-dealer device mask, 0 = the dealer's round-1 ciphertexts are missing data
+// e_ok (may be null): per-dealer device mask, 0 = the dealer's round-1 data is missing (round 2:
+// DKG_MISSING); a_ok (may be null): 0 = its phase-3 commitments are missing (round 4: accusation)
 // (full mode), folded into the round-2 decisions like an undecodable commitment.
 template <typename F>
 void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
                    const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
-                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr) {
+                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
   if (ctx->overlap) {
-    VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok}, {4, D, dealer_base, Acomp, s, nullptr, dec4}};
+    VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok}, {4, D, dealer_base, Acomp, s, nullptr, dec4, a_ok}};
     verify_device(ctx, n, t, g, 2, true, "r24");
     if (after2) HCK(hipEventRecord(after2, ctx->stream));
     sync(ctx);
@@ -275,7 +276,7 @@ void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_bas
     sync(ctx);
     collect_phases(ctx);
     between();
-    verify_one(ctx, n, t, 4, D, dealer_base, Acomp, s, nullptr, dec4, true);
+    verify_one(ctx, n, t, 4, D, dealer_base, Acomp, s, nullptr, dec4, true, a_ok);
     sync(ctx);
     collect_phases(ctx);
   }
@@ -287,9 +288,6 @@ double ev_ms(dkg_ctx* ctx, int a, int b) {
   return ms;
 }
 
-// Lagrange reconstruction (polynomial.rs:172-184 at 0; the reference interpolates the disclosed
-// shares, committee.rs:748-789) of the secret of every dealer i with recon[i], from the shares of
-// the first t+1 parties outside the reconstructable set.  hs: the ceremony's shares [n][n][32].
 // lagrange_interpolation at zero (polynomial.rs:162-184) of `rows` share vectors: row r holds the
 // evaluations at x = j + 1 at byte offset 32 * (r * stride + j); the abscissae used are xs (0-based j).
 std::vector<uint8_t> lagrange_at_zero(const std::vector<size_t>& xs, const uint8_t* ys, size_t rows, size_t stride) {
@@ -336,7 +334,7 @@ std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, 
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
 void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
                       const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
-                      const uint8_t* e_ok = nullptr) {
+                      const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
   const size_t N = t + 1;
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
@@ -367,7 +365,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     dkgk::encode_points(pub, n, n, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
-  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok);
+  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok, a_ok);
   d2h(ctx, h4.data(), dec4, n * n);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
@@ -426,6 +424,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   int32_t nq = 0;
   for (auto q : qualified) nq += q;
   out->n_qualified = nq;
+  out->phase4_error = nq - (int32_t)nrecon <= (int32_t)t;  // committee.rs:673-677
   if (copy_big) {
     if (out->dec2) memcpy(out->dec2, h2.data(), n * n);
     if (out->dec4) memcpy(out->dec4, h4.data(), n * n);
@@ -558,6 +557,12 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), V);
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * V);
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), V);
+  if (out->phase4_error)
+    for (size_t c = 0; c < B; c++) {
+      int32_t h = 0;
+      for (size_t i = c * n; i < (c + 1) * n; i++) h += qualified[i] && !recon[i];
+      out->phase4_error[c] = h <= (int32_t)t;  // committee.rs:673-677
+    }
   if (out->n_qualified)
     for (size_t c = 0; c < B; c++) {
       int32_t q = 0;
@@ -1042,6 +1047,37 @@ int dkg_ceremony_verify(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E, cons
     HCK(hipEventRecord(ctx->ev[0], ctx->stream));
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, true);
+    out->ms_round1 = 0;
+    out->ms_round2 = ev_ms(ctx, 1, 2);
+    out->ms_round3 = ev_ms(ctx, 2, 3);
+    out->ms_round4 = ev_ms(ctx, 3, 4);
+    out->ms_finalise = ev_ms(ctx, 4, 5);
+    out->ms_total = ev_ms(ctx, 0, 5);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_verify_fetched(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E, const uint8_t* A,
+                                const uint8_t* s, const uint8_t* s_prime, const uint8_t* fetched1,
+                                const uint8_t* fetched3, dkg_ceremony_out* out) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (dkg_env_check(t, n) != DKG_OK || !out || !fetched1 || !fetched3) return DKG_E_ARG;
+    const size_t N = t + 1;
+    uint32_t* Ec = buf<uint32_t>(ctx, "cer_E", 32 * n * N);
+    uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
+    h2d(ctx, Ec, E, 32 * n * N);
+    h2d(ctx, Ac, A, 32 * n * N);
+    uint32_t* ds = upload_scalars(ctx, "cer_s", s, n * n);
+    uint32_t* dsp = upload_scalars(ctx, "cer_sp", s_prime, n * n);
+    uint8_t* f1 = buf<uint8_t>(ctx, "cer_f1", n);
+    uint8_t* f3 = buf<uint8_t>(ctx, "cer_f3", n);
+    h2d(ctx, f1, fetched1, n);
+    h2d(ctx, f3, fetched3, n);
+    HCK(hipEventRecord(ctx->ev[0], ctx->stream));
+    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, true, f1, f3);
     out->ms_round1 = 0;
     out->ms_round2 = ev_ms(ctx, 1, 2);
     out->ms_round3 = ev_ms(ctx, 2, 3);

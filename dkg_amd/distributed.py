@@ -39,6 +39,7 @@ class Decisions:
     reconstruct: np.ndarray   # [n] uint8, qualified dealers accused in round 4
     r4_error: np.ndarray      # [n] uint8, receiver j saw fewer than t+1 honest dealers in round 4
     honest: np.ndarray        # [n] uint8, qualified and not reconstructed (their A_i0 enter mpk)
+    phase4_error: bool        # qualified minus reconstructable <= t: Phase4::proceed fails (:673-677)
 
 
 def combine_decisions(dec2: np.ndarray, dec4: np.ndarray, n: int, t: int) -> Decisions:
@@ -62,7 +63,8 @@ def combine_decisions(dec2: np.ndarray, dec4: np.ndarray, n: int, t: int) -> Dec
     # receiver j counts itself plus the qualified dealers it accepted in round 4 (:515-516, 567-569)
     honest4 = 1 + ((dec4 == ACCEPT) & off & (qualified == 1)[:, None]).sum(axis=0)
     r4_error = (honest4 < t + 1).astype(np.uint8)
-    return Decisions(dec2, dec4, qualified, complaints, r2_error, recon, r4_error, honest)
+    return Decisions(dec2, dec4, qualified, complaints, r2_error, recon, r4_error, honest,
+                     bool(int(honest.sum()) <= t))
 
 
 @dataclass

@@ -124,6 +124,9 @@ typedef struct {
   uint8_t *public_share;        /* [n][32] g * s_j (committee.rs:464-466) */
   uint8_t mpk[32];              /* MasterPublicKey (committee.rs:726-805) */
   int32_t n_qualified;
+  int32_t phase4_error;         /* 1: qualified minus reconstructable <= t, every party's
+                                   Phases<Phase4>::proceed fails with MisbehaviourHigherThreshold
+                                   (committee.rs:673-677) -- mpk is then the value it would have */
   /* device times of each phase, milliseconds (HIP events) */
   double ms_round1, ms_round2, ms_round3, ms_round4, ms_finalise, ms_total;
 } dkg_ceremony_out;
@@ -134,6 +137,16 @@ int dkg_ceremony_run(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *a, const u
  * E, A [n][t+1][32]; s, s_prime [n][n][32]. */
 int dkg_ceremony_verify(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *E, const uint8_t *A, const uint8_t *s,
                         const uint8_t *s_prime, dkg_ceremony_out *out);
+/* dkg_ceremony_verify after the broadcast intake of MembersFetchedState1/3::from_broadcast
+ * (committee.rs:825-870, 921-966): fetched1[i] = 0 when dealer i's phase-1 broadcast is absent or
+ * malformed (committed_coefficients.len() != t+1 or encrypted_shares.len() != n): no fetched data,
+ * DKG_MISSING for every receiver in round 2 (disqualified, no complaint, :331-335).
+ * fetched3[i] = 0 when its phase-3 broadcast is absent or has the wrong length: a qualified dealer
+ * is accused by every receiver in round 4 (:549-555) and reconstructed.  The E / A rows of such
+ * dealers are not read for decisions (any bytes). */
+int dkg_ceremony_verify_fetched(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *E, const uint8_t *A,
+                                const uint8_t *s, const uint8_t *s_prime, const uint8_t *fetched1,
+                                const uint8_t *fetched3, dkg_ceremony_out *out);
 /* Device-resident variant for benchmarks: d_a, d_b are device pointers to [n][t+1][32] canonical
  * scalars; intermediates stay in HBM; only the small outputs (mpk, flags, counts, timings) are
  * copied back into *out (its array pointers are ignored except qualified / r2_error / r4_error / complaints2). */
@@ -176,6 +189,7 @@ typedef struct {
   /* host outputs; any pointer may be NULL */
   uint8_t *mpk;                 /* [B][32] MasterPublicKey per ceremony (committee.rs:726-805) */
   int32_t *n_qualified;         /* [B] */
+  uint8_t *phase4_error;        /* [B] qualified minus reconstructable <= t (committee.rs:673-677) */
   uint8_t *qualified;           /* [B][n] */
   uint8_t *r2_error;            /* [B][n] receiver saw more than t complaints */
   uint8_t *r4_error;            /* [B][n] receiver saw fewer than t+1 honest dealers in round 4 */

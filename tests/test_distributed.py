@@ -69,6 +69,7 @@ def _rank_main(rank, ws, port, names, errq):
             assert d.r2_error.tolist() == [int(x) for x in c["r2_error"]], name
             assert d.reconstruct.tolist() == c["reconstruct"], name
             assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]], name
+            assert d.phase4_error == c["phase4_error"], name
             assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"], name
             parts = gpart.numpy().reshape(ws, n, 32)
             fs = b"".join((sum(int.from_bytes(bytes(parts[r, j]), "little") for r in range(ws)) % L)
@@ -115,4 +116,5 @@ def test_combine_single_process(golden):
         assert d.qualified.tolist() == c["qualified"]
         assert d.reconstruct.tolist() == c["reconstruct"]
         assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
+        assert d.phase4_error == c["phase4_error"]
         assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]

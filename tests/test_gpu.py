@@ -163,6 +163,7 @@ def _check_ceremony(c, r, n):
     assert r.complaints2 == c["complaints2"]
     assert r.reconstruct == c["reconstruct"]
     assert r.r4_error == [int(x) for x in c["r4_error"]]
+    assert r.phase4_error == int(c["phase4_error"])
     assert r.final_share.hex() == c["final_share"]
     assert r.public_share.hex() == c["public_share"]
     assert r.mpk.hex() == c["mpk"]
@@ -351,6 +352,7 @@ def test_sharded_ceremony_matches_golden(be, golden, name, ws):
     d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
     assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
     assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
+    assert d.phase4_error == c["phase4_error"]
     assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
     fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
@@ -404,6 +406,7 @@ def test_sharded_verify_faults(be, golden, name, ws):
     d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
     assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
     assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
+    assert d.phase4_error == c["phase4_error"]
     assert d.complaints2.tolist() == c["complaints2"]
     assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
     fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
@@ -424,6 +427,7 @@ def _check_batch_member(c, d, n):
     assert d["complaints2"] == c["complaints2"]
     assert d["reconstruct"] == c["reconstruct"]
     assert d["r4_error"] == [int(x) for x in c["r4_error"]]
+    assert d["phase4_error"] == int(c["phase4_error"])
     assert d["final_share"].hex() == c["final_share"]
     assert d["public_share"].hex() == c["public_share"]
     assert d["mpk"].hex() == c["mpk"]
@@ -650,6 +654,46 @@ def test_complaint_proofs_device(be, golden):
                                b"".join(H(x["randomness"]) for x in r3), Es, As)
     assert res == [VERDICT[x["verdict"]] for x in r3]
     assert be.misbehaviour_prove(b"", b"", b"") == b""
+
+
+def test_ceremony_from_broadcasts(be, golden):
+    """a committee's broadcasts through the intake (dkg_amd.broadcast) and
+    dkg_ceremony_verify_fetched.  Dealers 3 and 7 send no / a malformed phase-1 broadcast (MISSING,
+    disqualified without complaints, committee.rs:331-335); dealers 5 and 10 send no / a malformed
+    phase-3 broadcast (accused by everyone, :549-555, and reconstructed).  The expected outputs are
+    restated here from the reference's rules on the fixture's values."""
+    from dkg_amd.broadcast import BroadcastPhase1, BroadcastPhase3, verify_broadcasts
+    from tests.test_broadcast import committee_broadcasts
+
+    c = golden("ceremony_n10_t4.json")
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    p1, p3 = committee_broadcasts(c)
+    p1[2] = None
+    p1[6] = BroadcastPhase1(p1[6].committed_coefficients[:t], p1[6].encrypted_shares)
+    p3[4] = None
+    p3[9] = BroadcastPhase3(p3[9].committed_coefficients + p3[9].committed_coefficients[:1])
+    for overlap in (True, False):
+        be.set_overlap(overlap)
+        r = verify_broadcasts(be, n, t, p1, p3)
+        miss, acc = {2, 6}, {4, 9}
+        exp2 = [[2 if i == j else (MISSING if i in miss else ACCEPT) for j in range(n)] for i in range(n)]
+        exp4 = [[2 if i == j else (3 if i in miss else (REJECT if i in acc else ACCEPT)) for j in range(n)]
+                for i in range(n)]
+        assert list(r.dec2) == [x for row in exp2 for x in row]
+        assert list(r.dec4) == [x for row in exp4 for x in row]
+        qualified = [int(i not in miss) for i in range(n)]
+        assert r.qualified == qualified and r.complaints2 == [0] * n and r.r2_error == [0] * n
+        assert r.reconstruct == [int(i in acc) for i in range(n)]
+        honest4 = [1 + sum(1 for i in range(n) if i != j and exp4[i][j] == ACCEPT) for j in range(n)]
+        assert r.r4_error == [int(h < t + 1) for h in honest4] and r.phase4_error == 0
+        s, a = H(c["s"]), H(c["a"])
+        fs = [sum(int.from_bytes(s[32 * (i * n + j):32 * (i * n + j + 1)], "little") for i in range(n) if qualified[i]) % L
+              for j in range(n)]
+        assert r.final_share == b"".join(x.to_bytes(32, "little") for x in fs)
+        sec = sum(int.from_bytes(a[32 * (t + 1) * i:32 * (t + 1) * i + 32], "little") for i in range(n) if qualified[i]) % L
+        assert r.mpk == O.base_mul(sec.to_bytes(32, "little"))  # committee.rs:1633-1647 property
+    be.set_overlap(True)
 
 
 def test_ceremony_n4096_device(be):

@@ -218,6 +218,8 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
                 for j in range(n)]
     # round 5 / finalise (committee.rs:625-805): accused-and-valid dealers are reconstructed
     recon = [int(qualified[i] and any(dec4[i][j] == 0 for j in range(n) if j != i)) for i in range(n)]
+    # Phases<Phase4>::proceed (committee.rs:673-677): too few honest (qualified, not reconstructed)
+    phase4_error = sum(qualified) - sum(recon) <= t
     mpk = ID
     for i in range(n):
         if recon[i]:
@@ -240,7 +242,8 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
         "s_prime": "".join(hx(scb(x)) for row in SPw for x in row),
         "dec2": "".join(str(d) for row in dec2 for d in row),
         "dec4": "".join(str(d) for row in dec4 for d in row),
-        "complaints2": complaints2, "r2_error": r2_error, "r4_error": r4_error, "qualified": qualified,
+        "complaints2": complaints2, "r2_error": r2_error, "r4_error": r4_error, "phase4_error": phase4_error,
+        "qualified": qualified,
         "reconstruct": recon,
         "final_share": "".join(hx(scb(x)) for x in final_share),
         "public_share": "".join(hx(p) for p in public_share),
