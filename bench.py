@@ -59,11 +59,13 @@ def _naf(m):
     return digits
 
 
-def algorithmic_valu(n, t, rnd=2):
+def algorithmic_valu(n, t, rnd=2, U=1):
     """Closed-form VALU instruction count of one verification round over all n dealers as
-    implemented (DESIGN.md "Work per unit"): binomial-basis Horner, stepping, fixed-base check."""
+    implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces of L = ceil((t+1)/U)
+    coefficients, stepping, recombination by y_j = j^L (U > 1), fixed-base check."""
+    L_ = -(-(t + 1) // U)
     cost_m = {}
-    for m in range(1, t + 1):
+    for m in range(1, L_):
         ds = _naf(m)
         c = VALU["ge_to_cached"] + VALU["ge_add"]          # e_{m-1} + e_m
         if len(ds) > 1:
@@ -74,18 +76,32 @@ def algorithmic_valu(n, t, rnd=2):
                 if nz:
                     c += VALU["ge_add_signed"]
         cost_m[m] = c
-    binom = sum(cost_m[m] * (t - m + 1) for m in range(1, t + 1))   # position m is live for t-m+1 steps
-    stepping = n * ((t + 1) * VALU["ge_to_cached"] + t * VALU["ge_add"])
+    # position m of a piece is live for L-m steps
+    binom = U * sum(cost_m[m] * (L_ - m) for m in range(1, L_))
+    stepping = U * n * (L_ * VALU["ge_to_cached"] + (L_ - 1) * VALU["ge_add"])
+    combine = 0
+    if U > 1:
+        for j in range(1, n + 1):
+            ds = _naf(pow(j, L_, L))
+            c = 2 * VALU["ge_to_cached"] + VALU["ge_add"]   # addend, Q_u, + Q_u
+            for i in range(len(ds) - 2, -1, -1):
+                nz = ds[i] != 0
+                c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
+                if nz:
+                    c += VALU["ge_add_signed"]
+            combine += (U - 1) * c
     check = n * ((2 if rnd == 2 else 1) * 64 * VALU["comb_window"] + VALU["eq"])
-    return {"binomial": binom * n, "stepping": stepping * n, "check": check * n}
+    return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
-def fused_valu(n, t):
-    """Work of the fused round-2 + round-4 pipeline: both tables' binomial and stepping; one check
-    kernel computing g*s once (64 comb windows), h*s' (64 more) and both equalities per pair."""
-    w2, w4 = algorithmic_valu(n, t, 2), algorithmic_valu(n, t, 4)
-    return {"binomial": w2["binomial"] + w4["binomial"], "stepping": w2["stepping"] + w4["stepping"],
-            "check": n * n * (2 * 64 * VALU["comb_window"] + 2 * VALU["eq"])}
+def fused_valu(n, t, U=1):
+    """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
+    recombination; one check kernel computing g*s once (64 comb windows), h*s' (64 more) and both
+    equalities per pair."""
+    w2, w4 = algorithmic_valu(n, t, 2, U), algorithmic_valu(n, t, 4, U)
+    out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
+    out["check"] = n * n * (2 * 64 * VALU["comb_window"] + 2 * VALU["eq"])
+    return out
 
 
 def cpu_baseline(n, t, seconds_target=15.0):
@@ -203,6 +219,7 @@ def main():
     ap.add_argument("--config", default="D", choices=sorted(CONFIGS) + sorted(BATCH))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="dealer-chunk streams of the round-2/4 checks")
+    ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")
@@ -225,6 +242,7 @@ def main():
     be = dkg_amd.Backend(local)
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
+    be.set_split(args.split)
     h = be.env_init(t, n)
     N = t + 1
     master = b"\xbe" * 32
@@ -301,8 +319,10 @@ def main():
         out["config"]["verify_streams"] = args.streams
         out["config"]["rounds_2_4_fused"] = not args.no_overlap
         ov = not args.no_overlap
-        w2, w4 = algorithmic_valu(n, t, 2), algorithmic_valu(n, t, 4)
-        work = fused_valu(n, t) if ov else w2
+        U = be.last_split()
+        out["config"]["degree_split"] = U
+        w2, w4 = algorithmic_valu(n, t, 2, U), algorithmic_valu(n, t, 4, U)
+        work = fused_valu(n, t, U) if ov else w2
         # per-kernel device times need the serialised schedule (one chunk stream): one extra,
         # untimed ceremony in the same round order as the timed ones
         be.set_streams(1)
@@ -314,10 +334,10 @@ def main():
         # VALU efficiency of all checks: closed-form work of rounds 2 and 4 (as scheduled) over the
         # timed ceremony's rounds 2-4 wall time
         vms = res.ms["round2"] + res.ms["round3"] + res.ms["round4"]
-        wall = fused_valu(n, t) if ov else {k: w2[k] + w4[k] for k in w2}
+        wall = work if ov else {k: w2[k] + w4[k] for k in w2}
         out["checks_valu_frac"] = sum(wall.values()) / (vms / 1e3) / INT32_PEAK
         rl = {}
-        for k in ("binomial", "stepping", "check"):
+        for k in ("binomial", "stepping", "combine", "check"):
             ms = ph.get(k, 0.0)
             if ms > 0:
                 rl[k] = {"ms_per_pass": round(ms, 3), "valu_instr": work[k],

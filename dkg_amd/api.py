@@ -109,18 +109,26 @@ class Backend:
         """Dealer-chunk streams of the round-2/4 checks (1 = serialised, phase times recorded)."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_streams(self._ctx, nsub))
 
+    def set_split(self, pieces: int):
+        """Degree split of the difference tables (0 = cost model, 1 = off); results are identical."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_split(self._ctx, pieces))
+
+    def last_split(self) -> int:
+        return _lib.lib().dkg_ctx_last_split(self._ctx)
+
     def set_overlap(self, on: bool):
         """Verify rounds 2 and 4 as one fused pipeline (default) or in protocol order."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_overlap(self._ctx, 1 if on else 0))
 
     def phase_times(self, tag="r24") -> dict:
-        """Device ms of binomial / stepping / check in the last ceremony's checks: tag "r24" (rounds
+        """Device ms of binomial / stepping / combine / check in the last ceremony's checks: tag "r24" (rounds
         2 and 4 fused, the default schedule), "r2" or "r4" (protocol order).  Only recorded with
         set_streams(1); -1 otherwise."""
         L = _lib.lib()
         if isinstance(tag, int):
             tag = f"r{tag}"
-        return {k: L.dkg_ctx_phase_ms(self._ctx, f"{tag}.{k}".encode()) for k in ("binomial", "stepping", "check")}
+        return {k: L.dkg_ctx_phase_ms(self._ctx, f"{tag}.{k}".encode())
+                for k in ("binomial", "stepping", "combine", "check")}
 
     def env_init(self, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT) -> bytes:
         out = ctypes.create_string_buffer(32)

@@ -13,8 +13,10 @@ void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t str
 // K5 straight into the binomial's position-major layout: D dealers x N commitments ([D][N][8],
 // dealer-major) -> [40][N][npad].  nseg segments are interleaved in 64-column groups: dealer i of
 // segment seg lands in column (i / 64) * 64 * nseg + seg * 64 + i % 64; ok[column * N + k].
+// npad = the table's row width (columns); with a degree split (L < N) coefficient k of column c goes
+// to position k % L, column (k / L) * pstride + c, in a table of L rows.
 void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
-                           hipStream_t stream, int nseg = 1, int seg = 0);
+                           hipStream_t stream, int nseg = 1, int seg = 0, size_t L = 0, size_t pstride = 0);
 // every column of a position-major table [40][S] set to the identity
 void fill_identity(size_t S, uint32_t* out, hipStream_t stream);
 // fused round-2/4 check over interleaved E/A columns (see k_check_both): dealers
@@ -44,13 +46,17 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 // dealer-minor); e0/e1 ping-pong buffers of the same shape.  Processes `width` (multiple of 64)
 // dealer columns starting at the given pointers (a dealer chunk: pass C + c0, e0 + c0, e1 + c0).
 // Returns the buffer holding e_m = Delta^m P_i(0), m = 0..t.
+// pieces > 1: the same for the columns [u * pstride, u * pstride + width) of every piece u
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
-                   hipStream_t stream);
+                   hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
 // K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][rstride]
 // (element i*nrecv + j).  stream_a / stream_b: scratch for the inter-block boundary streams, each
 // >= ndealers*nrecv*160 B (unused when N <= 512).
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
-              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream);
+              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
+// Degree-split recombination: R[c][j] = sum_u y_j^u R[u * pstride + c][j] (Horner, NAF of y_j)
+void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
+             uint32_t* R, size_t rstride, hipStream_t stream);
 // K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);
 // dealer_ok[i] == 0 forces 0; self ((i + dealer_base) mod nmod == j + recv_base, nmod = parties per
 // ceremony, so batched ceremonies stacked dealer-wise work too) gives 2.

@@ -23,7 +23,7 @@ constexpr int COMB_WORDS = AFF_WORDS * COMB_ENTRIES;  // 15360 words = 61440 B p
 __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ comp, size_t count,
                                                 uint32_t* __restrict__ ext, size_t stride,
                                                 uint8_t* __restrict__ ok, size_t pm_N, size_t pm_npad,
-                                                uint32_t nseg, uint32_t seg) {
+                                                uint32_t nseg, uint32_t seg, size_t pm_L, size_t pm_pstride) {
   size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
   uint32_t w[8];
@@ -35,7 +35,9 @@ __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ com
   if (pm_N) {
     const size_t i = e / pm_N, k = e % pm_N;
     const size_t col = (i / 64) * 64 * nseg + seg * 64 + i % 64;
-    idx = k * pm_npad + col;
+    // degree split: coefficient k of column col is position k % L of piece k / L, whose columns
+    // start pm_pstride apart (pm_L == pm_N: one piece)
+    idx = (k % pm_L) * pm_npad + (k / pm_L) * pm_pstride + col;
     oidx = col * pm_N + k;
   }
   pt_store(ext, stride, idx, p);
@@ -68,15 +70,16 @@ void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t str
                    hipStream_t stream) {
   if (!count) return;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count,
-                     ext, stride, ok, (size_t)0, (size_t)0, 1u, 0u);
+                     ext, stride, ok, (size_t)0, (size_t)0, 1u, 0u, (size_t)1, (size_t)0);
 }
 
 void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
-                           hipStream_t stream, int nseg, int seg) {
+                           hipStream_t stream, int nseg, int seg, size_t L, size_t pstride) {
   const size_t count = D * N;
   if (!count) return;
+  if (!L) L = N;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count, out,
-                     N * npad, ok, N, npad, (uint32_t)nseg, (uint32_t)seg);
+                     L * npad, ok, N, npad, (uint32_t)nseg, (uint32_t)seg, L, pstride);
 }
 
 void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream) {
@@ -295,9 +298,10 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
 }
 
 __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, size_t N, const uint32_t* __restrict__ C,
-                                                  size_t kpos, uint32_t* __restrict__ e) {
-  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= width) return;
+                                                  size_t kpos, uint32_t* __restrict__ e, size_t pstride) {
+  const size_t dl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (dl >= width) return;
+  const size_t d = blockIdx.y * pstride + dl;  // piece blockIdx.y of a degree-split table
   const size_t S = N * npad;
 #pragma unroll 8
   for (int w = 0; w < PT_WORDS; w++) e[w * S + d] = C[w * S + kpos * npad + d];
@@ -310,10 +314,11 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 // (largest m) start first and the launch tail is made of the short ones.
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
-                                                    const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout) {
+                                                    const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
+                                                    size_t pstride) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
-  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t d = blockIdx.z * pstride + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t S = N * npad;
   const int m = r - (int)blockIdx.y;
   if (m == 0) {
@@ -344,17 +349,17 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
 }
 
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
-                   hipStream_t stream) {
+                   hipStream_t stream, size_t pieces, size_t pstride) {
   const size_t t = N - 1;
-  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, stream, width, npad, N, C, t,
-                     e0);
+  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,
+                     npad, N, C, t, e0, pstride);
   uint32_t* in = e0;
   uint32_t* out = e1;
   for (size_t r = 1; r <= t; r++) {
     const size_t k = t - r;
-    // width is a multiple of 64: one wave per (position 0..r, 64 dealers)
-    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64), (unsigned)(r + 1)), dim3(64), 0, stream, (int)r,
-                       (int)k, npad, N, C, in, out);
+    // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
+    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64), (unsigned)(r + 1), (unsigned)pieces), dim3(64), 0,
+                       stream, (int)r, (int)k, npad, N, C, in, out, pstride);
     uint32_t* tmp = in;
     in = out;
     out = tmp;
@@ -388,7 +393,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ e, size_t nrecv, size_t pos0, int P,
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
-    uint32_t* __restrict__ R, size_t rstride) {
+    uint32_t* __restrict__ R, size_t rstride, size_t pstride) {
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
   // segment position q adds column q + 1 of its segment.  Column q = 0 is never read inside a
   // segment (its value leaves through `down` / R), so the segment's top lane parks the upstream
@@ -398,8 +403,9 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __shared__ uint32_t cols[PT_WORDS * MAXBS];
   const int l = threadIdx.x, bs = blockDim.x;
   const int seg = l / P, q = l - seg * P;
-  const size_t d = (size_t)blockIdx.x * (bs / P) + seg;
-  const bool live = seg < bs / P && d < ndealers;
+  const size_t dl = (size_t)blockIdx.x * (bs / P) + seg;
+  const bool live = seg < bs / P && dl < ndealers;
+  const size_t d = blockIdx.y * pstride + dl;  // piece blockIdx.y of a degree-split table
   const size_t S = N * npad;
   const size_t pos = pos0 + q;
   ge_p3 D;
@@ -444,15 +450,15 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 }
 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
-              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream) {
+              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride) {
   if (!ndealers || !nrecv) return;
   if (N > 256) {  // 512-lane blocks, one dealer per workgroup, top block first
     const size_t bs = 512, nblk = (N + bs - 1) / bs;
     uint32_t* up = nullptr;
     for (size_t b = nblk; b-- > 0;) {
       uint32_t* down = b ? ((nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
-      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers), dim3((unsigned)bs), 0, stream,
-                         ndealers, npad, N, e, nrecv, b * bs, (int)bs, up, down, b ? nullptr : R, rstride);
+      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)pieces), dim3((unsigned)bs), 0, stream,
+                         ndealers, npad, N, e, nrecv, b * bs, (int)bs, up, down, b ? nullptr : R, rstride, pstride);
       up = down;
     }
     return;
@@ -460,8 +466,57 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
   // whole table in one segment of N lanes; floor(256 / N) dealers per 256-lane workgroup
   const size_t P = N, per = 256 / P, bs = ((per * P + 63) / 64) * 64;
   const size_t grid = (ndealers + per - 1) / per;
-  hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid), dim3((unsigned)bs), 0, stream, ndealers,
-                     npad, N, e, nrecv, (size_t)0, (int)P, (const uint32_t*)nullptr, (uint32_t*)nullptr, R, rstride);
+  hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)bs), 0, stream, ndealers,
+                     npad, N, e, nrecv, (size_t)0, (int)P, (const uint32_t*)nullptr, (uint32_t*)nullptr, R, rstride,
+                     pstride);
+}
+
+// Degree split: P(x) = sum_u x^(uL) Q_u(x).  With the stepped values Q_u(j) of
+// the U pieces in columns u * pstride + c, P(j) = Q_0 + y (Q_1 + y (Q_2 + ...)), y = j^L mod l,
+// replaces the piece-0 value.  Lanes = columns, blockIdx.y = receiver: y is wave-uniform, its NAF
+// (digits[j][0..255] in {0, +1, -1}, top[j] = highest nonzero digit) drives a branch-uniform
+// double-and-add with the addend parked in LDS (as k_dec_mul).
+__global__ __launch_bounds__(64, 4) void k_combine(size_t width, size_t pstride, int pieces, size_t nrecv,
+                                                 const int8_t* __restrict__ digits, const int16_t* __restrict__ top,
+                                                 uint32_t* __restrict__ R, size_t rstride) {
+  __shared__ uint32_t qs[PT_WORDS * 64];
+  uint32_t* qcol = qs + threadIdx.x;
+  const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t j = blockIdx.y;
+  const bool live = c < width;
+  const size_t cc = live ? c : 0;
+  const int tp = top[j];
+  const int8_t* dj = digits + j * 256;
+  ge_p3 acc;
+  pt_load(acc, R, rstride, ((size_t)(pieces - 1) * pstride + cc) * nrecv + j);
+#pragma unroll 1
+  for (int u = pieces - 2; u >= 0; u--) {
+    {
+      ge_cached xc;
+      ge_to_cached(xc, acc);
+      lds_put_cached(qcol, xc);
+    }
+    // y * acc: the leading NAF digit is +1, acc already holds 1 * acc
+#pragma unroll 1
+    for (int b = tp - 1; b >= 0; b--) {
+      const int dg = __builtin_amdgcn_readfirstlane((int)dj[b]);
+      ge_dbl_lean(acc, acc, dg != 0 || b == 0);
+      if (dg != 0) ge_add_lds(acc, acc, qcol, dg < 0);
+    }
+    ge_p3 qv;
+    pt_load(qv, R, rstride, ((size_t)u * pstride + cc) * nrecv + j);
+    ge_cached qc;
+    ge_to_cached(qc, qv);
+    ge_add(acc, acc, qc);
+  }
+  if (live) pt_store(R, rstride, c * nrecv + j, acc);
+}
+
+void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
+             uint32_t* R, size_t rstride, hipStream_t stream) {
+  if (!width || !nrecv || pieces < 2) return;
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((width + 63) / 64), (unsigned)nrecv), dim3(64), 0, stream, width,
+                     pstride, (int)pieces, nrecv, digits, top, R, rstride);
 }
 
 // ------------------------------------------------------------------ K3c check

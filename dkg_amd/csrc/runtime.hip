@@ -25,12 +25,15 @@ struct dkg_ctx {
   bool have_h = false;
   size_t threshold = 0, nr_members = 0;
   hipEvent_t ev[8] = {};
-  hipEvent_t pev[4] = {};               // phase profiling inside verify_device (nsub == 1)
+  hipEvent_t pev[5] = {};               // phase profiling inside verify_device (nsub == 1)
   static constexpr int MAX_SUB = 8;
   int nsub = 2;                         // dealer-chunk streams of verify_device
   hipStream_t sub[MAX_SUB] = {};
   hipEvent_t fork = nullptr, join[MAX_SUB] = {};
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
+  int split = 0;                        // degree split U of the difference tables (0: cost model)
+  int last_split = 1;                   // U used by the last verify_device
+  size_t ydig_n = 0, ydig_L = 0;        // key of the cached combine multipliers (v.ydig)
   std::string timed_tag;                // set while pev[] hold a serialised verify_device's phases
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
@@ -130,8 +133,8 @@ uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, si
 // when it ran serialised and timed (names "<tag>.binomial" etc.; tag r2, r4 or r24 = fused).
 void collect_phases(dkg_ctx* ctx) {
   if (ctx->timed_tag.empty()) return;
-  const char* names[3] = {"binomial", "stepping", "check"};
-  for (int i = 0; i < 3; i++) {
+  const char* names[4] = {"binomial", "stepping", "combine", "check"};
+  for (int i = 0; i < 4; i++) {
     float ms = 0;
     HCK(hipEventElapsedTime(&ms, ctx->pev[i], ctx->pev[i + 1]));
     ctx->phase_ms[ctx->timed_tag + "." + names[i]] = ms;
@@ -151,6 +154,121 @@ struct VerifySeg {
   uint8_t* dec;
   const uint8_t* extra_ok = nullptr;  // [D] device: 0 = the dealer's other broadcast data is missing
 };
+
+// ---- degree split ----
+// P(x) = sum_{u<U} x^(uL) Q_u(x), deg Q_u < L = ceil(N / U): the binomial-basis Horner runs on the
+// U pieces (quadratic in the degree: ~1/U of the work, and ~1/U of the dependent chain), the
+// stepping does the same number of additions, and one recombination per (column, receiver) adds
+// U-1 multiplications by y_j = j^L mod l (k_combine).  Split when that is cheaper.
+// Instruction-count model of binomial + stepping + recombination (static VALU counts of the
+// kernels; the check does not depend on U) in SIMD
+// cycles: a SIMD retires one wave instruction per ~4.5 cycles of this mix when it has >= 2 waves,
+// one per ~8 when a lone wave runs a dependent chain (tools/ubench/ilp.hip); 1024 SIMDs.
+double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
+  const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAUNCH = 3e-3 * 2.4e6;
+  const size_t L = (N + U - 1) / U;
+  auto cost = [&](size_t m) {  // one binomial position-step: add + NAF multiplication by m
+    int len = 0, nz = 0;  // NAF length and weight of m (as mul_small_lds recodes it)
+    for (size_t v = m; v; v >>= 1, len++) {
+      if (v & 1) {
+        nz++;
+        if ((v & 3) == 1) v -= 1;
+        else v += 1;
+      }
+    }
+    return ADD + (len > 1 ? (len - 1) * DBL + (nz - 1) * ADD : 0.0);
+  };
+  std::vector<double> pre(L + 1, 0.0);
+  for (size_t m = 1; m <= L; m++) pre[m] = pre[m - 1] + cost(m);
+  const double waves_col = (double)cols * U / 64;
+  double cyc = 0;
+  for (size_t r = 1; r < L; r++) {
+    const double work = waves_col * pre[r] * THR / SIMDS;  // wave-instructions of step r
+    cyc += std::max(work, cost(r) * LAT) + LAUNCH;
+  }
+  if (U > 1) {
+    const double per = 253 * 950 + 85 * ADD;  // y * Q: 253 doublings + NAF additions
+    const double waves = (double)cols / 64 * n;
+    cyc += std::max(waves * (U - 1) * per * THR / SIMDS, (U - 1) * per * LAT);
+  }
+  // stepping: n dependent additions per lane on the lanes k_stepping allocates to an L-position
+  // table (512-lane blocks above 256 positions, else floor(256/L) tables per 256-lane group),
+  // slower when a group leaves a SIMD fewer than 4 waves
+  {
+    double lanes, occ = 1.0;
+    if (L > 256) {
+      lanes = (double)((L + 511) / 512) * 512;
+    } else {
+      const size_t per = 256 / L, bs = (per * L + 63) / 64 * 64;
+      lanes = (double)bs / per;
+      if (bs < 256) occ = bs >= 192 ? 0.8 : 0.65;
+    }
+    const double waves = (double)cols * U * lanes / 64;
+    cyc += std::max(waves * n * ADD * THR / SIMDS / occ, n * ADD * LAT);
+  }
+  return cyc / 2.4e6;
+}
+
+size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
+  if (ctx->split > 0) return std::min<size_t>((size_t)ctx->split, N);
+  size_t best = 1;
+  const double base = split_model_ms(cols, n, N, 1);
+  double best_ms = base;
+  for (size_t U = 2; U <= 16; U++) {
+    if (N < 64 * U) break;  // pieces of degree < 63: the binomial is cheap already
+    const double ms = split_model_ms(cols, n, N, U);
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = U;
+    }
+  }
+  return best_ms < 0.9 * base ? best : 1;  // only for a clear win
+}
+
+// NAF of y_j = (j+1)^L mod l for receivers j = 0..n-1 (k_combine's wave-uniform multipliers),
+// cached per (n, L) on the device: digits [n][256] int8, top [n] int16.
+void split_digits(dkg_ctx* ctx, size_t n, size_t L, const int8_t** digits, const int16_t** top) {
+  int8_t* dd = buf<int8_t>(ctx, "v.ydig", 256 * n);
+  int16_t* dt = buf<int16_t>(ctx, "v.ytop", 2 * n);
+  *digits = dd;
+  *top = dt;
+  if (ctx->ydig_n == n && ctx->ydig_L == L) return;
+  std::vector<int8_t> hd(256 * n, 0);
+  std::vector<int16_t> ht(n, -1);
+  for (size_t j = 0; j < n; j++) {
+    dkgh::Zl x = dkgh::zl_from_u64(j + 1), y = dkgh::zl_from_u64(1);
+    for (size_t e = L; e; e >>= 1) {  // y = x^L
+      if (e & 1) y = dkgh::zl_mul(y, x);
+      x = dkgh::zl_mul(x, x);
+    }
+    uint8_t b[32];
+    dkgh::zl_to_bytes(b, y);
+    uint32_t k[9] = {0};
+    for (int w = 0; w < 8; w++) k[w] = (uint32_t)b[4 * w] | (uint32_t)b[4 * w + 1] << 8 | (uint32_t)b[4 * w + 2] << 16 |
+                                       (uint32_t)b[4 * w + 3] << 24;
+    for (int i = 0; i < 256; i++) {  // left-to-right NAF digits, k < 2^253
+      if (!((k[i >> 5] >> (i & 31)) & 1u)) continue;
+      int8_t d = 1;
+      if ((k[(i + 1) >> 5] >> ((i + 1) & 31)) & 1u) {  // ...11: -1 and carry
+        d = -1;
+        for (int w = i >> 5, c = 1; c && w < 9; w++) {
+          const uint32_t add = (w == (i >> 5)) ? (1u << (i & 31)) : 1u;
+          const uint32_t old = k[w];
+          k[w] = old + add;
+          c = k[w] < old;
+        }
+      } else {
+        k[i >> 5] &= ~(1u << (i & 31));
+      }
+      hd[256 * j + i] = d;
+      ht[j] = (int16_t)i;
+    }
+  }
+  h2d(ctx, dd, hd.data(), hd.size());
+  h2d(ctx, dt, ht.data(), 2 * n);
+  ctx->ydig_n = n;
+  ctx->ydig_L = L;
+}
 
 // One or two segments on device, as ONE pipeline over "virtual dealers" (table columns).  With two
 // segments (round 2 on E and round 4 on A of the SAME dealers) a dealer's E row and A row are two
@@ -174,23 +292,30 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   }
   const size_t groups = (D + 63) / 64, gw = 64 * nseg;  // columns per dealer group
   const size_t npad = groups * gw;
+  // degree split: U pieces of L positions; piece u of column c is table column u * npad + c
+  const size_t U = choose_split(ctx, npad, n, N), L = (N + U - 1) / U, W = U * npad;
+  ctx->last_split = (int)U;
   hipStream_t home = ctx->stream;
   uint8_t* pok = buf<uint8_t>(ctx, "v.pok", npad * N);
   uint8_t* dok = buf<uint8_t>(ctx, "v.dok", npad);
-  uint32_t* Cpm = buf<uint32_t>(ctx, "v.Cpm", PTB * N * npad);
-  uint32_t* e0 = buf<uint32_t>(ctx, "v.binom0", PTB * N * npad);
-  uint32_t* e1 = buf<uint32_t>(ctx, "v.binom1", PTB * N * npad);
-  uint32_t* R = buf<uint32_t>(ctx, "v.R", PTB * npad * n);
+  uint32_t* Cpm = buf<uint32_t>(ctx, "v.Cpm", PTB * L * W);
+  uint32_t* e0 = buf<uint32_t>(ctx, "v.binom0", PTB * L * W);
+  uint32_t* e1 = buf<uint32_t>(ctx, "v.binom1", PTB * L * W);
+  uint32_t* R = buf<uint32_t>(ctx, "v.R", PTB * W * n);
   uint32_t *sa = nullptr, *sb = nullptr;
-  if (N > 512) {
-    sa = buf<uint32_t>(ctx, "v.step_a", PTB * npad * n);
-    sb = buf<uint32_t>(ctx, "v.step_b", PTB * npad * n);
+  if (L > 512) {
+    sa = buf<uint32_t>(ctx, "v.step_a", PTB * W * n);
+    sb = buf<uint32_t>(ctx, "v.step_b", PTB * W * n);
   }
-  const size_t rstride = npad * n;
-  if (npad != D * nseg) dkgk::fill_identity(N * npad, Cpm, home);  // padding columns
+  const int8_t* ydig = nullptr;
+  const int16_t* ytop = nullptr;
+  if (U > 1) split_digits(ctx, n, L, &ydig, &ytop);
+  const size_t rstride = W * n;
+  // padding columns, and the positions past t of the last piece, are the identity
+  if (npad != D * nseg || U * L != N) dkgk::fill_identity(L * W, Cpm, home);
   HCK(hipMemsetAsync(pok, 1, npad * N, home));
   for (int k = 0; k < nseg; k++)  // K5 (groups.rs:78-81) into the position-major table
-    dkgk::decode_position_major(segs[k].Ccomp, D, N, npad, Cpm, pok, home, nseg, k);
+    dkgk::decode_position_major(segs[k].Ccomp, D, N, W, Cpm, pok, home, nseg, k, L, npad);
   dkgk::dealer_ok(npad, N, pok, dok, home);
   for (int k = 0; k < nseg; k++)
     if (segs[k].extra_ok) dkgk::and_dealer_mask(D, nseg, k, segs[k].extra_ok, dok, home);
@@ -211,19 +336,21 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    uint32_t* e = dkgk::binomial(w, npad, N, Cpm + c0, e0 + c0, e1 + c0, st);
+    uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad);
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
-    dkgk::stepping(w, npad, N, e, n, R + c0 * n, rstride, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st);
+    dkgk::stepping(w, W, L, e, n, R + c0 * n, rstride, sa ? sa + c0 * n * 40 : nullptr,
+                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
-    checks(g0 * 64, std::min(D, g1 * 64), st);
+    dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n, rstride, st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));
+    checks(g0 * 64, std::min(D, g1 * 64), st);
+    if (tm) HCK(hipEventRecord(ctx->pev[4], st));
   };
   // Chunk streams only pay when the binomial saturates the GPU: chunk c+1's triangle then fills
   // the CUs that chunk c's launch tails leave idle.  A small shard (few dealers, e.g. one rank of
   // 8) is latency-bound -- every step is one dependent NAF chain long whatever its width -- so all
   // its columns go through one launch per step (average waves per step < 4 per SIMD -> nsub = 1).
-  const bool saturating = (npad / 64) * (N / 2) >= 4 * 1024;
+  const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
   const size_t nsub = saturating ? std::min<size_t>(ctx->nsub, groups) : 1;
   ctx->timed_tag.clear();
   if (nsub <= 1) {
@@ -763,6 +890,19 @@ int dkg_ctx_set_streams(dkg_ctx* ctx, int nsub) {
   if (!ctx || nsub < 1 || nsub > dkg_ctx::MAX_SUB) return DKG_E_ARG;
   ctx->nsub = nsub;
   return DKG_OK;
+}
+
+int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
+  if (!ctx || pieces < 0 || pieces > 16) return DKG_E_ARG;
+  ctx->split = pieces;
+  return DKG_OK;
+}
+
+int dkg_ctx_last_split(const dkg_ctx* ctx) { return ctx ? ctx->last_split : 0; }
+
+double dkg_split_model_ms(size_t columns, size_t n, size_t t, int pieces) {
+  if (pieces < 1 || t + 1 < (size_t)pieces) return -1;
+  return split_model_ms(columns, n, t + 1, (size_t)pieces);
 }
 
 int dkg_ctx_set_overlap(dkg_ctx* ctx, int on) {

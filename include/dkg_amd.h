@@ -43,7 +43,8 @@ int dkg_ctx_create(int device, dkg_ctx **out);
 void dkg_ctx_destroy(dkg_ctx *ctx);
 const char *dkg_ctx_last_error(const dkg_ctx *ctx);
 /* Device time (ms) of one phase of the last ceremony's round-2 / round-4 checks, by name
- * "r2.binomial", "r2.stepping", "r2.check", "r4.*", or "r24.*" for the fused rounds (HIP events
+ * "r2.binomial", "r2.stepping", "r2.combine" (degree split only, else 0), "r2.check", "r4.*", or
+ * "r24.*" for the fused rounds (HIP events
  * on the ctx stream, recorded only with dkg_ctx_set_streams(ctx, 1)); -1 if unknown. */
 double dkg_ctx_phase_ms(const dkg_ctx *ctx, const char *name);
 /* Scheduling of the round-2/4 checks: the dealers are cut into nsub chunks (1..8, default 2)
@@ -57,6 +58,15 @@ int dkg_ctx_set_streams(dkg_ctx *ctx, int nsub);
  * then covers both rounds' checks and ms_round4 only the copy-back.  on == 0: protocol order.
  * Phase times (dkg_ctx_phase_ms, nsub == 1) are recorded under "r24.*" when fused. */
 int dkg_ctx_set_overlap(dkg_ctx *ctx, int on);
+/* Degree split of the difference tables: pieces = U > 1 evaluates the
+ * committed polynomial as U pieces of degree < ceil((t+1)/U) recombined per receiver with U-1
+ * multiplications by j^L; 0 (default) picks U with the cost model dkg_split_model_ms; 1 disables.
+ * Decisions and outputs do not depend on it. */
+int dkg_ctx_set_split(dkg_ctx *ctx, int pieces);
+/* U used by the last ceremony's checks on this ctx. */
+int dkg_ctx_last_split(const dkg_ctx *ctx);
+/* The cost model's estimate (ms) of binomial + recombination for `columns` difference tables. */
+double dkg_split_model_ms(size_t columns, size_t n, size_t t, int pieces);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
 int dkg_device_count(void);
 

@@ -68,3 +68,15 @@ def test_enc_randomness_golden(golden, name):
     c = golden(name)
     r = dkg_amd.enc_randomness(bytes.fromhex(c["master_seed"]), c["ceremony"], 0, c["n"], c["n"], c["t"])
     assert r.hex() == c["enc_r"]
+
+
+def test_split_cost_model():
+    """The degree-split cost model (runtime.hip choose_split) picks a split where the binomial
+    dominates (n=1024, t=511 and n=4096, t=2047) and none for small tables (config 5)."""
+    L = _lib.lib()
+    ms = lambda cols, n, t, U: L.dkg_split_model_ms(cols, n, t, U)  # noqa: E731
+    assert ms(2048, 1024, 511, 2) < 0.9 * ms(2048, 1024, 511, 1)
+    assert min(range(1, 9), key=lambda U: ms(2048, 1024, 511, U)) == 2
+    assert min(range(1, 17), key=lambda U: ms(8192, 4096, 2047, U)) == 4
+    assert ms(16384, 64, 31, 1) < ms(16384, 64, 31, 2)
+    assert ms(64, 10, 4, 6) == -1.0  # more pieces than coefficients

@@ -237,13 +237,21 @@ def _gsum(values):
     return sum(values) % L
 
 
-@pytest.mark.parametrize("n,t", [(256, 127), (1024, 511)])
-def test_ceremony_large_properties(be, n, t):
-    """BASELINE configs 2 and 3 at full size: size-independent properties plus oracle spot pairs."""
+@pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0), (1024, 511, 1), (1024, 511, 3),
+                                       (1024, 511, 4)])
+def test_ceremony_large_properties(be, n, t, split):
+    """BASELINE configs 2 and 3 at full size: size-independent properties plus oracle spot pairs,
+    with the cost model's degree split (0), none (1) and forced ragged / 4-way splits."""
     be.env_init(t, n, CK)
     master = bytes([7]) * 32
     a, b = dkg_amd.dealer_coefficients(master, 3, 0, n, t)
-    r = be.ceremony(a, b, n, t)
+    be.set_split(split)
+    try:
+        r = be.ceremony(a, b, n, t)
+        if split:
+            assert be.last_split() == split
+    finally:
+        be.set_split(0)
     N = t + 1
     # every share verifies in both rounds, nobody complains, everyone is qualified
     assert r.dec2.count(bytes([ACCEPT])) == n * (n - 1) and r.dec4.count(bytes([ACCEPT])) == n * (n - 1)
@@ -694,6 +702,61 @@ def test_ceremony_from_broadcasts(be, golden):
         sec = sum(int.from_bytes(a[32 * (t + 1) * i:32 * (t + 1) * i + 32], "little") for i in range(n) if qualified[i]) % L
         assert r.mpk == O.base_mul(sec.to_bytes(32, "little"))  # committee.rs:1633-1647 property
     be.set_overlap(True)
+
+
+@pytest.mark.parametrize("pieces", [2, 3, 5])
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n16_t7.json", "ceremony_n11_t5.json"])
+def test_degree_split_goldens(be, golden, name, pieces):
+    """The degree-split evaluation (P = sum_u x^(uL) Q_u, recombined per receiver by k_combine) forced
+    on the fixtures, fused and in protocol order, including ragged pieces (t+1 not a multiple of U)
+    and pieces of one coefficient: every output bit-exact."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    if pieces > t + 1:
+        pytest.skip("more pieces than coefficients")
+    be.env_init(t, n, CK)
+    try:
+        be.set_split(pieces)
+        for overlap in (True, False):
+            be.set_overlap(overlap)
+            r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+            assert be.last_split() == pieces
+            _check_ceremony(c, r, n)
+    finally:
+        be.set_split(0)
+        be.set_overlap(True)
+
+
+@pytest.mark.parametrize("pieces", [1, 2, 3])
+def test_degree_split_n256_matches_unsplit(be, pieces):
+    """n = 256, t = 127 (BASELINE config 2) from device coefficients with one E row made undecodable
+    and one A row replaced: the split and unsplit runs give identical decision matrices, and the
+    honest rows accept everywhere."""
+    import torch
+
+    n, t = 256, 127
+    N = t + 1
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes(range(32)), 9, 0, n, t)
+    r0 = be.ceremony(a, b, n, t)
+    E, A = bytearray(r0.E), bytearray(r0.A)
+    E[32 * N * 17:32 * N * 17 + 32] = b"\xff" * 32
+    A[32 * N * 200 + 32 * 5:32 * N * 200 + 32 * 6] = r0.A[32 * N * 3:32 * N * 3 + 32]
+    try:
+        be.set_split(pieces)
+        r = be.ceremony_verify(bytes(E), bytes(A), r0.s, r0.s_prime, n, t)
+        assert be.last_split() == pieces
+    finally:
+        be.set_split(0)
+    dec2 = torch.frombuffer(bytearray(r.dec2), dtype=torch.uint8).reshape(n, n)
+    dec4 = torch.frombuffer(bytearray(r.dec4), dtype=torch.uint8).reshape(n, n)
+    assert set(dec2[17].tolist()) == {MISSING, SELF}
+    assert set(dec4[200].tolist()) == {REJECT, SELF}
+    ok2 = [i for i in range(n) if i != 17]
+    ok4 = [i for i in range(n) if i not in (17, 200)]
+    assert set(dec2[ok2].reshape(-1).tolist()) == {ACCEPT, SELF}
+    assert set(dec4[ok4].reshape(-1).tolist()) == {ACCEPT, SELF}
+    assert r.reconstruct == [int(i == 200) for i in range(n)]
 
 
 def test_ceremony_n4096_device(be):

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--split", type=int, default=0, help="degree split (0: cost model)")
     args = ap.parse_args()
     import torch
 
@@ -32,6 +33,7 @@ def main():
     be = dkg_amd.Backend(0)
     be.set_overlap(not args.no_overlap)
     be.set_streams(args.streams)
+    be.set_split(args.split)
     be.env_init(t, n)
     dev = torch.device("cuda", 0)
     res = {}
@@ -57,7 +59,7 @@ def main():
         res[ws] = round(min(ms), 2)
         ph = be.phase_times("r24" if not args.no_overlap else "r4")
         print(json.dumps({"n": n, "t": t, "ws": ws, "dealers": D, "ms_wall": res[ws],
-                          "overlap": not args.no_overlap, "streams": args.streams,
+                          "overlap": not args.no_overlap, "streams": args.streams, "split": be.last_split(),
                           "phases_ms_if_serialised": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     base = res.get(1)
     if base:
