@@ -80,16 +80,26 @@ def algorithmic_valu(n, t, rnd=2, U=1):
     binom = U * sum(cost_m[m] * (L_ - m) for m in range(1, L_))
     stepping = U * n * (L_ * VALU["ge_to_cached"] + (L_ - 1) * VALU["ge_add"])
     combine = 0
-    if U > 1:
+    if U > 1:  # k_combine: pairwise Horner in y^2 with joint NAF chains (kernels.hip)
         for j in range(1, n + 1):
-            ds = _naf(pow(j, L_, L))
-            c = 2 * VALU["ge_to_cached"] + VALU["ge_add"]   # addend, Q_u, + Q_u
-            for i in range(len(ds) - 2, -1, -1):
-                nz = ds[i] != 0
-                c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
-                if nz:
-                    c += VALU["ge_add_signed"]
-            combine += (U - 1) * c
+            y = pow(j, L_, L)
+            d1, d2 = _naf(y), _naf(y * y % L)
+            c = 0
+            if U % 2 == 0:  # top pair: y Q + Q'
+                c += 2 * VALU["ge_to_cached"] + VALU["ge_add"]
+                for i in range(len(d1) - 2, -1, -1):
+                    nz = d1[i] != 0
+                    c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
+                    if nz:
+                        c += VALU["ge_add_signed"]
+            joint = 3 * VALU["ge_to_cached"] + VALU["ge_add"]  # two addends, Q_2v, + Q_2v
+            for i in range(max(len(d1), len(d2)) - 1, -1, -1):
+                e1 = d1[i] if i < len(d1) else 0
+                e2 = d2[i] if i < len(d2) else 0
+                joint += VALU["ge_dbl_t"] if (e1 or e2 or i == 0) else VALU["ge_dbl_not"]
+                joint += VALU["ge_add_signed"] * ((e1 != 0) + (e2 != 0))
+            c += ((U + 1) // 2 - 1) * joint
+            combine += c
     check = n * ((2 if rnd == 2 else 1) * 64 * VALU["comb_window"] + VALU["eq"])
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 

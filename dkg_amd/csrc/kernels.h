@@ -52,9 +52,16 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
 // K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][rstride]
 // (element i*nrecv + j).  stream_a / stream_b: scratch for the inter-block boundary streams, each
 // >= ndealers*nrecv*160 B (unused when N <= 512).
+// How k_stepping covers an N-position table: nblk blocks of P positions on bs lanes (nblk > 1), or
+// `per` tables of P = N lanes each per bs-lane workgroup; maxbs = the LDS variant (256 or 512).
+struct StepShape {
+  size_t nblk, P, per, bs, maxbs;
+};
+StepShape stepping_shape(size_t N);
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
-// Degree-split recombination: R[c][j] = sum_u y_j^u R[u * pstride + c][j] (Horner, NAF of y_j)
+// Degree-split recombination: R[c][j] = sum_u y_j^u R[u * pstride + c][j] (pairwise Horner in y^2
+// with joint NAF chains; digits [n][2][256] = NAF of y_j and y_j^2, top [n][2])
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
              uint32_t* R, size_t rstride, hipStream_t stream);
 // K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);

@@ -449,65 +449,125 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   }
 }
 
+// Lanes given to an N-position table: 512-lane blocks (balanced when N > 512), or P = N lanes per
+// segment with floor(MAXBS / N) segments per workgroup; the variant wasting the fewest lanes wins
+// (ties to the 256-lane one: half the LDS per workgroup).
+StepShape stepping_shape(size_t N) {
+  StepShape sh;
+  if (N > 512) {
+    sh.nblk = (N + 511) / 512;
+    sh.P = (N + sh.nblk - 1) / sh.nblk;
+    sh.per = 1;
+    sh.bs = (sh.P + 63) / 64 * 64;
+    sh.maxbs = 512;
+    return sh;
+  }
+  auto fit = [&](size_t maxbs, StepShape& o) {
+    o.nblk = 1;
+    o.P = N;
+    o.per = maxbs / N;
+    o.bs = (o.per * N + 63) / 64 * 64;
+    o.maxbs = maxbs;
+    return (double)(o.per * N) / o.bs;
+  };
+  StepShape a, b;
+  const double ea = N <= 256 ? fit(256, a) : 0.0, eb = fit(512, b);
+  return ea >= eb - 0.02 ? a : b;
+}
+
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride) {
   if (!ndealers || !nrecv) return;
-  if (N > 256) {  // 512-lane blocks, one dealer per workgroup, top block first
-    const size_t bs = 512, nblk = (N + bs - 1) / bs;
+  const StepShape sh = stepping_shape(N);
+  if (sh.nblk > 1) {  // one dealer per workgroup, top block first, block values streamed down
     uint32_t* up = nullptr;
-    for (size_t b = nblk; b-- > 0;) {
-      uint32_t* down = b ? ((nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
-      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)pieces), dim3((unsigned)bs), 0, stream,
-                         ndealers, npad, N, e, nrecv, b * bs, (int)bs, up, down, b ? nullptr : R, rstride, pstride);
+    for (size_t b = sh.nblk; b-- > 0;) {
+      uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
+      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)pieces), dim3((unsigned)sh.bs), 0,
+                         stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down, b ? nullptr : R,
+                         rstride, pstride);
       up = down;
     }
     return;
   }
-  // whole table in one segment of N lanes; floor(256 / N) dealers per 256-lane workgroup
-  const size_t P = N, per = 256 / P, bs = ((per * P + 63) / 64) * 64;
-  const size_t grid = (ndealers + per - 1) / per;
-  hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)bs), 0, stream, ndealers,
-                     npad, N, e, nrecv, (size_t)0, (int)P, (const uint32_t*)nullptr, (uint32_t*)nullptr, R, rstride,
-                     pstride);
+  // whole table in one segment of N lanes, sh.per tables per workgroup
+  const size_t grid = (ndealers + sh.per - 1) / sh.per;
+  if (sh.maxbs == 256)
+    hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)sh.bs), 0, stream,
+                       ndealers, npad, N, e, nrecv, (size_t)0, (int)sh.P, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                       R, rstride, pstride);
+  else
+    hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)sh.bs), 0, stream,
+                       ndealers, npad, N, e, nrecv, (size_t)0, (int)sh.P, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                       R, rstride, pstride);
 }
 
 // Degree split: P(x) = sum_u x^(uL) Q_u(x).  With the stepped values Q_u(j) of
-// the U pieces in columns u * pstride + c, P(j) = Q_0 + y (Q_1 + y (Q_2 + ...)), y = j^L mod l,
-// replaces the piece-0 value.  Lanes = columns, blockIdx.y = receiver: y is wave-uniform, its NAF
-// (digits[j][0..255] in {0, +1, -1}, top[j] = highest nonzero digit) drives a branch-uniform
-// double-and-add with the addend parked in LDS (as k_dec_mul).
-__global__ __launch_bounds__(64, 4) void k_combine(size_t width, size_t pstride, int pieces, size_t nrecv,
+// the U pieces in columns u * pstride + c, P(j) = sum_u y^u Q_u(j), y = j^L mod l, replaces the
+// piece-0 value.  Lanes = columns, blockIdx.y = receiver: the multipliers are wave-uniform.  The
+// pieces are taken in pairs, Horner in y^2:  acc <- y^2 acc + y Q_{2v+1} + Q_{2v},  each step one
+// joint (Straus-Shamir) double-and-add over the NAFs of y^2 and y (253 doublings for both
+// products) with the two addends' cached forms parked in LDS; the top pair of an even U starts
+// with y Q_{U-1} + Q_{U-2}.  digits[j][s][0..255] in {0, +1, -1} is the NAF of y (s = 0) and
+// y^2 (s = 1), top[j][s] its highest nonzero digit (-1: zero).
+template <int SLOTS>
+__global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width, size_t pstride, int pieces, size_t nrecv,
                                                  const int8_t* __restrict__ digits, const int16_t* __restrict__ top,
                                                  uint32_t* __restrict__ R, size_t rstride) {
-  __shared__ uint32_t qs[PT_WORDS * 64];
-  uint32_t* qcol = qs + threadIdx.x;
+  __shared__ uint32_t qs[SLOTS * PT_WORDS * 64];
+  uint32_t* slot_y = qs + threadIdx.x;                   // addend of y's digits
+  uint32_t* slot_y2 = qs + (SLOTS - 1) * PT_WORDS * 64 + threadIdx.x;  // of y^2's (SLOTS == 2)
   const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
   const size_t j = blockIdx.y;
   const bool live = c < width;
   const size_t cc = live ? c : 0;
-  const int tp = top[j];
-  const int8_t* dj = digits + j * 256;
-  ge_p3 acc;
-  pt_load(acc, R, rstride, ((size_t)(pieces - 1) * pstride + cc) * nrecv + j);
+  const int8_t* d1 = digits + j * 512;
+  const int8_t* d2 = d1 + 256;
+  const int t1 = top[2 * j], t2 = top[2 * j + 1];
+  auto load_q = [&](ge_p3& q, int u) { pt_load(q, R, rstride, ((size_t)u * pstride + cc) * nrecv + j); };
+  auto put = [&](uint32_t* slot, const ge_p3& p) {
+    ge_cached xc;
+    ge_to_cached(xc, p);
+    lds_put_cached(slot, xc);
+  };
+  ge_p3 acc, q;
+  int v = (pieces - 1) / 2;
+  if (pieces % 2 == 0) {  // top pair: y Q_{2v+1} + Q_{2v}
+    load_q(acc, 2 * v + 1);
+    put(slot_y, acc);
 #pragma unroll 1
-  for (int u = pieces - 2; u >= 0; u--) {
-    {
-      ge_cached xc;
-      ge_to_cached(xc, acc);
-      lds_put_cached(qcol, xc);
-    }
-    // y * acc: the leading NAF digit is +1, acc already holds 1 * acc
-#pragma unroll 1
-    for (int b = tp - 1; b >= 0; b--) {
-      const int dg = __builtin_amdgcn_readfirstlane((int)dj[b]);
+    for (int b = t1 - 1; b >= 0; b--) {  // leading NAF digit +1: acc already holds 1 * Q
+      const int dg = __builtin_amdgcn_readfirstlane((int)d1[b]);
       ge_dbl_lean(acc, acc, dg != 0 || b == 0);
-      if (dg != 0) ge_add_lds(acc, acc, qcol, dg < 0);
+      if (dg != 0) ge_add_lds(acc, acc, slot_y, dg < 0);
     }
-    ge_p3 qv;
-    pt_load(qv, R, rstride, ((size_t)u * pstride + cc) * nrecv + j);
+    load_q(q, 2 * v);
     ge_cached qc;
-    ge_to_cached(qc, qv);
+    ge_to_cached(qc, q);
     ge_add(acc, acc, qc);
+  } else {
+    load_q(acc, 2 * v);
+  }
+  if (SLOTS == 2) {
+#pragma unroll 1
+    for (v = v - 1; v >= 0; v--) {  // acc <- y^2 acc + y Q_{2v+1} + Q_{2v}
+      put(slot_y2, acc);
+      load_q(q, 2 * v + 1);
+      put(slot_y, q);
+      ge_identity(acc);
+#pragma unroll 1
+      for (int b = (t1 > t2 ? t1 : t2); b >= 0; b--) {
+        const int e1 = __builtin_amdgcn_readfirstlane((int)d1[b]);
+        const int e2 = __builtin_amdgcn_readfirstlane((int)d2[b]);
+        ge_dbl_lean(acc, acc, e1 != 0 || e2 != 0 || b == 0);
+        if (e2 != 0) ge_add_lds(acc, acc, slot_y2, e2 < 0);
+        if (e1 != 0) ge_add_lds(acc, acc, slot_y, e1 < 0);
+      }
+      load_q(q, 2 * v);
+      ge_cached qc;
+      ge_to_cached(qc, q);
+      ge_add(acc, acc, qc);
+    }
   }
   if (live) pt_store(R, rstride, c * nrecv + j, acc);
 }
@@ -515,8 +575,13 @@ __global__ __launch_bounds__(64, 4) void k_combine(size_t width, size_t pstride,
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
              uint32_t* R, size_t rstride, hipStream_t stream) {
   if (!width || !nrecv || pieces < 2) return;
-  hipLaunchKernelGGL(k_combine, dim3((unsigned)((width + 63) / 64), (unsigned)nrecv), dim3(64), 0, stream, width,
-                     pstride, (int)pieces, nrecv, digits, top, R, rstride);
+  const dim3 grid((unsigned)((width + 63) / 64), (unsigned)nrecv);
+  if (pieces == 2)  // one product, one LDS slot (10 KB per wave: occupancy bound by VGPRs only)
+    hipLaunchKernelGGL(k_combine<1>, grid, dim3(64), 0, stream, width, pstride, (int)pieces, nrecv, digits, top, R,
+                       rstride);
+  else
+    hipLaunchKernelGGL(k_combine<2>, grid, dim3(64), 0, stream, width, pstride, (int)pieces, nrecv, digits, top, R,
+                       rstride);
 }
 
 // ------------------------------------------------------------------ K3c check

@@ -187,22 +187,23 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
     cyc += std::max(work, cost(r) * LAT) + LAUNCH;
   }
   if (U > 1) {
-    const double per = 253 * 950 + 85 * ADD;  // y * Q: 253 doublings + NAF additions
+    // pairwise joint chains: an even U starts with one product (253 doublings + ~85 NAF
+    // additions), then (ceil(U/2) - 1) joint y^2 / y steps (253 doublings + ~170 additions)
+    const double per = (U % 2 == 0 ? 253 * 950 + 85 * ADD : 0.0) + ((U + 1) / 2 - 1) * (253 * 950 + 170 * ADD);
     const double waves = (double)cols / 64 * n;
-    cyc += std::max(waves * (U - 1) * per * THR / SIMDS, (U - 1) * per * LAT);
+    const double occ = U > 2 ? 0.85 : 1.0;  // two LDS addend slots: 2 waves per SIMD
+    cyc += std::max(waves * per * THR / SIMDS / occ, per * LAT);
   }
   // stepping: n dependent additions per lane on the lanes k_stepping allocates to an L-position
   // table (512-lane blocks above 256 positions, else floor(256/L) tables per 256-lane group),
   // slower when a group leaves a SIMD fewer than 4 waves
   {
-    double lanes, occ = 1.0;
-    if (L > 256) {
-      lanes = (double)((L + 511) / 512) * 512;
-    } else {
-      const size_t per = 256 / L, bs = (per * L + 63) / 64 * 64;
-      lanes = (double)bs / per;
-      if (bs < 256) occ = bs >= 192 ? 0.8 : 0.65;
-    }
+    const dkgk::StepShape sh = dkgk::stepping_shape(L);
+    const double lanes = (double)sh.nblk * sh.bs / sh.per;
+    // resident waves per SIMD: LDS (160 B per lane of maxbs) and 16 waves per CU
+    const double wgs = std::min(160.0 * 1024 / (160.0 * sh.maxbs), 16.0 / (sh.bs / 64.0));
+    const double wps = std::floor(wgs) * sh.bs / 64 / 4;
+    const double occ = wps >= 4 ? 1.0 : (wps >= 3 ? 0.85 : 0.7);
     const double waves = (double)cols * U * lanes / 64;
     cyc += std::max(waves * n * ADD * THR / SIMDS / occ, n * ADD * LAT);
   }
@@ -225,47 +226,54 @@ size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
   return best_ms < 0.9 * base ? best : 1;  // only for a clear win
 }
 
-// NAF of y_j = (j+1)^L mod l for receivers j = 0..n-1 (k_combine's wave-uniform multipliers),
-// cached per (n, L) on the device: digits [n][256] int8, top [n] int16.
+// NAF of y = (j+1)^L mod l and of y^2 for receivers j = 0..n-1 (k_combine's wave-uniform
+// multipliers), cached per (n, L) on the device: digits [n][2][256] int8, top [n][2] int16.
+void naf_digits(const dkgh::Zl& v, int8_t* d, int16_t* tp) {
+  uint8_t b[32];
+  dkgh::zl_to_bytes(b, v);
+  uint32_t k[9] = {0};
+  for (int w = 0; w < 8; w++)
+    k[w] = (uint32_t)b[4 * w] | (uint32_t)b[4 * w + 1] << 8 | (uint32_t)b[4 * w + 2] << 16 | (uint32_t)b[4 * w + 3] << 24;
+  *tp = -1;
+  for (int i = 0; i < 256; i++) {  // k < 2^253: the NAF fits in 254 digits
+    d[i] = 0;
+    if (!((k[i >> 5] >> (i & 31)) & 1u)) continue;
+    int8_t dg = 1;
+    if ((k[(i + 1) >> 5] >> ((i + 1) & 31)) & 1u) {  // ...11: digit -1, k += 2^i
+      dg = -1;
+      uint64_t carry = 1ull << (i & 31);
+      for (int w = i >> 5; carry && w < 9; w++) {
+        const uint64_t sum = (uint64_t)k[w] + carry;
+        k[w] = (uint32_t)sum;
+        carry = sum >> 32;
+      }
+    } else {
+      k[i >> 5] &= ~(1u << (i & 31));
+    }
+    d[i] = dg;
+    *tp = (int16_t)i;
+  }
+}
+
 void split_digits(dkg_ctx* ctx, size_t n, size_t L, const int8_t** digits, const int16_t** top) {
-  int8_t* dd = buf<int8_t>(ctx, "v.ydig", 256 * n);
-  int16_t* dt = buf<int16_t>(ctx, "v.ytop", 2 * n);
+  int8_t* dd = buf<int8_t>(ctx, "v.ydig", 512 * n);
+  int16_t* dt = buf<int16_t>(ctx, "v.ytop", 4 * n);
   *digits = dd;
   *top = dt;
   if (ctx->ydig_n == n && ctx->ydig_L == L) return;
-  std::vector<int8_t> hd(256 * n, 0);
-  std::vector<int16_t> ht(n, -1);
+  std::vector<int8_t> hd(512 * n, 0);
+  std::vector<int16_t> ht(2 * n, -1);
   for (size_t j = 0; j < n; j++) {
     dkgh::Zl x = dkgh::zl_from_u64(j + 1), y = dkgh::zl_from_u64(1);
     for (size_t e = L; e; e >>= 1) {  // y = x^L
       if (e & 1) y = dkgh::zl_mul(y, x);
       x = dkgh::zl_mul(x, x);
     }
-    uint8_t b[32];
-    dkgh::zl_to_bytes(b, y);
-    uint32_t k[9] = {0};
-    for (int w = 0; w < 8; w++) k[w] = (uint32_t)b[4 * w] | (uint32_t)b[4 * w + 1] << 8 | (uint32_t)b[4 * w + 2] << 16 |
-                                       (uint32_t)b[4 * w + 3] << 24;
-    for (int i = 0; i < 256; i++) {  // left-to-right NAF digits, k < 2^253
-      if (!((k[i >> 5] >> (i & 31)) & 1u)) continue;
-      int8_t d = 1;
-      if ((k[(i + 1) >> 5] >> ((i + 1) & 31)) & 1u) {  // ...11: -1 and carry
-        d = -1;
-        for (int w = i >> 5, c = 1; c && w < 9; w++) {
-          const uint32_t add = (w == (i >> 5)) ? (1u << (i & 31)) : 1u;
-          const uint32_t old = k[w];
-          k[w] = old + add;
-          c = k[w] < old;
-        }
-      } else {
-        k[i >> 5] &= ~(1u << (i & 31));
-      }
-      hd[256 * j + i] = d;
-      ht[j] = (int16_t)i;
-    }
+    naf_digits(y, &hd[512 * j], &ht[2 * j]);
+    naf_digits(dkgh::zl_mul(y, y), &hd[512 * j + 256], &ht[2 * j + 1]);
   }
   h2d(ctx, dd, hd.data(), hd.size());
-  h2d(ctx, dt, ht.data(), 2 * n);
+  h2d(ctx, dt, ht.data(), 4 * n);
   ctx->ydig_n = n;
   ctx->ydig_L = L;
 }

@@ -238,7 +238,7 @@ def _gsum(values):
 
 
 @pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0), (1024, 511, 1), (1024, 511, 3),
-                                       (1024, 511, 4)])
+                                       (1024, 511, 4), (1024, 511, 6), (1024, 511, 7)])
 def test_ceremony_large_properties(be, n, t, split):
     """BASELINE configs 2 and 3 at full size: size-independent properties plus oracle spot pairs,
     with the cost model's degree split (0), none (1) and forced ragged / 4-way splits."""
@@ -704,7 +704,7 @@ def test_ceremony_from_broadcasts(be, golden):
     be.set_overlap(True)
 
 
-@pytest.mark.parametrize("pieces", [2, 3, 5])
+@pytest.mark.parametrize("pieces", [2, 3, 4, 5])
 @pytest.mark.parametrize("name", FAULTS + ["ceremony_n16_t7.json", "ceremony_n11_t5.json"])
 def test_degree_split_goldens(be, golden, name, pieces):
     """The degree-split evaluation (P = sum_u x^(uL) Q_u, recombined per receiver by k_combine) forced
