@@ -45,6 +45,26 @@ def dist_env():
     return ws, rank, local
 
 
+def init_dist(args, local):
+    """One process per GPU over RCCL ("nccl").  --dist-backend gloo is a rehearsal mode for boxes
+    with fewer GPUs than ranks: ranks share GPUs (local % device_count) and the exchange is staged
+    through host memory; its timings say nothing about xGMI."""
+    import torch
+    import torch.distributed as dist
+
+    if args.dist_backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+    return dist
+
+
+def gpu_index(args, local):
+    import torch
+
+    return local % torch.cuda.device_count() if args.dist_backend == "gloo" else local
+
+
 def _naf(m):
     digits = []
     v = m
@@ -164,12 +184,9 @@ def bench_batch(args, ws, rank, local):
 
     B, n, t = BATCH[args.config]
     N = t + 1
+    local = gpu_index(args, local)
     torch.cuda.set_device(local)
-    dist = None
-    if ws > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = init_dist(args, local) if ws > 1 else None
     be = dkg_amd.Backend(local)
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
@@ -198,7 +215,7 @@ def bench_batch(args, ws, rank, local):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     assert all(q == n for q in res.n_qualified), "an honest ceremony disqualified a dealer"
@@ -229,6 +246,8 @@ def main():
     ap.add_argument("--config", default="D", choices=sorted(CONFIGS) + sorted(BATCH))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="dealer-chunk streams of the round-2/4 checks")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal with ranks sharing GPUs")
     ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
@@ -241,14 +260,11 @@ def main():
 
     import torch
 
+    local = gpu_index(args, local)
     torch.cuda.set_device(local)
     import dkg_amd
 
-    dist = None
-    if ws > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = init_dist(args, local) if ws > 1 else None
     be = dkg_amd.Backend(local)
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
@@ -301,10 +317,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    if ws > 1:  # the sharded honest ceremony: everyone qualified, an mpk, no round errors
+        assert res.decisions.qualified.all() and not res.decisions.r2_error.any() and res.mpk is not None
     pairs = n * (n - 1)
     value = pairs * args.steps / elapsed
     metric = "verified shares/sec (whole node) at n=1024,t=511; full-ceremony wall time"

@@ -86,6 +86,7 @@ class ShardedCeremony:
         self.torch = torch
         self.be, self.dist, self.n, self.t, self.dev = be, dist, n, t, device
         self.ws, self.rank = dist.get_world_size(), dist.get_rank()
+        self.staged = dist.get_backend() == "gloo" and getattr(device, "type", str(device)) != "cpu"
         self.d0, self.d1 = dealer_range(self.rank, self.ws, n)
         D, R = self.d1 - self.d0, max_rows(self.ws, n)
         u8 = dict(dtype=torch.uint8, device=device)
@@ -99,14 +100,21 @@ class ShardedCeremony:
         self.g_part = torch.empty(self.ws * n * 32, **u8)
         self.D, self.R = D, R
 
+    def _all_gather(self, out, inp):
+        if self.staged:  # gloo with device buffers: through host memory (rehearsal / CPU runs)
+            o = out.cpu()
+            self.dist.all_gather_into_tensor(o, inp.cpu())
+            out.copy_(o)
+        else:
+            self.dist.all_gather_into_tensor(out, inp)
+
     def exchange(self):
         """All-gather the padded per-rank rows; returns (dec2 [n][n], dec4 [n][n], A0 [n][32])
         tensors with the padding removed, and the gathered partial sums [ws][n][32]."""
-        d = self.dist
-        d.all_gather_into_tensor(self.g_dec2, self.dec2)
-        d.all_gather_into_tensor(self.g_dec4, self.dec4)
-        d.all_gather_into_tensor(self.g_A0, self.A0)
-        d.all_gather_into_tensor(self.g_part, self.part)
+        self._all_gather(self.g_dec2, self.dec2)
+        self._all_gather(self.g_dec4, self.dec4)
+        self._all_gather(self.g_A0, self.A0)
+        self._all_gather(self.g_part, self.part)
         n, R = self.n, self.R
         rows = []
         for r in range(self.ws):
