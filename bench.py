@@ -35,7 +35,7 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 # as one instruction although it issues at about half rate -- see DESIGN.md "Roofline").
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
 VALU = {"fe_mul": 144, "ge_add": 1318, "ge_add_signed": 1361, "ge_dbl_t": 1158, "ge_dbl_not": 1019,
-        "comb_window": 1272, "ge_to_cached": 197, "eq": 4 * 144 + 120}
+        "comb_window": 1272, "comb8_window": 1245, "ge_to_cached": 197, "eq": 4 * 144 + 120}
 
 
 def dist_env():
@@ -120,17 +120,17 @@ def algorithmic_valu(n, t, rnd=2, U=1):
                 joint += VALU["ge_add_signed"] * ((e1 != 0) + (e2 != 0))
             c += ((U + 1) // 2 - 1) * joint
             combine += c
-    check = n * ((2 if rnd == 2 else 1) * 64 * VALU["comb_window"] + VALU["eq"])
+    check = n * ((2 if rnd == 2 else 1) * 32 * VALU["comb8_window"] + VALU["eq"])  # radix-256 combs
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
 def fused_valu(n, t, U=1):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
-    recombination; one check kernel computing g*s once (64 comb windows), h*s' (64 more) and both
+    recombination; one check kernel computing g*s once (32 radix-256 comb windows), h*s' (32 more) and both
     equalities per pair."""
     w2, w4 = algorithmic_valu(n, t, 2, U), algorithmic_valu(n, t, 4, U)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
-    out["check"] = n * n * (2 * 64 * VALU["comb_window"] + 2 * VALU["eq"])
+    out["check"] = n * n * (2 * 32 * VALU["comb8_window"] + 2 * VALU["eq"])
     return out
 
 

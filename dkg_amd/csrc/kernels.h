@@ -13,6 +13,12 @@ void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t str
 // K5 straight into the binomial's position-major layout: D dealers x N commitments ([D][N][8],
 // dealer-major) -> [40][N][npad].  nseg segments are interleaved in 64-column groups: dealer i of
 // segment seg lands in column (i / 64) * 64 * nseg + seg * 64 + i % 64; ok[column * N + k].
+// k_decode's placement for points already in extended form (src [D][N], word stride sstride)
+void place_position_major(const uint32_t* src, size_t sstride, size_t D, size_t N, size_t npad, uint32_t* out,
+                          hipStream_t stream, int nseg = 1, int seg = 0, size_t L = 0, size_t pstride = 0);
+// dst[i] = src[i * step + k0], i < count (extended points)
+void gather_points(const uint32_t* src, size_t sstride, size_t step, size_t k0, size_t count, uint32_t* dst,
+                   size_t dstride, hipStream_t stream);
 // npad = the table's row width (columns); with a degree split (L < N) coefficient k of column c goes
 // to position k % L, column (k / L) * pstride + c, in a table of L rows.
 void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad, uint32_t* out, uint8_t* ok,
@@ -31,6 +37,9 @@ void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipSt
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream);
 // comb tables of the decoded points ext[.., e0 + c], c < count, into tab + c * 15360 (30 x 512 words each)
 void build_comb(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count = 1);
+// radix-256 combs (COMB8_WORDS words each) of `count` points: the tables of commit / check /
+// fixed_base (global memory, L2-resident)
+void build_comb8(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count = 1);
 
 // K2: A_k = g a_k, E_k = A_k + h b_k for D*N coefficients (scalars [D*N][8]); outputs SoA [40][DN].
 void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g,

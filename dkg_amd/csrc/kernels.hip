@@ -44,6 +44,47 @@ __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ com
   ok[oidx] = v ? 1 : 0;
 }
 
+// Same placement as k_decode's position-major mode for points that are already in extended form
+// (round-1 commitments generated on this device: the reference's broadcasts carry group elements,
+// not encodings, so nothing is decoded).  src: [D][N] points, word stride sstride.
+__global__ __launch_bounds__(256) void k_place_pm(const uint32_t* __restrict__ src, size_t sstride, size_t count,
+                                                  uint32_t* __restrict__ out, size_t N, size_t npad, uint32_t nseg,
+                                                  uint32_t seg, size_t L, size_t pstride) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const size_t i = e / N, k = e % N;
+  const size_t col = (i / 64) * 64 * nseg + seg * 64 + i % 64;
+  const size_t idx = (k % L) * npad + (k / L) * pstride + col;
+  const size_t ostride = L * npad;
+#pragma unroll 8
+  for (int w = 0; w < PT_WORDS; w++) out[w * ostride + idx] = src[w * sstride + e];
+}
+
+void place_position_major(const uint32_t* src, size_t sstride, size_t D, size_t N, size_t npad, uint32_t* out,
+                          hipStream_t stream, int nseg, int seg, size_t L, size_t pstride) {
+  const size_t count = D * N;
+  if (!count) return;
+  if (!L) L = N;
+  hipLaunchKernelGGL(k_place_pm, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, src, sstride, count, out,
+                     N, npad, (uint32_t)nseg, (uint32_t)seg, L, pstride);
+}
+
+// dst[i] = src[i * step + k0] for i < count (extended points; word strides sstride / dstride)
+__global__ void k_gather_pts(const uint32_t* __restrict__ src, size_t sstride, size_t step, size_t k0, size_t count,
+                             uint32_t* __restrict__ dst, size_t dstride) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+#pragma unroll 8
+  for (int w = 0; w < PT_WORDS; w++) dst[w * dstride + i] = src[w * sstride + i * step + k0];
+}
+
+void gather_points(const uint32_t* src, size_t sstride, size_t step, size_t k0, size_t count, uint32_t* dst,
+                   size_t dstride, hipStream_t stream) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_gather_pts, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, src, sstride, step, k0,
+                     count, dst, dstride);
+}
+
 // Identity points in dealer columns [V, npad) of a position-major table [40][N][npad].
 __global__ void k_fill_identity(size_t N, size_t npad, size_t V, uint32_t* __restrict__ out) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = k * (npad - V) + c
@@ -143,42 +184,31 @@ __device__ __forceinline__ void lds_fill(uint32_t* lds, const uint32_t* __restri
   for (int i = threadIdx.x; i < words / 4; i += blockDim.x) dst[i] = src[i];
 }
 
-static int comb_grid(size_t items, int threads) {
-  size_t want = (items + threads - 1) / threads;
-  size_t cap = 256 * 2;  // one 1024-thread workgroup per CU holds the 120 KB of tables
-  return (int)(want < cap ? (want ? want : 1) : cap);
-}
 
 // ------------------------------------------------------------------ K2 commitments
-__global__ __launch_bounds__(1024) void k_commit(size_t count, const uint32_t* __restrict__ a,
-                                                 const uint32_t* __restrict__ b,
-                                                 const uint32_t* __restrict__ tab_g,
-                                                 const uint32_t* __restrict__ tab_h,
-                                                 uint32_t* __restrict__ A_ext, uint32_t* __restrict__ E_ext) {
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
-  lds_fill(lds, tab_g, COMB_WORDS);
-  lds_fill(lds + COMB_WORDS, tab_h, COMB_WORDS);
-  __syncthreads();
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count;
-       e += (size_t)gridDim.x * blockDim.x) {
-    sc sa, sb;
-    sc_load(sa, a + 8 * e);
-    sc_load(sb, b + 8 * e);
-    ge_p3 acc;
-    ge_identity(acc);
-    comb_mul_add(acc, sa, lds);                 // apub = G::generator() * a   (committee.rs:155)
-    pt_store(A_ext, count, e, acc);
-    comb_mul_add(acc, sb, lds + COMB_WORDS);    // coeff_comm = h * b + apub   (committee.rs:156)
-    pt_store(E_ext, count, e, acc);
-  }
+__global__ __launch_bounds__(256, 4) void k_commit(size_t count, const uint32_t* __restrict__ a,
+                                                const uint32_t* __restrict__ b,
+                                                const uint32_t* __restrict__ tab_g,
+                                                const uint32_t* __restrict__ tab_h,
+                                                uint32_t* __restrict__ A_ext, uint32_t* __restrict__ E_ext) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  sc sa, sb;
+  sc_load(sa, a + 8 * e);
+  sc_load(sb, b + 8 * e);
+  ge_p3 acc;
+  ge_identity(acc);
+  comb8_mul_add(acc, sa, tab_g);               // apub = G::generator() * a   (committee.rs:155)
+  pt_store(A_ext, count, e, acc);
+  comb8_mul_add(acc, sb, tab_h);               // coeff_comm = h * b + apub   (committee.rs:156)
+  pt_store(E_ext, count, e, acc);
 }
 
 void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g, const uint32_t* tab_h,
             uint32_t* A_ext, uint32_t* E_ext, hipStream_t stream) {
   if (!count) return;
-  hipLaunchKernelGGL(k_commit, dim3(comb_grid(count, 1024)), dim3(1024), 2 * COMB_WORDS * 4, stream, count,
-                     a, b, tab_g, tab_h, A_ext, E_ext);
+  hipLaunchKernelGGL(k_commit, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, a, b, tab_g, tab_h,
+                     A_ext, E_ext);
 }
 
 // ------------------------------------------------------------------ K1 share evaluation
@@ -295,6 +325,44 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
     ge_dbl_rt(y, y, nz || i == 0);           // T only when an addition (or the result) needs it
     if (nz) ge_add_signed(y, y, xc, (neg & bit) != 0);
   }
+}
+
+// Radix-256 comb of point e0 + blockIdx.y of ext: block (window w = blockIdx.x, 128 threads),
+// thread d-1 writes d * 256^w B in affine Niels form (points.h comb8_mul_add).
+__global__ __launch_bounds__(128) void k_build_comb8(const uint32_t* __restrict__ ext, size_t stride, size_t e0,
+                                                   uint32_t* __restrict__ tab) {
+  const int w = blockIdx.x, d = threadIdx.x + 1;
+  tab += (size_t)blockIdx.y * COMB8_WORDS;
+  ge_p3 b, m;
+  pt_load(b, ext, stride, e0 + blockIdx.y);
+  for (int i = 0; i < 8 * w; i++) ge_dbl<true>(b, b);
+  mul_small_uniform(m, b, (uint32_t)d);
+  fe zi, x, y, t, d2;
+  fe_ld(d2, ge_const::D2);
+  fe_invert(zi, m.Z);
+  fe_mul(x, m.X, zi);
+  fe_mul(y, m.Y, zi);
+  uint32_t* out = tab + ((size_t)w * COMB8_ENTRIES + (d - 1)) * COMB8_STRIDE;
+  fe_add(t, y, x);
+  fe_carry(t, t);
+#pragma unroll
+  for (int i = 0; i < 10; i++) out[i] = t.v[i];
+  fe_sub(t, y, x);
+  fe_carry(t, t);
+#pragma unroll
+  for (int i = 0; i < 10; i++) out[10 + i] = t.v[i];
+  fe_mul(t, x, y);
+  fe_mul(t, t, d2);
+#pragma unroll
+  for (int i = 0; i < 10; i++) out[20 + i] = t.v[i];
+  out[30] = 0;
+  out[31] = 0;
+}
+
+void build_comb8(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_build_comb8, dim3((unsigned)COMB8_WINDOWS, (unsigned)count), dim3(COMB8_ENTRIES), 0, stream,
+                     ext, stride, e0, tab);
 }
 
 __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, size_t N, const uint32_t* __restrict__ C,
@@ -585,38 +653,32 @@ void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const in
 }
 
 // ------------------------------------------------------------------ K3c check
-__global__ __launch_bounds__(1024) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base,
-                                                uint32_t nmod, int round,
-                                                const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
-                                                const uint32_t* __restrict__ R, size_t rstride,
-                                                const uint32_t* __restrict__ tab_g,
-                                                const uint32_t* __restrict__ tab_h,
-                                                const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec) {
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
-  lds_fill(lds, tab_g, COMB_WORDS);
-  if (round == 2) lds_fill(lds + COMB_WORDS, tab_h, COMB_WORDS);
-  __syncthreads();
-  const size_t total = ndealers * nrecv;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
-    const size_t i = p / nrecv, j = p % nrecv;
-    ge_p3 acc, r;
-    ge_identity(acc);
-    sc x;
-    sc_load(x, s + 8 * p);
-    comb_mul_add(acc, x, lds);                       // G::generator() * s       (committee.rs:294, :537)
-    if (round == 2) {
-      sc_load(x, sp + 8 * p);
-      comb_mul_add(acc, x, lds + COMB_WORDS);        // + h * s'                 (committee.rs:292-293)
-    }
-    pt_load(r, R, rstride, p);
-    const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
-    // a dealer whose broadcast does not decode is missing data: disqualified without a complaint in
-    // round 2 (committee.rs:331-335), an accusation in round 4 (:549-555)
-    uint8_t v = dok[i] ? (eq ? 1 : 0) : (round == 2 ? 4 : 0);
-    if ((uint32_t)((i + dealer_base) % nmod) == (uint32_t)(j + recv_base)) v = 2;  // self (batched: per ceremony)
-    dec[p] = v;
+__global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base,
+                                               uint32_t nmod, int round,
+                                               const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
+                                               const uint32_t* __restrict__ R, size_t rstride,
+                                               const uint32_t* __restrict__ tab_g,
+                                               const uint32_t* __restrict__ tab_h,
+                                               const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ndealers * nrecv) return;
+  const size_t i = p / nrecv, j = p % nrecv;
+  ge_p3 acc, r;
+  ge_identity(acc);
+  sc x;
+  sc_load(x, s + 8 * p);
+  comb8_mul_add(acc, x, tab_g);                    // G::generator() * s       (committee.rs:294, :537)
+  if (round == 2) {
+    sc_load(x, sp + 8 * p);
+    comb8_mul_add(acc, x, tab_h);                  // + h * s'                 (committee.rs:292-293)
   }
+  pt_load(r, R, rstride, p);
+  const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
+  // a dealer whose broadcast does not decode is missing data: disqualified without a complaint in
+  // round 2 (committee.rs:331-335), an accusation in round 4 (:549-555)
+  uint8_t v = dok[i] ? (eq ? 1 : 0) : (round == 2 ? 4 : 0);
+  if ((uint32_t)((i + dealer_base) % nmod) == (uint32_t)(j + recv_base)) v = 2;  // self (batched: per ceremony)
+  dec[p] = v;
 }
 
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
@@ -624,9 +686,8 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
            const uint32_t* tab_h, const uint8_t* dok, uint8_t* dec, hipStream_t stream) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
-  const size_t lds = (round == 2 ? 2 : 1) * COMB_WORDS * 4;
-  hipLaunchKernelGGL(k_check, dim3(comb_grid(total, 1024)), dim3(1024), lds, stream, ndealers, nrecv, dealer_base,
-                     recv_base, (uint32_t)nmod, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
+  hipLaunchKernelGGL(k_check, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
+                     dealer_base, recv_base, (uint32_t)nmod, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
 }
 
 // Fused round-2 + round-4 check of dealers [dealer0, dealer0 + ndealers) (local indices) whose E and A
@@ -634,38 +695,32 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
 // and its A row the column 64 after it.  g*s_ij is computed ONCE: compared with R_A (round 4,
 // committee.rs:537-541), then h*s'_ij is added and the sum compared with R_E (round 2,
 // committee.rs:292-305) -- the same group elements the two rounds compute separately.
-__global__ __launch_bounds__(1024) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
-                                                     uint32_t nmod, const uint32_t* __restrict__ s,
-                                                     const uint32_t* __restrict__ sp, const uint32_t* __restrict__ R,
-                                                     size_t rstride, const uint32_t* __restrict__ tab_g,
-                                                     const uint32_t* __restrict__ tab_h,
-                                                     const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
-                                                     uint8_t* __restrict__ dec4) {
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
-  lds_fill(lds, tab_g, COMB_WORDS);
-  lds_fill(lds + COMB_WORDS, tab_h, COMB_WORDS);
-  __syncthreads();
-  const size_t total = ndealers * nrecv;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
-    const size_t i = dealer0 + p / nrecv, j = p % nrecv;
-    const size_t cE = (i / 64) * 128 + i % 64, cA = cE + 64;
-    const size_t q = i * nrecv + j;  // share / decision index
-    const bool self = (uint32_t)((i + dealer_base) % nmod) == (uint32_t)j;
-    ge_p3 acc, r;
-    ge_identity(acc);
-    sc x;
-    sc_load(x, s + 8 * q);
-    comb_mul_add(acc, x, lds);                       // G::generator() * s   (committee.rs:294, :537)
-    pt_load(r, R, rstride, cA * nrecv + j);
-    bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
-    dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
-    sc_load(x, sp + 8 * q);
-    comb_mul_add(acc, x, lds + COMB_WORDS);          // + h * s'              (committee.rs:292-293)
-    pt_load(r, R, rstride, cE * nrecv + j);
-    eq = ristretto_eq(acc, r);                       // round 2 (:305)
-    dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)
-  }
+__global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
+                                                    uint32_t nmod, const uint32_t* __restrict__ s,
+                                                    const uint32_t* __restrict__ sp, const uint32_t* __restrict__ R,
+                                                    size_t rstride, const uint32_t* __restrict__ tab_g,
+                                                    const uint32_t* __restrict__ tab_h,
+                                                    const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
+                                                    uint8_t* __restrict__ dec4) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ndealers * nrecv) return;
+  const size_t i = dealer0 + p / nrecv, j = p % nrecv;
+  const size_t cE = (i / 64) * 128 + i % 64, cA = cE + 64;
+  const size_t q = i * nrecv + j;  // share / decision index
+  const bool self = (uint32_t)((i + dealer_base) % nmod) == (uint32_t)j;
+  ge_p3 acc, r;
+  ge_identity(acc);
+  sc x;
+  sc_load(x, s + 8 * q);
+  comb8_mul_add(acc, x, tab_g);                    // G::generator() * s   (committee.rs:294, :537)
+  pt_load(r, R, rstride, cA * nrecv + j);
+  bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
+  dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
+  sc_load(x, sp + 8 * q);
+  comb8_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
+  pt_load(r, R, rstride, cE * nrecv + j);
+  eq = ristretto_eq(acc, r);                       // round 2 (:305)
+  dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)
 }
 
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
@@ -673,8 +728,8 @@ void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_bas
                 const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
-  hipLaunchKernelGGL(k_check_both, dim3(comb_grid(total, 1024)), dim3(1024), 2 * COMB_WORDS * 4, stream, ndealers,
-                     nrecv, dealer0, dealer_base, (uint32_t)nmod, s, sp, R, rstride, tab_g, tab_h, dok, dec2, dec4);
+  hipLaunchKernelGGL(k_check_both, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
+                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, rstride, tab_g, tab_h, dok, dec2, dec4);
 }
 
 // Identity in every column of a position-major table [40][S] (S = N * npad words apart).
@@ -904,26 +959,23 @@ void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts,
   hipLaunchKernelGGL(k_msm, dim3((unsigned)B), dim3(256), 0, stream, N, scalars, pts, stride, out_ext, B);
 }
 
-__global__ __launch_bounds__(1024) void k_fixed_base(size_t count, const uint32_t* __restrict__ scalars,
-                                                     const uint32_t* __restrict__ tab, uint32_t* __restrict__ out) {
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
-  lds_fill(lds, tab, COMB_WORDS);
-  __syncthreads();
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
-    sc x;
-    sc_load(x, scalars + 8 * e);
-    ge_p3 acc;
-    ge_identity(acc);
-    comb_mul_add(acc, x, lds);
-    pt_store(out, count, e, acc);
-  }
+__global__ __launch_bounds__(256, 4) void k_fixed_base(size_t count, const uint32_t* __restrict__ scalars,
+                                                    const uint32_t* __restrict__ tab, uint32_t* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  sc x;
+  sc_load(x, scalars + 8 * e);
+  ge_p3 acc;
+  ge_identity(acc);
+  comb8_mul_add(acc, x, tab);
+  pt_store(out, count, e, acc);
 }
 
+// tab: a radix-256 comb (build_comb8)
 void fixed_base(size_t count, const uint32_t* scalars, const uint32_t* tab, uint32_t* out_ext, hipStream_t stream) {
   if (!count) return;
-  hipLaunchKernelGGL(k_fixed_base, dim3(comb_grid(count, 1024)), dim3(1024), COMB_WORDS * 4, stream, count, scalars,
-                     tab, out_ext);
+  hipLaunchKernelGGL(k_fixed_base, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, scalars, tab,
+                     out_ext);
 }
 
 // ------------------------------------------------------------------ layout / scalar helpers

@@ -92,6 +92,69 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
   }
 }
 
+// Radix-256 comb in global memory (L2-resident, 512 KB per base): 32 windows B_w = 256^w B of
+// 128 affine Niels entries d B_w (d = 1..128), entry-major, 32 words per entry (ypx | ymx |
+// xy2d | 2 pad).  Signed digits in [-128, 127]: one mixed addition per 8 scalar bits, half the
+// additions of the LDS radix-16 comb, for the bases every kernel shares (g, h).
+constexpr int COMB8_WINDOWS = 32;
+constexpr int COMB8_ENTRIES = 128;
+constexpr int COMB8_STRIDE = 32;
+constexpr size_t COMB8_WORDS = (size_t)COMB8_WINDOWS * COMB8_ENTRIES * COMB8_STRIDE;
+
+DKG_DEV void comb8_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < COMB8_WINDOWS; w++) {
+    const int wi = w >> 2;
+    uint32_t word = s.v[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) word = (wi == k) ? s.v[k] : word;
+    int d = (int)((word >> (8 * (w & 3))) & 255u) + carry;
+    carry = (d + 128) >> 8;
+    d -= carry << 8;
+    const int ad = d < 0 ? -d : d;
+    const uint32_t* ep = tab + ((size_t)w * COMB8_ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMB8_STRIDE;
+    const bool neg = d < 0, zero = ad == 0;
+    // the entry's 30 words, selected as they arrive: -Q = (y-x, y+x, -2dxy), 0 = (1, 1, 0)
+    ge_aff r;
+    {
+      uint32_t qa[12], qb[12];
+      const uint4* e4 = reinterpret_cast<const uint4*>(ep);
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const uint4 u = e4[k], v = e4[k + 2];  // words 4k..4k+3 (ypx...) and 8+4k.. (ymx...)
+        qa[4 * k] = u.x; qa[4 * k + 1] = u.y; qa[4 * k + 2] = u.z; qa[4 * k + 3] = u.w;
+        (void)v;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const uint4 v = e4[2 + k];  // words 8..19
+        qb[4 * k] = v.x; qb[4 * k + 1] = v.y; qb[4 * k + 2] = v.z; qb[4 * k + 3] = v.w;
+      }
+      // qa[0..9] = ypx, qa[10..11] = ymx[0..1]; qb = words 8..19: ymx = qa[10..11] ++ qb[4..11]
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        const uint32_t ypx = qa[i], ymx = i < 2 ? qa[10 + i] : qb[2 + i];
+        r.ypx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? ymx : ypx);
+        r.ymx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? ypx : ymx);
+      }
+      const uint4* x4 = reinterpret_cast<const uint4*>(ep + 20);
+      uint32_t xw[12];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const uint4 v = x4[k];
+        xw[4 * k] = v.x; xw[4 * k + 1] = v.y; xw[4 * k + 2] = v.z; xw[4 * k + 3] = v.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        const uint32_t p2 = i == 0 ? fe_const::P2_0 : ((i & 1) ? fe_const::P2_O : fe_const::P2_E);
+        r.xy2d.v[i] = zero ? 0u : (neg ? p2 - xw[i] : xw[i]);
+      }
+    }
+    ge_madd(acc, acc, r);
+  }
+}
+
 // Register-lean variants for the m-chains: the cached addend lives in LDS (lane-interleaved,
 // word w of lane l at q[w * 64 + l], conflict-free) and is read field by field when the addition
 // needs it, so a chain keeps one point + the doubling temporaries in VGPRs (<= 128: 4 waves/SIMD).

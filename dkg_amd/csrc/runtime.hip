@@ -21,6 +21,8 @@ struct dkg_ctx {
   std::map<std::string, std::pair<void*, size_t>> bufs;
   uint32_t* tab_g = nullptr;  // comb table of the generator (15360 words)
   uint32_t* tab_h = nullptr;  // comb table of the commitment key h
+  uint32_t* tab_g8 = nullptr;  // radix-256 combs (global, L2-resident) of g and h: commit, check,
+  uint32_t* tab_h8 = nullptr;  // fixed-base products
   uint8_t h[32] = {0};
   bool have_h = false;
   size_t threshold = 0, nr_members = 0;
@@ -34,6 +36,12 @@ struct dkg_ctx {
   int split = 0;                        // degree split U of the difference tables (0: cost model)
   int last_split = 1;                   // U used by the last verify_device
   size_t ydig_n = 0, ydig_L = 0;        // key of the cached combine multipliers (v.ydig)
+  // round-1 commitments of the ceremony being verified, in extended form on this device (set by
+  // the drivers that generate them, ExtScope): verify_device places them instead of decoding the
+  // encodings, finalise reads A_i0 from them.  E/A [D][t+1] points, word stride ext_stride.
+  const uint32_t* ext_E = nullptr;
+  const uint32_t* ext_A = nullptr;
+  size_t ext_stride = 0;
   std::string timed_tag;                // set while pev[] hold a serialised verify_device's phases
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
@@ -42,6 +50,7 @@ namespace {
 
 constexpr size_t PTB = 160;  // bytes of one extended point (40 words)
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
+constexpr size_t COMB8_BYTES = 32 * 128 * 32 * 4;  // points.h COMB8_WORDS
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
                                0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
                                0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
@@ -106,13 +115,15 @@ int guarded(dkg_ctx* ctx, F&& f) {
 }
 
 // Decode one 32-byte point and build its comb table into `tab`.
-void comb_for_point(dkg_ctx* ctx, const uint8_t p[32], uint32_t* tab, bool* ok) {
+// Comb tables of one point: radix-16 (LDS kernels; may be null) and radix-256 (may be null).
+void comb_for_point(dkg_ctx* ctx, const uint8_t p[32], uint32_t* tab, bool* ok, uint32_t* tab8 = nullptr) {
   uint32_t* comp = buf<uint32_t>(ctx, "comb_in", 32);
   uint32_t* ext = buf<uint32_t>(ctx, "comb_ext", PTB);
   uint8_t* okd = buf<uint8_t>(ctx, "comb_ok", 1);
   h2d(ctx, comp, p, 32);
   dkgk::decode_points(comp, 1, ext, 1, okd, ctx->stream);
-  dkgk::build_comb(ext, 1, 0, tab, ctx->stream);
+  if (tab) dkgk::build_comb(ext, 1, 0, tab, ctx->stream);
+  if (tab8) dkgk::build_comb8(ext, 1, 0, tab8, ctx->stream);
   check_launch(ctx);
   uint8_t v = 0;
   d2h(ctx, &v, okd, 1);
@@ -322,8 +333,13 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // padding columns, and the positions past t of the last piece, are the identity
   if (npad != D * nseg || U * L != N) dkgk::fill_identity(L * W, Cpm, home);
   HCK(hipMemsetAsync(pok, 1, npad * N, home));
-  for (int k = 0; k < nseg; k++)  // K5 (groups.rs:78-81) into the position-major table
-    dkgk::decode_position_major(segs[k].Ccomp, D, N, W, Cpm, pok, home, nseg, k, L, npad);
+  for (int k = 0; k < nseg; k++) {
+    const uint32_t* ext = segs[k].round == 2 ? ctx->ext_E : ctx->ext_A;
+    if (ext)  // generated on this device: group elements, as the reference's broadcasts carry them
+      dkgk::place_position_major(ext, ctx->ext_stride, D, N, W, Cpm, home, nseg, k, L, npad);
+    else  // K5 (groups.rs:78-81) into the position-major table
+      dkgk::decode_position_major(segs[k].Ccomp, D, N, W, Cpm, pok, home, nseg, k, L, npad);
+  }
   dkgk::dealer_ok(npad, N, pok, dok, home);
   for (int k = 0; k < nseg; k++)
     if (segs[k].extra_ok) dkgk::and_dealer_mask(D, nseg, k, segs[k].extra_ok, dok, home);
@@ -332,11 +348,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (d1 <= d0) return;
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
-      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, n, g.s, g.sp, R, rstride, ctx->tab_g, ctx->tab_h, dok,
+      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, n, g.s, g.sp, R, rstride, ctx->tab_g8, ctx->tab_h8, dok,
                        g.dec, segs[1].dec, st);
     } else {
       dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, n, g.round, g.s + d0 * n * 8,
-                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n, rstride, ctx->tab_g, ctx->tab_h,
+                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n, rstride, ctx->tab_g8, ctx->tab_h8,
                   dok + d0, g.dec + d0 * n, st);
     }
   };
@@ -496,7 +512,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     h2d(ctx, qmask, qualified.data(), n);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
     uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
-    dkgk::fixed_base(n, fs, ctx->tab_g, pub, ctx->stream);
+    dkgk::fixed_base(n, fs, ctx->tab_g8, pub, ctx->stream);
     dkgk::encode_points(pub, n, n, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
@@ -520,11 +536,15 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     honest_mask[i] = qualified[i] && !recon[i];
     nrecon += recon[i];
   }
-  uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
-  HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
   uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
-  uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
-  dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
+  if (ctx->ext_A) {
+    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, n, A0, n, ctx->stream);
+  } else {
+    uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
+    HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
+    uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
+    dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
+  }
   uint8_t* hmask = buf<uint8_t>(ctx, "hmask", n);
   h2d(ctx, hmask, honest_mask.data(), n);
   uint32_t* parts = buf<uint32_t>(ctx, "mpk_parts", PTB * 2);
@@ -537,7 +557,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
     h2d(ctx, sec, secrets.data(), secrets.size());
     uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
-    dkgk::fixed_base(nrecon, sec, ctx->tab_g, gsec, ctx->stream);
+    dkgk::fixed_base(nrecon, sec, ctx->tab_g8, gsec, ctx->stream);
     dkgk::sum_points(nrecon, gsec, nrecon, nullptr, parts, 2, 1, ctx->stream);
   } else {
     dkgk::sum_points(0, A0, n, nullptr, parts, 2, 1, ctx->stream);  // identity
@@ -570,17 +590,36 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
 }
 
 // Round 1 for D dealers on device: a, b canonical [D][N][8] -> Ecomp, Acomp [D][N][8], s, sp [D][n][8].
+// Round 1 on device.  encode = false: the commitments stay group elements (Ecomp / Acomp are not
+// written; the caller verifies through an ExtScope, as the reference's in-memory broadcasts).
 void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a, const uint32_t* b,
-                   uint32_t* Ecomp, uint32_t* Acomp, uint32_t* s, uint32_t* sp) {
+                   uint32_t* Ecomp, uint32_t* Acomp, uint32_t* s, uint32_t* sp, bool encode = true) {
   const size_t N = t + 1;
   uint32_t* Aext = buf<uint32_t>(ctx, "Aext", PTB * D * N);
   uint32_t* Eext = buf<uint32_t>(ctx, "Eext", PTB * D * N);
-  dkgk::commit(D * N, a, b, ctx->tab_g, ctx->tab_h, Aext, Eext, ctx->stream);  // K2 (committee.rs:151-159)
-  dkgk::encode_points(Eext, D * N, D * N, Ecomp, ctx->stream);                    // broadcast encodings
-  dkgk::encode_points(Aext, D * N, D * N, Acomp, ctx->stream);
+  dkgk::commit(D * N, a, b, ctx->tab_g8, ctx->tab_h8, Aext, Eext, ctx->stream);  // K2 (committee.rs:151-159)
+  if (encode) {
+    dkgk::encode_points(Eext, D * N, D * N, Ecomp, ctx->stream);                  // broadcast encodings
+    dkgk::encode_points(Aext, D * N, D * N, Acomp, ctx->stream);
+  }
   dkgk::share_eval(D, n, N, a, b, s, sp, ctx->stream);                            // K1 (:164-167)
   check_launch(ctx);
 }
+
+// Verify what round1_device just generated from its extended-form commitments (no encode/decode
+// round trip); restores the ctx on exit.
+struct ExtScope {
+  dkg_ctx* ctx;
+  ExtScope(dkg_ctx* c, size_t D, size_t N) : ctx(c) {
+    ctx->ext_E = buf<uint32_t>(ctx, "Eext", PTB * D * N);
+    ctx->ext_A = buf<uint32_t>(ctx, "Aext", PTB * D * N);
+    ctx->ext_stride = D * N;
+  }
+  ~ExtScope() {
+    ctx->ext_E = ctx->ext_A = nullptr;
+    ctx->ext_stride = 0;
+  }
+};
 
 // ---- batches of independent ceremonies (BASELINE config 5: many small key ceremonies)
 // B ceremonies of n parties are stacked dealer-wise: dealer c*n + i is party i of ceremony c, and
@@ -614,7 +653,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
     // round 3 (committee.rs:433-476) per ceremony
     h2d(ctx, qmask, qualified.data(), V);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
-    dkgk::fixed_base(V, fs, ctx->tab_g, pub, ctx->stream);
+    dkgk::fixed_base(V, fs, ctx->tab_g8, pub, ctx->stream);
     dkgk::encode_points(pub, V, V, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
@@ -636,11 +675,15 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
     if (any) recon_cer.push_back(c);
   }
   // finalise (committee.rs:726-805): mpk_c = sum of honest A_i0 (+ g * reconstructed secrets)
-  uint32_t* A0c = buf<uint32_t>(ctx, "b.A0c", 32 * V);
-  HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, V, hipMemcpyDeviceToDevice, ctx->stream));
   uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
-  uint8_t* a0ok = buf<uint8_t>(ctx, "b.A0ok", V);
-  dkgk::decode_points(A0c, V, A0, V, a0ok, ctx->stream);
+  if (ctx->ext_A) {
+    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, V, A0, V, ctx->stream);
+  } else {
+    uint32_t* A0c = buf<uint32_t>(ctx, "b.A0c", 32 * V);
+    HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, V, hipMemcpyDeviceToDevice, ctx->stream));
+    uint8_t* a0ok = buf<uint8_t>(ctx, "b.A0ok", V);
+    dkgk::decode_points(A0c, V, A0, V, a0ok, ctx->stream);
+  }
   uint8_t* hmask = buf<uint8_t>(ctx, "b.hmask", V);
   h2d(ctx, hmask, honest.data(), V);
   uint32_t* mpk_ext = buf<uint32_t>(ctx, "b.mpk_ext", PTB * B);
@@ -656,7 +699,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
       uint32_t* sec = buf<uint32_t>(ctx, "b.recon_sec", 32 * nr);
       h2d(ctx, sec, secrets.data(), secrets.size());
       uint32_t* gsec = buf<uint32_t>(ctx, "b.recon_ext", PTB * nr);
-      dkgk::fixed_base(nr, sec, ctx->tab_g, gsec, ctx->stream);
+      dkgk::fixed_base(nr, sec, ctx->tab_g8, gsec, ctx->stream);
       dkgk::sum_points(nr, gsec, nr, nullptr, extra, B, c, ctx->stream);
       dkgk::add_points(1, mpk_ext + c, extra + c, B, mpk_ext + c, ctx->stream);
       sync(ctx);  // sec / gsec are reused by the next ceremony
@@ -849,8 +892,10 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
+    HCK(hipMalloc(&ctx->tab_g8, COMB8_BYTES));
+    HCK(hipMalloc(&ctx->tab_h8, COMB8_BYTES));
     bool ok = false;
-    comb_for_point(ctx, BASEPOINT, ctx->tab_g, &ok);
+    comb_for_point(ctx, BASEPOINT, ctx->tab_g, &ok, ctx->tab_g8);
     if (!ok) {
       ctx->err = "basepoint failed to decode on device";
       return DKG_E_DEVICE;
@@ -873,6 +918,8 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   for (auto& kv : ctx->bufs) (void)hipFree(kv.second.first);
   if (ctx->tab_g) (void)hipFree(ctx->tab_g);
   if (ctx->tab_h) (void)hipFree(ctx->tab_h);
+  if (ctx->tab_g8) (void)hipFree(ctx->tab_g8);
+  if (ctx->tab_h8) (void)hipFree(ctx->tab_h8);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->pev)
@@ -946,7 +993,7 @@ int dkg_env_init(dkg_ctx* ctx, size_t threshold, size_t nr_members, const uint8_
     d2h(ctx, ctx->h, comp, 32);
     sync(ctx);
     bool ok = false;
-    comb_for_point(ctx, ctx->h, ctx->tab_h, &ok);
+    comb_for_point(ctx, ctx->h, ctx->tab_h, &ok, ctx->tab_h8);
     if (!ok) return DKG_E_DEVICE;
     ctx->have_h = true;
     ctx->threshold = threshold;
@@ -986,11 +1033,11 @@ int dkg_msm_batch(dkg_ctx* ctx, size_t B, size_t N, const uint8_t* scalars, cons
 int dkg_fixed_base_batch(dkg_ctx* ctx, const uint8_t base[32], size_t count, const uint8_t* scalars, uint8_t* out) {
   return guarded(ctx, [&] {
     if (count == 0) return DKG_OK;
-    const uint32_t* tab = ctx->tab_g;
+    const uint32_t* tab = ctx->tab_g8;
     if (base) {
-      uint32_t* t = buf<uint32_t>(ctx, "fb_tab", COMB_BYTES);
+      uint32_t* t = buf<uint32_t>(ctx, "fb_tab8", COMB8_BYTES);
       bool ok = false;
-      comb_for_point(ctx, base, t, &ok);
+      comb_for_point(ctx, base, nullptr, &ok, t);
       if (!ok) {
         ctx->err = "fixed_base: base point failed to decode";
         return DKG_E_DECODE;
@@ -1116,7 +1163,7 @@ int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, c
     uint32_t* ds = upload_scalars(ctx, "vr_s", s, n);
     uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vr_sp", s_prime, n) : nullptr;
     uint8_t* dec = buf<uint8_t>(ctx, "vr_dec", n);
-    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, n, ctx->tab_g, ctx->tab_h, dok, dec, ctx->stream);
+    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, n, ctx->tab_g8, ctx->tab_h8, dok, dec, ctx->stream);
     check_launch(ctx);
     d2h(ctx, decision, dec, n);
     sync(ctx);
@@ -1136,8 +1183,9 @@ int dkg_ceremony_run_device(dkg_ctx* ctx, size_t n, size_t t, const void* d_a, c
     uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
     uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
-    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    ExtScope ext(ctx, n, N);
     receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, false);  // small outputs only
     out->ms_round1 = ev_ms(ctx, 0, 1);
     out->ms_round2 = ev_ms(ctx, 1, 2);
@@ -1168,6 +1216,7 @@ int dkg_ceremony_run(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* a, const u
     if (out->A) d2h(ctx, out->A, Ac, 32 * n * N);
     if (out->s) d2h(ctx, out->s, ds, 32 * n * n);
     if (out->s_prime) d2h(ctx, out->s_prime, dsp, 32 * n * n);
+    ExtScope ext(ctx, n, N);
     receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, true);
     out->ms_round1 = ev_ms(ctx, 0, 1);
     out->ms_round2 = ev_ms(ctx, 1, 2);
@@ -1259,7 +1308,13 @@ void shard_rows(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t D, const uin
       for (size_t j = 0; j < n; j++)
         if (rows[i * n + j] == DKG_REJECT || rows[i * n + j] == DKG_MISSING) q[i] = 0;
   });
-  HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->ext_A) {  // the exchanged A_i0 encodings
+    uint32_t* a0 = buf<uint32_t>(ctx, "sh_a0ext", PTB * D);
+    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, D, a0, D, ctx->stream);
+    dkgk::encode_points(a0, D, D, (uint32_t*)d_A0, ctx->stream);
+  } else {
+    HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
+  }
   // Round-4 accusations against a qualified dealer put it in the reconstructable set
   // (committee.rs:660-670) -- again a function of its own row.  Its mpk term becomes g * a_i0
   // recovered by Lagrange interpolation of its shares (finalise, :747-783); the shares of this
@@ -1287,7 +1342,7 @@ void shard_rows(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t D, const uin
     uint32_t* gsec = buf<uint32_t>(ctx, "sh_rext", PTB * R);
     uint32_t* gc = buf<uint32_t>(ctx, "sh_rcomp", 32 * R);
     h2d(ctx, sec, secrets.data(), secrets.size());
-    dkgk::fixed_base(R, sec, ctx->tab_g, gsec, ctx->stream);
+    dkgk::fixed_base(R, sec, ctx->tab_g8, gsec, ctx->stream);
     dkgk::encode_points(gsec, R, R, gc, ctx->stream);
     for (size_t r = 0; r < R; r++)
       HCK(hipMemcpyAsync((uint8_t*)d_A0 + 32 * recon[r], gc + 8 * r, 32, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1312,7 +1367,8 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     uint32_t* Ac = buf<uint32_t>(ctx, "sh_A", 32 * D * N);
     uint32_t* ds = buf<uint32_t>(ctx, "sh_s", 32 * D * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "sh_sp", 32 * D * n);
-    if (D) round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    if (D) round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
+    ExtScope ext(ctx, D, N);
     shard_rows(ctx, n, t, d0, D, Ec, Ac, ds, dsp, d_dec2, d_dec4, d_A0, d_partial);
     check_launch(ctx);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -1398,8 +1454,9 @@ int dkg_ceremony_batch_device(dkg_ctx* ctx, size_t B, size_t n, size_t t, const 
     uint32_t* Ac = buf<uint32_t>(ctx, "bat_A", 32 * V * N);
     uint32_t* ds = buf<uint32_t>(ctx, "bat_s", 32 * V * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "bat_sp", 32 * V * n);
-    round1_device(ctx, V, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    round1_device(ctx, V, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+    ExtScope ext(ctx, V, N);
     batch_receivers(ctx, B, n, t, Ec, Ac, ds, dsp, out);
     batch_times(ctx, out, true);
     return DKG_OK;
@@ -1467,7 +1524,7 @@ int dkg_member_keys(dkg_ctx* ctx, const uint8_t master[32], uint32_t ceremony, s
     uint32_t* dpe = buf<uint32_t>(ctx, "mk_pk_ext", PTB * n);
     uint32_t* dpc = buf<uint32_t>(ctx, "mk_pk", 32 * n);
     h2d(ctx, dsk, sk.data(), 32 * n);
-    dkgk::fixed_base(n, dsk, ctx->tab_g, dpe, ctx->stream);  // to_public (procedure_keys.rs:78-82)
+    dkgk::fixed_base(n, dsk, ctx->tab_g8, dpe, ctx->stream);  // to_public (procedure_keys.rs:78-82)
     dkgk::encode_points(dpe, n, n, dpc, ctx->stream);
     check_launch(ctx);
     d2h(ctx, pk.data(), dpc, 32 * n);
@@ -1593,7 +1650,7 @@ int dkg_ceremony_run_full_device(dkg_ctx* ctx, size_t n, size_t t, const void* d
     uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
     uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
-    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp);
+    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
     uint32_t* e1 = buf<uint32_t>(ctx, "fm_e1", 32 * items);
     uint32_t* ct = buf<uint32_t>(ctx, "fm_ct", 32 * items);
     encrypt_device(ctx, n, n, dpk, ds, dsp, (const uint32_t*)d_r, e1, ct);  // committee.rs:169-172
@@ -1603,6 +1660,7 @@ int dkg_ceremony_run_full_device(dkg_ctx* ctx, size_t n, size_t t, const void* d
     uint8_t* iok = buf<uint8_t>(ctx, "fm_iok", items);
     uint8_t* eok = buf<uint8_t>(ctx, "fm_eok", n);
     decrypt_device(ctx, n, n, dsk, e1, ct, rs, rsp, iok, eok);  // committee.rs:282-286
+    ExtScope ext(ctx, n, N);
     receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, false, eok);
     out->ms_round1 = ev_ms(ctx, 0, 1);
     out->ms_round2 = ev_ms(ctx, 1, 2);
