@@ -190,6 +190,7 @@ def bench_batch(args, ws, rank, local):
     be = dkg_amd.Backend(local)
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
+    be.set_verify_mode(args.verify)
     be.env_init(t, n)
     dev = torch.device("cuda", local)
     ta = torch.empty(B * n * N * 32, dtype=torch.uint8, device=dev)
@@ -248,6 +249,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="dealer-chunk streams of the round-2/4 checks")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal with ranks sharing GPUs")
+    ap.add_argument("--verify", default="group", choices=["group", "interp"],
+                    help="group: every P_i(j) computed in the group (default); interp: committee verification "
+                         "by interpolation (identical decisions, DESIGN.md section 2)")
     ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
@@ -269,6 +273,7 @@ def main():
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
     be.set_split(args.split)
+    be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1
     master = b"\xbe" * 32
@@ -342,7 +347,15 @@ def main():
         out["config"]["mode"] = "full: shares hybrid-encrypted (elgamal.rs) and decrypted by each receiver"
     if rank == 0 and ws == 1 and res is not None and args.mode == "full":
         out["phases_ms"] = {k: round(v, 3) for k, v in res.ms.items()}
-    elif rank == 0 and ws == 1 and res is not None:
+    if args.verify == "interp":
+        out["metric"] += " -- committee verification by interpolation (identical decisions)"
+        out["config"]["verify"] = ("interp: shares at receivers 1..t+1 fix F, F'; commitments tested once; "
+                                   "remaining pairs by scalar comparison (DESIGN.md section 2)")
+    if rank == 0 and ws == 1 and res is not None and args.verify == "interp" and args.mode != "full":
+        out["phases_ms"] = {k: round(v, 3) for k, v in res.ms.items()}
+        out["verify_phases_ms"] = {k: round(v, 3) for k, v in be.phase_times("interp").items()}
+        out["fallback_rows"] = be.fallback_rows()
+    elif rank == 0 and ws == 1 and res is not None and args.mode != "full":
         out["phases_ms"] = {k: round(v, 3) for k, v in res.ms.items()}
         out["config"]["verify_streams"] = args.streams
         out["config"]["rounds_2_4_fused"] = not args.no_overlap

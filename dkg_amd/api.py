@@ -109,6 +109,15 @@ class Backend:
         """Dealer-chunk streams of the round-2/4 checks (1 = serialised, phase times recorded)."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_streams(self._ctx, nsub))
 
+    def set_verify_mode(self, mode):
+        """0 / "group": difference tables (every P_i(j) in the group, default); 1 / "interp":
+        committee verification by interpolation (identical decisions; dkg_ctx_set_verify_mode)."""
+        m = {"group": 0, "interp": 1}.get(mode, mode)
+        _check(self._ctx, _lib.lib().dkg_ctx_set_verify_mode(self._ctx, int(m)))
+
+    def fallback_rows(self) -> int:
+        return _lib.lib().dkg_ctx_fallback_rows(self._ctx)
+
     def set_split(self, pieces: int):
         """Degree split of the difference tables (0 = cost model, 1 = off); results are identical."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_split(self._ctx, pieces))
@@ -127,8 +136,9 @@ class Backend:
         L = _lib.lib()
         if isinstance(tag, int):
             tag = f"r{tag}"
-        return {k: L.dkg_ctx_phase_ms(self._ctx, f"{tag}.{k}".encode())
-                for k in ("binomial", "stepping", "combine", "check")}
+        names = (("interpolate", "coef_check", "decide", "fallback") if tag == "interp"
+                 else ("binomial", "stepping", "combine", "check"))
+        return {k: L.dkg_ctx_phase_ms(self._ctx, f"{tag}.{k}".encode()) for k in names}
 
     def env_init(self, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT) -> bytes:
         out = ctypes.create_string_buffer(32)

@@ -142,4 +142,20 @@ void dealer_seeds(size_t rows, size_t D, size_t d0, uint32_t c0, const uint32_t*
 // encryption randomness rows (seedgen.hip): r [rows][n][2][8] = wide(block 2N + 2q + w) of each dealer stream
 void enc_randomness(size_t rows, size_t n, size_t N, const uint32_t* seeds, uint32_t* r, hipStream_t stream);
 
+// ---- committee verification by interpolation (interp.hip)
+// F[d][k] = sum_j W[k][j] s[d][j] (and F' from s'; sp may be null), WT[j][k] = W[k][j] in Montgomery form
+void interp(size_t D, size_t N, size_t nrecv, const uint32_t* WT, const uint32_t* s, const uint32_t* sp, uint32_t* F,
+            uint32_t* Fp, hipStream_t stream);
+// per (d, k): okA = (g F_k == A_k), okE = (g F_k + h F'_k == E_k); commitments [D][N] extended
+void coef_check(size_t D, size_t N, const uint32_t* F, const uint32_t* Fp, const uint32_t* Eext, const uint32_t* Aext,
+                size_t cstride, const uint32_t* tab_g, const uint32_t* tab_h, uint8_t* okE, uint8_t* okA,
+                hipStream_t stream);
+// round-2 / round-4 decisions of the rows whose coefficient test passed (others: 0, re-verified)
+void interp_decide(size_t D, size_t nrecv, size_t N, size_t dealer_base, size_t nmod, const uint32_t* s,
+                   const uint32_t* sp, const uint32_t* F, const uint32_t* Fp, const uint8_t* dokE, const uint8_t* dokA,
+                   const uint8_t* cE, const uint8_t* cA, const uint32_t* tab_g, const uint32_t* tab_h, uint8_t* dec2,
+                   uint8_t* dec4, hipStream_t stream);
+// ok[i] &= extra[i], i < D
+void and_mask(size_t D, const uint8_t* extra, uint8_t* ok, hipStream_t stream);
+
 }  // namespace dkgk

@@ -34,6 +34,9 @@ struct dkg_ctx {
   hipEvent_t fork = nullptr, join[MAX_SUB] = {};
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
+  int verify_mode = 0;                  // 0: difference tables (every P_i(j) in the group); 1: interpolation
+  size_t vinv_N = 0;                    // key of the cached inverse Vandermonde (v.vinv)
+  size_t fallback_rows = 0;             // interpolation mode: rows re-verified the general way
   int last_split = 1;                   // U used by the last verify_device
   size_t ydig_n = 0, ydig_L = 0;        // key of the cached combine multipliers (v.ydig)
   // round-1 commitments of the ceremony being verified, in extended form on this device (set by
@@ -49,6 +52,7 @@ struct dkg_ctx {
 namespace {
 
 constexpr size_t PTB = 160;  // bytes of one extended point (40 words)
+constexpr size_t PT_WORDS_H = 40;
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
 constexpr size_t COMB8_BYTES = 32 * 128 * 32 * 4;  // points.h COMB8_WORDS
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
@@ -164,6 +168,7 @@ struct VerifySeg {
   const uint32_t* sp;
   uint8_t* dec;
   const uint8_t* extra_ok = nullptr;  // [D] device: 0 = the dealer's other broadcast data is missing
+  size_t self_mod = 0;                // self = (dealer + dealer_base) mod self_mod == j; 0: n
 };
 
 // ---- degree split ----
@@ -348,10 +353,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (d1 <= d0) return;
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
-      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, n, g.s, g.sp, R, rstride, ctx->tab_g8, ctx->tab_h8, dok,
-                       g.dec, segs[1].dec, st);
+      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R, rstride,
+                       ctx->tab_g8, ctx->tab_h8, dok, g.dec, segs[1].dec, st);
     } else {
-      dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, n, g.round, g.s + d0 * n * 8,
+      dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, g.self_mod ? g.self_mod : n, g.round, g.s + d0 * n * 8,
                   g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n, rstride, ctx->tab_g8, ctx->tab_h8,
                   dok + d0, g.dec + d0 * n, st);
     }
@@ -410,9 +415,9 @@ void verify_one(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t de
 // DKG_MISSING); a_ok (may be null): 0 = its phase-3 commitments are missing (round 4: accusation)
 // (full mode), folded into the round-2 decisions like an undecodable commitment.
 template <typename F>
-void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
-                   const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
-                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
+void verify_rounds_group(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
+                         const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
+                         hipEvent_t after2, F&& between, const uint8_t* e_ok, const uint8_t* a_ok) {
   if (ctx->overlap) {
     VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok}, {4, D, dealer_base, Acomp, s, nullptr, dec4, a_ok}};
     verify_device(ctx, n, t, g, 2, true, "r24");
@@ -431,6 +436,184 @@ void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_bas
     sync(ctx);
     collect_phases(ctx);
   }
+}
+
+// ---- committee verification by interpolation (ctx->verify_mode == 1; interp.hip) ----
+// Inverse Vandermonde of the points 1..N mod l, transposed and in Montgomery form:
+// WT[j][k] = [x^k] L_j(x) * 2^256, L_j the Lagrange basis polynomial of point j+1.  Cached per N.
+const uint32_t* vinv_table(dkg_ctx* ctx, size_t N) {
+  uint32_t* dev = buf<uint32_t>(ctx, "v.vinv", 32 * N * N);
+  if (ctx->vinv_N == N) return dev;
+  using dkgh::Zl;
+  const Zl zero = dkgh::zl_from_u64(0);
+  std::vector<Zl> M(N + 1, zero);  // M(x) = prod_m (x - (m+1)), ascending coefficients
+  M[0] = dkgh::zl_from_u64(1);
+  for (size_t m = 0; m < N; m++) {
+    const Zl xm = dkgh::zl_from_u64(m + 1);
+    for (size_t k = m + 1; k > 0; k--) M[k] = dkgh::zl_sub(M[k - 1], dkgh::zl_mul(xm, M[k]));
+    M[0] = dkgh::zl_sub(zero, dkgh::zl_mul(xm, M[0]));
+  }
+  uint8_t r256[33] = {0};
+  r256[32] = 1;
+  const Zl R = dkgh::zl_from_bytes_wide(r256, 33);  // 2^256 mod l
+  std::vector<uint8_t> host(32 * N * N);
+  std::vector<Zl> q(N);
+  for (size_t j = 0; j < N; j++) {
+    const Zl xj = dkgh::zl_from_u64(j + 1);
+    q[N - 1] = M[N];  // Q_j = M / (x - x_j), synthetic division
+    for (size_t k = N - 1; k > 0; k--) q[k - 1] = dkgh::zl_add(M[k], dkgh::zl_mul(xj, q[k]));
+    Zl den = zero;  // Q_j(x_j) = prod_{m != j} (x_j - x_m)
+    for (size_t k = N; k-- > 0;) den = dkgh::zl_add(dkgh::zl_mul(den, xj), q[k]);
+    const Zl scale = dkgh::zl_mul(dkgh::zl_inv(den), R);
+    for (size_t k = 0; k < N; k++) dkgh::zl_to_bytes(&host[32 * (j * N + k)], dkgh::zl_mul(q[k], scale));
+  }
+  h2d(ctx, dev, host.data(), host.size());
+  ctx->vinv_N = N;
+  return dev;
+}
+
+template <typename F>
+void verify_rounds_interp(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
+                          const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
+                          hipEvent_t after2, F&& between, const uint8_t* e_ok, const uint8_t* a_ok) {
+  const size_t N = t + 1;
+  hipStream_t st = ctx->stream;
+  if (D) {
+    HCK(hipEventRecord(ctx->pev[0], st));
+    // the commitments as group elements [D][N]
+    const uint32_t *Ee, *Ae;
+    size_t cs;
+    uint8_t* dokE = buf<uint8_t>(ctx, "i.dokE", D);
+    uint8_t* dokA = buf<uint8_t>(ctx, "i.dokA", D);
+    if (ctx->ext_E) {
+      Ee = ctx->ext_E;
+      Ae = ctx->ext_A;
+      cs = ctx->ext_stride;
+      HCK(hipMemsetAsync(dokE, 1, D, st));
+      HCK(hipMemsetAsync(dokA, 1, D, st));
+    } else {  // K5 (groups.rs:78-81): a row that does not decode is missing data
+      uint32_t* ee = buf<uint32_t>(ctx, "i.Eext", PTB * D * N);
+      uint32_t* ae = buf<uint32_t>(ctx, "i.Aext", PTB * D * N);
+      uint8_t* pok = buf<uint8_t>(ctx, "i.pok", D * N);
+      dkgk::decode_points(Ecomp, D * N, ee, D * N, pok, st);
+      dkgk::dealer_ok(D, N, pok, dokE, st);
+      dkgk::decode_points(Acomp, D * N, ae, D * N, pok, st);
+      dkgk::dealer_ok(D, N, pok, dokA, st);
+      Ee = ee;
+      Ae = ae;
+      cs = D * N;
+    }
+    dkgk::and_mask(D, e_ok, dokE, st);
+    dkgk::and_mask(D, a_ok, dokA, st);
+    const uint32_t* WT = vinv_table(ctx, N);
+    uint32_t* Fa = buf<uint32_t>(ctx, "i.F", 32 * D * N);
+    uint32_t* Fb = buf<uint32_t>(ctx, "i.Fp", 32 * D * N);
+    dkgk::interp(D, N, n, WT, s, sp, Fa, Fb, st);  // F, F' through receivers 1..t+1
+    HCK(hipEventRecord(ctx->pev[1], st));
+    uint8_t* okE = buf<uint8_t>(ctx, "i.okE", D * N);
+    uint8_t* okA = buf<uint8_t>(ctx, "i.okA", D * N);
+    dkgk::coef_check(D, N, Fa, Fb, Ee, Ae, cs, ctx->tab_g8, ctx->tab_h8, okE, okA, st);
+    uint8_t* cE = buf<uint8_t>(ctx, "i.cE", D);
+    uint8_t* cA = buf<uint8_t>(ctx, "i.cA", D);
+    dkgk::dealer_ok(D, N, okE, cE, st);
+    dkgk::dealer_ok(D, N, okA, cA, st);
+    HCK(hipEventRecord(ctx->pev[2], st));
+    dkgk::interp_decide(D, n, N, dealer_base, n, s, sp, Fa, Fb, dokE, dokA, cE, cA, ctx->tab_g8, ctx->tab_h8, dec2,
+                        dec4, st);
+    HCK(hipEventRecord(ctx->pev[3], st));
+    check_launch(ctx);
+    // rows whose commitments are not g F + h F' (case B): difference tables, every P_i(j) in the group
+    std::vector<uint8_t> h_dE(D), h_dA(D), h_cE(D), h_cA(D);
+    d2h(ctx, h_dE.data(), dokE, D);
+    d2h(ctx, h_dA.data(), dokA, D);
+    d2h(ctx, h_cE.data(), cE, D);
+    d2h(ctx, h_cA.data(), cA, D);
+    sync(ctx);
+    std::vector<size_t> rows;
+    for (size_t d = 0; d < D; d++)
+      if ((h_dE[d] && !h_cE[d]) || (h_dA[d] && !h_cA[d])) rows.push_back(d);
+    if (!rows.empty()) {
+      const size_t R = rows.size();
+      uint32_t* rs = buf<uint32_t>(ctx, "i.rs", 32 * R * n);
+      uint32_t* rsp = buf<uint32_t>(ctx, "i.rsp", 32 * R * n);
+      uint8_t* r2 = buf<uint8_t>(ctx, "i.r2", R * n);
+      uint8_t* r4 = buf<uint8_t>(ctx, "i.r4", R * n);
+      uint32_t *rE = nullptr, *rA = nullptr, *rEx = nullptr, *rAx = nullptr;
+      if (ctx->ext_E) {
+        rEx = buf<uint32_t>(ctx, "i.rEx", PTB * R * N);
+        rAx = buf<uint32_t>(ctx, "i.rAx", PTB * R * N);
+      } else {
+        rE = buf<uint32_t>(ctx, "i.rE", 32 * R * N);
+        rA = buf<uint32_t>(ctx, "i.rA", 32 * R * N);
+      }
+      for (size_t r = 0; r < R; r++) {
+        const size_t d = rows[r];
+        HCK(hipMemcpyAsync(rs + 8 * r * n, s + 8 * d * n, 32 * n, hipMemcpyDeviceToDevice, st));
+        HCK(hipMemcpyAsync(rsp + 8 * r * n, sp + 8 * d * n, 32 * n, hipMemcpyDeviceToDevice, st));
+        if (rEx) {  // SoA planes: 40 words x N points per row
+          HCK(hipMemcpy2DAsync(rEx + r * N, 4 * R * N, ctx->ext_E + d * N, 4 * ctx->ext_stride, 4 * N, PT_WORDS_H,
+                               hipMemcpyDeviceToDevice, st));
+          HCK(hipMemcpy2DAsync(rAx + r * N, 4 * R * N, ctx->ext_A + d * N, 4 * ctx->ext_stride, 4 * N, PT_WORDS_H,
+                               hipMemcpyDeviceToDevice, st));
+        } else {
+          HCK(hipMemcpyAsync(rE + 8 * r * N, Ecomp + 8 * d * N, 32 * N, hipMemcpyDeviceToDevice, st));
+          HCK(hipMemcpyAsync(rA + 8 * r * N, Acomp + 8 * d * N, 32 * N, hipMemcpyDeviceToDevice, st));
+        }
+      }
+      // fused round-2/4 pipeline on the compact rows; dealer_base = n with modulus 2n + R marks no
+      // pair as self (the diagonal is restored below)
+      const uint32_t *sE = ctx->ext_E, *sA = ctx->ext_A;
+      const size_t sstr = ctx->ext_stride;
+      if (rEx) {
+        ctx->ext_E = rEx;
+        ctx->ext_A = rAx;
+        ctx->ext_stride = R * N;
+      }
+      VerifySeg g[2] = {{2, R, n, rE, rs, rsp, r2, nullptr, 2 * n + R}, {4, R, n, rA, rs, nullptr, r4, nullptr, 2 * n + R}};
+      const bool ov = ctx->overlap;
+      ctx->overlap = true;
+      verify_device(ctx, n, t, g, 2, false, "");
+      ctx->overlap = ov;
+      ctx->ext_E = sE;
+      ctx->ext_A = sA;
+      ctx->ext_stride = sstr;
+      for (size_t r = 0; r < R; r++) {
+        const size_t d = rows[r], jself = (d + dealer_base) % n;
+        if (h_dE[d] && !h_cE[d]) {
+          HCK(hipMemcpyAsync(dec2 + d * n, r2 + r * n, n, hipMemcpyDeviceToDevice, st));
+          HCK(hipMemsetAsync(dec2 + d * n + jself, DKG_SELF, 1, st));
+        }
+        if (h_dA[d] && !h_cA[d]) {
+          HCK(hipMemcpyAsync(dec4 + d * n, r4 + r * n, n, hipMemcpyDeviceToDevice, st));
+          HCK(hipMemsetAsync(dec4 + d * n + jself, DKG_SELF, 1, st));
+        }
+      }
+      check_launch(ctx);
+    }
+    HCK(hipEventRecord(ctx->pev[4], st));
+    ctx->fallback_rows = rows.size();
+  }
+  if (after2) HCK(hipEventRecord(after2, st));
+  sync(ctx);
+  if (D) {
+    const char* names[4] = {"interpolate", "coef_check", "decide", "fallback"};
+    for (int i = 0; i < 4; i++) {
+      float ms = 0;
+      HCK(hipEventElapsedTime(&ms, ctx->pev[i], ctx->pev[i + 1]));
+      ctx->phase_ms[std::string("interp.") + names[i]] = ms;
+    }
+  }
+  between();
+}
+
+template <typename F>
+void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
+                   const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
+                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
+  if (ctx->verify_mode == 1)
+    verify_rounds_interp(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok);
+  else
+    verify_rounds_group(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok);
 }
 
 double ev_ms(dkg_ctx* ctx, int a, int b) {
@@ -946,6 +1129,14 @@ int dkg_ctx_set_streams(dkg_ctx* ctx, int nsub) {
   ctx->nsub = nsub;
   return DKG_OK;
 }
+
+int dkg_ctx_set_verify_mode(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
+  ctx->verify_mode = mode;
+  return DKG_OK;
+}
+
+size_t dkg_ctx_fallback_rows(const dkg_ctx* ctx) { return ctx ? ctx->fallback_rows : 0; }
 
 int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
   if (!ctx || pieces < 0 || pieces > 16) return DKG_E_ARG;

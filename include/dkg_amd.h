@@ -63,6 +63,19 @@ int dkg_ctx_set_overlap(dkg_ctx *ctx, int on);
  * multiplications by j^L; 0 (default) picks U with the cost model dkg_split_model_ms; 1 disables.
  * Decisions and outputs do not depend on it. */
 int dkg_ctx_set_split(dkg_ctx *ctx, int pieces);
+/* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
+ *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and
+ *                 compared with g s_ij + h s'_ij, as each receiver of the reference does;
+ *  1           -- committee verification by interpolation: the shares at receivers 1..t+1 fix the
+ *                 dealer's scalar polynomials F, F' (inverse Vandermonde); its commitments are
+ *                 tested once against g F_k + h F'_k, and each remaining pair reduces to comparing
+ *                 s_ij with F(j) (a deviating share is decided by its own group equation); rows
+ *                 whose commitments are not of that form are re-verified with mode 0.  Every
+ *                 decision equals mode 0's.  Needs all n shares of a dealer,
+ *                 so dkg_verify_receiver (one party's column) always uses its own path. */
+int dkg_ctx_set_verify_mode(dkg_ctx *ctx, int mode);
+/* Mode 1: rows of the last verification that were re-verified with difference tables. */
+size_t dkg_ctx_fallback_rows(const dkg_ctx *ctx);
 /* U used by the last ceremony's checks on this ctx. */
 int dkg_ctx_last_split(const dkg_ctx *ctx);
 /* The cost model's estimate (ms) of binomial + recombination for `columns` difference tables. */

@@ -759,6 +759,132 @@ def test_degree_split_n256_matches_unsplit(be, pieces):
     assert r.reconstruct == [int(i == 200) for i in range(n)]
 
 
+@pytest.fixture
+def interp(be):
+    be.set_verify_mode("interp")
+    yield be
+    be.set_verify_mode("group")
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("name", CEREMONIES + FAULTS + ["ceremony_n64_t31.json"])
+def test_interp_mode_goldens(interp, golden, name, overlap):
+    """Committee verification by interpolation (dkg_ctx_set_verify_mode 1) on every fixture: all
+    outputs bit-exact.  The fault fixtures exercise both of its branches: dealers whose
+    commitments are not g F + h F' (E := identity, A := generator, a flipped share among
+    receivers 1..t+1) are re-verified with difference tables; a flipped randomness share beyond
+    t+1 is decided by its own group equation."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    interp.env_init(t, n, CK)
+    interp.set_overlap(overlap)
+    try:
+        r = interp.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+    finally:
+        interp.set_overlap(True)
+    _check_ceremony(c, r, n)
+    expect_fallback = {"fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
+                       "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json",
+                       "fault_a_many_n10_t4.json"}
+    assert (interp.fallback_rows() > 0) == (name in expect_fallback), interp.fallback_rows()
+
+
+@pytest.mark.parametrize("j,which", [(12, "s"), (12, "s_prime"), (3, "s"), (15, "both")])
+def test_interp_mode_flipped_shares(be, golden, j, which):
+    """A single tampered share of an honest n=16, t=7 ceremony, beyond and within receivers 1..t+1:
+    group and interpolation modes give the same decision matrices, equal to the oracle's
+    per-pair MSM check (committee.rs:287-305, 532-541)."""
+    c = golden("ceremony_n16_t7.json")
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    s, sp = bytearray(H(c["s"])), bytearray(H(c["s_prime"]))
+    i = 5
+    for name, buf in (("s", s), ("s_prime", sp)):
+        if which in (name, "both"):
+            k = 32 * (i * n + j)
+            buf[k] ^= 1
+    out = {}
+    for mode in ("group", "interp"):
+        be.set_verify_mode(mode)
+        try:
+            r = be.ceremony_verify(H(c["E"]), H(c["A"]), bytes(s), bytes(sp), n, t)
+        finally:
+            be.set_verify_mode("group")
+        out[mode] = (r.dec2, r.dec4, r.mpk, r.final_share)
+    assert out["group"] == out["interp"]
+    acc2, _ = O.verify_pairs(n, t, 2, H(c["E"]), H(c["h"]), bytes(s), bytes(sp), 0, n, 0, n)
+    acc4, _ = O.verify_pairs(n, t, 4, H(c["A"]), H(c["h"]), bytes(s), bytes(sp), 0, n, 0, n)
+    assert list(out["group"][0]) == list(acc2)
+    d4 = list(out["group"][1])
+    assert all(d4[q] == acc4[q] for q in range(n * n) if d4[q] != 3)
+    assert out["group"][0][i * n + j] == REJECT
+
+
+@pytest.mark.parametrize("n,t", [(256, 127), (1024, 511)])
+def test_interp_mode_large(interp, n, t):
+    """Configs 2 and 3 end to end from device coefficients in interpolation mode: same decisions,
+    mpk and final shares as the difference-table mode, and no fallback on an honest ceremony."""
+    import torch
+
+    interp.env_init(t, n, CK)
+    N = t + 1
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(n * N * 32, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    interp.dealer_coefficients_device(b"\x33" * 32, 2, 1, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    r1 = interp.ceremony_device(ta.data_ptr(), tb.data_ptr(), n, t)
+    assert interp.fallback_rows() == 0
+    interp.set_verify_mode("group")
+    r0 = interp.ceremony_device(ta.data_ptr(), tb.data_ptr(), n, t)
+    assert r1.mpk == r0.mpk and r1.qualified == r0.qualified == [1] * n and r1.complaints2 == [0] * n
+
+
+def test_interp_mode_batch_and_shard(interp, golden):
+    """Batched ceremonies (config-5 path) and the dealer-sharded rows in interpolation mode."""
+    _ = golden
+    n, t, B = 64, 31, 6
+    N = t + 1
+    interp.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(b"\x44" * 32, 0, 0, n, t)
+    import torch
+
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(B * n * N * 32, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    interp.dealer_coefficients_device(b"\x44" * 32, 0, B, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    res1 = dkg_amd.ceremony_batch_device(interp, B, n, t, ta.data_ptr(), tb.data_ptr())
+    interp.set_verify_mode("group")
+    res0 = dkg_amd.ceremony_batch_device(interp, B, n, t, ta.data_ptr(), tb.data_ptr())
+    assert res1.mpk == res0.mpk and res1.n_qualified == res0.n_qualified == [n] * B
+    interp.set_verify_mode("interp")
+    # one rank of a 3-way shard on tampered broadcasts (fixture): equal to the group mode's rows
+    c = golden("fault_share_flip_n10_t4.json")
+    n, t = c["n"], c["t"]
+    N = t + 1
+    interp.env_init(t, n, CK)
+    E, A, s, sp = (H(c[k]) for k in ("E", "A", "s", "s_prime"))
+    d0, d1 = 3, 7
+    D = d1 - d0
+
+    def put(x):
+        return torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev)
+
+    outs = []
+    for mode in ("interp", "group"):
+        interp.set_verify_mode(mode)
+        o2 = torch.zeros(D * n, dtype=torch.uint8, device=dev)
+        o4 = torch.zeros_like(o2)
+        oA = torch.zeros(D * 32, dtype=torch.uint8, device=dev)
+        op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+        tE, tA = put(E[32 * N * d0:32 * N * d1]), put(A[32 * N * d0:32 * N * d1])
+        ts, tsp = put(s[32 * n * d0:32 * n * d1]), put(sp[32 * n * d0:32 * n * d1])
+        interp.ceremony_shard_verify_device(n, t, d0, d1, tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr(),
+                                            o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+        outs.append([bytes(x.cpu().numpy()) for x in (o2, o4, oA, op)])
+    assert outs[0] == outs[1]
+    assert dec_str(outs[0][0]) == c["dec2"][d0 * n:d1 * n]
+
+
 def test_ceremony_n4096_device(be):
     """BASELINE config 4 (n = 4096, t = 2047) end to end on one GPU from device-generated
     coefficients: every share of both rounds verifies and mpk == g * sum_i a_i0 (committee.rs:
