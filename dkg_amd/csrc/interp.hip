@@ -42,40 +42,105 @@ DKG_DEV bool sc_eq(const sc& a, const sc& b) {
   return d == 0;
 }
 
-// F[d][k] = sum_j W[k][j] s[d][j] (and F' from s'), j, k < N.  WT[j][k] = W[k][j] * 2^256 mod l
-// (Montgomery form: sc_mont_mul gives the canonical product).  Lanes = k (coalesced WT rows),
-// blockIdx.y = dealer (its shares are wave-uniform loads).
-__global__ __launch_bounds__(64) void k_interp(size_t N, size_t nrecv, const uint32_t* __restrict__ WT,
+// F[d][k] = sum_j W[k][j] s[d][j] (and F' from s'), j, k < N, as an exact integer dot product with
+// one reduction at the end: W[k][j] * 2^256 mod l is stored in 11 limbs of 24 bits (W24[j][a][k],
+// coalesced over k = lanes), the dealer's shares (wave-uniform) are split the same way, and the
+// 21 radix-2^24 columns accumulate in 64 bits (<= 11 * N * 2^48 < 2^64 for N <= 2^13): 121
+// v_mad_u64_u32 per term, no carries.  The sum (< N l^2) is then Montgomery-reduced (REDC by 2^256
+// cancels W's factor) and folded to canonical form.
+constexpr int L24 = 11;
+
+DKG_DEV void to_limbs24(uint32_t (&o)[L24], const uint32_t* w) {
+  uint32_t v[8];
+  ld_words8(v, w);
+#pragma unroll
+  for (int a = 0; a < L24; a++) {
+    const int bit = 24 * a, wi = bit >> 5, sh = bit & 31;
+    uint64_t x = (uint64_t)(wi < 8 ? v[wi] : 0u) | ((uint64_t)(wi + 1 < 8 ? v[wi + 1] : 0u) << 32);
+    o[a] = (uint32_t)(x >> sh) & 0xffffffu;
+  }
+}
+
+// acc (21 columns of radix 2^24, 64-bit) -> canonical scalar: repack into 17 words, REDC, fold
+DKG_DEV void limbs24_redc(sc& r, const uint64_t (&col)[2 * L24 - 1]) {
+  uint32_t t[18];
+#pragma unroll
+  for (int i = 0; i < 18; i++) t[i] = 0;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int c = 0; c < 2 * L24; c++) {  // value = sum_c col[c] 2^(24c); emit 24 bits per column
+    const uint64_t v = (c < 2 * L24 - 1 ? col[c] : 0ull) + carry;
+    const uint32_t limb = (uint32_t)v & 0xffffffu;
+    carry = v >> 24;
+    const int bit = 24 * c, wi = bit >> 5, sh = bit & 31;
+    t[wi] |= limb << sh;
+    if (sh > 8) t[wi + 1] |= limb >> (32 - sh);
+  }
+  // REDC: t <- (t + m l) / 2^256, 8 word steps (t < 2^515 -> result < 2^260)
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t m = t[i] * sc_const::LINV;
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      c += (uint64_t)m * sc_const::L[j] + t[i + j];
+      t[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+#pragma unroll
+    for (int j = i + 8; j < 18; j++) {
+      c += t[j];
+      t[j] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  uint32_t w9[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) w9[i] = t[8 + i];
+  sc_reduce9(r, w9);
+}
+
+__global__ __launch_bounds__(64) void k_interp(size_t N, size_t nrecv, const uint32_t* __restrict__ W24,
                                                const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
                                                uint32_t* __restrict__ F, uint32_t* __restrict__ Fp) {
   const size_t k = (size_t)blockIdx.x * 64 + threadIdx.x, d = blockIdx.y;
-  if (k >= N) return;
-  sc acc, accp, w, x, m;
-  sc_zero(acc);
-  sc_zero(accp);
+  const bool live = k < N;
+  const size_t kk = live ? k : 0;
+  uint64_t acc[2 * L24 - 1], accp[2 * L24 - 1];
+#pragma unroll
+  for (int c = 0; c < 2 * L24 - 1; c++) acc[c] = accp[c] = 0;
   const uint32_t* sd = s + 8 * d * nrecv;
-  const uint32_t* spd = sp ? sp + 8 * d * nrecv : nullptr;
+  const uint32_t* spd = sp ? sp + 8 * d * nrecv : sd;
 #pragma unroll 1
   for (size_t j = 0; j < N; j++) {
-    sc_load(w, WT + 8 * (j * N + k));
-    sc_load(x, sd + 8 * j);
-    sc_mont_mul(m, w, x);
-    sc_add(acc, acc, m);
-    if (spd) {
-      sc_load(x, spd + 8 * j);
-      sc_mont_mul(m, w, x);
-      sc_add(accp, accp, m);
-    }
+    uint32_t w[L24], x[L24], y[L24];
+#pragma unroll
+    for (int a = 0; a < L24; a++) w[a] = W24[(j * L24 + a) * N + kk];
+    to_limbs24(x, sd + 8 * j);
+    to_limbs24(y, spd + 8 * j);
+#pragma unroll
+    for (int a = 0; a < L24; a++)
+#pragma unroll
+      for (int b = 0; b < L24; b++) {
+        acc[a + b] += (uint64_t)w[a] * x[b];
+        accp[a + b] += (uint64_t)w[a] * y[b];
+      }
   }
-  st_words8(F + 8 * (d * N + k), acc.v);
-  if (Fp) st_words8(Fp + 8 * (d * N + k), accp.v);
+  if (!live) return;
+  sc r;
+  limbs24_redc(r, acc);
+  st_words8(F + 8 * (d * N + k), r.v);
+  if (Fp) {
+    limbs24_redc(r, accp);
+    st_words8(Fp + 8 * (d * N + k), r.v);
+  }
 }
 
-void interp(size_t D, size_t N, size_t nrecv, const uint32_t* WT, const uint32_t* s, const uint32_t* sp, uint32_t* F,
+void interp(size_t D, size_t N, size_t nrecv, const uint32_t* W24, const uint32_t* s, const uint32_t* sp, uint32_t* F,
             uint32_t* Fp, hipStream_t stream) {
   if (!D || !N) return;
-  hipLaunchKernelGGL(k_interp, dim3((unsigned)((N + 63) / 64), (unsigned)D), dim3(64), 0, stream, N, nrecv, WT, s, sp,
-                     F, Fp);
+  hipLaunchKernelGGL(k_interp, dim3((unsigned)((N + 63) / 64), (unsigned)D), dim3(64), 0, stream, N, nrecv, W24, s,
+                     sp, F, Fp);
 }
 
 // Coefficient test of (dealer d, k): okA = (g F_k == A_k), okE = (g F_k + h F'_k == E_k).

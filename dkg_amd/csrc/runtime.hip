@@ -439,10 +439,11 @@ void verify_rounds_group(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t deal
 }
 
 // ---- committee verification by interpolation (ctx->verify_mode == 1; interp.hip) ----
-// Inverse Vandermonde of the points 1..N mod l, transposed and in Montgomery form:
-// WT[j][k] = [x^k] L_j(x) * 2^256, L_j the Lagrange basis polynomial of point j+1.  Cached per N.
+// Inverse Vandermonde of the points 1..N mod l in Montgomery form, [x^k] L_j(x) * 2^256 (L_j the
+// Lagrange basis polynomial of point j+1), as 11 limbs of 24 bits: W24[j][a][k] (k_interp).
+// Cached per N.
 const uint32_t* vinv_table(dkg_ctx* ctx, size_t N) {
-  uint32_t* dev = buf<uint32_t>(ctx, "v.vinv", 32 * N * N);
+  uint32_t* dev = buf<uint32_t>(ctx, "v.vinv", 4 * 11 * N * N);
   if (ctx->vinv_N == N) return dev;
   using dkgh::Zl;
   const Zl zero = dkgh::zl_from_u64(0);
@@ -456,7 +457,7 @@ const uint32_t* vinv_table(dkg_ctx* ctx, size_t N) {
   uint8_t r256[33] = {0};
   r256[32] = 1;
   const Zl R = dkgh::zl_from_bytes_wide(r256, 33);  // 2^256 mod l
-  std::vector<uint8_t> host(32 * N * N);
+  std::vector<uint32_t> host(11 * N * N);
   std::vector<Zl> q(N);
   for (size_t j = 0; j < N; j++) {
     const Zl xj = dkgh::zl_from_u64(j + 1);
@@ -465,9 +466,16 @@ const uint32_t* vinv_table(dkg_ctx* ctx, size_t N) {
     Zl den = zero;  // Q_j(x_j) = prod_{m != j} (x_j - x_m)
     for (size_t k = N; k-- > 0;) den = dkgh::zl_add(dkgh::zl_mul(den, xj), q[k]);
     const Zl scale = dkgh::zl_mul(dkgh::zl_inv(den), R);
-    for (size_t k = 0; k < N; k++) dkgh::zl_to_bytes(&host[32 * (j * N + k)], dkgh::zl_mul(q[k], scale));
+    for (size_t k = 0; k < N; k++) {
+      uint8_t b[33] = {0};
+      dkgh::zl_to_bytes(b, dkgh::zl_mul(q[k], scale));
+      for (size_t a = 0; a < 11; a++) {  // bits 24a .. 24a+23
+        const size_t by = 3 * a;
+        host[(j * 11 + a) * N + k] = (uint32_t)b[by] | (uint32_t)b[by + 1] << 8 | (uint32_t)b[by + 2] << 16;
+      }
+    }
   }
-  h2d(ctx, dev, host.data(), host.size());
+  h2d(ctx, dev, host.data(), 4 * host.size());
   ctx->vinv_N = N;
   return dev;
 }
