@@ -396,6 +396,33 @@ def main():
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(n, t)
             out["gpu_vs_cpu"] = value / out["cpu_baseline"]["value"]
+    if ws > 1 and args.mode != "full" and args.verify == "group":
+        # per-GPU roofline of this rank's shard: one extra serialised pass (every rank joins its
+        # collectives); the rank's work is its D dealers' share of the closed form
+        be.set_streams(1)
+        sc.run(ta.data_ptr(), tb.data_ptr())
+        torch.cuda.synchronize()
+        be.set_streams(args.streams)
+        ph = be.phase_times("r24" if not args.no_overlap else "r2")
+        U = be.last_split()
+        D = ((rank + 1) * n) // ws - (rank * n) // ws
+        work = fused_valu(n, t, U)
+        rl = {}
+        for k in ("binomial", "stepping", "combine", "check"):
+            ms = ph.get(k, 0.0)
+            if ms > 0:
+                w = work[k] * D / n
+                rl[k] = {"ms_per_pass": round(ms, 3), "valu_instr": w, "achieved_Tops": w / (ms / 1e3) / 1e12,
+                         "frac": w / (ms / 1e3) / INT32_PEAK}
+        out["config"]["degree_split"] = U
+        if rl:
+            dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
+            ach = rl[dom]["achieved_Tops"]
+            out["roofline"] = {"bound": "valu-int32", "kernel": dom, "achieved": ach, "peak": INT32_PEAK / 1e12,
+                               "unit": "T int32 VALU instr/s", "frac": ach / (INT32_PEAK / 1e12), "traffic": None,
+                               "work": f"rank 0's shard ({D} dealers): {rl[dom]['valu_instr']:.4g} VALU instructions "
+                                       f"per pass (closed form); device time in a serialised pass",
+                               "all_kernels": rl}
     if rank == 0:
         print(json.dumps(out), flush=True)
     be.close()
