@@ -31,8 +31,8 @@ def max_rows(world_size: int, n: int) -> int:
 
 @dataclass
 class Decisions:
-    dec2: np.ndarray          # [n][n] uint8
-    dec4: np.ndarray          # [n][n] uint8, SKIPPED rows for disqualified dealers
+    dec2: np.ndarray          # [n][n] uint8 (a torch tensor on the exchange device when combined there)
+    dec4: np.ndarray          # [n][n] uint8, SKIPPED rows for disqualified dealers (idem)
     qualified: np.ndarray     # [n] uint8
     complaints2: np.ndarray   # [n] int32, complaints raised by receiver j
     r2_error: np.ndarray      # [n] uint8, receiver j saw more than t complaints
@@ -42,7 +42,36 @@ class Decisions:
     phase4_error: bool        # qualified minus reconstructable <= t: Phase4::proceed fails (:673-677)
 
 
-def combine_decisions(dec2: np.ndarray, dec4: np.ndarray, n: int, t: int) -> Decisions:
+def combine_decisions(dec2, dec4, n: int, t: int) -> Decisions:
+    """See _combine_np; torch tensors (e.g. the gathered rows, still on the GPU) are combined on
+    their device and only the per-party vectors come back to the host (dec2 / dec4 stay tensors)."""
+    if not isinstance(dec2, np.ndarray) and hasattr(dec2, "device"):
+        return _combine_torch(dec2, dec4, n, t)
+    return _combine_np(dec2, dec4, n, t)
+
+
+def _combine_torch(dec2, dec4, n: int, t: int) -> Decisions:
+    import torch
+
+    d2 = dec2.reshape(n, n)
+    d4 = dec4.reshape(n, n).clone()
+    rej2 = d2 == REJECT
+    qualified = ~(rej2 | (d2 == MISSING)).any(dim=1)
+    complaints = rej2.sum(dim=0, dtype=torch.int32)
+    off = ~torch.eye(n, dtype=torch.bool, device=d2.device)
+    d4[(~qualified)[:, None] & off] = SKIPPED
+    recon = ((d4 == REJECT) & off & qualified[:, None]).any(dim=1)
+    honest = qualified & ~recon
+    honest4 = 1 + ((d4 == ACCEPT) & off & qualified[:, None]).sum(dim=0)
+    small = torch.stack([qualified.to(torch.int32), complaints, (complaints > t).to(torch.int32), recon.to(torch.int32),
+                         (honest4 < t + 1).to(torch.int32), honest.to(torch.int32)]).cpu().numpy()
+    q, c, r2e, rc, r4e, h = small
+    hon = h.astype(np.uint8)
+    return Decisions(d2, d4, q.astype(np.uint8), c.astype(np.int32), r2e.astype(np.uint8), rc.astype(np.uint8),
+                     r4e.astype(np.uint8), hon, bool(int(hon.sum()) <= t))
+
+
+def _combine_np(dec2: np.ndarray, dec4: np.ndarray, n: int, t: int) -> Decisions:
     """Host combine of the gathered decision matrices, the same rules as the single-GPU driver:
     a REJECT by receiver j is a complaint of j against dealer i (committee.rs:311-316) and a valid
     complaint disqualifies i for everyone (:370-398); more than t complaints raise
@@ -146,7 +175,7 @@ class ShardedCeremony:
     def _finish(self, ms: float, finalise: bool) -> ShardResult:
         n, t = self.n, self.t
         dec2, dec4, A0, parts = self.exchange()
-        dec = combine_decisions(dec2.cpu().numpy(), dec4.cpu().numpy(), n, t)
+        dec = combine_decisions(dec2, dec4, n, t)
         fs = mpk = None
         if finalise:
             torch = self.torch

@@ -118,3 +118,22 @@ def test_combine_single_process(golden):
         assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
         assert d.phase4_error == c["phase4_error"]
         assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
+
+
+def test_combine_torch_matches_numpy(golden):
+    """The device-side combine (torch tensors, as ShardedCeremony hands over the gathered rows)
+    equals the numpy combine on every golden ceremony."""
+    import torch
+
+    from dkg_amd.distributed import combine_decisions
+
+    for name in NAMES + ["ceremony_n64_t31.json"]:
+        c = golden(name)
+        n, t = c["n"], c["t"]
+        dec2 = np.frombuffer(bytes(int(x) for x in c["dec2"]), dtype=np.uint8).copy()
+        dec4 = np.frombuffer(bytes(1 if x == "3" else int(x) for x in c["dec4"]), dtype=np.uint8).copy()
+        a = combine_decisions(dec2, dec4, n, t)
+        b = combine_decisions(torch.from_numpy(dec2), torch.from_numpy(dec4), n, t)
+        for f in ("qualified", "complaints2", "r2_error", "reconstruct", "r4_error", "honest"):
+            assert getattr(a, f).tolist() == getattr(b, f).tolist(), (name, f)
+        assert a.dec4.reshape(-1).tolist() == b.dec4.reshape(-1).tolist() and a.phase4_error == b.phase4_error
