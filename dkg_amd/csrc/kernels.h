@@ -105,7 +105,7 @@ void from_uniform(const uint32_t* in16, uint32_t* out, hipStream_t stream);
 
 // Generic batched MSM (trait boundary): out[b] = sum_k scalars[b][k] * points[b][k];
 // points given decoded SoA [40][B*N] (element b*N + k), scalars [B*N][8].
-void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts, size_t stride,
+void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts, size_t stride, uint32_t* tab,
                uint32_t* out_ext, hipStream_t stream);
 // Fixed-base batch: out = s * base via comb table; out SoA [40][count]
 void fixed_base(size_t count, const uint32_t* scalars, const uint32_t* tab, uint32_t* out_ext,

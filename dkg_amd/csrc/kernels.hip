@@ -893,59 +893,82 @@ void from_uniform(const uint32_t* in16, uint32_t* out, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------ generic MSM / fixed base
-// One workgroup per MSM; each lane accumulates s_k P_k over a strided subset of terms with a
-// uniform double-and-add (the addend is selected, never branched on), then a tree reduction.
+// PrimeGroupElement::vartime_multiscalar_multiplication (traits.rs:234-237) for B independent MSMs
+// of N terms: Straus with 4-bit windows split over the workgroup.  k_msm_tables stores d*P_k,
+// d = 1..15, of every term (cached form, 15 x 40 words); in k_msm thread q of an MSM keeps its own
+// accumulator over the terms k = q, q + T, ...: per window 4 doublings and one table addition per
+// term, then a tree reduction of the T partial sums.  T = min(256, N up to a power of two >= 64).
+__global__ __launch_bounds__(256) void k_msm_tables(size_t count, const uint32_t* __restrict__ pts, size_t stride,
+                                                  uint32_t* __restrict__ tab) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  ge_p3 p, acc;
+  pt_load(p, pts, stride, e);
+  ge_cached pc;
+  ge_to_cached(pc, p);
+  acc = p;
+  uint4* out = reinterpret_cast<uint4*>(tab + e * 15 * PT_WORDS);
+#pragma unroll 1
+  for (int d = 1; d <= 15; d++) {
+    if (d > 1) ge_add(acc, acc, pc);
+    ge_cached c;
+    ge_to_cached(c, acc);
+    const uint4* c4 = reinterpret_cast<const uint4*>(&c);
+#pragma unroll
+    for (int w = 0; w < PT_WORDS / 4; w++) out[(d - 1) * (PT_WORDS / 4) + w] = c4[w];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_msm(size_t N, const uint32_t* __restrict__ scalars,
-                                             const uint32_t* __restrict__ pts, size_t stride,
-                                             uint32_t* __restrict__ out, size_t ostride) {
+                                             const uint32_t* __restrict__ tab, uint32_t* __restrict__ out,
+                                             size_t ostride) {
   __shared__ uint32_t red[256][PT_WORDS];
   const size_t b = blockIdx.x;
+  const int T = blockDim.x, q = threadIdx.x;
   ge_p3 acc;
   ge_identity(acc);
-  for (size_t k = threadIdx.x; k < N; k += blockDim.x) {
-    ge_p3 p, q;
-    pt_load(p, pts, stride, b * N + k);
-    sc s;
-    sc_load(s, scalars + 8 * (b * N + k));
-    ge_cached pc, idc;
-    ge_to_cached(pc, p);
-    cached_identity(idc);
-    ge_identity(q);
-    for (int bit = 252; bit >= 0; bit--) {
-      ge_dbl<true>(q, q);
-      const bool on = (s.v[bit >> 5] >> (bit & 31)) & 1u;
-      ge_cached sel;
-      uint32_t* sw = reinterpret_cast<uint32_t*>(&sel);
-      const uint32_t* pw = reinterpret_cast<const uint32_t*>(&pc);
-      const uint32_t* iw = reinterpret_cast<const uint32_t*>(&idc);
+  if ((size_t)q < N) {
+#pragma unroll 1
+    for (int w = 63; w >= 0; w--) {
+      if (w != 63) {
+#pragma unroll 1
+        for (int i = 0; i < 4; i++) ge_dbl_lean(acc, acc, i == 3);
+      }
+#pragma unroll 1
+      for (size_t k = q; k < N; k += T) {
+        const uint32_t word = scalars[8 * (b * N + k) + (w >> 3)];
+        const uint32_t nib = (word >> (4 * (w & 7))) & 15u;
+        if (nib) {
+          ge_cached c;
+          const uint4* src = reinterpret_cast<const uint4*>(tab + ((b * N + k) * 15 + nib - 1) * PT_WORDS);
+          uint4* c4 = reinterpret_cast<uint4*>(&c);
 #pragma unroll
-      for (int w = 0; w < PT_WORDS; w++) sw[w] = on ? pw[w] : iw[w];
-      ge_add(q, q, sel);
+          for (int x = 0; x < PT_WORDS / 4; x++) c4[x] = src[x];
+          ge_add(acc, acc, c);
+        }
+      }
     }
-    ge_cached qc;
-    ge_to_cached(qc, q);
-    ge_add(acc, acc, qc);
   }
   uint32_t* aw = reinterpret_cast<uint32_t*>(&acc);
-  for (int w = 0; w < PT_WORDS; w++) red[threadIdx.x][w] = aw[w];
+  for (int w = 0; w < PT_WORDS; w++) red[q][w] = aw[w];
   __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) {
+  for (int h = T / 2; h > 0; h >>= 1) {
+    if (q < h) {
       ge_p3 x, y;
       uint32_t* xw = reinterpret_cast<uint32_t*>(&x);
       uint32_t* yw = reinterpret_cast<uint32_t*>(&y);
       for (int w = 0; w < PT_WORDS; w++) {
-        xw[w] = red[threadIdx.x][w];
-        yw[w] = red[threadIdx.x + h][w];
+        xw[w] = red[q][w];
+        yw[w] = red[q + h][w];
       }
       ge_cached yc;
       ge_to_cached(yc, y);
       ge_add(x, x, yc);
-      for (int w = 0; w < PT_WORDS; w++) red[threadIdx.x][w] = xw[w];
+      for (int w = 0; w < PT_WORDS; w++) red[q][w] = xw[w];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (q == 0) {
     ge_p3 r;
     uint32_t* rw = reinterpret_cast<uint32_t*>(&r);
     for (int w = 0; w < PT_WORDS; w++) rw[w] = red[0][w];
@@ -953,10 +976,17 @@ __global__ __launch_bounds__(256) void k_msm(size_t N, const uint32_t* __restric
   }
 }
 
-void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts, size_t stride, uint32_t* out_ext,
-               hipStream_t stream) {
+// tab: scratch of B * N * 15 * 40 words
+void msm_batch(size_t B, size_t N, const uint32_t* scalars, const uint32_t* pts, size_t stride, uint32_t* tab,
+               uint32_t* out_ext, hipStream_t stream) {
   if (!B) return;
-  hipLaunchKernelGGL(k_msm, dim3((unsigned)B), dim3(256), 0, stream, N, scalars, pts, stride, out_ext, B);
+  const size_t count = B * N;
+  if (count)
+    hipLaunchKernelGGL(k_msm_tables, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, pts, stride,
+                       tab);
+  size_t T = 64;  // a power of two (tree reduction), 64..256
+  while (T < N && T < 256) T <<= 1;
+  hipLaunchKernelGGL(k_msm, dim3((unsigned)B), dim3((unsigned)T), 0, stream, N, scalars, tab, out_ext, B);
 }
 
 __global__ __launch_bounds__(256, 4) void k_fixed_base(size_t count, const uint32_t* __restrict__ scalars,

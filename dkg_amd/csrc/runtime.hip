@@ -1002,7 +1002,8 @@ void msm_host(dkg_ctx* ctx, size_t B, size_t N, const uint8_t* scalars, const ui
   dkgk::decode_points(pc, B * N, pe, B * N, pok, ctx->stream);
   uint32_t* oe = buf<uint32_t>(ctx, "cp_oe", PTB * B);
   uint32_t* oc = buf<uint32_t>(ctx, "cp_oc", 32 * B);
-  dkgk::msm_batch(B, N, sc, pe, B * N, oe, ctx->stream);
+  uint32_t* mt = buf<uint32_t>(ctx, "msm_tab", 4 * 15 * PT_WORDS_H * B * N);
+  dkgk::msm_batch(B, N, sc, pe, B * N, mt, oe, ctx->stream);
   dkgk::encode_points(oe, B, B, oc, ctx->stream);
   check_launch(ctx);
   std::vector<uint8_t> okh(B * N);
@@ -1213,7 +1214,8 @@ int dkg_msm_batch(dkg_ctx* ctx, size_t B, size_t N, const uint8_t* scalars, cons
     dkgk::decode_points(pc, B * N, pe, B * N, ok, ctx->stream);
     uint32_t* oe = buf<uint32_t>(ctx, "msm_oe", PTB * B);
     uint32_t* oc = buf<uint32_t>(ctx, "msm_oc", 32 * B);
-    dkgk::msm_batch(B, N, sc, pe, B * N, oe, ctx->stream);
+    uint32_t* mt = buf<uint32_t>(ctx, "msm_tab", 4 * 15 * PT_WORDS_H * B * N);
+  dkgk::msm_batch(B, N, sc, pe, B * N, mt, oe, ctx->stream);
     dkgk::encode_points(oe, B, B, oc, ctx->stream);
     check_launch(ctx);
     std::vector<uint8_t> okh(B * N);
