@@ -219,7 +219,10 @@ __global__ __launch_bounds__(256) void k_share_eval(size_t D, size_t n, size_t N
                                                     uint32_t* __restrict__ sp) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= D * n) return;
-  const size_t i = e / n, j = e % n;
+  size_t i = e / n;
+  const size_t j = e % n;
+  // n % 64 == 0: a wave's lanes share the dealer, so its coefficients are scalar (broadcast) loads
+  if (n % 64 == 0) i = (size_t)__builtin_amdgcn_readfirstlane((uint32_t)i);
   const uint32_t x = (uint32_t)(j + 1);
   const uint32_t* ai = a + 8 * i * N;
   const uint32_t* bi = b + 8 * i * N;
