@@ -31,8 +31,6 @@ void fill_identity(size_t S, uint32_t* out, hipStream_t stream);
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
                 const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
                 const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream);
-// identity points in dealer columns [V, npad) of a position-major table [40][N][npad]
-void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream);
 // extended SoA -> encodings [count][8]
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream);
 // comb tables of the decoded points ext[.., e0 + c], c < count, into tab + c * 15360 (30 x 512 words each)

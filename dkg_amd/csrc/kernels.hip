@@ -85,17 +85,6 @@ void gather_points(const uint32_t* src, size_t sstride, size_t step, size_t k0, 
                      count, dst, dstride);
 }
 
-// Identity points in dealer columns [V, npad) of a position-major table [40][N][npad].
-__global__ void k_fill_identity(size_t N, size_t npad, size_t V, uint32_t* __restrict__ out) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = k * (npad - V) + c
-  const size_t w = npad - V;
-  if (e >= N * w) return;
-  const size_t k = e / w, c = e % w;
-  ge_p3 id;
-  ge_identity(id);
-  pt_store(out, N * npad, k * npad + V + c, id);
-}
-
 __global__ __launch_bounds__(256) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
                                                 size_t count, uint32_t* __restrict__ comp) {
   size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,12 +110,6 @@ void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad
   if (!L) L = N;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, comp, count, out,
                      L * npad, ok, N, npad, (uint32_t)nseg, (uint32_t)seg, L, pstride);
-}
-
-void fill_identity_columns(size_t N, size_t npad, size_t V, uint32_t* out, hipStream_t stream) {
-  const size_t tot = N * (npad - V);
-  if (!tot) return;
-  hipLaunchKernelGGL(k_fill_identity, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, N, npad, V, out);
 }
 
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream) {
