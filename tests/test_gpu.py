@@ -885,6 +885,74 @@ def test_interp_mode_batch_and_shard(interp, golden):
     assert dec_str(outs[0][0]) == c["dec2"][d0 * n:d1 * n]
 
 
+@pytest.mark.parametrize("seed", range(40))
+def test_random_ceremonies_vs_oracle(be, seed):
+    """Random committees (3 <= n < 48, every valid t) with random faults -- tampered shares or
+    randomness, a replaced E or A coefficient, an undecodable commitment -- under a random schedule
+    (verify mode, degree split, fused or protocol order): the decisions equal the oracle's per-pair
+    MSM checks (committee.rs:287-305, 532-548) and the final shares and mpk equal the reference's
+    rules recomputed here (committee.rs:454-462, 726-805)."""
+    rng = random.Random(7000 + seed)
+    n = rng.randrange(3, 48)
+    t = rng.randrange(0, (n + 1) // 2)
+    N = t + 1
+    h = be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes(rng.randrange(256) for _ in range(32)), seed, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in O.share_gen(n, n, t, a, b, h))
+    faults = []
+    for _ in range(rng.randrange(0, 4)):
+        kind = rng.choice(["s", "sp", "E", "A", "Ebad"])
+        i = rng.randrange(n)
+        if kind in ("s", "sp"):
+            j = rng.choice([x for x in range(n) if x != i])
+            buf = s if kind == "s" else sp
+            v = (int.from_bytes(buf[32 * (i * n + j):32 * (i * n + j) + 32], "little") + 1) % L
+            buf[32 * (i * n + j):32 * (i * n + j) + 32] = v.to_bytes(32, "little")
+        elif kind in ("E", "A"):
+            k = rng.randrange(N)
+            buf = E if kind == "E" else A
+            buf[32 * (i * N + k):32 * (i * N + k) + 32] = O.base_mul(rng.randrange(1, L).to_bytes(32, "little"))
+        else:
+            k = rng.randrange(N)
+            E[32 * (i * N + k):32 * (i * N + k) + 32] = b"\xff" * 32
+        faults.append((kind, i))
+    mode, split, overlap = rng.choice(["group", "interp"]), rng.choice([0, 1, 2, 3]), rng.choice([True, False])
+    be.set_verify_mode(mode)
+    be.set_split(min(split, N))
+    be.set_overlap(overlap)
+    try:
+        r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+    finally:
+        be.set_verify_mode("group")
+        be.set_split(0)
+        be.set_overlap(True)
+    ctx = (n, t, faults, mode, split, overlap)
+    acc2, _ = O.verify_pairs(n, t, 2, bytes(E), h, bytes(s), bytes(sp), 0, n, 0, n)
+    acc4, _ = O.verify_pairs(n, t, 4, bytes(A), h, bytes(s), None, 0, n, 0, n)
+    assert list(r.dec2) == list(acc2), ctx
+    qualified = [int(all(r.dec2[i * n + j] in (ACCEPT, SELF) for j in range(n))) for i in range(n)]
+    assert r.qualified == qualified, ctx
+    for q in range(n * n):
+        i, j = divmod(q, n)
+        if i == j:
+            assert r.dec4[q] == SELF
+        elif not qualified[i]:
+            assert r.dec4[q] == 3, ctx  # SKIPPED
+        else:
+            assert r.dec4[q] == acc4[q], ctx
+    recon = [int(qualified[i] and any(r.dec4[i * n + j] == REJECT for j in range(n) if j != i)) for i in range(n)]
+    assert r.reconstruct == recon, ctx
+    fs = b"".join((sum(int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+                       for i in range(n) if qualified[i]) % L).to_bytes(32, "little") for j in range(n))
+    assert r.final_share == fs, ctx
+    # mpk: A_i0 of the honest dealers + g * (secrets of the reconstructed ones)
+    honest = [i for i in range(n) if qualified[i] and not recon[i]]
+    sec = sum(int.from_bytes(a[32 * N * i:32 * N * i + 32], "little") for i in range(n) if recon[i]) % L
+    pts = b"".join(bytes(A[32 * N * i:32 * N * i + 32]) for i in honest) + O.base_mul((1).to_bytes(32, "little"))
+    scs = b"".join((1).to_bytes(32, "little") for _ in honest) + sec.to_bytes(32, "little")
+    assert r.mpk == O.msm(scs, pts), ctx
+
+
 def test_ceremony_n4096_device(be):
     """BASELINE config 4 (n = 4096, t = 2047) end to end on one GPU from device-generated
     coefficients: every share of both rounds verifies and mpk == g * sum_i a_i0 (committee.rs:
