@@ -204,11 +204,23 @@ __global__ __launch_bounds__(256, 4) void k_interp_decide(size_t D, size_t nrecv
     const uint32_t x = (uint32_t)(j + 1);
     const uint32_t* Fd = F + 8 * d * N;
     const uint32_t* Fpd = Fp + 8 * d * N;
-    sc c;
+    sc c, c0;
     sc_load(fx, Fd + 8 * (N - 1));
     sc_load(fpx, Fpd + 8 * (N - 1));
+    size_t k = N - 1;
+    if (x < 2048) {  // Horner (Polynomial::evaluate's value, polynomial.rs:68-74), two steps per reduction
 #pragma unroll 1
-    for (size_t k = N - 1; k-- > 0;) {  // Horner: the value of Polynomial::evaluate (polynomial.rs:68-74)
+      for (; k >= 2; k -= 2) {
+        sc_load(c, Fd + 8 * (k - 1));
+        sc_load(c0, Fd + 8 * (k - 2));
+        sc_horner2(fx, fx, x, c, c0);
+        sc_load(c, Fpd + 8 * (k - 1));
+        sc_load(c0, Fpd + 8 * (k - 2));
+        sc_horner2(fpx, fpx, x, c, c0);
+      }
+    }
+#pragma unroll 1
+    while (k-- > 0) {
       sc_load(c, Fd + 8 * k);
       sc_mul_small_add(fx, fx, x, c);
       sc_load(c, Fpd + 8 * k);

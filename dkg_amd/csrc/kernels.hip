@@ -212,7 +212,19 @@ __global__ __launch_bounds__(256) void k_share_eval(size_t D, size_t n, size_t N
   sc fa, fb, c;
   sc_load(fa, ai + 8 * (N - 1));
   sc_load(fb, bi + 8 * (N - 1));
-  for (size_t k = N - 1; k-- > 0;) {
+  size_t k = N - 1;
+  if (x < 2048) {  // two Horner steps per reduction (sc_horner2)
+    sc c0;
+    for (; k >= 2; k -= 2) {
+      sc_load(c, ai + 8 * (k - 1));
+      sc_load(c0, ai + 8 * (k - 2));
+      sc_horner2(fa, fa, x, c, c0);
+      sc_load(c, bi + 8 * (k - 1));
+      sc_load(c0, bi + 8 * (k - 2));
+      sc_horner2(fb, fb, x, c, c0);
+    }
+  }
+  while (k-- > 0) {
     sc_load(c, ai + 8 * k);
     sc_mul_small_add(fa, fa, x, c);
     sc_load(c, bi + 8 * k);

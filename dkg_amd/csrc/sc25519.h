@@ -90,6 +90,28 @@ DKG_DEV void sc_mul_small_add(sc& r, const sc& a, uint32_t x, const sc& c) {
   sc_reduce9(r, w);
 }
 
+// Horner with one reduction per two steps: r = ((a x + c1) x + c0) mod l for a, c1, c0 < l and
+// x < 2^11 -- the unreduced 9-word intermediate (< 2^265) times x stays below 2^277, sc_reduce9's range.
+DKG_DEV void sc_horner2(sc& r, const sc& a, uint32_t x, const sc& c1, const sc& c0) {
+  uint32_t w[9];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    acc += (uint64_t)a.v[i] * x + c1.v[i];
+    w[i] = (uint32_t)acc;
+    acc >>= 32;
+  }
+  w[8] = (uint32_t)acc;
+  acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc += (uint64_t)w[i] * x + (i < 8 ? c0.v[i] : 0u);
+    w[i] = (uint32_t)acc;
+    acc >>= 32;
+  }
+  sc_reduce9(r, w);
+}
+
 // r = a + b mod l
 DKG_DEV void sc_add(sc& r, const sc& a, const sc& b) {
   uint32_t w[9];
