@@ -1043,22 +1043,39 @@ void reduce_scalars(size_t count, const uint32_t* in, uint32_t* out, hipStream_t
 }
 
 // Group g (blockIdx.y) of D dealers: out[g][j] = sum over dealers i of group g with mask of s[g][i][j].
-__global__ void k_sum_shares(size_t D, size_t n, const uint32_t* __restrict__ s, const uint8_t* __restrict__ mask,
-                             uint32_t* __restrict__ out) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+// 256-thread blocks of 64 receivers x 4 dealer slices when D is large (one ceremony: the dealer
+// loop is the latency), one thread per receiver otherwise (batches: many groups already).
+template <int SLICES>
+__global__ __launch_bounds__(64 * SLICES) void k_sum_shares(size_t D, size_t n, const uint32_t* __restrict__ s,
+                                                          const uint8_t* __restrict__ mask,
+                                                          uint32_t* __restrict__ out) {
+  __shared__ uint32_t part[SLICES > 1 ? SLICES * 8 * 64 : 1];
+  const int lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const size_t j = (size_t)blockIdx.x * 64 + lane;
   const size_t g = blockIdx.y;
   s += g * D * n * 8;
   mask += g * D;
   out += g * n * 8;
   sc acc, x;
   sc_zero(acc);
-  for (size_t i = 0; i < D; i++) {
-    if (!mask[i]) continue;
-    sc_load(x, s + 8 * (i * n + j));
-    sc_add(acc, acc, x);
+  if (j < n)
+    for (size_t i = slice; i < D; i += SLICES) {
+      if (!mask[i]) continue;
+      sc_load(x, s + 8 * (i * n + j));
+      sc_add(acc, acc, x);
+    }
+  if (SLICES > 1) {
+#pragma unroll
+    for (int w = 0; w < 8; w++) part[(slice * 8 + w) * 64 + lane] = acc.v[w];
+    __syncthreads();
+    if (slice != 0) return;
+    for (int q = 1; q < SLICES; q++) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) x.v[w] = part[(q * 8 + w) * 64 + lane];
+      sc_add(acc, acc, x);
+    }
   }
-  st_words8(out + 8 * j, acc.v);
+  if (j < n) st_words8(out + 8 * j, acc.v);
 }
 
 void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint32_t* out, hipStream_t stream,
@@ -1066,8 +1083,13 @@ void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint
   if (!n) return;
   for (size_t g0 = 0; g0 < groups; g0 += 65535) {  // grid.y limit
     const size_t gc = groups - g0 < 65535 ? groups - g0 : 65535;
-    hipLaunchKernelGGL(k_sum_shares, dim3((unsigned)((n + 255) / 256), (unsigned)gc), dim3(256), 0, stream, D, n,
-                       s + g0 * D * n * 8, mask + g0 * D, out + g0 * n * 8);
+    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)gc);
+    if (gc * ((n + 63) / 64) >= 1024)
+      hipLaunchKernelGGL(k_sum_shares<1>, grid, dim3(64), 0, stream, D, n, s + g0 * D * n * 8, mask + g0 * D,
+                         out + g0 * n * 8);
+    else
+      hipLaunchKernelGGL(k_sum_shares<16>, grid, dim3(1024), 0, stream, D, n, s + g0 * D * n * 8, mask + g0 * D,
+                         out + g0 * n * 8);
   }
 }
 
