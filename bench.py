@@ -38,6 +38,39 @@ VALU = {"fe_mul": 144, "ge_add": 1318, "ge_add_signed": 1361, "ge_dbl_t": 1158, 
         "comb_window": 1272, "comb8_window": 1245, "ge_to_cached": 197, "eq": 4 * 144 + 120}
 
 
+PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def algorithmic_bytes(kernel, n, t, U):
+    """(bytes per launch, launches per pass) of a check-pipeline kernel in the serialised fused pass:
+    columns = 2n (E and A rows) x U pieces of L = ceil((t+1)/U) positions (DESIGN.md sections 3-4)."""
+    L = -(-(t + 1) // U)
+    cols = 2 * n * U
+    if kernel == "binomial":  # step r: position 0 copies C_k (load+store), positions 1..r load 2, store 1
+        per_pass = sum(cols * (2 * PT_BYTES + r * 3 * PT_BYTES) for r in range(1, L))
+        return per_pass / max(L - 1, 1), max(L - 1, 1)
+    if kernel == "stepping":  # the table once, then D_0 out per receiver (one launch while L <= 512)
+        nblk = -(-L // 512)
+        return cols * (L + n) * PT_BYTES / nblk, nblk
+    if kernel == "combine":  # U piece values in, P(j) out per (column, receiver)
+        return 2 * n * n * (U + 1) * PT_BYTES, 1
+    return None, None
+
+
+def pmc_traffic(kernel, n, t, U):
+    """HBM-side bytes per launch of `kernel` from the committed PMC passes (tools/profile.sh ->
+    tools/pmc_summary.py), when they were taken on this workload; else None."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if (doc.get("n"), doc.get("t"), doc.get("split")) != (n, t, U) or kernel not in doc.get("kernels", {}):
+        return None
+    return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -393,6 +426,18 @@ def main():
                                "work": f"{work[dom]:.4g} VALU instructions per pass over {what} (closed form); "
                                        f"device time of the kernel's launches (HIP events) in a serialised pass",
                                "all_kernels": rl}
+            alg, launches = algorithmic_bytes(dom, n, t, U) if ov else (None, None)
+            pmc = pmc_traffic(dom, n, t, U) if ov else None
+            if alg is not None:
+                ms_launch = rl[dom]["ms_per_pass"] / launches
+                out["roofline"]["algorithmic_bytes_per_launch"] = alg
+                out["roofline"]["algorithmic_GBps"] = alg / (ms_launch / 1e3) / 1e9
+            if pmc is not None:
+                out["roofline"]["traffic"] = pmc[0]
+                out["roofline"]["traffic_unit"] = "HBM-side bytes per launch (average)"
+                out["roofline"]["traffic_source"] = pmc[1]
+                if alg:
+                    out["roofline"]["traffic_over_algorithmic"] = pmc[0] / alg
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(n, t)
             out["gpu_vs_cpu"] = value / out["cpu_baseline"]["value"]

@@ -29,7 +29,7 @@ void fill_identity(size_t S, uint32_t* out, hipStream_t stream);
 // [dealer0, dealer0 + ndealers) of this call, s / sp / dec2 / dec4 indexed dealer * nrecv + j from
 // their bases, self = (dealer + dealer_base) mod nmod == j.
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
-                const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
+                const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
                 const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream);
 // extended SoA -> encodings [count][8]
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream);
@@ -56,8 +56,8 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 // pieces > 1: the same for the columns [u * pstride, u * pstride + width) of every piece u
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
                    hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
-// K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), SoA [40][rstride]
-// (element i*nrecv + j).  stream_a / stream_b: scratch for the inter-block boundary streams, each
+// K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), point-major (AoS)
+// [i*nrecv + j][40] (pt_store_aos).  stream_a / stream_b: scratch for the inter-block boundary streams, each
 // >= ndealers*nrecv*160 B (unused when N <= 512).
 // How k_stepping covers an N-position table: nblk blocks of P positions on bs lanes (nblk > 1), or
 // `per` tables of P = N lanes each per bs-lane workgroup; maxbs = the LDS variant (256 or 512).
@@ -65,24 +65,24 @@ struct StepShape {
   size_t nblk, P, per, bs, maxbs;
 };
 StepShape stepping_shape(size_t N);
-void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
+void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
 // Degree-split recombination: R[c][j] = sum_u y_j^u R[u * pstride + c][j] (pairwise Horner in y^2
 // with joint NAF chains; digits [n][2][256] = NAF of y_j and y_j^2, top [n][2])
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
-             uint32_t* R, size_t rstride, hipStream_t stream);
+             uint32_t* R, hipStream_t stream);
 // K3c: decision[i][j] = (g s_ij + h s'_ij == R[i][j]) (round 2) or (g s_ij == R[i][j]) (round 4);
 // dealer_ok[i] == 0 forces 0; self ((i + dealer_base) mod nmod == j + recv_base, nmod = parties per
 // ceremony, so batched ceremonies stacked dealer-wise work too) gives 2.
-// R: SoA [40][rstride], element i*nrecv + j.
+// R: point-major (AoS) [i*nrecv + j][40].
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
-           const uint32_t* s, const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g,
+           const uint32_t* s, const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g,
            const uint32_t* tab_h, const uint8_t* dealer_ok, uint8_t* decision, hipStream_t stream);
 // dok[column of dealer i of segment seg] &= extra[i] (verify_device's interleaved column layout)
 void and_dealer_mask(size_t D, int nseg, int seg, const uint8_t* extra, uint8_t* dok, hipStream_t stream);
 // per-dealer validity: dealer_ok[i] = AND of point_ok over its N commitments (dealer-major [D][N])
 void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream);
-// Horner in the exponent for receivers x0 .. x0+nrecv-1 (1-based indices): R [40][ndealers*nrecv]
+// Horner in the exponent for receivers x0 .. x0+nrecv-1 (1-based indices): R point-major [ndealers*nrecv][40]
 void horner(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t x0, size_t nrecv, uint32_t* R,
             hipStream_t stream);
 // out column col + g (SoA, stride ostride) = sum over e in [g*count, (g+1)*count) of mask[e] * P_e

@@ -459,7 +459,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ e, size_t nrecv, size_t pos0, int P,
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
-    uint32_t* __restrict__ R, size_t rstride, size_t pstride) {
+    uint32_t* __restrict__ R, size_t pstride) {
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
   // segment position q adds column q + 1 of its segment.  Column q = 0 is never read inside a
   // segment (its value leaves through `down` / R), so the segment's top lane parks the upstream
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     __syncthreads();
     if (live && pos + 1 < N) ge_add_lds(D, D, nbr, false, MAXBS);
     __syncthreads();  // every column read before the next step overwrites it
-    if (live && q == 0 && R) pt_store(R, rstride, d * nrecv + j, D);
+    if (live && q == 0 && R) pt_store_aos(R, d * nrecv + j, D);
   }
 }
 
@@ -541,7 +541,7 @@ StepShape stepping_shape(size_t N) {
   return ea >= eb - 0.02 ? a : b;
 }
 
-void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R, size_t rstride,
+void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride) {
   if (!ndealers || !nrecv) return;
   const StepShape sh = stepping_shape(N);
@@ -551,7 +551,7 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
       uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
       hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)pieces), dim3((unsigned)sh.bs), 0,
                          stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down, b ? nullptr : R,
-                         rstride, pstride);
+                         pstride);
       up = down;
     }
     return;
@@ -561,11 +561,11 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
   if (sh.maxbs == 256)
     hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)sh.bs), 0, stream,
                        ndealers, npad, N, e, nrecv, (size_t)0, (int)sh.P, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                       R, rstride, pstride);
+                       R, pstride);
   else
     hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)sh.bs), 0, stream,
                        ndealers, npad, N, e, nrecv, (size_t)0, (int)sh.P, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                       R, rstride, pstride);
+                       R, pstride);
 }
 
 // Degree split: P(x) = sum_u x^(uL) Q_u(x).  With the stepped values Q_u(j) of
@@ -579,7 +579,7 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
 template <int SLOTS>
 __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width, size_t pstride, int pieces, size_t nrecv,
                                                  const int8_t* __restrict__ digits, const int16_t* __restrict__ top,
-                                                 uint32_t* __restrict__ R, size_t rstride) {
+                                                 uint32_t* __restrict__ R) {
   __shared__ uint32_t qs[SLOTS * PT_WORDS * 64];
   uint32_t* slot_y = qs + threadIdx.x;                   // addend of y's digits
   uint32_t* slot_y2 = qs + (SLOTS - 1) * PT_WORDS * 64 + threadIdx.x;  // of y^2's (SLOTS == 2)
@@ -590,7 +590,7 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
   const int8_t* d1 = digits + j * 512;
   const int8_t* d2 = d1 + 256;
   const int t1 = top[2 * j], t2 = top[2 * j + 1];
-  auto load_q = [&](ge_p3& q, int u) { pt_load(q, R, rstride, ((size_t)u * pstride + cc) * nrecv + j); };
+  auto load_q = [&](ge_p3& q, int u) { pt_load_aos(q, R, ((size_t)u * pstride + cc) * nrecv + j); };
   auto put = [&](uint32_t* slot, const ge_p3& p) {
     ge_cached xc;
     ge_to_cached(xc, p);
@@ -635,26 +635,24 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
       ge_add(acc, acc, qc);
     }
   }
-  if (live) pt_store(R, rstride, c * nrecv + j, acc);
+  if (live) pt_store_aos(R, c * nrecv + j, acc);
 }
 
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
-             uint32_t* R, size_t rstride, hipStream_t stream) {
+             uint32_t* R, hipStream_t stream) {
   if (!width || !nrecv || pieces < 2) return;
   const dim3 grid((unsigned)((width + 63) / 64), (unsigned)nrecv);
   if (pieces == 2)  // one product, one LDS slot (10 KB per wave: occupancy bound by VGPRs only)
-    hipLaunchKernelGGL(k_combine<1>, grid, dim3(64), 0, stream, width, pstride, (int)pieces, nrecv, digits, top, R,
-                       rstride);
+    hipLaunchKernelGGL(k_combine<1>, grid, dim3(64), 0, stream, width, pstride, (int)pieces, nrecv, digits, top, R);
   else
-    hipLaunchKernelGGL(k_combine<2>, grid, dim3(64), 0, stream, width, pstride, (int)pieces, nrecv, digits, top, R,
-                       rstride);
+    hipLaunchKernelGGL(k_combine<2>, grid, dim3(64), 0, stream, width, pstride, (int)pieces, nrecv, digits, top, R);
 }
 
 // ------------------------------------------------------------------ K3c check
 __global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base,
                                                uint32_t nmod, int round,
                                                const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
-                                               const uint32_t* __restrict__ R, size_t rstride,
+                                               const uint32_t* __restrict__ R,
                                                const uint32_t* __restrict__ tab_g,
                                                const uint32_t* __restrict__ tab_h,
                                                const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec) {
@@ -670,7 +668,7 @@ __global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv,
     sc_load(x, sp + 8 * p);
     comb8_mul_add(acc, x, tab_h);                  // + h * s'                 (committee.rs:292-293)
   }
-  pt_load(r, R, rstride, p);
+  pt_load_aos(r, R, p);
   const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
   // a dealer whose broadcast does not decode is missing data: disqualified without a complaint in
   // round 2 (committee.rs:331-335), an accusation in round 4 (:549-555)
@@ -680,12 +678,12 @@ __global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv,
 }
 
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
-           const uint32_t* s, const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g,
+           const uint32_t* s, const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g,
            const uint32_t* tab_h, const uint8_t* dok, uint8_t* dec, hipStream_t stream) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
   hipLaunchKernelGGL(k_check, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
-                     dealer_base, recv_base, (uint32_t)nmod, round, s, sp, R, rstride, tab_g, tab_h, dok, dec);
+                     dealer_base, recv_base, (uint32_t)nmod, round, s, sp, R, tab_g, tab_h, dok, dec);
 }
 
 // Fused round-2 + round-4 check of dealers [dealer0, dealer0 + ndealers) (local indices) whose E and A
@@ -696,7 +694,7 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
 __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
                                                     uint32_t nmod, const uint32_t* __restrict__ s,
                                                     const uint32_t* __restrict__ sp, const uint32_t* __restrict__ R,
-                                                    size_t rstride, const uint32_t* __restrict__ tab_g,
+                                                    const uint32_t* __restrict__ tab_g,
                                                     const uint32_t* __restrict__ tab_h,
                                                     const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
                                                     uint8_t* __restrict__ dec4) {
@@ -711,23 +709,23 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
   sc x;
   sc_load(x, s + 8 * q);
   comb8_mul_add(acc, x, tab_g);                    // G::generator() * s   (committee.rs:294, :537)
-  pt_load(r, R, rstride, cA * nrecv + j);
+  pt_load_aos(r, R, cA * nrecv + j);
   bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
   dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
   sc_load(x, sp + 8 * q);
   comb8_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
-  pt_load(r, R, rstride, cE * nrecv + j);
+  pt_load_aos(r, R, cE * nrecv + j);
   eq = ristretto_eq(acc, r);                       // round 2 (:305)
   dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)
 }
 
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
-                const uint32_t* sp, const uint32_t* R, size_t rstride, const uint32_t* tab_g, const uint32_t* tab_h,
+                const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
                 const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
   hipLaunchKernelGGL(k_check_both, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
-                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, rstride, tab_g, tab_h, dok, dec2, dec4);
+                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4);
 }
 
 // Identity in every column of a position-major table [40][S] (S = N * npad words apart).
@@ -791,7 +789,7 @@ __global__ __launch_bounds__(64, 3) void k_horner(size_t ndealers, size_t npad, 
     ge_to_cached(cc, c);
     ge_add(acc, acc, cc);
   }
-  if (d < ndealers) pt_store(R, ndealers * nrecv, d * nrecv + blockIdx.y, acc);
+  if (d < ndealers) pt_store_aos(R, d * nrecv + blockIdx.y, acc);
 }
 
 void horner(size_t ndealers, size_t npad, size_t N, const uint32_t* C, uint32_t x0, size_t nrecv, uint32_t* R,

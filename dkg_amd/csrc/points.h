@@ -32,6 +32,23 @@ DKG_DEV void pt_store(uint32_t* __restrict__ base, size_t stride, size_t e, cons
   }
 }
 
+// Point-major (AoS) element e: 40 consecutive words, moved as ten 16-B accesses.  Used for the
+// per-(column, receiver) evaluations R, which one lane writes per step (stepping, recombination):
+// a point fills whole cache lines instead of 40 scattered 4-B words.  base must be 16-B aligned.
+DKG_DEV void pt_load_aos(ge_p3& p, const uint32_t* __restrict__ base, size_t e) {
+  const uint4* b = reinterpret_cast<const uint4*>(base + e * PT_WORDS);
+  uint4* w = reinterpret_cast<uint4*>(&p);
+#pragma unroll
+  for (int k = 0; k < PT_WORDS / 4; k++) w[k] = b[k];
+}
+
+DKG_DEV void pt_store_aos(uint32_t* __restrict__ base, size_t e, const ge_p3& p) {
+  uint4* b = reinterpret_cast<uint4*>(base + e * PT_WORDS);
+  const uint4* w = reinterpret_cast<const uint4*>(&p);
+#pragma unroll
+  for (int k = 0; k < PT_WORDS / 4; k++) b[k] = w[k];
+}
+
 DKG_DEV void ld_words8(uint32_t (&w)[8], const uint32_t* __restrict__ p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
   uint4 a = q[0], b = q[1];

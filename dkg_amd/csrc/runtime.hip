@@ -334,7 +334,6 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const int8_t* ydig = nullptr;
   const int16_t* ytop = nullptr;
   if (U > 1) split_digits(ctx, n, L, &ydig, &ytop);
-  const size_t rstride = W * n;
   // padding columns, and the positions past t of the last piece, are the identity
   if (npad != D * nseg || U * L != N) dkgk::fill_identity(L * W, Cpm, home);
   HCK(hipMemsetAsync(pok, 1, npad * N, home));
@@ -353,11 +352,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (d1 <= d0) return;
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
-      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R, rstride,
+      dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
                        ctx->tab_g8, ctx->tab_h8, dok, g.dec, segs[1].dec, st);
     } else {
       dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, g.self_mod ? g.self_mod : n, g.round, g.s + d0 * n * 8,
-                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n, rstride, ctx->tab_g8, ctx->tab_h8,
+                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n * PT_WORDS_H, ctx->tab_g8, ctx->tab_h8,
                   dok + d0, g.dec + d0 * n, st);
     }
   };
@@ -367,10 +366,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
     uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad);
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
-    dkgk::stepping(w, W, L, e, n, R + c0 * n, rstride, sa ? sa + c0 * n * 40 : nullptr,
+    dkgk::stepping(w, W, L, e, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st, U, npad);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
-    dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n, rstride, st);
+    dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));
     checks(g0 * 64, std::min(D, g1 * 64), st);
     if (tm) HCK(hipEventRecord(ctx->pev[4], st));
@@ -1364,7 +1363,7 @@ int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, c
     uint32_t* ds = upload_scalars(ctx, "vr_s", s, n);
     uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vr_sp", s_prime, n) : nullptr;
     uint8_t* dec = buf<uint8_t>(ctx, "vr_dec", n);
-    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, n, ctx->tab_g8, ctx->tab_h8, dok, dec, ctx->stream);
+    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, ctx->tab_g8, ctx->tab_h8, dok, dec, ctx->stream);
     check_launch(ctx);
     d2h(ctx, decision, dec, n);
     sync(ctx);

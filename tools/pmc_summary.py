@@ -1,11 +1,14 @@
 """Summarise rocprofv3 CSV output of tools/profile.sh per kernel (sums over dispatches).
 
-usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag>
+usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag> [traffic.json n t U]
 Prints kernel-trace stats (calls, total/avg ms) and, per kernel, the SQ issue/wait split,
 VALU instructions (wave-level x 64 lanes) and HBM-side bytes: FETCH_SIZE doubled (gfx950 counts
 half the bytes of wide coalesced reads, MI355X_MICROARCH.md "HBM") and WRITE_SIZE, both in KB.
+With a traffic.json path (and the profiled ceremony's n, t and degree split U) it also writes the
+per-launch HBM bytes of the check-pipeline kernels, which bench.py reports as roofline.traffic.
 """
 import csv
+import json
 import os
 import sys
 from collections import defaultdict
@@ -51,5 +54,35 @@ def main(d):
               f"{2 * fe[k].get('FETCH_SIZE', 0) / 1e3:12.1f} {wr[k].get('WRITE_SIZE', 0) / 1e3:10.1f}")
 
 
+PHASE = {"k_binom_step": "binomial", "void k_stepping<256>": "stepping", "void k_stepping<512>": "stepping",
+         "void k_combine<1>": "combine", "void k_combine<2>": "combine", "k_check_both": "check", "k_check": "check"}
+
+
+def write_traffic(d, out, n, t, U):
+    """Per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, counted in separate --pmc passes) of the
+    check-pipeline kernels, summed over every dispatch the profiled run made."""
+    fe, fcalls = load_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
+    wr, wcalls = load_counters(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
+    kern = {}
+    for k, ph in PHASE.items():
+        if k not in fe or k not in wr:
+            continue
+        e = kern.setdefault(ph, {"fetch_bytes_x2": 0.0, "write_bytes": 0.0, "fetch_launches": 0, "write_launches": 0})
+        e["fetch_bytes_x2"] += 2 * fe[k].get("FETCH_SIZE", 0) * 1024  # FETCH_SIZE and WRITE_SIZE are in KiB
+        e["write_bytes"] += wr[k].get("WRITE_SIZE", 0) * 1024
+        e["fetch_launches"] += len(fcalls[k])
+        e["write_launches"] += len(wcalls[k])
+    for e in kern.values():
+        e["bytes_per_launch"] = (e["fetch_bytes_x2"] / max(e["fetch_launches"], 1)
+                                 + e["write_bytes"] / max(e["write_launches"], 1))
+    doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
+                     f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
+           "n": n, "t": t, "split": U, "kernels": kern}
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
 if __name__ == "__main__":
     main(sys.argv[1])
+    if len(sys.argv) > 2:
+        write_traffic(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
