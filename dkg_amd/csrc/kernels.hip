@@ -608,9 +608,8 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
       if (dg != 0) ge_add_lds(acc, acc, slot_y, dg < 0);
     }
     load_q(q, 2 * v);
-    ge_cached qc;
-    ge_to_cached(qc, q);
-    ge_add(acc, acc, qc);
+    put(slot_y, q);  // the chain is done with slot_y: the last addend goes through LDS too
+    ge_add_lds(acc, acc, slot_y, false);
   } else {
     load_q(acc, 2 * v);
   }
@@ -630,9 +629,8 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
         if (e1 != 0) ge_add_lds(acc, acc, slot_y, e1 < 0);
       }
       load_q(q, 2 * v);
-      ge_cached qc;
-      ge_to_cached(qc, q);
-      ge_add(acc, acc, qc);
+      put(slot_y, q);
+      ge_add_lds(acc, acc, slot_y, false);
     }
   }
   if (live) pt_store_aos(R, c * nrecv + j, acc);

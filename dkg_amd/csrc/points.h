@@ -35,18 +35,33 @@ DKG_DEV void pt_store(uint32_t* __restrict__ base, size_t stride, size_t e, cons
 // Point-major (AoS) element e: 40 consecutive words, moved as ten 16-B accesses.  Used for the
 // per-(column, receiver) evaluations R, which one lane writes per step (stepping, recombination):
 // a point fills whole cache lines instead of 40 scattered 4-B words.  base must be 16-B aligned.
+// word w of a point (X, Y, Z, T limbs in order); constant w after unrolling, so no address is taken
+DKG_DEV uint32_t& pt_word(ge_p3& p, int w) {
+  fe& f = w < 10 ? p.X : (w < 20 ? p.Y : (w < 30 ? p.Z : p.T));
+  return f.v[w % 10];
+}
+DKG_DEV uint32_t pt_word(const ge_p3& p, int w) {
+  const fe& f = w < 10 ? p.X : (w < 20 ? p.Y : (w < 30 ? p.Z : p.T));
+  return f.v[w % 10];
+}
+
 DKG_DEV void pt_load_aos(ge_p3& p, const uint32_t* __restrict__ base, size_t e) {
   const uint4* b = reinterpret_cast<const uint4*>(base + e * PT_WORDS);
-  uint4* w = reinterpret_cast<uint4*>(&p);
 #pragma unroll
-  for (int k = 0; k < PT_WORDS / 4; k++) w[k] = b[k];
+  for (int k = 0; k < PT_WORDS / 4; k++) {
+    const uint4 v = b[k];
+    pt_word(p, 4 * k) = v.x;
+    pt_word(p, 4 * k + 1) = v.y;
+    pt_word(p, 4 * k + 2) = v.z;
+    pt_word(p, 4 * k + 3) = v.w;
+  }
 }
 
 DKG_DEV void pt_store_aos(uint32_t* __restrict__ base, size_t e, const ge_p3& p) {
   uint4* b = reinterpret_cast<uint4*>(base + e * PT_WORDS);
-  const uint4* w = reinterpret_cast<const uint4*>(&p);
 #pragma unroll
-  for (int k = 0; k < PT_WORDS / 4; k++) b[k] = w[k];
+  for (int k = 0; k < PT_WORDS / 4; k++)
+    b[k] = make_uint4(pt_word(p, 4 * k), pt_word(p, 4 * k + 1), pt_word(p, 4 * k + 2), pt_word(p, 4 * k + 3));
 }
 
 DKG_DEV void ld_words8(uint32_t (&w)[8], const uint32_t* __restrict__ p) {
