@@ -200,7 +200,10 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
   double cyc = 0;
   for (size_t r = 1; r < L; r++) {
     const double work = waves_col * pre[r] * THR / SIMDS;  // wave-instructions of step r
-    cyc += std::max(work, cost(r) * LAT) + LAUNCH;
+    // a step pays its issue work AND its longest chain: the last waves of a launch run their chains
+    // on partly idle SIMDs (the sum fits the measured shards within 5 %: 1-, 2-, 4-, 8-way n=1024,
+    // one-GPU n=4096; the max alone picked U=2 for a 4-way n=1024 shard, 3 % slower than U=4)
+    cyc += work + cost(r) * LAT + LAUNCH;
   }
   if (U > 1) {
     // pairwise joint chains: an even U starts with one product (253 doublings + ~85 NAF

@@ -78,5 +78,10 @@ def test_split_cost_model():
     assert ms(2048, 1024, 511, 2) < 0.9 * ms(2048, 1024, 511, 1)
     assert min(range(1, 9), key=lambda U: ms(2048, 1024, 511, U)) == 2
     assert min(range(1, 17), key=lambda U: ms(8192, 4096, 2047, U)) == 4
+    # dealer shards of n=1024 (2 rows per dealer): U=2 for 512 dealers, U=4 for 256 and 128
+    # (measured: profiles/r01_shard_scaling_n1024_v10.txt)
+    assert min((1, 2, 4, 8), key=lambda U: ms(1024, 1024, 511, U)) == 2
+    assert min((1, 2, 4, 8), key=lambda U: ms(512, 1024, 511, U)) == 4
+    assert min((1, 2, 4, 8), key=lambda U: ms(256, 1024, 511, U)) == 4
     assert ms(16384, 64, 31, 1) < ms(16384, 64, 31, 2)
     assert ms(64, 10, 4, 6) == -1.0  # more pieces than coefficients
