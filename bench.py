@@ -279,6 +279,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="D", choices=sorted(CONFIGS) + sorted(BATCH))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-interp", action="store_true",
+                    help="skip the side measurement of the opt-in interpolation verify mode")
     ap.add_argument("--streams", type=int, default=2, help="dealer-chunk streams of the round-2/4 checks")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal with ranks sharing GPUs")
@@ -438,6 +440,22 @@ def main():
                 out["roofline"]["traffic_source"] = pmc[1]
                 if alg:
                     out["roofline"]["traffic_over_algorithmic"] = pmc[0] / alg
+        if not args.no_interp:
+            # the opt-in committee verification on the same inputs, reported
+            # beside the headline, never as it: every P_i(j) is NOT computed in the group there
+            be.set_verify_mode("interp")
+            step()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                ri = step()
+            torch.cuda.synchronize()
+            ms_i = (time.perf_counter() - t1) / args.steps * 1e3
+            be.set_verify_mode("group")
+            assert ri.n_qualified == n and ri.mpk == res.mpk, "interpolation mode disagrees with the group mode"
+            out["interp_mode"] = {"ms_per_step": ms_i, "value": pairs / (ms_i / 1e3), "unit": "verified shares/s",
+                                  "note": "opt-in dkg_ctx_set_verify_mode(ctx, 1): committee verification by "
+                                          "interpolation, identical decisions; not the headline"}
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(n, t)
             out["gpu_vs_cpu"] = value / out["cpu_baseline"]["value"]
