@@ -1,0 +1,58 @@
+"""CPU checks of bench.py's accounting: the closed-form work and byte counts behind the roofline
+fields, and the per-launch traffic read from the committed PMC passes (no GPU needed)."""
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def test_algorithmic_bytes_binomial():
+    # step r: position 0 copies C_k (load + store), positions 1..r load two points and store one
+    n, t, U = 1024, 511, 2
+    L = (t + 1) // U
+    per_launch, launches = bench.algorithmic_bytes("binomial", n, t, U)
+    assert launches == L - 1
+    cols = 2 * n * U
+    total = sum(cols * 160 * (2 + 3 * r) for r in range(1, L))
+    assert per_launch * launches == pytest.approx(total)
+    assert per_launch == pytest.approx(252968960.0)
+
+
+def test_algorithmic_bytes_stepping_and_combine():
+    n, t, U = 1024, 511, 2
+    step, nl = bench.algorithmic_bytes("stepping", n, t, U)
+    assert nl == 1 and step == 2 * n * U * (256 + n) * 160  # the table once, D_0 out per receiver
+    comb, nl = bench.algorithmic_bytes("combine", n, t, U)
+    assert nl == 1 and comb == 2 * n * n * 3 * 160  # two piece values in, P(j) out
+    assert bench.algorithmic_bytes("check", n, t, U) == (None, None)
+
+
+def test_pmc_traffic_matches_workload():
+    """The committed traffic file belongs to the n=1024, t=511, U=2 pipeline; other workloads get
+    None (their traffic was not measured), and the binomial's measured bytes are within 10 % of
+    its algorithmic bytes (no re-reads)."""
+    got = bench.pmc_traffic("binomial", 1024, 511, 2)
+    assert got is not None
+    measured, source = got
+    alg, _ = bench.algorithmic_bytes("binomial", 1024, 511, 2)
+    assert 0.9 < measured / alg < 1.1
+    assert "FETCH_SIZE" in source and "WRITE_SIZE" in source
+    assert bench.pmc_traffic("binomial", 4096, 2047, 4) is None
+    assert bench.pmc_traffic("binomial", 1024, 511, 4) is None
+
+
+def test_closed_form_work_per_pair():
+    """DESIGN.md section 2's per-pair figures at n=1024, t=511, U=2 (VALU instructions per pair
+    per round): binomial 0.68 M, stepping 0.77 M, recombination 0.38 M."""
+    n, t = 1024, 511
+    w = bench.algorithmic_valu(n, t, 2, 2)
+    pairs = n * n  # the closed form counts every (dealer, receiver) position
+    assert w["binomial"] / pairs == pytest.approx(0.68e6, rel=0.05)
+    assert w["stepping"] / pairs == pytest.approx(0.77e6, rel=0.05)
+    assert w["combine"] / pairs == pytest.approx(0.38e6, rel=0.05)
+    # the fused schedule carries both rounds' tables through binomial, stepping and recombination
+    f = bench.fused_valu(n, t, 2)
+    assert f["binomial"] == pytest.approx(2 * w["binomial"])
