@@ -56,8 +56,13 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 // pieces > 1: the same for the columns [u * pstride, u * pstride + width) of every piece u
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
                    hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
+// Position-major [40][N][npad] -> column-major [40][npad][N] (element c * N + m) for the columns
+// [u * pstride, u * pstride + width) of each of `pieces` pieces (the stepping's input layout).
+void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uint32_t* eT, size_t pieces,
+                     size_t pstride, hipStream_t stream);
 // K3b: finite-difference stepping: R[i][j] = P_i(j+1) for j in [0, nrecv), point-major (AoS)
-// [i*nrecv + j][40] (pt_store_aos).  stream_a / stream_b: scratch for the inter-block boundary streams, each
+// [i*nrecv + j][40] (pt_store_aos), from the column-major difference table e (to_column_major;
+// word stride N * npad).  stream_a / stream_b: scratch for the inter-block boundary streams, each
 // >= ndealers*nrecv*160 B (unused when N <= 512).
 // How k_stepping covers an N-position table: nblk blocks of P positions on bs lanes (nblk > 1), or
 // `per` tables of P = N lanes each per bs-lane workgroup; maxbs = the LDS variant (256 or 512).

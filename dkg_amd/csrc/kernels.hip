@@ -443,6 +443,41 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
 // keeps t = 511 in ONE launch: each launch is a chain of n dependent additions per lane, so fewer,
 // wider blocks shorten the serial part when few dealers are resident (a small multi-GPU shard).
 
+// The binomial's position-major table [40][N][npad] (lanes = columns) -> column-major [40][npad][N]
+// (lanes = positions of one column, as the stepping reads it), for the columns
+// [u * pstride, u * pstride + width) of each piece u.  64 x 64 tiles through LDS: both sides move
+// 256 contiguous bytes per wave and word; read straight from the position-major table, a stepping
+// lane's 4-byte word would cost a whole line (npad words apart).
+__global__ __launch_bounds__(256) void k_to_column_major(size_t width, size_t npad, size_t N,
+                                                         const uint32_t* __restrict__ e, uint32_t* __restrict__ eT,
+                                                         size_t pstride) {
+  __shared__ uint32_t tile[64][65];
+  // one word of one 64 x 64 tile per workgroup: grid.z = piece * PT_WORDS + word
+  const size_t w = blockIdx.z % PT_WORDS, base = (blockIdx.z / PT_WORDS) * pstride;
+  const size_t c0 = (size_t)blockIdx.x * 64, p0 = (size_t)blockIdx.y * 64;
+  const size_t S = N * npad;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const size_t p = p0 + ty + 4 * i, c = c0 + tx;
+    if (p < N && c < width) tile[ty + 4 * i][tx] = e[w * S + p * npad + base + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const size_t c = c0 + ty + 4 * i, p = p0 + tx;
+    if (p < N && c < width) eT[w * S + (base + c) * N + p] = tile[tx][ty + 4 * i];
+  }
+}
+
+void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uint32_t* eT, size_t pieces,
+                     size_t pstride, hipStream_t stream) {
+  if (!width || !N) return;
+  hipLaunchKernelGGL(k_to_column_major,
+                     dim3((unsigned)((width + 63) / 64), (unsigned)((N + 63) / 64), (unsigned)(pieces * PT_WORDS)),
+                     dim3(256), 0, stream, width, npad, N, e, eT, pstride);
+}
+
 __device__ __forceinline__ void cached_identity(ge_cached& c) {
   fe_one(c.YpX);
   fe_one(c.YmX);
@@ -475,7 +510,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const size_t S = N * npad;
   const size_t pos = pos0 + q;
   ge_p3 D;
-  if (live && pos < N) pt_load(D, e, S, pos * npad + d);
+  if (live && pos < N) pt_load(D, e, S, d * N + pos);  // column-major table: a segment reads contiguously
   else ge_identity(D);
   const bool top_lane = live && (q == P - 1);
   const uint4* upd = (up && live) ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;

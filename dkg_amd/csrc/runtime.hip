@@ -328,6 +328,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   uint32_t* Cpm = buf<uint32_t>(ctx, "v.Cpm", PTB * L * W);
   uint32_t* e0 = buf<uint32_t>(ctx, "v.binom0", PTB * L * W);
   uint32_t* e1 = buf<uint32_t>(ctx, "v.binom1", PTB * L * W);
+  uint32_t* eT = buf<uint32_t>(ctx, "v.binomT", PTB * L * W);  // column-major copy for the stepping
   uint32_t* R = buf<uint32_t>(ctx, "v.R", PTB * W * n);
   uint32_t *sa = nullptr, *sb = nullptr;
   if (L > 512) {
@@ -367,9 +368,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad);
+    const uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad);
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
-    dkgk::stepping(w, W, L, e, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
+    dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
+    dkgk::stepping(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st, U, npad);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);

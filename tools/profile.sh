@@ -11,7 +11,7 @@ OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-B="$REPO/bench.py --no-cpu --streams 1 $*"
+B="$REPO/bench.py --no-cpu --no-interp --streams 1 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B --steps 2 --warmup 1 > "$OUT/trace.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_sq" -o run -- python3 $B --steps 1 --warmup 0 > "$OUT/pmc_sq.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $B --steps 1 --warmup 0 > "$OUT/pmc_fetch.log" 2>&1
