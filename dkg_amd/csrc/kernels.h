@@ -130,8 +130,9 @@ void dealer_coeffs(size_t rows, size_t D, size_t d0, uint32_t c0, const uint32_t
 // ---- full (encrypted-share) mode, hybrid.hip (elgamal.rs:134-193) ----
 // Items are (dealer i, recipient q, w) at index (i * n + q) * 2 + w; w = 0 is the randomness (s')
 // ciphertext, w = 1 the share (s) ciphertext (committee.rs:171-172 order).
-// R = g r, K = pk_q r for every item (r [items][8]); tabs_pk: one comb table per recipient.
-void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_g, const uint32_t* tabs_pk, uint32_t* R_ext,
+// R = g r, K = pk_q r for every item (r [items][8]); tab_g8: the generator's radix-256 comb;
+// tabs_pk: one (radix-16) comb table per recipient.
+void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_g8, const uint32_t* tabs_pk, uint32_t* R_ext,
              uint32_t* K_ext, hipStream_t stream);
 // K = sk_q * R for every item, R decoded SoA [40][items] (sk [n][8], wave-uniform per recipient)
 void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream);

@@ -966,7 +966,7 @@ void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
   uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
   uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
-  dkgk::enc_mul(D, n, r, ctx->tab_g, tabs, R, K, st);
+  dkgk::enc_mul(D, n, r, ctx->tab_g8, tabs, R, K, st);
   dkgk::encode_points(R, items, items, e1, st);
   dkgk::encode_points(K, items, items, Kc, st);
   dkgk::sym_xor(D, n, Kc, false, ct, const_cast<uint32_t*>(s), const_cast<uint32_t*>(sp), st);
