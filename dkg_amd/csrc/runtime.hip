@@ -379,12 +379,17 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     checks(g0 * 64, std::min(D, g1 * 64), st);
     if (tm) HCK(hipEventRecord(ctx->pev[4], st));
   };
-  // Chunk streams only pay when the binomial saturates the GPU: chunk c+1's triangle then fills
-  // the CUs that chunk c's launch tails leave idle.  A small shard (few dealers, e.g. one rank of
-  // 8) is latency-bound -- every step is one dependent NAF chain long whatever its width -- so all
-  // its columns go through one launch per step (average waves per step < 4 per SIMD -> nsub = 1).
+  // Chunk streams pay when the binomial saturates the GPU (chunk c+1's triangle fills the CUs that
+  // chunk c's launch tails leave idle), or when the stepping is long enough (W * L * n lane-steps)
+  // that the chunks' phases drift apart and one chunk's recombination and checks run beside the
+  // other's stepping.  A small ceremony or shard is latency-bound -- every binomial step is one
+  // dependent NAF chain long whatever its width -- and two half-width pipelines only double its
+  // launches.  Measured (tools/shard_time.py): chunks gain 1.2-2.4 ms on n=1024 4- and 8-way
+  // shards and n=512 1- and 2-way (>= 6.7e7 lane-steps) and lose 0.9-2.5 ms on n=512 4-way and
+  // n=256 (<= 3.4e7).
   const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
-  const size_t nsub = saturating ? std::min<size_t>(ctx->nsub, groups) : 1;
+  const bool long_stepping = (double)W * (double)L * (double)n >= 5e7;
+  const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
   ctx->timed_tag.clear();
   if (nsub <= 1) {
     chunk(0, groups, home, timed);
