@@ -288,18 +288,20 @@ def test_ceremony_large_properties(be, n, t, split):
     assert s == r.s[32 * n * i:32 * n * (i + 1)] and sp == r.s_prime[32 * n * i:32 * n * (i + 1)]
 
 
+@pytest.mark.parametrize("n,t", [(200, 99), (512, 255)])
 @pytest.mark.parametrize("round_", [2, 4])
-def test_chunked_streams_identical(be, round_):
-    """Dealer chunks on 1..8 HIP streams (dkg_ctx_set_streams) give identical decisions, with a
-    ragged dealer count (200, not a multiple of 64), flipped shares and one undecodable dealer."""
-    n, t = 200, 99
+def test_chunked_streams_identical(be, round_, n, t):
+    """Dealer chunks on 1..8 HIP streams (dkg_ctx_set_streams) give identical decisions, with
+    flipped shares and one undecodable dealer.  n=200 (ragged: not a multiple of 64) is below both
+    chunk gates of verify_device (runtime.hip: saturating binomial, W*L*n >= 5e7 lane-steps) and
+    runs one pipeline whatever nsub; n=512 (6.7e7 lane-steps) takes the chunked path for nsub > 1."""
     N = t + 1
     be.env_init(t, n, CK)
     a, b = dkg_amd.dealer_coefficients(bytes([9]) * 32, 1, 0, n, t)
     E, A, s, sp = be.share_gen(a, b, n, n, t)
     C = bytearray(E if round_ == 2 else A)
     s = bytearray(s)
-    rng = random.Random(round_)
+    rng = random.Random(round_ * 1000 + n)
     flips = {(rng.randrange(n), rng.randrange(n)) for _ in range(40)}
     for i, j in flips:
         s[32 * (i * n + j) + 5] ^= 0x10
