@@ -372,7 +372,7 @@ def main():
         "metric": metric,
         "value": value, "unit": "verified shares/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if ws > 1 else "weak", "vs_baseline": None, "dtype": "u32 (GF(2^255-19), Z_l)",
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32 (GF(2^255-19), Z_l)",
         "data": "synthetic: seeded ChaCha20 coefficients (SURVEY.md 8d), honest ceremony",
         "config": {"workload": f"one DKG ceremony n={n}, t={t} (share gen + round-2/4 checks + finalise)",
                    "n": n, "t": t, "pairs_per_step": pairs,
