@@ -71,6 +71,26 @@ def pmc_traffic(kernel, n, t, U):
     return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
 
 
+def spawn_ranks(args):
+    """`--gpus N` (N > 1) without a launcher: start N fresh worker processes of this script, one per
+    GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torchrun sets),
+    before this process touches the GPU; rank 0 prints the JSON line.  Returns the worst exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -167,44 +187,89 @@ def fused_valu(n, t, U=1):
     return out
 
 
-def cpu_baseline(n, t, seconds_target=15.0):
-    """Reference-algorithm CPU baseline: the oracle (dalek-3 u64 algorithms: radix-16 variable-base
-    mul + Pippenger w=7 MSM for N=512) verifying a bounded sample of round-2 pairs on all cores:
-    batches of 8 dealers x all their receivers until about `seconds_target` of checking."""
+def host_cpu():
+    """(threads to use, description): every core of this process's affinity mask, capped by a cgroup
+    CPU quota when one is set (a GPU box grants a share of a larger machine), and the CPU model."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {"cpu_model": model, "affinity_cores": aff, "cgroup_quota_cores": quota,
+                   "os_cpu_count": os.cpu_count()}
+
+
+def cpu_baseline(n, t, seconds_target=20.0):
+    """Reference-algorithm CPU baseline of the WHOLE ceremony, extrapolated from a bounded sample.
+    The oracle follows dalek-3's u64 algorithms (5x51 field, radix-16 variable-base mul, Straus /
+    Pippenger MSM at dalek's thresholds) loop for loop with committee.rs.  On batches of 8 dealers it
+    times round-1 share generation (commitments + all n shares, committee.rs:148-186), round-2 checks
+    (:287-305) and round-4 checks (:532-548) against all receivers on every host core, until about
+    `seconds_target` seconds; the ceremony time is n x (share gen per dealer) + n(n-1) x (round-2 +
+    round-4 per pair) -- rounds 3 and 5 are negligible -- and value = n(n-1) / that time."""
+    import ctypes
+
     from tests import oracle_lib as O
     import dkg_amd
 
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    cores, cpu = host_cpu()
+    lib = O.lib()
+    lib.or_bench_fe_mul.restype = ctypes.c_double
+    lib.or_bench_fe_mul.argtypes = [ctypes.c_uint64]
+    lib.or_bench_msm.restype = ctypes.c_double
+    lib.or_bench_msm.argtypes = [ctypes.c_size_t, ctypes.c_int]
+    fe_ns = lib.or_bench_fe_mul(5_000_000)
+    msm_ms = lib.or_bench_msm(t + 1, 3)
     master = b"\x05" * 32
     nd = 8
     h = O.call32("or_pt_hash_to_group", b"Example of a shared string.", 27)[0]
-    pairs, dt, batches = 0, 0.0, 0
-    while dt < seconds_target and (batches + 1) * nd <= n:
-        d0 = batches * nd
+    t_gen = t_r2 = t_r4 = 0.0
+    dealers = pairs = 0
+    while t_gen + t_r2 + t_r4 < seconds_target and dealers + nd <= n:
+        d0 = dealers
         a, b = dkg_amd.dealer_coefficients(master, 0, d0, nd, t)
+        t0 = time.perf_counter()
         E, A, s, sp = O.share_gen(nd, n, t, a, b, h, cores)
-        # rows of the sampled dealers placed at their own indices; other rows are never read
-        C = bytes(32 * (t + 1) * d0) + E + bytes(32 * (t + 1) * (n - d0 - nd))
-        S = bytes(32 * n * d0) + s + bytes(32 * n * (n - d0 - nd))
-        SP = bytes(32 * n * d0) + sp + bytes(32 * n * (n - d0 - nd))
-        if batches == 0:
-            O.verify_pairs(n, t, 2, C, h, S, SP, d0, d0 + nd, 0, 1, cores)  # warm the thread pool
-        chunk = 2 * cores
-        j0 = 0
-        while dt < seconds_target and j0 < n:
-            j1 = min(n, j0 + chunk)
-            t0 = time.perf_counter()
-            acc, _ = O.verify_pairs(n, t, 2, C, h, S, SP, d0, d0 + nd, j0, j1, cores)
-            dt += time.perf_counter() - t0
-            assert all(x in (1, 2) for x in acc)
-            pairs += sum(1 for x in acc if x == 1)
-            j0 = j1
-        batches += 1
-    return {"value": pairs / dt, "unit": "verified shares/sec", "cores": cores, "kind": "port",
-            "sample": f"round-2 checks (h*s'+g*s == vartime MSM over t+1={t+1} points, dalek-3 Pippenger w=7) "
-                      f"of {pairs} (dealer, receiver) pairs from {batches} batches of {nd} dealers at n={n}, t={t} "
-                      f"on {cores} threads in {dt:.1f} s; excludes share generation and round 4 (so it "
-                      f"overstates the CPU ceremony rate)"}
+        t_gen += time.perf_counter() - t0
+        # rows of the sampled dealers at their own indices; other rows are never read
+        pad = lambda x, w: bytes(w * d0) + x + bytes(w * (n - d0 - nd))  # noqa: E731
+        C2, C4, S, SP = pad(E, 32 * (t + 1)), pad(A, 32 * (t + 1)), pad(s, 32 * n), pad(sp, 32 * n)
+        if dealers == 0:
+            O.verify_pairs(n, t, 2, C2, h, S, SP, d0, d0 + nd, 0, 1, cores)  # warm the thread pool
+        t0 = time.perf_counter()
+        acc2, _ = O.verify_pairs(n, t, 2, C2, h, S, SP, d0, d0 + nd, 0, n, cores)
+        t_r2 += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        acc4, _ = O.verify_pairs(n, t, 4, C4, h, S, None, d0, d0 + nd, 0, n, cores)
+        t_r4 += time.perf_counter() - t0
+        assert set(acc2) <= {1, 2} and set(acc4) <= {1, 2}
+        dealers += nd
+        pairs += sum(1 for x in acc2 if x == 1)
+    gen_per_dealer, r2_per_pair, r4_per_pair = t_gen / dealers, t_r2 / pairs, t_r4 / pairs
+    ceremony_s = n * gen_per_dealer + n * (n - 1) * (r2_per_pair + r4_per_pair)
+    return {"value": n * (n - 1) / ceremony_s, "unit": "verified shares/s", "cores": cores, "kind": "port",
+            "ceremony_s_extrapolated": ceremony_s,
+            "round1_ms_per_dealer": gen_per_dealer * 1e3, "round2_ms_per_pair": r2_per_pair * 1e3,
+            "round4_ms_per_pair": r4_per_pair * 1e3,
+            "fe_mul_ns_1thread": fe_ns, f"msm_N{t + 1}_ms_1thread": msm_ms, **cpu,
+            "sample": f"{dealers} dealers x all {n} receivers at n={n}, t={t} ({pairs} pairs): share generation, "
+                      f"round-2 and round-4 checks (vartime MSM over t+1={t + 1} points per pair, dalek-3's "
+                      f"algorithms) timed on {cores} threads in {t_gen + t_r2 + t_r4:.1f} s; whole-ceremony "
+                      f"time extrapolated linearly in dealers and pairs"}
 
 
 def bench_batch(args, ws, rank, local):
@@ -253,9 +318,9 @@ def bench_batch(args, ws, rank, local):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     assert all(q == n for q in res.n_qualified), "an honest ceremony disqualified a dealer"
-    pairs = B * n * (n - 1) * ws
-    out = {"metric": f"verified shares/sec (whole node), {B} independent n={n},t={t} ceremonies per GPU "
-                     f"(BASELINE config 5)",
+    pairs = B * n * (n - 1) * ws  # whole node: every rank runs its own B ceremonies
+    out = {"metric": f"verified shares/sec (whole node) of {B} independent n={n},t={t} ceremonies per GPU "
+                     f"x {ws} GPU(s) (BASELINE config 5)",
            "value": pairs * args.steps / elapsed, "unit": "verified shares/s", "n_gpus": ws, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (GF(2^255-19), Z_l)",
@@ -292,7 +357,11 @@ def main():
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
     if args.config in BATCH:
         return bench_batch(args, ws, rank, local)
     n, t = CONFIGS[args.config]
@@ -365,7 +434,7 @@ def main():
         assert res.decisions.qualified.all() and not res.decisions.r2_error.any() and res.mpk is not None
     pairs = n * (n - 1)
     value = pairs * args.steps / elapsed
-    metric = "verified shares/sec (whole node) at n=1024,t=511; full-ceremony wall time"
+    metric = f"verified shares/sec (whole node) at n={n},t={t}; full-ceremony wall time"
     if args.mode == "full":
         metric += " -- FULL mode (hybrid-encrypted shares, SURVEY 8 f1)"
     out = {

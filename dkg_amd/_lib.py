@@ -15,6 +15,8 @@ DKG_E_DECODE = -2
 DKG_E_DEVICE = -3
 DKG_E_NOMEM = -4
 REJECT, ACCEPT, SELF, SKIPPED, MISSING = 0, 1, 2, 3, 4
+# per-party finalise status (dkg_finalise_parties)
+FIN_OK, FIN_R2_ERROR, FIN_R4_ERROR, FIN_PHASE4_ERROR, FIN_INSUFFICIENT, FIN_PANIC = 0, 1, 2, 3, 4, 5
 
 _lib = None
 
@@ -112,6 +114,9 @@ def lib():
     L.dkg_dealer_coeffs.argtypes = [u8p, ctypes.c_uint32, sz, sz, sz, p, p]
     L.dkg_scalar_sum_device.argtypes = [p, sz, sz, p, p, p]
     L.dkg_point_sum_device.argtypes = [p, sz, p, p, p]
+    L.dkg_share_gen_device.argtypes = [p, sz, sz, sz, p, p, p, p, p, p]
+    L.dkg_ceremony_shard_recon_device.argtypes = [p, sz, sz, sz, sz, u8p, u8p, p, p]
+    L.dkg_finalise_parties.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, u8p, u8p, u8p, p, p, p]
     _lib = L
     return L
 
@@ -127,5 +132,6 @@ EXPORTED = [
     "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_member_keys", "dkg_enc_randomness",
     "dkg_enc_randomness_device", "dkg_encrypt_shares", "dkg_decrypt_shares", "dkg_ceremony_run_full_device",
     "dkg_ceremony_verify_full", "dkg_misbehaviour_prove", "dkg_complaint1_verify", "dkg_complaint3_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
-    "dkg_scalar_sum_device", "dkg_point_sum_device",
+    "dkg_scalar_sum_device", "dkg_point_sum_device", "dkg_ceremony_shard_recon_device", "dkg_finalise_parties",
+    "dkg_share_gen_device",
 ]

@@ -78,6 +78,15 @@ class CeremonyResult:
     public_share: Optional[bytes] = None
 
 
+@dataclass
+class PartyFinalise:
+    """Per-party outcome of Phases<Phase5>::finalise (dkg_finalise_parties): status[p] is one of
+    dkg_amd._lib.FIN_* and recovery_index[p] the dealer of InsufficientSharesForRecovery (else -1)."""
+    mpk: List[bytes]
+    status: List[int]
+    recovery_index: List[int]
+
+
 class Backend:
     """One GPU (one process per GPU).  Owns a dkg_ctx."""
 
@@ -179,6 +188,13 @@ class Backend:
         s, sp = ctypes.create_string_buffer(32 * D * n), ctypes.create_string_buffer(32 * D * n)
         _check(self._ctx, _lib.lib().dkg_share_gen(self._ctx, D, n, t, a, b, E, A, s, sp))
         return E.raw, A.raw, s.raw, sp.raw
+
+    def share_gen_device(self, D: int, n: int, t: int, d_a: int, d_b: int, d_E: Optional[int], d_A: Optional[int],
+                         d_s: int, d_sp: int):
+        """dkg_share_gen on device buffers (pointers): compressed E/A [D][t+1][32], shares [D][n][32]."""
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_share_gen_device(self._ctx, D, n, t, vp(d_a), vp(d_b), vp(d_E), vp(d_A),
+                                                           vp(d_s), vp(d_sp)))
 
     # ---- rounds 2 / 4
     def verify_pairs(self, n: int, t: int, rnd: int, d0: int, d1: int, C: bytes, s: bytes,
@@ -341,6 +357,27 @@ class Backend:
             self._ctx, n, t, d0, d1, vp(d_E), vp(d_A), vp(d_s), vp(d_sp), vp(d_dec2), vp(d_dec4), vp(d_A0),
             vp(d_partial), ctypes.byref(ms)))
         return ms.value
+
+    def ceremony_shard_recon_device(self, n, t, d0, d1, qualified, reconstruct, d_s: Optional[int], d_terms: int):
+        """After the exchange: replace the terms of this rank's reconstructed dealers by g * a_i0
+        interpolated over the final parties' shares (d_s None = the last shard call's rows)."""
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_ceremony_shard_recon_device(
+            self._ctx, n, t, d0, d1, bytes(bytearray(qualified)), bytes(bytearray(reconstruct)), vp(d_s),
+            vp(d_terms)))
+
+    def finalise_parties(self, n: int, t: int, qualified, reconstruct, A0: bytes, s: bytes, r2_error=None,
+                         r4_error=None, disclosed=None) -> "PartyFinalise":
+        """Phases<Phase5>::finalise as every party runs it (committee.rs:726-805), with optional
+        per-party earlier failures and missing phase-5 disclosures (dkg_finalise_parties)."""
+        mpk = ctypes.create_string_buffer(32 * max(n, 1))
+        st = (ctypes.c_int32 * max(n, 1))()
+        ri = (ctypes.c_int32 * max(n, 1))()
+        mask = lambda x: None if x is None else bytes(bytearray(x))  # noqa: E731
+        _check(self._ctx, _lib.lib().dkg_finalise_parties(
+            self._ctx, n, t, mask(qualified), mask(reconstruct), mask(r2_error), mask(r4_error), mask(disclosed),
+            A0, s, mpk, st, ri))
+        return PartyFinalise([mpk.raw[32 * p:32 * p + 32] for p in range(n)], list(st)[:n], list(ri)[:n])
 
     def scalar_sum_device(self, rows: int, n: int, d_in: int, d_mask: Optional[int], d_out: int):
         """out[j] = sum over rows r with mask[r] of in[r][j] mod l (device pointers)."""

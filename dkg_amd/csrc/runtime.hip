@@ -45,6 +45,10 @@ struct dkg_ctx {
   const uint32_t* ext_E = nullptr;
   const uint32_t* ext_A = nullptr;
   size_t ext_stride = 0;
+  // share rows [shard_D][shard_n][8] of the last sharded call's dealers [shard_d0, +shard_D)
+  // (arena-owned; dkg_ceremony_shard_recon_device reads them after the exchange)
+  const uint32_t* shard_s = nullptr;
+  size_t shard_n = 0, shard_d0 = 0, shard_D = 0;
   std::string timed_tag;                // set while pev[] hold a serialised verify_device's phases
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
@@ -639,47 +643,62 @@ double ev_ms(dkg_ctx* ctx, int a, int b) {
   return ms;
 }
 
-// lagrange_interpolation at zero (polynomial.rs:162-184) of `rows` share vectors: row r holds the
-// evaluations at x = j + 1 at byte offset 32 * (r * stride + j); the abscissae used are xs (0-based j).
-std::vector<uint8_t> lagrange_at_zero(const std::vector<size_t>& xs, const uint8_t* ys, size_t rows, size_t stride) {
-  std::vector<dkgh::Zl> lambda(xs.size());
-  for (size_t a = 0; a < xs.size(); a++) {
-    dkgh::Zl num = dkgh::zl_from_u64(1), den = dkgh::zl_from_u64(1);
-    for (size_t b = 0; b < xs.size(); b++) {
-      if (a == b) continue;
-      num = dkgh::zl_mul(num, dkgh::zl_sub(dkgh::zl_from_u64(0), dkgh::zl_from_u64(xs[b] + 1)));
-      den = dkgh::zl_mul(den, dkgh::zl_sub(dkgh::zl_from_u64(xs[a] + 1), dkgh::zl_from_u64(xs[b] + 1)));
-    }
-    lambda[a] = dkgh::zl_mul(num, dkgh::zl_inv(den));
+// Lagrange coefficients at zero (polynomial.rs:162-170 with x = 0) over the abscissae x = j + 1 of
+// the parties j < n with in_set[j]: lambda_a = prod_{b != a} x_b / (x_b - x_a).  Over the full
+// range 1..n the denominator is (-1)^(x_a - 1) (x_a - 1)! (n - x_a)!, so with U = {1..n}
+//   lambda_a = P * prod_{e in U \ set} (x_e - x_a) * (-1)^j / ((j+1)! (n-1-j)!),  P = prod_set x_b,
+// which costs O(n + |set| * |U \ set|) multiplications and one inversion (inverse factorials),
+// instead of |set|^2 products and |set| inversions.  Zero for j outside the set.
+std::vector<dkgh::Zl> lagrange_zero_coeffs(size_t n, const uint8_t* in_set) {
+  using namespace dkgh;
+  const Zl zero = zl_from_u64(0), one = zl_from_u64(1);
+  std::vector<Zl> fact(n + 1), ifact(n + 1), lam(n, zero);
+  fact[0] = one;
+  for (size_t k = 1; k <= n; k++) fact[k] = zl_mul(fact[k - 1], zl_from_u64(k));
+  ifact[n] = zl_inv(fact[n]);
+  for (size_t k = n; k > 0; k--) ifact[k - 1] = zl_mul(ifact[k], zl_from_u64(k));
+  Zl P = one;
+  std::vector<size_t> outside;
+  for (size_t j = 0; j < n; j++) {
+    if (in_set[j]) P = zl_mul(P, zl_from_u64(j + 1));
+    else outside.push_back(j);
   }
-  std::vector<uint8_t> secrets;
-  for (size_t r = 0; r < rows; r++) {
-    dkgh::Zl acc = dkgh::zl_from_u64(0);
-    for (size_t a = 0; a < xs.size(); a++) {
-      dkgh::Zl y = dkgh::zl_from_bytes_wide(&ys[32 * (r * stride + xs[a])], 32);
-      acc = dkgh::zl_add(acc, dkgh::zl_mul(lambda[a], y));
-    }
-    uint8_t b[32];
-    dkgh::zl_to_bytes(b, acc);
-    secrets.insert(secrets.end(), b, b + 32);
+  for (size_t j = 0; j < n; j++) {
+    if (!in_set[j]) continue;
+    Zl v = zl_mul(P, zl_mul(ifact[j + 1], ifact[n - 1 - j]));
+    for (size_t e : outside) v = zl_mul(v, zl_sub(zl_from_u64(e + 1), zl_from_u64(j + 1)));
+    lam[j] = (j & 1) ? zl_sub(zero, v) : v;
   }
-  return secrets;
+  return lam;
 }
 
-// Secrets of the reconstructed dealers from the shares of parties 1..t+1 (hs = all shares
-// [n][n][32]).  Shares of a qualified dealer passed every round-2 check, so any t+1 of them
-// interpolate to the same a_i0: the reference's choice at a finalising party -- its own share plus
-// those disclosed by the final parties, committee.rs:755-773 -- gives the same value whenever it
-// has t+1 of them.  (With exactly t points the reference interpolates anyway -- :776-778 compares
-// against `threshold`, not t+1 -- and that party's mpk is wrong; this per-party quirk is not
-// reproduced: DESIGN.md section 2.)
-std::vector<uint8_t> lagrange_secrets(size_t n, size_t t, const uint8_t* recon, const uint8_t* hs) {
-  std::vector<size_t> xs;
-  for (size_t j = 0; j < t + 1; j++) xs.push_back(j);
-  std::vector<uint8_t> rows;
-  for (size_t i = 0; i < n; i++)
-    if (recon[i]) rows.insert(rows.end(), hs + 32 * n * i, hs + 32 * n * (i + 1));
-  return lagrange_at_zero(xs, rows.data(), rows.size() / (32 * n), n);
+// sum_j lambda[j] * y[j] with y[j] the 32-byte scalar at ys + 32 * j (j < n, lambda[j] != 0)
+dkgh::Zl lagrange_dot(const std::vector<dkgh::Zl>& lam, const uint8_t* ys, size_t n) {
+  dkgh::Zl acc = dkgh::zl_from_u64(0);
+  for (size_t j = 0; j < n; j++)
+    if (!dkgh::zl_is_zero(lam[j])) acc = dkgh::zl_add(acc, dkgh::zl_mul(lam[j], dkgh::zl_from_bytes_wide(ys + 32 * j, 32)));
+  return acc;
+}
+
+// The final parties of finalise: qualified and not reconstructable (committee.rs:733-739).
+std::vector<uint8_t> final_parties(size_t n, const uint8_t* qualified, const uint8_t* recon) {
+  std::vector<uint8_t> f(n);
+  for (size_t j = 0; j < n; j++) f[j] = qualified[j] && !recon[j];
+  return f;
+}
+
+// Secrets of the reconstructed dealers (rows `rows` of hs, share row r at hs + 32 * n * r) as the
+// final parties recover them in finalise: a final party p interpolates dealer i's shares at its own
+// index and at every other final party's (committee.rs:754-788), i.e. at exactly the final set, so
+// every final party computes this same value (when all of their phase-5 disclosures arrive; the
+// per-party view with missing disclosures is dkg_finalise_parties).  The dealer's share to itself
+// is never used (it is not a final party), and its other shares all passed round 2.
+std::vector<uint8_t> recon_secrets(size_t n, const std::vector<uint8_t>& fin, const uint8_t* hs,
+                                   const std::vector<size_t>& rows) {
+  const std::vector<dkgh::Zl> lam = lagrange_zero_coeffs(n, fin.data());
+  std::vector<uint8_t> secrets(32 * rows.size());
+  for (size_t r = 0; r < rows.size(); r++) dkgh::zl_to_bytes(&secrets[32 * r], lagrange_dot(lam, hs + 32 * n * rows[r], n));
+  return secrets;
 }
 
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
@@ -730,44 +749,56 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
       else if (h4[i * n + j] == DKG_ACCEPT) honest4[j]++;
     }
   // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
-  std::vector<uint8_t> honest_mask(n);
+  std::vector<uint8_t> honest_mask = final_parties(n, qualified.data(), recon.data());
   size_t nrecon = 0;
+  int32_t nq = 0;
   for (size_t i = 0; i < n; i++) {
-    honest_mask[i] = qualified[i] && !recon[i];
     nrecon += recon[i];
+    nq += qualified[i];
   }
-  uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
-  if (ctx->ext_A) {
-    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, n, A0, n, ctx->stream);
-  } else {
-    uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
-    HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
-    uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
-    dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
+  // Phases<Phase4>::proceed fails for every party when qualified minus reconstructable <= t
+  // (committee.rs:673-677): nobody finalises, so there is no master public key (mpk zeroed)
+  const bool phase4_error = nq - (int32_t)nrecon <= (int32_t)t;
+  memset(out->mpk, 0, 32);
+  if (!phase4_error) {
+    uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
+    if (ctx->ext_A) {
+      dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, n, A0, n, ctx->stream);
+    } else {
+      uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
+      HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
+      uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
+      dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
+    }
+    uint8_t* hmask = buf<uint8_t>(ctx, "hmask", n);
+    h2d(ctx, hmask, honest_mask.data(), n);
+    uint32_t* parts = buf<uint32_t>(ctx, "mpk_parts", PTB * 2);
+    dkgk::sum_points(n, A0, n, hmask, parts, 2, 0, ctx->stream);
+    if (nrecon) {
+      std::vector<size_t> rows;
+      std::vector<uint8_t> hs(32 * n * nrecon);
+      for (size_t i = 0; i < n; i++)
+        if (recon[i]) {
+          d2h(ctx, &hs[32 * n * rows.size()], s + 8 * n * i, 32 * n);
+          rows.push_back(rows.size());
+        }
+      sync(ctx);
+      std::vector<uint8_t> secrets = recon_secrets(n, honest_mask, hs.data(), rows);
+      uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
+      h2d(ctx, sec, secrets.data(), secrets.size());
+      uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
+      dkgk::fixed_base(nrecon, sec, ctx->tab_g8, gsec, ctx->stream);
+      dkgk::sum_points(nrecon, gsec, nrecon, nullptr, parts, 2, 1, ctx->stream);
+    } else {
+      dkgk::sum_points(0, A0, n, nullptr, parts, 2, 1, ctx->stream);  // identity
+    }
+    uint32_t* mpk_ext = buf<uint32_t>(ctx, "mpk_ext", PTB);
+    dkgk::sum_points(2, parts, 2, nullptr, mpk_ext, 1, 0, ctx->stream);
+    uint32_t* mpk_c = buf<uint32_t>(ctx, "mpk_comp", 32);
+    dkgk::encode_points(mpk_ext, 1, 1, mpk_c, ctx->stream);
+    check_launch(ctx);
+    d2h(ctx, out->mpk, mpk_c, 32);
   }
-  uint8_t* hmask = buf<uint8_t>(ctx, "hmask", n);
-  h2d(ctx, hmask, honest_mask.data(), n);
-  uint32_t* parts = buf<uint32_t>(ctx, "mpk_parts", PTB * 2);
-  dkgk::sum_points(n, A0, n, hmask, parts, 2, 0, ctx->stream);
-  if (nrecon) {
-    std::vector<uint8_t> hs(32 * n * n);
-    d2h(ctx, hs.data(), s, 32 * n * n);
-    sync(ctx);
-    std::vector<uint8_t> secrets = lagrange_secrets(n, t, recon.data(), hs.data());
-    uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
-    h2d(ctx, sec, secrets.data(), secrets.size());
-    uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
-    dkgk::fixed_base(nrecon, sec, ctx->tab_g8, gsec, ctx->stream);
-    dkgk::sum_points(nrecon, gsec, nrecon, nullptr, parts, 2, 1, ctx->stream);
-  } else {
-    dkgk::sum_points(0, A0, n, nullptr, parts, 2, 1, ctx->stream);  // identity
-  }
-  uint32_t* mpk_ext = buf<uint32_t>(ctx, "mpk_ext", PTB);
-  dkgk::sum_points(2, parts, 2, nullptr, mpk_ext, 1, 0, ctx->stream);
-  uint32_t* mpk_c = buf<uint32_t>(ctx, "mpk_comp", 32);
-  dkgk::encode_points(mpk_ext, 1, 1, mpk_c, ctx->stream);
-  check_launch(ctx);
-  d2h(ctx, out->mpk, mpk_c, 32);
   HCK(hipEventRecord(ctx->ev[5], ctx->stream));
   // ---- outputs
   if (out->qualified) memcpy(out->qualified, qualified.data(), n);
@@ -776,10 +807,8 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     for (size_t j = 0; j < n; j++) out->r4_error[j] = honest4[j] < t + 1;  // :567-569
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * n);
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
-  int32_t nq = 0;
-  for (auto q : qualified) nq += q;
   out->n_qualified = nq;
-  out->phase4_error = nq - (int32_t)nrecon <= (int32_t)t;  // committee.rs:673-677
+  out->phase4_error = phase4_error;  // committee.rs:673-677
   if (copy_big) {
     if (out->dec2) memcpy(out->dec2, h2.data(), n * n);
     if (out->dec4) memcpy(out->dec4, h4.data(), n * n);
@@ -865,14 +894,18 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
   std::vector<size_t> recon_cer;
+  std::vector<uint8_t> p4err(B, 0);
   for (size_t c = 0; c < B; c++) {
     bool any = false;
+    int32_t h = 0;
     for (size_t i = c * n; i < (c + 1) * n; i++) {
       recon[i] = qualified[i] && rej4[i];
       honest[i] = qualified[i] && !recon[i];
       any |= recon[i] != 0;
+      h += honest[i];
     }
-    if (any) recon_cer.push_back(c);
+    p4err[c] = h <= (int32_t)t;  // committee.rs:673-677: nobody finalises, no mpk
+    if (any && !p4err[c]) recon_cer.push_back(c);
   }
   // finalise (committee.rs:726-805): mpk_c = sum of honest A_i0 (+ g * reconstructed secrets)
   uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
@@ -894,7 +927,11 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
     for (size_t c : recon_cer) {
       d2h(ctx, hs.data(), s + c * n * n * 8, 32 * n * n);
       sync(ctx);
-      std::vector<uint8_t> secrets = lagrange_secrets(n, t, &recon[c * n], hs.data());
+      std::vector<size_t> rows;
+      for (size_t i = 0; i < n; i++)
+        if (recon[c * n + i]) rows.push_back(i);
+      std::vector<uint8_t> secrets = recon_secrets(n, std::vector<uint8_t>(&honest[c * n], &honest[(c + 1) * n]),
+                                                   hs.data(), rows);
       const size_t nr = secrets.size() / 32;
       uint32_t* sec = buf<uint32_t>(ctx, "b.recon_sec", 32 * nr);
       h2d(ctx, sec, secrets.data(), secrets.size());
@@ -935,12 +972,10 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), V);
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * V);
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), V);
-  if (out->phase4_error)
-    for (size_t c = 0; c < B; c++) {
-      int32_t h = 0;
-      for (size_t i = c * n; i < (c + 1) * n; i++) h += qualified[i] && !recon[i];
-      out->phase4_error[c] = h <= (int32_t)t;  // committee.rs:673-677
-    }
+  if (out->phase4_error) memcpy(out->phase4_error, p4err.data(), B);  // committee.rs:673-677
+  if (out->mpk)
+    for (size_t c = 0; c < B; c++)
+      if (p4err[c]) memset(out->mpk + 32 * c, 0, 32);  // no party finalises: no master key
   if (out->n_qualified)
     for (size_t c = 0; c < B; c++) {
       int32_t q = 0;
@@ -1326,6 +1361,23 @@ int dkg_share_gen(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint8_t* a, 
   });
 }
 
+int dkg_share_gen_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const void* d_a, const void* d_b, void* d_E,
+                         void* d_A, void* d_s, void* d_s_prime) {
+  return guarded(ctx, [&] {
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    if (!d_a || !d_b || !d_s || !d_s_prime) return DKG_E_ARG;
+    if (D == 0) return DKG_OK;
+    const size_t N = t + 1;
+    uint32_t* Ec = d_E ? (uint32_t*)d_E : buf<uint32_t>(ctx, "sgd_E", 32 * D * N);
+    uint32_t* Ac = d_A ? (uint32_t*)d_A : buf<uint32_t>(ctx, "sgd_A", 32 * D * N);
+    round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, (uint32_t*)d_s,
+                  (uint32_t*)d_s_prime, d_E || d_A);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
 int dkg_verify_pairs(dkg_ctx* ctx, size_t n, size_t t, int round, size_t d0, size_t d1, const uint8_t* C,
                      const uint8_t* s, const uint8_t* s_prime, uint8_t* decision) {
   return guarded(ctx, [&] {
@@ -1525,38 +1577,12 @@ void shard_rows(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t D, const uin
   } else {
     HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
   }
-  // Round-4 accusations against a qualified dealer put it in the reconstructable set
-  // (committee.rs:660-670) -- again a function of its own row.  Its mpk term becomes g * a_i0
-  // recovered by Lagrange interpolation of its shares (finalise, :747-783); the shares of this
-  // rank's dealers are on this GPU, so the term is computed here and sent in place of A_i0.
-  std::vector<uint8_t> r4(D * n);
-  d2h(ctx, r4.data(), d_dec4, D * n);
-  sync(ctx);
-  std::vector<size_t> recon;
-  for (size_t i = 0; i < D; i++) {
-    bool acc = false;
-    for (size_t j = 0; j < n; j++) acc |= j != d0 + i && r4[i * n + j] == DKG_REJECT;
-    if (q[i] && acc) recon.push_back(i);
-  }
-  if (!recon.empty()) {
-    const size_t R = recon.size();
-    std::vector<uint8_t> hs(32 * n * R);
-    for (size_t r = 0; r < R; r++) d2h(ctx, &hs[32 * n * r], ds + 8 * n * recon[r], 32 * n);
-    sync(ctx);
-    // the first t+1 parties' shares: a qualified dealer's shares all passed round 2, so any t+1
-    // of them interpolate to the same a_i0 as the single-GPU driver's choice
-    std::vector<size_t> xs(N);
-    for (size_t j = 0; j < N; j++) xs[j] = j;
-    std::vector<uint8_t> secrets = lagrange_at_zero(xs, hs.data(), R, n);
-    uint32_t* sec = buf<uint32_t>(ctx, "sh_rsec", 32 * R);
-    uint32_t* gsec = buf<uint32_t>(ctx, "sh_rext", PTB * R);
-    uint32_t* gc = buf<uint32_t>(ctx, "sh_rcomp", 32 * R);
-    h2d(ctx, sec, secrets.data(), secrets.size());
-    dkgk::fixed_base(R, sec, ctx->tab_g8, gsec, ctx->stream);
-    dkgk::encode_points(gsec, R, R, gc, ctx->stream);
-    for (size_t r = 0; r < R; r++)
-      HCK(hipMemcpyAsync((uint8_t*)d_A0 + 32 * recon[r], gc + 8 * r, 32, hipMemcpyDeviceToDevice, ctx->stream));
-  }
+  // A dealer accused in round 4 (committee.rs:660-670) has its term replaced after the exchange,
+  // once the final parties are known (dkg_ceremony_shard_recon_device): its shares stay here.
+  ctx->shard_s = ds;
+  ctx->shard_n = n;
+  ctx->shard_d0 = d0;
+  ctx->shard_D = D;
   uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
   h2d(ctx, qm, q.data(), D);
   dkgk::sum_shares(D, n, ds, qm, (uint32_t*)d_partial, ctx->stream);  // partial of :454-462
@@ -1610,6 +1636,187 @@ int dkg_ceremony_shard_verify_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     sync(ctx);
     if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
+    return DKG_OK;
+  });
+}
+
+int dkg_ceremony_shard_recon_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t d1, const uint8_t* qualified,
+                                    const uint8_t* reconstruct, const void* d_s, void* d_terms) {
+  return guarded(ctx, [&] {
+    if (!qualified || !reconstruct || !d_terms || d1 < d0 || d1 > n || dkg_env_check(t, n) != DKG_OK) return DKG_E_ARG;
+    const size_t D = d1 - d0;
+    std::vector<size_t> rows;
+    for (size_t i = 0; i < D; i++) {
+      if (reconstruct[d0 + i] && !qualified[d0 + i]) {
+        ctx->err = "shard_recon: only qualified members are reconstructed (committee.rs:746-747)";
+        return DKG_E_ARG;
+      }
+      if (reconstruct[d0 + i]) rows.push_back(i);
+    }
+    if (rows.empty()) return DKG_OK;
+    const uint32_t* ds = nullptr;
+    if (d_s) {  // received shares: Scalar::from_bytes semantics
+      uint32_t* red = buf<uint32_t>(ctx, "shr_s", 32 * D * n);
+      dkgk::reduce_scalars(D * n, (const uint32_t*)d_s, red, ctx->stream);
+      ds = red;
+    } else {
+      if (!ctx->shard_s || ctx->shard_n != n || ctx->shard_d0 != d0 || ctx->shard_D != D) {
+        ctx->err = "shard_recon: d_s is NULL and the last sharded call on this ctx had other dealers";
+        return DKG_E_ARG;
+      }
+      ds = ctx->shard_s;
+    }
+    const size_t R = rows.size();
+    std::vector<uint8_t> hs(32 * n * R);
+    for (size_t r = 0; r < R; r++) d2h(ctx, &hs[32 * n * r], ds + 8 * n * rows[r], 32 * n);
+    sync(ctx);
+    std::vector<size_t> idx(R);
+    for (size_t r = 0; r < R; r++) idx[r] = r;
+    std::vector<uint8_t> secrets = recon_secrets(n, final_parties(n, qualified, reconstruct), hs.data(), idx);
+    uint32_t* sec = buf<uint32_t>(ctx, "sh_rsec", 32 * R);
+    uint32_t* gsec = buf<uint32_t>(ctx, "sh_rext", PTB * R);
+    uint32_t* gc = buf<uint32_t>(ctx, "sh_rcomp", 32 * R);
+    h2d(ctx, sec, secrets.data(), secrets.size());
+    dkgk::fixed_base(R, sec, ctx->tab_g8, gsec, ctx->stream);  // G::generator() * recovered (:789)
+    dkgk::encode_points(gsec, R, R, gc, ctx->stream);
+    for (size_t r = 0; r < R; r++)
+      HCK(hipMemcpyAsync((uint8_t*)d_terms + 32 * rows[r], gc + 8 * r, 32, hipMemcpyDeviceToDevice, ctx->stream));
+    check_launch(ctx);
+    sync(ctx);
+    return DKG_OK;
+  });
+}
+
+int dkg_finalise_parties(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* qualified, const uint8_t* reconstruct,
+                         const uint8_t* r2_error, const uint8_t* r4_error, const uint8_t* disclosed, const uint8_t* A0,
+                         const uint8_t* s, uint8_t* mpk, int32_t* status, int32_t* recovery_index) {
+  return guarded(ctx, [&] {
+    using namespace dkgh;
+    if (!qualified || !reconstruct || !A0 || !s || !mpk || !status) return DKG_E_ARG;
+    if (!n) return DKG_OK;
+    std::vector<size_t> recon;
+    int32_t nq = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (reconstruct[i] && !qualified[i]) {
+        ctx->err = "finalise: only qualified members should be reconstructed (committee.rs:746-747 panics)";
+        return DKG_E_ARG;
+      }
+      nq += qualified[i] != 0;
+      if (reconstruct[i]) recon.push_back(i);
+    }
+    const std::vector<uint8_t> fin = final_parties(n, qualified, reconstruct);
+    const bool phase4 = nq - (int32_t)recon.size() <= (int32_t)t;  // committee.rs:673-677
+    // S: final parties whose phase-5 disclosures the finalising party fetched (committee.rs:763-775)
+    std::vector<uint8_t> S(n);
+    size_t nS = 0;
+    for (size_t j = 0; j < n; j++) nS += S[j] = fin[j] && (!disclosed || disclosed[j]);
+    const Zl zero = zl_from_u64(0), one = zl_from_u64(1);
+    std::vector<Zl> lamS, yrows;  // Lagrange coefficients over S; the reconstructed rows' shares
+    if (!recon.empty() && !phase4) {
+      lamS = lagrange_zero_coeffs(n, S.data());
+      yrows.resize(recon.size() * n);
+      for (size_t r = 0; r < recon.size(); r++)
+        for (size_t j = 0; j < n; j++) yrows[r * n + j] = zl_from_bytes_wide(s + 32 * (recon[r] * n + j), 32);
+    }
+    Zl PS = one;
+    for (size_t j = 0; j < n; j++)
+      if (S[j]) PS = zl_mul(PS, zl_from_u64(j + 1));
+    std::vector<uint8_t> sig(32 * n, 0), ok(n, 0);
+    std::vector<Zl> mu(n), inv(n), pre(n);
+    for (size_t p = 0; p < n; p++) {
+      if (recovery_index) recovery_index[p] = -1;
+      if (r2_error && r2_error[p]) { status[p] = DKG_FIN_R2_ERROR; continue; }   // committee.rs:340-347
+      if (r4_error && r4_error[p]) { status[p] = DKG_FIN_R4_ERROR; continue; }   // :567-569
+      if (phase4) { status[p] = DKG_FIN_PHASE4_ERROR; continue; }                // :673-677
+      // the party's own share plus the fetched disclosures of the other final parties (:754-775)
+      const size_t cnt = nS + (S[p] ? 0 : 1);
+      // finalise walks the dealers in index order (:745-797) and stops at the first of: a
+      // reconstructed dealer with fewer than `threshold` (t, not t + 1) points ->
+      // InsufficientSharesForRecovery(i) (:779-781); a disqualified dealer other than itself ->
+      // the reference PANICS: its committed coefficients were never recorded (committed_shares[i]
+      // is set only for itself, :190, and for qualified dealers in Phase3::proceed, :527-530) and
+      // :791-794 expect() them.  A disqualified party p adds its own A_p0 (its init state).
+      status[p] = DKG_FIN_OK;
+      for (size_t i = 0; i < n && status[p] == DKG_FIN_OK; i++) {
+        if (reconstruct[i] && cnt < t) status[p] = DKG_FIN_INSUFFICIENT;
+        else if (!reconstruct[i] && !qualified[i] && i != p) status[p] = DKG_FIN_PANIC;
+        if (status[p] != DKG_FIN_OK && recovery_index) recovery_index[p] = (int32_t)i;
+      }
+      if (status[p] != DKG_FIN_OK) continue;
+      ok[p] = 1;
+      if (recon.empty()) continue;
+      const std::vector<Zl>* lam = &lamS;
+      if (!S[p]) {
+        // T = S u {p}: mu_a = lambda^S_a x_p / (x_p - x_a) (a in S), mu_p = prod_{b in S} x_b / (x_b - x_p)
+        const Zl xp = zl_from_u64(p + 1);
+        std::vector<size_t> as;
+        for (size_t a = 0; a < n; a++)
+          if (S[a]) as.push_back(a);
+        Zl acc = one;  // batch inversion of (x_p - x_a)
+        for (size_t k = 0; k < as.size(); k++) {
+          pre[k] = acc;
+          inv[k] = zl_sub(xp, zl_from_u64(as[k] + 1));
+          acc = zl_mul(acc, inv[k]);
+        }
+        Zl ia = zl_inv(acc);
+        for (size_t k = as.size(); k-- > 0;) {
+          const Zl d = inv[k];
+          inv[k] = zl_mul(ia, pre[k]);
+          ia = zl_mul(ia, d);
+        }
+        Zl prod = one;
+        for (size_t a = 0; a < n; a++) mu[a] = zero;
+        for (size_t k = 0; k < as.size(); k++) {
+          mu[as[k]] = zl_mul(zl_mul(lamS[as[k]], xp), inv[k]);
+          prod = zl_mul(prod, zl_sub(zero, inv[k]));  // 1 / (x_b - x_p)
+        }
+        mu[p] = zl_mul(PS, prod);
+        lam = &mu;
+      }
+      Zl sigma = zero;  // sum over the reconstructed dealers of the recovered secrets (:784-789)
+      for (size_t r = 0; r < recon.size(); r++)
+        for (size_t a = 0; a < n; a++)
+          if (!zl_is_zero((*lam)[a])) sigma = zl_add(sigma, zl_mul((*lam)[a], yrows[r * n + a]));
+      zl_to_bytes(&sig[32 * p], sigma);
+    }
+    memset(mpk, 0, 32 * n);
+    size_t nok = 0;
+    for (auto v : ok) nok += v;
+    if (!nok) return DKG_OK;
+    // mpk_p = sum_{final i} A_i0 + G::generator() * sigma_p (:789-795), on the device
+    uint32_t* a0c = buf<uint32_t>(ctx, "fp_a0c", 32 * n);
+    uint32_t* a0e = buf<uint32_t>(ctx, "fp_a0e", PTB * n);
+    uint8_t* a0ok = buf<uint8_t>(ctx, "fp_a0ok", n);
+    uint8_t* fm = buf<uint8_t>(ctx, "fp_fin", n);
+    uint32_t* hsum = buf<uint32_t>(ctx, "fp_h", PTB);
+    uint32_t* hrep = buf<uint32_t>(ctx, "fp_hrep", PTB * n);
+    uint32_t* sd = buf<uint32_t>(ctx, "fp_sig", 32 * n);
+    uint32_t* ge = buf<uint32_t>(ctx, "fp_ge", PTB * n);
+    uint32_t* oc = buf<uint32_t>(ctx, "fp_out", 32 * n);
+    h2d(ctx, a0c, A0, 32 * n);
+    h2d(ctx, fm, fin.data(), n);
+    h2d(ctx, sd, sig.data(), 32 * n);
+    dkgk::decode_points(a0c, n, a0e, n, a0ok, ctx->stream);
+    dkgk::sum_points(n, a0e, n, fm, hsum, 1, 0, ctx->stream);
+    dkgk::gather_points(hsum, 1, 0, 0, n, hrep, n, ctx->stream);
+    // a finalising disqualified party (the only disqualified dealer) also adds its own A_p0
+    for (size_t p = 0; p < n; p++)
+      if (ok[p] && !qualified[p]) dkgk::add_points(1, hrep + p, a0e + p, n, hrep + p, ctx->stream);
+    dkgk::fixed_base(n, sd, ctx->tab_g8, ge, ctx->stream);
+    dkgk::add_points(n, ge, hrep, n, ge, ctx->stream);
+    dkgk::encode_points(ge, n, n, oc, ctx->stream);
+    check_launch(ctx);
+    std::vector<uint8_t> okh(n), outh(32 * n);
+    d2h(ctx, okh.data(), a0ok, n);
+    d2h(ctx, outh.data(), oc, 32 * n);
+    sync(ctx);
+    for (size_t i = 0; i < n; i++)
+      if ((fin[i] || (ok[i] && !qualified[i])) && !okh[i]) {
+        ctx->err = "finalise: a summed A_0 commitment does not decode";
+        return DKG_E_DECODE;
+      }
+    for (size_t p = 0; p < n; p++)
+      if (ok[p]) memcpy(mpk + 32 * p, &outh[32 * p], 32);
     return DKG_OK;
   });
 }

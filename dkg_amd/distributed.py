@@ -170,9 +170,9 @@ class ShardedCeremony:
         ms = self.be.ceremony_shard_verify_device(self.n, self.t, self.d0, self.d1, d_E, d_A, d_s, d_sp,
                                                   self.dec2.data_ptr(), self.dec4.data_ptr(),
                                                   self.A0.data_ptr(), self.part.data_ptr())
-        return self._finish(ms, finalise)
+        return self._finish(ms, finalise, d_s)
 
-    def _finish(self, ms: float, finalise: bool) -> ShardResult:
+    def _finish(self, ms: float, finalise: bool, d_s: Optional[int] = None) -> ShardResult:
         n, t = self.n, self.t
         dec2, dec4, A0, parts = self.exchange()
         dec = combine_decisions(dec2, dec4, n, t)
@@ -182,10 +182,20 @@ class ShardedCeremony:
             fs_t = torch.empty(n * 32, dtype=torch.uint8, device=self.dev)
             self.be.scalar_sum_device(self.ws, n, parts.data_ptr(), None, fs_t.data_ptr())
             fs = bytes(fs_t.cpu().numpy())
-            # the gathered terms are A_i0 for honest dealers and g * a_i0 (reconstructed on the
-            # owning rank) for the reconstructable set, so the sum runs over the qualified set
-            mask = torch.from_numpy(dec.qualified).to(self.dev)
-            mpk_t = torch.empty(32, dtype=torch.uint8, device=self.dev)
-            self.be.point_sum_device(n, A0.data_ptr(), mask.data_ptr(), mpk_t.data_ptr())
-            mpk = bytes(mpk_t.cpu().numpy())
+            if dec.reconstruct.any() and not dec.phase4_error:
+                # a dealer accused in round 4 (committee.rs:660-670) enters mpk as g * a_i0 over the
+                # final parties' shares (:747-789): the owning rank replaces its term and the terms
+                # are gathered again (the interpolation points depend on every rank's rows)
+                self.be.ceremony_shard_recon_device(n, t, self.d0, self.d1, dec.qualified, dec.reconstruct, d_s,
+                                                    self.A0.data_ptr())
+                self._all_gather(self.g_A0, self.A0)
+                A0 = torch.cat([self.g_A0[r * self.R * 32:(r * self.R + b - a) * 32]
+                                for r, (a, b) in enumerate(dealer_range(q, self.ws, n) for q in range(self.ws))])
+            if not dec.phase4_error:  # else Phases<Phase4>::proceed fails for everyone: no mpk (:673-677)
+                # the terms are A_i0 for honest dealers and g * a_i0 for the reconstructable set, so
+                # the sum runs over the qualified set
+                mask = torch.from_numpy(dec.qualified).to(self.dev)
+                mpk_t = torch.empty(32, dtype=torch.uint8, device=self.dev)
+                self.be.point_sum_device(n, A0.data_ptr(), mask.data_ptr(), mpk_t.data_ptr())
+                mpk = bytes(mpk_t.cpu().numpy())
         return ShardResult(dec, fs, mpk, ms)

@@ -113,6 +113,11 @@ int dkg_points_valid_batch(dkg_ctx *ctx, size_t count, const uint8_t *points, ui
  * Requires dkg_env_init (for h).  Any output may be NULL to skip it. */
 int dkg_share_gen(dkg_ctx *ctx, size_t D, size_t n, size_t t, const uint8_t *a, const uint8_t *b, uint8_t *E,
                   uint8_t *A, uint8_t *s, uint8_t *s_prime);
+/* The same on device buffers (canonical scalars d_a, d_b [D][t+1][32] in; d_E, d_A [D][t+1][32]
+ * compressed -- either may be NULL -- and d_s, d_s_prime [D][n][32] out), e.g. to build the
+ * broadcasts of a large committee in HBM for dkg_ceremony_shard_verify_device. */
+int dkg_share_gen_device(dkg_ctx *ctx, size_t D, size_t n, size_t t, const void *d_a, const void *d_b, void *d_E,
+                         void *d_A, void *d_s, void *d_s_prime);
 
 /* ---- rounds 2 and 4: share checks ----
  * round 2 (Phases<Phase1>::proceed, committee.rs:273-338): h*s' + g*s == sum_k (j+1)^k E_i[k]
@@ -145,11 +150,17 @@ typedef struct {
   uint8_t *reconstruct;         /* [n] dealers whose secret is reconstructed in finalise */
   uint8_t *final_share;         /* [n][32] s_j = sum_{i in Q} s_ij (committee.rs:454-462) */
   uint8_t *public_share;        /* [n][32] g * s_j (committee.rs:464-466) */
-  uint8_t mpk[32];              /* MasterPublicKey (committee.rs:726-805) */
+  uint8_t mpk[32];              /* MasterPublicKey (committee.rs:726-805) that every final party
+                                   (qualified, not reconstructable) computes when all final parties'
+                                   phase-5 disclosures arrive: a reconstructed dealer's secret is
+                                   interpolated at zero over exactly the final parties' shares
+                                   (:754-788).  ALL ZERO and meaningless when phase4_error == 1.
+                                   Other parties' views, and missing disclosures:
+                                   dkg_finalise_parties. */
   int32_t n_qualified;
   int32_t phase4_error;         /* 1: qualified minus reconstructable <= t, every party's
                                    Phases<Phase4>::proceed fails with MisbehaviourHigherThreshold
-                                   (committee.rs:673-677) -- mpk is then the value it would have */
+                                   (committee.rs:673-677): nobody finalises, there is no mpk */
   /* device times of each phase, milliseconds (HIP events) */
   double ms_round1, ms_round2, ms_round3, ms_round4, ms_finalise, ms_total;
 } dkg_ceremony_out;
@@ -179,11 +190,11 @@ int dkg_ceremony_run_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, c
  * ceremony.  Produces this rank's commitments E/A and decision rows; the caller all-gathers
  * (RCCL over xGMI) the rows, A_0 values and share partial sums.  Device pointers throughout:
  * d_a, d_b [d1-d0][t+1][32]; d_dec2, d_dec4 [d1-d0][n]; d_A0 [d1-d0][32] = each dealer's
- * compressed master-key term: A_i0, or g * a_i0 recovered by Lagrange interpolation of its shares
- * when round-4 accusations put a qualified dealer in the reconstructable set (committee.rs:747-783;
- * both are decided by the dealer's own rows, so mpk = sum of the terms of qualified dealers);
- * d_partial [n][32] = sum over this rank's QUALIFIED dealers of s_ij (qualification of a dealer is
- * decided by its own round-2 row, so it needs no exchange). */
+ * compressed master-key term A_i0 (a dealer that round-4 accusations put in the reconstructable set
+ * gets g * a_i0 after the exchange, dkg_ceremony_shard_recon_device, because the interpolation
+ * points -- the final parties -- depend on every rank's rows; then mpk = sum of the qualified
+ * dealers' terms); d_partial [n][32] = sum over this rank's QUALIFIED dealers of s_ij (qualification
+ * of a dealer is decided by its own round-2 row, so it needs no exchange). */
 int dkg_ceremony_shard_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const void *d_a,
                               const void *d_b, void *d_dec2, void *d_dec4, void *d_A0, void *d_partial,
                               double *ms_total);
@@ -195,6 +206,15 @@ int dkg_ceremony_shard_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_
 int dkg_ceremony_shard_verify_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const void *d_E,
                                      const void *d_A, const void *d_s, const void *d_s_prime, void *d_dec2,
                                      void *d_dec4, void *d_A0, void *d_partial, double *ms_total);
+/* Finalise step of a sharded run, after the exchange (committee.rs:747-789): for this rank's dealers
+ * [d0, d1) with reconstruct[i] (host [n], the combined round-4 outcome), d_terms[i - d0] (device
+ * [d1-d0][32], the rank's exchanged master-key terms, in/out) is replaced by g * a_i0 recovered by
+ * Lagrange interpolation at zero over the shares of the final parties (qualified[j] && !reconstruct[j],
+ * host [n]) -- the value every final party computes.  d_s: the dealers' share rows [d1-d0][n][32]
+ * (from_bits semantics), or NULL for the rows of the last dkg_ceremony_shard_device /
+ * _shard_verify_device call on this ctx (same n, d0, d1).  Dealers without reconstruct are untouched. */
+int dkg_ceremony_shard_recon_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const uint8_t *qualified,
+                                    const uint8_t *reconstruct, const void *d_s, void *d_terms);
 /* Combine step of the sharded run (device pointers):
  * round-3 sum (committee.rs:454-462): out[j] = sum over rows r with mask[r] (NULL = all) of in[r][j]
  * mod l; in [rows][n][32] canonical scalars (e.g. the all-gathered per-rank partials), out [n][32]. */
@@ -203,6 +223,32 @@ int dkg_scalar_sum_device(dkg_ctx *ctx, size_t rows, size_t n, const void *d_in,
  * [count][32] compressed, out [32] compressed.  DKG_E_DECODE if a selected point does not decode. */
 int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const void *d_mask, void *d_out);
 
+/* ---- per-party finalise: Phases<Phase5>::finalise (committee.rs:726-805) as EVERY party p runs it ----
+ * Inputs are the ceremony's common outcome (host arrays [n]): qualified, reconstruct (round 4,
+ * committee.rs:660-670), r2_error / r4_error (may be NULL: a party whose Phase1 / Phase3 proceed failed
+ * never finalises), disclosed (may be NULL = all): 0 for a party whose phase-5 broadcast (its
+ * disclosed shares, BroadcastPhase5) party p does not fetch; A0 [n][32] the dealers' A_i0 (phase-3
+ * broadcasts); s [n dealer][n receiver][32] the shares.  For each reconstructed dealer i party p
+ * interpolates at zero over its own share s_ip and the disclosed shares of the OTHER final parties
+ * (:754-775); it fails with InsufficientSharesForRecovery(i) -- i the first reconstructed dealer --
+ * when it has fewer than `threshold` = t points (:779-781; exactly t points interpolate a wrong
+ * secret, as the reference does).  Outputs [n]: mpk[p] (32 bytes, zero unless status[p] == OK),
+ * status[p], recovery_index[p] (the dealer i of InsufficientSharesForRecovery / the panic, else
+ * -1; may be NULL).  Dealers are visited in index order and the first failure wins, as in the loop
+ * of committee.rs:745-797. */
+#define DKG_FIN_OK 0
+#define DKG_FIN_R2_ERROR 1      /* Phases<Phase1>::proceed: MisbehaviourHigherThreshold (committee.rs:340-347) */
+#define DKG_FIN_R4_ERROR 2      /* Phases<Phase3>::proceed: MisbehaviourHigherThreshold (committee.rs:567-569) */
+#define DKG_FIN_PHASE4_ERROR 3  /* Phases<Phase4>::proceed: MisbehaviourHigherThreshold (committee.rs:673-677) */
+#define DKG_FIN_INSUFFICIENT 4  /* finalise: InsufficientSharesForRecovery(i) (committee.rs:779-781) */
+#define DKG_FIN_PANIC 5         /* finalise panics at dealer i: i is disqualified and i != p, so its
+                                   committed coefficients were never recorded (committee.rs:791-794
+                                   expect()s them; they are stored only at :190 and :527-530).  A
+                                   disqualified party p itself adds its own A_p0 (:190). */
+int dkg_finalise_parties(dkg_ctx *ctx, size_t n, size_t t, const uint8_t *qualified, const uint8_t *reconstruct,
+                         const uint8_t *r2_error, const uint8_t *r4_error, const uint8_t *disclosed, const uint8_t *A0,
+                         const uint8_t *s, uint8_t *mpk, int32_t *status, int32_t *recovery_index);
+
 /* ---- batches of independent ceremonies (BASELINE config 5: e.g. 10,000 ceremonies of n = 64) ----
  * B ceremonies with the same (n, t) and commitment key, each played as dkg_ceremony_run plays one
  * (full_valid_run, committee.rs:1518-1656): rounds 1-5 for every party of every ceremony.
@@ -210,7 +256,8 @@ int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const
  * what B separate single-ceremony calls return (the work of all B shares each kernel launch). */
 typedef struct {
   /* host outputs; any pointer may be NULL */
-  uint8_t *mpk;                 /* [B][32] MasterPublicKey per ceremony (committee.rs:726-805) */
+  uint8_t *mpk;                 /* [B][32] MasterPublicKey per ceremony (committee.rs:726-805), as in
+                                   dkg_ceremony_out; all zero for a ceremony with phase4_error */
   int32_t *n_qualified;         /* [B] */
   uint8_t *phase4_error;        /* [B] qualified minus reconstructable <= t (committee.rs:673-677) */
   uint8_t *qualified;           /* [B][n] */

@@ -162,3 +162,45 @@ void or_lagrange(uint8_t out[32], const uint8_t x[32], const uint8_t *ys, const 
   }
   memcpy(out, result, 32);
 }
+
+/* ---- single-thread cost calibration of this port (bench.py cpu_baseline): dalek-3's published
+ * u64-backend figures are per field multiplication and per MSM, so the port's own are reported
+ * next to its verified-shares rate. */
+#include <time.h>
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+/* ns per fe51_mul in a dependent chain of `iters` multiplications */
+double or_bench_fe_mul(uint64_t iters) {
+  fe51 a = {{1234567, 7654321, 1111111, 2222222, 3333333}}, b = {{99, 98, 97, 96, 95}};
+  const double t0 = now_s();
+  for (uint64_t i = 0; i < iters; i++) fe51_mul(&a, &a, &b);
+  const double dt = now_s() - t0;
+  volatile uint64_t sink = a.v[0];
+  (void)sink;
+  return dt / (double)iters * 1e9;
+}
+
+/* ms per vartime MSM of N random-looking terms (dalek's Straus / Pippenger choice), `reps` runs */
+double or_bench_msm(size_t N, int reps) {
+  ge_ext g, *pts = malloc(N * sizeof *pts), r;
+  uint8_t *sc = malloc(32 * N), seed[32] = {7};
+  ge_base_point(&g);
+  or_chacha20_stream(seed, 0, sc, 32 * N);
+  for (size_t k = 0; k < N; k++) {
+    sc[32 * k + 31] &= 0x0f;
+    uint8_t e[32] = {0};
+    e[0] = (uint8_t)(k + 3);
+    e[1] = (uint8_t)((k + 3) >> 8);
+    ge_mul_vartime_base(&pts[k], &g, e);
+  }
+  const double t0 = now_s();
+  for (int i = 0; i < reps; i++) ge_msm(&r, N, sc, pts);
+  const double dt = now_s() - t0;
+  free(pts);
+  free(sc);
+  return dt / reps * 1e3;
+}

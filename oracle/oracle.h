@@ -100,6 +100,9 @@ int or_complaint3_verify(const uint8_t h[32], size_t t, uint32_t accuser, const 
                          const uint8_t randomness[32], const uint8_t *E, const uint8_t *A);
 /* Lagrange interpolation at x (polynomial.rs:162-184). */
 void or_lagrange(uint8_t out[32], const uint8_t x[32], const uint8_t *ys, const uint8_t *xs, size_t m);
+/* single-thread cost calibration (bench.py cpu_baseline): ns per field multiplication, ms per MSM */
+double or_bench_fe_mul(uint64_t iters);
+double or_bench_msm(size_t N, int reps);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,76 @@
+"""One rank of tests/test_gpu_dist.py (not a test module): a dealer-sharded ceremony end to end
+through dkg_amd.distributed.ShardedCeremony on GPU 0, ranks sharing the GPU over gloo (the
+rehearsal mode of bench.py --dist-backend gloo).  Started as a child process with RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT set; rank 0 writes every ceremony's combined outputs as
+JSON to argv[1]."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (before libdkg_amd.so: its HIP runtime must be torch's)
+import torch.distributed as dist  # noqa: E402
+
+import dkg_amd  # noqa: E402
+from dkg_amd.distributed import ShardedCeremony, dealer_range  # noqa: E402
+
+HONEST = ["ceremony_n16_t7.json", "ceremony_n64_t31.json"]
+FAULTS = ["fault_a_generator_n10_t4.json", "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json",
+          "fault_a_many_n10_t4.json", "fault_share_flip_n10_t4.json"]
+H = bytes.fromhex
+
+
+def golden(name):
+    with open(os.path.join(ROOT, "tests", "golden", name)) as f:
+        return json.load(f)
+
+
+def summary(res):
+    d = res.decisions
+    b = lambda x: bytes(x.reshape(-1).cpu().numpy()) if hasattr(x, "cpu") else bytes(x.reshape(-1))  # noqa: E731
+    return {"dec2": "".join(str(v) for v in b(d.dec2)), "dec4": "".join(str(v) for v in b(d.dec4)),
+            "qualified": [int(x) for x in d.qualified], "reconstruct": [int(x) for x in d.reconstruct],
+            "complaints2": [int(x) for x in d.complaints2], "r4_error": [int(x) for x in d.r4_error],
+            "phase4_error": bool(d.phase4_error), "final_share": res.final_share.hex(),
+            "mpk": res.mpk.hex() if res.mpk is not None else None}
+
+
+def main(out_path):
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo")
+    ws = dist.get_world_size()
+    dev = torch.device("cuda", 0)
+    be = dkg_amd.Backend(0)
+    put = lambda x: torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)  # noqa: E731
+    out = {}
+    for name in HONEST:  # share generation + checks of this rank's dealers, exchange, combine, finalise
+        c = golden(name)
+        n, t = c["n"], c["t"]
+        be.env_init(t, n)
+        d0, d1 = dealer_range(rank, ws, n)
+        a, b = dkg_amd.dealer_coefficients(H(c["master_seed"]), c["ceremony"], d0, d1 - d0, t)
+        ta, tb = put(a), put(b)  # keep both alive: a freed temporary's memory would be handed to the next
+        out[name] = summary(ShardedCeremony(be, dist, n, t, dev).run(ta.data_ptr(), tb.data_ptr()))
+    for name in FAULTS:  # received (tampered) broadcasts: rounds 2-5 incl. the reconstruction exchange
+        c = golden(name)
+        n, t = c["n"], c["t"]
+        N = t + 1
+        be.env_init(t, n)
+        d0, d1 = dealer_range(rank, ws, n)
+        E, A, s, sp = (H(c[k]) for k in ("E", "A", "s", "s_prime"))
+        tE, tA = put(E[32 * N * d0:32 * N * d1]), put(A[32 * N * d0:32 * N * d1])
+        ts, tsp = put(s[32 * n * d0:32 * n * d1]), put(sp[32 * n * d0:32 * n * d1])
+        sc = ShardedCeremony(be, dist, n, t, dev)
+        out[name] = summary(sc.run_verify(tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr()))
+    dist.barrier()
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(out, f)
+    be.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

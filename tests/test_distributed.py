@@ -137,3 +137,126 @@ def test_combine_torch_matches_numpy(golden):
         for f in ("qualified", "complaints2", "r2_error", "reconstruct", "r4_error", "honest"):
             assert getattr(a, f).tolist() == getattr(b, f).tolist(), (name, f)
         assert a.dec4.reshape(-1).tolist() == b.dec4.reshape(-1).tolist() and a.phase4_error == b.phase4_error
+
+
+class OracleBackend:
+    """Stand-in for dkg_amd.Backend on CPU tensors (test double, oracle arithmetic): the device
+    entry points ShardedCeremony calls, computed by the CPU oracle and written through the
+    tensors' pointers.  Lets the whole ShardedCeremony.run_verify orchestration -- exchange,
+    combine, the reconstruction exchange, finalise -- run in gloo processes without a GPU."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @staticmethod
+    def _rd(ptr, size):
+        import ctypes
+        return ctypes.string_at(ptr, size)
+
+    @staticmethod
+    def _wr(ptr, data):
+        import ctypes
+        ctypes.memmove(ptr, data, len(data))
+
+    def ceremony_shard_verify_device(self, n, t, d0, d1, dE, dA, ds, dsp, o2, o4, oA, op):
+        from tests import oracle_lib as O
+        N, D = t + 1, d1 - d0
+        if D:
+            E, A = self._rd(dE, 32 * N * D), self._rd(dA, 32 * N * D)
+            s, sp = self._rd(ds, 32 * n * D), self._rd(dsp, 32 * n * D)
+            pe, ps = bytes(32 * N * d0), bytes(32 * n * d0)  # the oracle indexes absolute dealers
+            r2, _ = O.verify_pairs(n, t, 2, pe + E, self.h, ps + s, ps + sp, d0, d1, 0, n)
+            r4, _ = O.verify_pairs(n, t, 4, pe + A, self.h, ps + s, None, d0, d1, 0, n)
+            self._wr(o2, r2)
+            self._wr(o4, r4)
+            self._wr(oA, b"".join(A[32 * N * i:32 * N * i + 32] for i in range(D)))
+            q = [all(r2[i * n + j] in (1, 2) for j in range(n)) for i in range(D)]
+            part = b"".join((sum(int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+                                 for i in range(D) if q[i]) % L).to_bytes(32, "little") for j in range(n))
+        else:
+            part = bytes(32 * n)
+        self._wr(op, part)
+        self._shares = (d0, d1, self._rd(ds, 32 * n * D) if D else b"")
+        return 0.0
+
+    def ceremony_shard_recon_device(self, n, t, d0, d1, qualified, reconstruct, d_s, d_terms):
+        from tests import finalise_ref as FR
+        s = self._rd(d_s, 32 * n * (d1 - d0))
+        final = [int(q and not r) for q, r in zip(qualified, reconstruct)]
+        xs = [j + 1 for j in range(n) if final[j]]
+        for i in range(d0, d1):
+            if reconstruct[i]:
+                row = s[32 * n * (i - d0):32 * n * (i - d0 + 1)]
+                ys = [int.from_bytes(row[32 * (x - 1):32 * x], "little") for x in xs]
+                self._wr(d_terms + 32 * (i - d0), FR.g_mul(FR.lagrange_at_zero(ys, xs)))
+
+    def scalar_sum_device(self, rows, n, d_in, d_mask, d_out):
+        data = self._rd(d_in, 32 * rows * n)
+        self._wr(d_out, b"".join((sum(int.from_bytes(data[32 * (r * n + j):32 * (r * n + j) + 32], "little")
+                                      for r in range(rows)) % L).to_bytes(32, "little") for j in range(n)))
+
+    def point_sum_device(self, count, d_points, d_mask, d_out):
+        from tests import finalise_ref as FR
+        pts, mask = self._rd(d_points, 32 * count), self._rd(d_mask, count)
+        self._wr(d_out, FR.gsum([pts[32 * c:32 * c + 32] for c in range(count) if mask[c]]))
+
+
+def _run_verify_main(rank, ws, port, names, errq):
+    import torch
+    import torch.distributed as dist
+
+    from dkg_amd.distributed import ShardedCeremony, dealer_range
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+        for name in names:
+            with open(os.path.join(ROOT, "tests", "golden", name)) as f:
+                c = json.load(f)
+            n, t = c["n"], c["t"]
+            N = t + 1
+            d0, d1 = dealer_range(rank, ws, n)
+            H = bytes.fromhex
+            E, A, s, sp = (H(c[k]) for k in ("E", "A", "s", "s_prime"))
+            put = lambda x: torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8)  # noqa: E731
+            tE, tA = put(E[32 * N * d0:32 * N * d1]), put(A[32 * N * d0:32 * N * d1])
+            ts, tsp = put(s[32 * n * d0:32 * n * d1]), put(sp[32 * n * d0:32 * n * d1])
+            sc = ShardedCeremony(OracleBackend(H(c["h"])), dist, n, t, torch.device("cpu"))
+            res = sc.run_verify(tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr())
+            d = res.decisions
+            assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"], name
+            assert res.final_share.hex() == c["final_share"], name
+            if c["phase4_error"]:
+                assert res.mpk is None, name
+            else:
+                assert res.mpk.hex() == c["mpk"], name
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_sharded_run_verify_gloo(ws):
+    """ShardedCeremony.run_verify end to end over gloo with the oracle standing in for the GPU:
+    the reconstruction exchange of dealers accused in round 4 (fault_a_generator, fault_self_share
+    with a tampered self-share, fault_recon_only) and the Phase4 failure (fault_a_many: no mpk)."""
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    names = ["fault_a_generator_n10_t4.json", "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json",
+             "fault_a_many_n10_t4.json", "ceremony_n11_t5.json"]
+    procs = [ctx.Process(target=_run_verify_main, args=(r, ws, port, names, errq)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not alive, "rank hung"
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

@@ -10,6 +10,7 @@ import pytest
 
 import dkg_amd
 from dkg_amd import ACCEPT, MISSING, REJECT, SELF
+from tests import finalise_ref as FR
 from tests import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
@@ -103,7 +104,8 @@ def test_poly_eval(be, golden):
 CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.json",
               "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
 FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
-          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json"]
+          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json",
+          "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json"]
 
 
 @pytest.mark.parametrize("name", CEREMONIES)
@@ -395,7 +397,7 @@ def test_sharded_verify_faults(be, golden, name, ws):
     def put(x):
         return torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)
 
-    dec2, dec4, terms, parts = [], [], [], []
+    dec2, dec4, terms, parts, shares = [], [], [], [], []
     for r in range(ws):
         d0, d1 = dealer_range(r, ws, n)
         D = d1 - d0
@@ -409,9 +411,10 @@ def test_sharded_verify_faults(be, golden, name, ws):
                                         o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
         dec2.append(o2[:D * n])
         dec4.append(o4[:D * n])
-        terms.append(oA[:D * 32])
+        terms.append(oA)
         parts.append(op)
-    g2, g4, gT, gp = (torch.cat(x) for x in (dec2, dec4, terms, parts))
+        shares.append(ts)
+    g2, g4, gp = (torch.cat(x) for x in (dec2, dec4, parts))
     assert dec_str(bytes(g2.cpu().numpy())) == c["dec2"]
     d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
     assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
@@ -422,6 +425,17 @@ def test_sharded_verify_faults(be, golden, name, ws):
     fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
     assert bytes(fs.cpu().numpy()).hex() == c["final_share"]
+    if d.phase4_error:  # Phases<Phase4>::proceed fails for everyone: no master key (committee.rs:673-677)
+        assert c["mpk"] == "00" * 32
+        return
+    # after the exchange: the owning rank of a dealer accused in round 4 replaces its term by g * a_i0
+    # over the final parties' shares (committee.rs:747-789)
+    for r in range(ws):
+        d0, d1 = dealer_range(r, ws, n)
+        if d1 > d0:
+            be.ceremony_shard_recon_device(n, t, d0, d1, d.qualified, d.reconstruct, shares[r].data_ptr(),
+                                           terms[r].data_ptr())
+    gT = torch.cat([terms[r][:32 * (dealer_range(r, ws, n)[1] - dealer_range(r, ws, n)[0])] for r in range(ws)])
     mask = torch.from_numpy(np.ascontiguousarray(d.qualified)).to(dev)
     mpk = torch.empty(32, dtype=torch.uint8, device=dev)
     be.point_sum_device(n, gT.data_ptr(), mask.data_ptr(), mpk.data_ptr())
@@ -785,9 +799,7 @@ def test_interp_mode_goldens(interp, golden, name, overlap):
     finally:
         interp.set_overlap(True)
     _check_ceremony(c, r, n)
-    expect_fallback = {"fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
-                       "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json",
-                       "fault_a_many_n10_t4.json"}
+    expect_fallback = set(FAULTS)
     assert (interp.fallback_rows() > 0) == (name in expect_fallback), interp.fallback_rows()
 
 
@@ -903,13 +915,15 @@ def test_random_ceremonies_vs_oracle(be, seed):
     E, A, s, sp = (bytearray(x) for x in O.share_gen(n, n, t, a, b, h))
     faults = []
     for _ in range(rng.randrange(0, 4)):
-        kind = rng.choice(["s", "sp", "E", "A", "Ebad"])
+        kind = rng.choice(["s", "sp", "E", "A", "Ebad", "self"])
         i = rng.randrange(n)
-        if kind in ("s", "sp"):
-            j = rng.choice([x for x in range(n) if x != i])
-            buf = s if kind == "s" else sp
+        if kind in ("s", "sp", "self"):
+            j = i if kind == "self" else rng.choice([x for x in range(n) if x != i])
+            buf = sp if kind == "sp" else s
             v = (int.from_bytes(buf[32 * (i * n + j):32 * (i * n + j) + 32], "little") + 1) % L
             buf[32 * (i * n + j):32 * (i * n + j) + 32] = v.to_bytes(32, "little")
+            if kind == "self":  # the unchecked self-share plus an A fault on the same dealer
+                A[32 * i * N:32 * i * N + 32] = O.base_mul(rng.randrange(1, L).to_bytes(32, "little"))
         elif kind in ("E", "A"):
             k = rng.randrange(N)
             buf = E if kind == "E" else A
@@ -947,12 +961,43 @@ def test_random_ceremonies_vs_oracle(be, seed):
     fs = b"".join((sum(int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
                        for i in range(n) if qualified[i]) % L).to_bytes(32, "little") for j in range(n))
     assert r.final_share == fs, ctx
-    # mpk: A_i0 of the honest dealers + g * (secrets of the reconstructed ones)
-    honest = [i for i in range(n) if qualified[i] and not recon[i]]
-    sec = sum(int.from_bytes(a[32 * N * i:32 * N * i + 32], "little") for i in range(n) if recon[i]) % L
-    pts = b"".join(bytes(A[32 * N * i:32 * N * i + 32]) for i in honest) + O.base_mul((1).to_bytes(32, "little"))
-    scs = b"".join((1).to_bytes(32, "little") for _ in honest) + sec.to_bytes(32, "little")
-    assert r.mpk == O.msm(scs, pts), ctx
+    # mpk: what every final party computes (committee.rs:726-805), none if Phase4 fails (:673-677)
+    A0 = [bytes(A[32 * N * i:32 * N * i + 32]) for i in range(n)]
+    share = lambda i, j: int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")  # noqa: E731
+    if sum(qualified) - sum(recon) <= t:
+        assert r.phase4_error == 1 and r.mpk == bytes(32), ctx
+    else:
+        assert r.phase4_error == 0 and r.mpk == FR.final_party_mpk(n, qualified, recon, A0, share), ctx
+    # per-party finalise with a random set of missing phase-5 disclosures (dkg_finalise_parties)
+    disclosed = [int(rng.random() < 0.7) for _ in range(n)]
+    pf = be.finalise_parties(n, t, qualified, recon, b"".join(A0), bytes(s), r.r2_error, r.r4_error, disclosed)
+    names = {"OK": 0, "R2_ERROR": 1, "R4_ERROR": 2, "PHASE4_ERROR": 3, "INSUFFICIENT": 4, "PANIC": 5}
+    for p in range(n):
+        st, idx, mk = FR.party_finalise(p, n, t, qualified, recon, A0, share, disclosed=disclosed,
+                                        r2_error=r.r2_error, r4_error=r.r4_error)
+        assert (pf.status[p], pf.recovery_index[p]) == (names[st], idx), (ctx, p)
+        assert pf.mpk[p] == (mk or bytes(32)), (ctx, p)
+
+
+@pytest.mark.parametrize("name", ["finalise_parties_n10_t4.json", "finalise_parties_recon_n10_t4.json"])
+def test_finalise_parties_golden(be, golden, name):
+    """dkg_finalise_parties: every party's Phases<Phase5>::finalise outcome (committee.rs:726-805) --
+    missing disclosures, exactly-t-point interpolation (a wrong secret, as the reference computes it),
+    InsufficientSharesForRecovery, the reference's panic on a disqualified dealer, earlier round
+    failures, a reconstructed dealer's own tampered self-share -- against the libsodium fixture."""
+    f = golden(name)
+    c = golden(f["source"])
+    n, t = c["n"], c["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    A0 = b"".join(H(c["A"])[32 * N * i:32 * N * i + 32] for i in range(n))
+    names = {"OK": 0, "R2_ERROR": 1, "R4_ERROR": 2, "PHASE4_ERROR": 3, "INSUFFICIENT": 4, "PANIC": 5}
+    for case in f["cases"]:
+        pf = be.finalise_parties(n, t, c["qualified"], c["reconstruct"], A0, H(c["s"]), case.get("r2_error"),
+                                 case.get("r4_error"), case.get("disclosed"))
+        assert pf.status == [names[x] for x in case["status"]], case["name"]
+        assert pf.recovery_index == case["index"], case["name"]
+        assert [m.hex() for m in pf.mpk] == case["mpk"], case["name"]
 
 
 def test_ceremony_n4096_device(be):

@@ -1,0 +1,296 @@
+"""Fault-injected parity at the BASELINE sizes (configs 2-5), through the C ABI, against the CPU oracle.
+
+The oracle (tests/oracle_lib.py: dalek-3's algorithms, a vartime MSM per pair, committee.rs:287-305,
+532-548) recomputes WHOLE decision rows of the tampered dealers; the honest rows are checked by
+properties.  Sizes: n=256 (t=127), n=1024 (t=511, the headline schedule: cost-model split U=2, two
+dealer-chunk streams, rounds 2 and 4 fused), n=1100 (t=549) and n=4096 (t=2047) with splits whose
+pieces exceed 512 positions, i.e. the block-chained stepping (kernels.hip k_stepping<512> with its
+up/down boundary streams), and the 10,000-ceremony batch of config 5.
+"""
+import random
+
+import pytest
+
+import dkg_amd
+from dkg_amd import ACCEPT, MISSING, REJECT, SELF, SKIPPED
+from tests import finalise_ref as FR
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+H = bytes.fromhex
+L = 2**252 + 27742317777372353535851937790883648493
+CK = b"Example of a shared string."
+
+
+@pytest.fixture(scope="module")
+def be():
+    b = dkg_amd.Backend(0)
+    yield b
+    b.close()
+
+
+def _rand_point(rng):
+    return O.base_mul(rng.randrange(1, L).to_bytes(32, "little"))
+
+
+def _bump(buf, off):
+    v = (int.from_bytes(buf[off:off + 32], "little") + 1) % L
+    buf[off:off + 32] = v.to_bytes(32, "little")
+
+
+def _inject(rng, n, t, E, A, s, sp):
+    """Tamper dealers 0..4 (rows of bytearrays E, A [n][t+1][32], s, sp [n][n][32]); returns
+    {dealer: description}.  Receivers and coefficient positions are chosen across the stepping
+    blocks (multiples of 512) and the degree-split pieces."""
+    N = t + 1
+    js = sorted({0, 1, min(511, n - 1), min(512, n - 1), n // 2, n - 1, rng.randrange(n)} - {0})
+    for j in js:                                           # dealer 0: flipped shares
+        _bump(s, 32 * (0 * n + j))
+    _bump(sp, 32 * (0 * n + n - 2))                        # ... and one flipped randomness share
+    for k in sorted({0, N // 2, N - 1}):                   # dealer 1: replaced E coefficients
+        E[32 * (1 * N + k):32 * (1 * N + k) + 32] = _rand_point(rng)
+    A[32 * (2 * N + N - 1):32 * (2 * N + N)] = _rand_point(rng)  # dealer 2: a replaced A coefficient
+    _bump(s, 32 * (2 * n + 2))                             # ... and its unchecked self-share
+    E[32 * (3 * N + N // 3) + 31] |= 0x80                  # dealer 3: an undecodable E row (MISSING)
+    for j in (7, n - 3):                                   # dealer 4: randomness only (round 2 only)
+        _bump(sp, 32 * (4 * n + j))
+    return {0: "shares", 1: "E", 2: "A+self", 3: "E undecodable", 4: "randomness"}
+
+
+# (dealer, round) pairs whose whole rows the oracle recomputes; every other row of the tampered
+# dealers is fixed by the tampering itself (untouched data accepts; an undecodable E row is MISSING)
+FULL_ROWS = [(0, 2), (0, 4), (1, 2), (2, 4), (4, 2)]
+
+
+def _expected_rows(n, t, h, E, A, s, sp, full=FULL_ROWS, sample=None):
+    """{(dealer, round): expected raw decision row} for dealers 0..4 (SKIPPED not applied).
+    Rows in `full` come from the oracle; with `sample` (a receiver list) the (4, 2) row is checked by
+    the oracle at those receivers only and completed analytically (large n)."""
+    N = t + 1
+    exp = {}
+    for i in range(5):
+        for rnd in (2, 4):
+            row = bytearray(SELF if j == i else ACCEPT for j in range(n))
+            if (i, rnd) == (3, 2):
+                row = bytearray(SELF if j == i else MISSING for j in range(n))
+            exp[(i, rnd)] = row
+    for j in (7, n - 3):
+        exp[(4, 2)][j] = REJECT
+    for (i, rnd) in full:
+        if sample is not None and (i, rnd) == (4, 2):
+            continue
+        C = E if rnd == 2 else A
+        acc, _ = O.verify_pairs(n, t, rnd, bytes(C[:32 * N * (i + 1)]), h, bytes(s[:32 * n * (i + 1)]),
+                                bytes(sp[:32 * n * (i + 1)]) if rnd == 2 else None, i, i + 1, 0, n)
+        exp[(i, rnd)] = bytearray(acc)
+    if sample is not None:
+        for j in sample:
+            acc, _ = O.verify_pairs(n, t, 2, bytes(E[:32 * N * 5]), h, bytes(s[:32 * n * 5]), bytes(sp[:32 * n * 5]),
+                                    4, 5, j, j + 1)
+            assert acc[0] == exp[(4, 2)][j], ("oracle disagrees with the injected fault", j)
+    return {k: bytes(v) for k, v in exp.items()}
+
+
+def _check_rows(n, dec2, dec4, qualified, exp, ctx):
+    """dec2 / dec4: row accessors of the ceremony outputs (dec4 with SKIPPED for disqualified
+    dealers).  Tampered dealers' rows equal `exp`; every other row accepts."""
+    for i in range(n):
+        r2, r4 = bytes(dec2(i)), bytes(dec4(i))
+        if i < 5:
+            assert r2 == exp[(i, 2)], (ctx, i, "round 2")
+            e4 = exp[(i, 4)] if qualified[i] else bytes(SELF if j == i else SKIPPED for j in range(n))
+            assert r4 == e4, (ctx, i, "round 4")
+        else:
+            row = bytes(SELF if j == i else ACCEPT for j in range(n))
+            assert r2 == row and r4 == row, (ctx, i)
+
+
+@pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0)])
+def test_faults_baseline_sizes(be, n, t, split):
+    """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=2 from the cost
+    model, two dealer-chunk streams, rounds 2 and 4 fused): tampered shares, randomness, E and A
+    coefficients, an undecodable E row and a tampered self-share.  Whole rows of every tampered
+    dealer equal the oracle's per-pair MSM checks; qualification, reconstruction, final shares and
+    the final parties' mpk follow the reference's rules (committee.rs:311-398, 454-467, 660-805)."""
+    N = t + 1
+    h = be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([n % 251]) * 32, 11, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
+    rng = random.Random(n)
+    faulty = _inject(rng, n, t, E, A, s, sp)
+    be.set_split(split)
+    try:
+        r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+        U = be.last_split()
+    finally:
+        be.set_split(0)
+    if n == 1024:
+        assert U == 2, "the headline schedule uses the cost model's U=2 at n=1024"
+    assert sorted(faulty) == [0, 1, 2, 3, 4]
+    exp = _expected_rows(n, t, h, E, A, s, sp)
+    qualified = [0 if i in (0, 1, 3, 4) else 1 for i in range(n)]
+    assert r.qualified == qualified
+    _check_rows(n, lambda i: r.dec2[i * n:(i + 1) * n], lambda i: r.dec4[i * n:(i + 1) * n], qualified, exp, (n, U))
+    recon = [int(i == 2) for i in range(n)]
+    assert r.reconstruct == recon and r.phase4_error == 0
+    complaints = [sum(1 for i in range(n) if i != j and r.dec2[i * n + j] == REJECT) for j in range(n)]
+    assert r.complaints2 == complaints
+    share = lambda i, j: int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")  # noqa: E731
+    for j in random.Random(1).sample(range(n), 4):
+        assert int.from_bytes(r.final_share[32 * j:32 * j + 32], "little") == \
+            sum(share(i, j) for i in range(n) if qualified[i]) % L
+    A0 = [bytes(A[32 * N * i:32 * N * i + 32]) for i in range(n)]
+    assert r.mpk == FR.final_party_mpk(n, qualified, recon, A0, share)
+    # the mpk is the honest one: dealer 2's secret recovered from the final parties, its bad s_22 unused
+    sec = sum(int.from_bytes(a[32 * N * i:32 * N * i + 32], "little") for i in range(n) if qualified[i]) % L
+    assert r.mpk == O.base_mul(sec.to_bytes(32, "little"))
+
+
+def _device_committee(be, n, t, master, ceremony):
+    import torch
+
+    N = t + 1
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(32 * n * N, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    be.dealer_coefficients_device(master, ceremony, 1, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    tE = torch.empty(32 * n * N, dtype=torch.uint8, device=dev)
+    tA = torch.empty_like(tE)
+    ts = torch.empty(32 * n * n, dtype=torch.uint8, device=dev)
+    tsp = torch.empty_like(ts)
+    be.share_gen_device(n, n, t, ta.data_ptr(), tb.data_ptr(), tE.data_ptr(), tA.data_ptr(), ts.data_ptr(),
+                        tsp.data_ptr())
+    return ta, tE, tA, ts, tsp
+
+
+def _shard_verify_all(be, n, t, tE, tA, ts, tsp):
+    import torch
+
+    dev = ts.device
+    o2 = torch.zeros(n * n, dtype=torch.uint8, device=dev)
+    o4 = torch.zeros_like(o2)
+    oA = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    be.ceremony_shard_verify_device(n, t, 0, n, tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr(),
+                                    o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+    return o2.view(n, n), o4.view(n, n)
+
+
+@pytest.mark.parametrize("n,t,splits", [(1100, 549, (1,)), (4096, 2047, (2, 1))])
+def test_faults_multiblock_stepping(be, golden, n, t, splits):
+    """Pieces longer than 512 positions take the block-chained stepping (k_stepping<512>, the top
+    block streaming its per-step values down): n=1100, t=549 unsplit (2 blocks of 275) and n=4096,
+    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks).  The committee is built on the
+    device (dkg_share_gen_device), tampered there, and verified as one shard of all dealers; whole
+    rows of the tampered dealers equal the oracle's (MSM over t+1 = 550 / 2048 points, Pippenger
+    w=7 / w=8).  At n=4096 the committee uses the seed of tests/golden/spot_n4096_t2047.json, whose
+    libsodium commitments and shares it must reproduce."""
+    import torch
+
+    N = t + 1
+    spot = golden("spot_n4096_t2047.json") if n == 4096 else None
+    master = H(spot["master_seed"]) if spot else bytes([3]) * 32
+    h = be.env_init(t, n, CK)
+    ta, tE, tA, ts, tsp = _device_committee(be, n, t, master, 0)
+    if spot:  # golden spot dealers (libsodium) inside the device-generated committee
+        assert h.hex() == spot["h"]
+        for d in spot["dealers"]:
+            i = d["dealer"]
+            assert bytes(tE[32 * N * i:32 * N * (i + 1)].cpu().numpy()).hex() == d["E"]
+            assert bytes(tA[32 * N * i:32 * N * (i + 1)].cpu().numpy()).hex() == d["A"]
+            for pr in d["pairs"]:
+                j = pr["receiver"]
+                assert bytes(ts[32 * (i * n + j):32 * (i * n + j + 1)].cpu().numpy()).hex() == pr["s"]
+                assert bytes(tsp[32 * (i * n + j):32 * (i * n + j + 1)].cpu().numpy()).hex() == pr["s_prime"]
+    # tamper dealers 0..4 on the host copies of their rows, write them back
+    D5 = 5
+    E = bytearray(tE[:32 * N * D5].cpu().numpy().tobytes())
+    A = bytearray(tA[:32 * N * D5].cpu().numpy().tobytes())
+    s = bytearray(ts[:32 * n * D5].cpu().numpy().tobytes())
+    sp = bytearray(tsp[:32 * n * D5].cpu().numpy().tobytes())
+    _inject(random.Random(n + 1), n, t, E, A, s, sp)
+    for t_, b_ in ((tE, E), (tA, A), (ts, s), (tsp, sp)):
+        t_[:len(b_)] = torch.frombuffer(bytearray(b_), dtype=torch.uint8).to(t_.device)
+    sample = [7, n - 3] + random.Random(n).sample(range(8, n - 3), 30) if n > 2000 else None
+    exp = _expected_rows(n, t, h, E, A, s, sp, sample=sample)
+    for U in splits:
+        be.set_split(U)
+        try:
+            d2, d4 = _shard_verify_all(be, n, t, tE, tA, ts, tsp)
+            assert be.last_split() == U
+        finally:
+            be.set_split(0)
+        assert -(-N // U) > 512  # pieces longer than one 512-lane block: the block-chained stepping ran
+        h2 = d2[:D5].cpu().numpy()
+        h4 = d4[:D5].cpu().numpy()
+        # shard rows carry the raw decisions (SKIPPED is applied by the combine step)
+        for i in range(D5):
+            assert bytes(h2[i]) == exp[(i, 2)], (n, U, i, "round 2")
+            assert bytes(h4[i]) == exp[(i, 4)], (n, U, i, "round 4")
+        # honest rows (dealers >= 5) on the device: ACCEPT everywhere but the SELF diagonal
+        eye = torch.eye(n, dtype=torch.bool, device=d2.device)[D5:]
+        for d in (d2[D5:], d4[D5:]):
+            assert bool(((d == ACCEPT) | (eye & (d == SELF))).all()) and int((d == SELF).sum()) == n - D5
+
+
+def test_batch_config5_full_size(be):
+    """BASELINE config 5 at its real size: 10,000 honest n=64, t=31 ceremonies in one batch from
+    device coefficients (640,000 dealer rows).  Every pair of every ceremony accepts in both rounds,
+    every ceremony qualifies all 64 dealers, every ceremony's mpk == g * sum_i a_i0
+    (committee.rs:1633-1647), and sampled ceremonies' final shares interpolate to the secret."""
+    import numpy as np
+    import torch
+
+    B, n, t = 10000, 64, 31
+    N = t + 1
+    be.env_init(t, n, CK)
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(B * n * N * 32, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    be.dealer_coefficients_device(b"\x5c" * 32, 0, B, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    r = dkg_amd.ceremony_batch_device(be, B, n, t, ta.data_ptr(), tb.data_ptr(), big=True)
+    assert r.n_qualified == [n] * B and set(r.phase4_error) == {0}
+    d2 = np.frombuffer(r.dec2, dtype=np.uint8).reshape(B, n, n)
+    d4 = np.frombuffer(r.dec4, dtype=np.uint8).reshape(B, n, n)
+    eye = np.eye(n, dtype=bool)[None]
+    for d in (d2, d4):
+        assert ((d == ACCEPT) | (eye & (d == SELF))).all() and int((d == SELF).sum()) == B * n
+    a0 = ta.view(B * n, N, 32)[:, 0, :].cpu().numpy()
+    for c in range(B):
+        sec = sum(int.from_bytes(a0[c * n + i].tobytes(), "little") for i in range(n)) % L
+        assert r.mpk[c] == O.base_mul(sec.to_bytes(32, "little")), c
+    rng = random.Random(5)
+    for c in [0, B - 1] + rng.sample(range(B), 6):
+        xs = rng.sample(range(1, n + 1), t + 1)
+        fs = [int.from_bytes(r.final_share[32 * (c * n + x - 1):32 * (c * n + x)], "little") for x in xs]
+        sec = sum(int.from_bytes(a0[c * n + i].tobytes(), "little") for i in range(n)) % L
+        assert FR.lagrange_at_zero(fs, xs) == sec, c
+
+
+def test_batch_faulty_members_at_scale(be, golden):
+    """A batch of 2,500 n=10, t=4 ceremonies in which the fault fixtures sit at the first, middle and
+    last positions (row offsets up to 25,000 dealers): each member equals its golden ceremony bit for
+    bit, the honest filler ceremonies equal the honest golden."""
+    names = ["fault_self_share_n10_t4.json", "fault_share_flip_n10_t4.json", "fault_a_many_n10_t4.json",
+             "fault_recon_only_n10_t4.json"]
+    honest = golden("ceremony_n10_t4.json")
+    fx = [golden(x) for x in names]
+    B, n, t = 2500, 10, 4
+    be.env_init(t, n, CK)
+    at = {0: fx[0], 1249: fx[1], 1250: fx[2], B - 1: fx[3]}
+    cs = [at.get(c, honest) for c in range(B)]
+    E = b"".join(H(c["E"]) for c in cs)
+    A = b"".join(H(c["A"]) for c in cs)
+    s = b"".join(H(c["s"]) for c in cs)
+    sp = b"".join(H(c["s_prime"]) for c in cs)
+    r = dkg_amd.ceremony_batch_verify(be, B, n, t, E, A, s, sp)
+    for k in sorted(set(at) | {1, 777, B - 2}):
+        c, d = cs[k], r.ceremony(k)
+        assert "".join(str(x) for x in d["dec2"]) == c["dec2"], k
+        assert "".join(str(x) for x in d["dec4"]) == c["dec4"], k
+        assert d["qualified"] == c["qualified"] and d["reconstruct"] == c["reconstruct"], k
+        assert d["r4_error"] == [int(x) for x in c["r4_error"]] and d["phase4_error"] == int(c["phase4_error"]), k
+        assert d["final_share"].hex() == c["final_share"] and d["mpk"].hex() == c["mpk"], k
+    hm = H(honest["mpk"])
+    assert sum(1 for c in range(B) if r.mpk[c] == hm) == B - len(at)

@@ -108,7 +108,8 @@ def test_dealer_rng(golden):
 CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.json",
               "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
 FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
-          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json"]
+          "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json",
+          "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json"]
 
 
 @pytest.mark.parametrize("name", CEREMONIES)
@@ -258,3 +259,43 @@ def test_complaint_proofs_oracle(golden):
         rc = O.complaint3_verify(H(p3["h"]), p3["t"], x["accuser"], H(x["share"]), H(x["randomness"]),
                                  H(p3["E"])[32 * N * i:32 * N * (i + 1)], H(p3["A"])[32 * N * i:32 * N * (i + 1)])
         assert rc == VERDICT[x["verdict"]], x
+
+
+# ---------------- finalise (committee.rs:625-805) per party: tests/finalise_ref.py ----------------
+def _fin_inputs(c):
+    n, t = c["n"], c["t"]
+    N = t + 1
+    A0 = [H(c["A"])[32 * N * i:32 * N * i + 32] for i in range(n)]
+    s = H(c["s"])
+    return n, t, A0, lambda i, j: int.from_bytes(s[32 * (i * n + j):32 * (i * n + j) + 32], "little")
+
+
+@pytest.mark.parametrize("name", CEREMONIES + FAULTS)
+def test_ceremony_mpk_rule(golden, name):
+    """The ceremony-level mpk of the fixtures is what every final party computes (an all-zero mpk
+    when Phases<Phase4>::proceed fails for everyone, committee.rs:673-677)."""
+    from tests.finalise_ref import final_party_mpk
+    c = golden(name)
+    n, t, A0, share = _fin_inputs(c)
+    if c["phase4_error"]:
+        assert c["mpk"] == "00" * 32
+    else:
+        assert final_party_mpk(n, c["qualified"], c["reconstruct"], A0, share).hex() == c["mpk"]
+
+
+@pytest.mark.parametrize("name", ["finalise_parties_n10_t4.json", "finalise_parties_recon_n10_t4.json"])
+def test_finalise_parties_fixtures(golden, name):
+    """Per-party finalise (missing disclosures, t-point interpolation, InsufficientSharesForRecovery,
+    the reference's panic on a disqualified dealer, earlier round failures) restated on the oracle
+    reproduces the libsodium fixture for every party."""
+    from tests.finalise_ref import party_finalise
+    f = golden(name)
+    c = golden(f["source"])
+    n, t, A0, share = _fin_inputs(c)
+    for case in f["cases"]:
+        for p in range(n):
+            st, idx, mpk = party_finalise(p, n, t, c["qualified"], c["reconstruct"], A0, share,
+                                          disclosed=case.get("disclosed"), r2_error=case.get("r2_error"),
+                                          r4_error=case.get("r4_error"))
+            assert (st, idx) == (case["status"][p], case["index"][p]), (case["name"], p)
+            assert (mpk or bytes(32)).hex() == case["mpk"][p], (case["name"], p)

@@ -148,7 +148,9 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
        {"kind": "E_identity", "dealer": i} (committee.rs:1127-1128 style),
        {"kind": "share_flip", "dealer": i, "receiver": j}   s_ij += 1,
        {"kind": "rand_flip", "dealer": i, "receiver": j}    s'_ij += 1,
-       {"kind": "A_generator", "dealer": i}                  round-3 broadcast := [g; t+1] (:1303-1306).
+       {"kind": "A_generator", "dealer": i}                  round-3 broadcast := [g; t+1] (:1303-1306),
+       {"kind": "self_share_flip", "dealer": i}              s_ii += 1 (the dealer's share to itself,
+                                                             never checked: the diagonal is "self").
        Dealers / receivers are 1-based as in the reference."""
     faults = faults or []
     assert t < (n + 1) // 2, "Environment::init asserts threshold < (nr_members + 1) / 2"
@@ -182,6 +184,8 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
             SPw[i][f["receiver"] - 1] = (SPw[i][f["receiver"] - 1] + 1) % L
         elif f["kind"] == "A_generator":
             Aw[i] = [g] * (t + 1)
+        elif f["kind"] == "self_share_flip":
+            Sw[i][i] = (Sw[i][i] + 1) % L
         else:
             raise ValueError(f)
     # round 2 (committee.rs:273-338): decision[i][j] = receiver j accepts dealer i
@@ -220,19 +224,23 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
     recon = [int(qualified[i] and any(dec4[i][j] == 0 for j in range(n) if j != i)) for i in range(n)]
     # Phases<Phase4>::proceed (committee.rs:673-677): too few honest (qualified, not reconstructed)
     phase4_error = sum(qualified) - sum(recon) <= t
-    mpk = ID
-    for i in range(n):
-        if recon[i]:
-            # a qualified dealer's shares all passed round 2: any t+1 of them give its secret
-            xs = [j + 1 for j in range(n) if j != i][: t + 1]
-            ys = [Sw[i][x - 1] for x in xs]
-            secret = lagrange_at_zero(ys, xs)                          # :784-788
-            assert secret == A[i][0]
-            mpk = gadd(mpk, gmul_base(secret))                         # :789
-        elif qualified[i]:
-            mpk = gadd(mpk, Aw[i][0])                                  # :790-795
-    # property of the honest run (committee.rs:1633-1647): mpk == g * sum of qualified secrets
-    assert mpk == gmul_base(sum(A[i][0] for i in range(n) if qualified[i]))
+    final = [int(qualified[i] and not recon[i]) for i in range(n)]              # :733-739
+    mpk = None
+    if not phase4_error:  # else nobody finalises: there is no master public key
+        mpk = ID
+        for i in range(n):
+            if recon[i]:
+                # what every final party computes: its own share plus the other final parties'
+                # disclosures, i.e. exactly the final set (:754-775); the dealer's own s_ii is unused
+                xs = [j + 1 for j in range(n) if final[j]]
+                ys = [Sw[i][x - 1] for x in xs]
+                secret = lagrange_at_zero(ys, xs)                                 # :784-788
+                assert secret == A[i][0]
+                mpk = gadd(mpk, gmul_base(secret))                                # :789
+            elif qualified[i]:
+                mpk = gadd(mpk, Aw[i][0])                                         # :790-795
+        # property of the honest run (committee.rs:1633-1647): mpk == g * sum of qualified secrets
+        assert mpk == gmul_base(sum(A[i][0] for i in range(n) if qualified[i]))
     out = {
         "n": n, "t": t, "ceremony": ceremony_id, "master_seed": hx(master), "ck_bytes": hx(CK_BYTES),
         "h": hx(h), "faults": faults,
@@ -247,13 +255,63 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
         "reconstruct": recon,
         "final_share": "".join(hx(scb(x)) for x in final_share),
         "public_share": "".join(hx(p) for p in public_share),
-        "mpk": hx(mpk),
+        "mpk": hx(mpk) if mpk is not None else hx(ID),  # all zero: no mpk when phase4_error
     }
     out.update(extra)
     if with_coeffs:
         out["a"] = "".join(hx(scb(x)) for row in A for x in row)
         out["b"] = "".join(hx(scb(x)) for row in B for x in row)
         out["dealer_seeds"] = [hx(dealer_seed(master, ceremony_id, i)) for i in range(n)]
+    out["_state"] = {"Sw": Sw, "Aw": Aw, "Apub": Apub, "qualified": qualified, "recon": recon,
+                     "r2_error": r2_error, "r4_error": r4_error}
+    return out
+
+
+def finalise_party(p, n, t, st, disclosed, r2_error=None, r4_error=None):
+    """Phases<Phase5>::finalise (committee.rs:726-805) as party p (0-based) runs it, after its own
+    Phase1 / Phase3 / Phase4 proceed (a failure there stops it): (status, index, mpk).
+    disclosed[q] = 0: party q's phase-5 broadcast is not fetched (MembersFetchedState5 drops None,
+    :1000-1022, and never includes the party's own, :1009-1010)."""
+    q, rec = st["qualified"], st["recon"]
+    if r2_error and r2_error[p]:
+        return "R2_ERROR", -1, None                           # :340-347
+    if r4_error and r4_error[p]:
+        return "R4_ERROR", -1, None                           # :567-569
+    if sum(q) - sum(rec) <= t:
+        return "PHASE4_ERROR", -1, None                       # :673-677
+    final = [x ^ y for x, y in zip(q, rec)]                   # :733-739
+    mk = ID
+    for i in range(n):
+        if rec[i] and q[i]:
+            xs, ys = [p + 1], [st["Sw"][i][p]]                # own index and share (:754-761)
+            for s_ in range(n):
+                if s_ != p and disclosed[s_] and final[s_]:   # :763-775
+                    xs.append(s_ + 1)
+                    ys.append(st["Sw"][i][s_])
+            if len(xs) < t:                                   # :779-781 (threshold, not t + 1)
+                return "INSUFFICIENT", i, None
+            mk = gadd(mk, gmul_base(lagrange_at_zero(ys, xs)))  # :784-789
+        else:
+            # committed_shares[i]: set for itself at init (:190) and for qualified dealers in
+            # Phase3::proceed (:527-530); expect() panics otherwise (:791-794)
+            if i == p:
+                mk = gadd(mk, st["Apub"][i][0])
+            elif q[i]:
+                mk = gadd(mk, st["Aw"][i][0])
+            else:
+                return "PANIC", i, None
+    return "OK", -1, mk
+
+
+def finalise_golden(c, cases):
+    """Per-party finalise outcomes of ceremony `c` under the given disclosure / earlier-error cases."""
+    n, t, st = c["n"], c["t"], c["_state"]
+    out = []
+    for case in cases:
+        disclosed = case.get("disclosed", [1] * n)
+        res = [finalise_party(p, n, t, st, disclosed, case.get("r2_error"), case.get("r4_error")) for p in range(n)]
+        out.append(dict(case, status=[r[0] for r in res], index=[r[1] for r in res],
+                        mpk=[hx(r[2]) if r[2] is not None else hx(ID) for r in res]))
     return out
 
 
@@ -678,6 +736,36 @@ def main():
         "round3": complaints3_golden(files["fault_a_generator_n10_t4.json"])}
     files["spot_n256_t127.json"] = spot(256, 127, m, [0, 200], [1, 17, 255])
     files["spot_n1024_t511.json"] = spot(1024, 511, m, [513], [0, 1023])
+    # the dealer's unchecked share to itself (s_ii) tampered, plus an A fault on the same dealer (i <= t):
+    # reconstructed in finalise, where s_ii must not be used; and a second reconstructed dealer
+    files["fault_self_share_n10_t4.json"] = ceremony(10, 4, m, ceremony_id=2, faults=[
+        {"kind": "self_share_flip", "dealer": 2}, {"kind": "A_generator", "dealer": 2},
+        {"kind": "A_generator", "dealer": 7}, {"kind": "E_identity", "dealer": 9}])
+    fs = files["fault_self_share_n10_t4.json"]
+    n10 = 10
+    cases = [
+        {"name": "all disclose"},
+        {"name": "t points (4 final parties disclose)", "disclosed": [1 if j in (0, 2, 3, 4) else 0 for j in range(n10)]},
+        {"name": "t-1 points", "disclosed": [1 if j in (0, 3, 4) else 0 for j in range(n10)]},
+        {"name": "none disclose", "disclosed": [0] * n10},
+        {"name": "earlier failures", "r2_error": [1 if j == 5 else 0 for j in range(n10)],
+         "r4_error": [1 if j == 0 else 0 for j in range(n10)]},
+    ]
+    files["finalise_parties_n10_t4.json"] = {"source": "fault_self_share_n10_t4.json",
+                                             "cases": finalise_golden(fs, cases)}
+    # no disqualified dealer: the per-party view without the reference's finalise panic
+    files["fault_recon_only_n10_t4.json"] = ceremony(10, 4, m, ceremony_id=5, faults=[
+        {"kind": "self_share_flip", "dealer": 3}, {"kind": "A_generator", "dealer": 3},
+        {"kind": "A_generator", "dealer": 8}])
+    fr = files["fault_recon_only_n10_t4.json"]
+    files["finalise_parties_recon_n10_t4.json"] = {"source": "fault_recon_only_n10_t4.json", "cases": finalise_golden(fr, [
+        {"name": "all disclose"},
+        {"name": "t points", "disclosed": [1 if j in (0, 1, 3, 4) else 0 for j in range(n10)]},
+        {"name": "t-1 points", "disclosed": [1 if j in (0, 1, 4) else 0 for j in range(n10)]},
+        {"name": "one missing", "disclosed": [0 if j == 5 else 1 for j in range(n10)]}])}
+    files["spot_n4096_t2047.json"] = spot(4096, 2047, m, [5, 3000], [0, 1500, 4095])
+    for obj in files.values():
+        obj.pop("_state", None)
     for name, obj in files.items():
         with open(os.path.join(OUT, name), "w") as f:
             json.dump(obj, f, separators=(",", ":"))
