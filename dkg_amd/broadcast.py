@@ -198,16 +198,21 @@ class Phase1Intake:
     share: bytes         # [n dealer][n recipient][w] (w = 32 plaintext, 64 full mode)
     randomness: bytes
     fetched1: bytes      # [n] 1 = the dealer's phase-1 data was fetched
+    fetch_invalid: bytes  # [n] 1 = receiver q's Phases<Phase1>::proceed returns Err(FetchedInvalidData)
 
 
 def intake_phase1(n: int, t: int, msgs: Sequence[Optional[BroadcastPhase1]], mode: int = 0) -> Phase1Intake:
     """Every party's phase-1 broadcast (msgs[i] from dealer i+1, None if it did not broadcast) as the
     committee sees it: from_broadcast's shape rule (committee.rs:841-852) per dealer; recipient q
-    takes encrypted_shares[q] (:856-858, by position, as the reference does)."""
+    takes encrypted_shares[q] (:856-858, by position, as the reference does).  A fetched share whose
+    recipient_index is not q+1 makes receiver q's round 2 abort with FetchedInvalidData
+    (committee.rs:277-280): flagged in fetch_invalid[q].  The rest of such a party's protocol is not
+    modelled (it never broadcasts again); its column of decisions is still computed."""
     if len(msgs) != n:
         raise ValueError("one entry per party expected")
     N, w = t + 1, 32 if mode == 0 else 64
     E, S, R, ok = bytearray(32 * n * N), bytearray(w * n * n), bytearray(w * n * n), bytearray(n)
+    bad = bytearray(n)
     for i, m in enumerate(msgs):
         if m is None or len(m.committed_coefficients) != N or len(m.encrypted_shares) != n:
             continue
@@ -218,7 +223,9 @@ def intake_phase1(n: int, t: int, msgs: Sequence[Optional[BroadcastPhase1]], mod
         for q, e in enumerate(m.encrypted_shares):
             S[w * (i * n + q):w * (i * n + q + 1)] = e.share
             R[w * (i * n + q):w * (i * n + q + 1)] = e.randomness
-    return Phase1Intake(bytes(E), bytes(S), bytes(R), bytes(ok))
+            if e.recipient_index != q + 1 and q != i:  # a party never fetches its own broadcast
+                bad[q] = 1
+    return Phase1Intake(bytes(E), bytes(S), bytes(R), bytes(ok), bytes(bad))
 
 
 def intake_phase3(n: int, t: int, msgs: Sequence[Optional[BroadcastPhase3]]) -> Tuple[bytes, bytes]:
@@ -240,4 +247,6 @@ def verify_broadcasts(be, n: int, t: int, phase1: Sequence[Optional[BroadcastPha
     """Rounds 2-5 of a plaintext-mode committee on its broadcasts (one dkg_ceremony_verify_fetched)."""
     p1 = intake_phase1(n, t, phase1, mode=0)
     A, f3 = intake_phase3(n, t, phase3)
-    return be.ceremony_verify_fetched(p1.E, A, p1.share, p1.randomness, p1.fetched1, f3, n, t)
+    r = be.ceremony_verify_fetched(p1.E, A, p1.share, p1.randomness, p1.fetched1, f3, n, t)
+    r.fetch_invalid = list(p1.fetch_invalid)  # receivers whose round 2 aborts (committee.rs:277-280)
+    return r

@@ -8,11 +8,15 @@
 // The pseudo-Mersenne fold 2^255 = 19 is applied inside the product (no Montgomery form: the
 // x19 fold is cheaper for this prime than a Montgomery reduction; see DESIGN.md "field").
 //
-// Bounds (checked by tools/fe_bounds.py): a "tight" element has limbs <= 2^26 (even) /
-// 2^25 (odd) plus a carry remainder < 2^18; fe_mul/fe_sq accept inputs with limbs < 2^27.585 on
-// both sides (sum over one output limb of the ten 19/38-weighted products stays < 2^64), and
-// produce tight output.  fe_add of two tight values and fe_sub(a, b) = a + 2p - b with tight b are
-// valid mul inputs; anything looser goes through fe_carry first.
+// Bounds (machine-checked: tools/fe_bounds.py propagates worst-case limb bounds through every
+// primitive and every formula of ge25519.h / points.h as written, and tests/test_bounds.py runs it).
+// TIGHT = every fe_mul / fe_sq / fe_carry output and every stored point coordinate: limbs below
+// 2^26 + 2^6 (even) / 2^25 + 2^12 (odd).  fe_mul(f, g) is overflow-free for uniform limb bounds up to
+// (f, g) = (2^28, 2^27.75), (2^28.32, 2^27.585) or (2^29, 2^26) -- g carries the x19 fold (19 g
+// < 2^32), f the x2 weight, and every 64-bit column sum stays below 2^64.  The formulas hand it at
+// most f = (h - t) + 2p <= 2^28 (doubling) and g = (d - c) + 2p <= 1.5 * 2^27 = 2^27.585 (additions)
+// or 2p - xy2d <= 2^27 (comb entries).  fe_sub(a, b) = a + 2p - b needs b <= 2p limbwise (a TIGHT b
+// always is); anything looser goes through fe_carry first.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -4,8 +4,8 @@
 // The reference reaches the same group through curve25519-dalek (groups.rs:55-90): every value
 // that leaves the device is a canonical 32-byte encoding, so results are implementation-independent.
 //
-// Operand-bound rules for fe_mul(f, g) (see fe25519.h): f limbs <= 2^31, g limbs <= 2^27.75,
-// max(f) * max(g) <= 2^55.9.  The comments "<= 2^x" below track the worst limb bound.
+// Operand bounds: see fe25519.h (machine-checked by tools/fe_bounds.py).  The comments "<= 2^x"
+// below track the worst limb bound of each temporary.
 #pragma once
 #include "fe25519.h"
 

@@ -1,0 +1,42 @@
+"""The limb-bound contract of the field arithmetic (dkg_amd/csrc/fe25519.h, ge25519.h), checked by
+tools/fe_bounds.py on worst-case bounds -- a property random tests cannot establish -- and a
+check that the checker itself detects overflows (it is not vacuous)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import fe_bounds as F  # noqa: E402
+
+
+def test_terms_follow_the_header():
+    """fe_mul has 10 x 10 products, fe_sq the 55 distinct ones, read from fe25519.h."""
+    assert sum(len(v) for v in F._parse_terms("fe_mul").values()) == 100
+    assert sum(len(v) for v in F._parse_terms("fe_sq").values()) == 55
+
+
+def test_no_overflow_anywhere():
+    tight = F.run()
+    assert F.violations == [], F.violations
+    # the stated TIGHT bound of fe25519.h
+    assert all(x < (1 << 26) + (1 << 6) for x in tight[0::2])
+    assert all(x < (1 << 25) + (1 << 12) for x in tight[1::2])
+    assert F.main() == 0
+
+
+def test_checker_detects_violations():
+    F.violations.clear()
+    F.fe_mul([1 << 29] * 10, [1 << 27] * 10, "probe")        # 19 * 2^27 fits, the columns do not
+    assert any("probe column" in v for v in F.violations)
+    F.violations.clear()
+    F.fe_mul([1 << 26] * 10, [1 << 28] * 10, "probe")        # 19 * 2^28 > 2^32
+    assert any("pre-multiply x19" in v for v in F.violations)
+    F.violations.clear()
+    F.fe_sub([0] * 10, [1 << 27] * 10, "probe")              # subtrahend above 2p: would wrap
+    assert any("subtrahend" in v for v in F.violations)
+    F.violations.clear()
+    F.fe_mul([int(2 ** 28.0)] * 10, [int(2 ** 27.75)] * 10, "probe")  # the stated admissible corner
+    F.fe_mul([int(2 ** 28.32)] * 10, [int(2 ** 27.585)] * 10, "probe")
+    F.fe_mul([1 << 29] * 10, [1 << 26] * 10, "probe")
+    assert F.violations == []

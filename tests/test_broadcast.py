@@ -84,3 +84,20 @@ def test_intake_shape_rules(golden):
     p1b, _ = committee_broadcasts(c)
     p1b[0].encrypted_shares[3] = EncryptedShares(4, bytes(64), bytes(64))
     assert intake_phase1(n, t, p1b).fetched1[0] == 0
+    assert list(got.fetch_invalid) == [0] * n
+
+
+def test_intake_recipient_index(golden):
+    """A share whose recipient_index is not the receiver's own makes that receiver's Phase1::proceed
+    return Err(FetchedInvalidData) (committee.rs:277-280): flagged per receiver; a party's own
+    broadcast is never fetched by itself, so its own mislabelled entry is not a failure."""
+    c = golden("ceremony_n10_t4.json")
+    n, t = c["n"], c["t"]
+    p1, _ = committee_broadcasts(c)
+    e = p1[3].encrypted_shares[5]
+    p1[3].encrypted_shares[5] = EncryptedShares(7, e.share, e.randomness)      # dealer 4 -> receiver 6
+    e = p1[1].encrypted_shares[1]
+    p1[1].encrypted_shares[1] = EncryptedShares(9, e.share, e.randomness)      # dealer 2's own entry
+    got = intake_phase1(n, t, p1)
+    assert list(got.fetch_invalid) == [int(q == 5) for q in range(n)]
+    assert list(got.fetched1) == [1] * n
