@@ -28,14 +28,39 @@ L = 2**252 + 27742317777372353535851937790883648493
 CONFIGS = {"D": (1024, 511), "C": (256, 127), "E": (4096, 2047), "B": (64, 31)}
 BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t=31 ceremonies
 
-# Peak INT32 VALU issue rate of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one wave64
-# instruction per 2 cycles per SIMD; full-rate v_add_u32 reaches it: tools/ubench/intrate2.hip).
-# Work is counted as VALU instructions of the implemented schedule: closed-form call counts of each
-# group primitive x its static gfx950 instruction count (tools/count_valu.py; v_mad_u64_u32 counted
-# as one instruction although it issues at about half rate -- see DESIGN.md "Roofline").
+# Peak VALU issue rate of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = one full-rate wave64
+# instruction per 2 cycles per SIMD (v_add_u32 reaches 0.85 of it: profiles/r02_ubench_intrate3.txt).
+# Work is counted on the implemented schedule: closed-form call counts of each group primitive x its
+# static gfx950 count (tools/count_valu.py), in two units:
+#   slots -- VALU issue slots: half-rate instructions (v_mad_u64_u32, v_mul_lo_u32, shifts, 3-operand
+#            fused ops, carry adds; measured by tools/ubench/intrate*.hip) count 2, full-rate 1.  This
+#            is the roofline's work: frac = 1 means every issue cycle of every SIMD was used.
+#   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
-VALU = {"fe_mul": 144, "ge_add": 1318, "ge_add_signed": 1361, "ge_dbl_t": 1158, "ge_dbl_not": 1019,
-        "comb_window": 1272, "comb8_window": 1245, "ge_to_cached": 197, "eq": 4 * 144 + 120}
+VALU = {"fe_mul": (140, 256), "ge_add": (1199, 2177), "ge_add_signed": (1242, 2223), "ge_dbl_t": (1082, 1898),
+        "ge_dbl_not": (943, 1643), "comb_window": (1195, 2107), "comb8_window": (1167, 2051),
+        "ge_to_cached": (143, 259), "eq": (633, 1151)}
+INSTR = {k: v[0] for k, v in VALU.items()}
+SLOTS = {k: v[1] for k, v in VALU.items()}
+
+
+def kernel_rooflines(ph, work, work_i):
+    """Per-kernel VALU roofline of a serialised pass: ph = device ms per kernel (HIP events)."""
+    rl = {}
+    for k in ("binomial", "stepping", "combine", "check"):
+        ms = ph.get(k, 0.0)
+        if ms > 0:
+            rl[k] = {"ms_per_pass": round(ms, 3), "valu_slots": work[k], "valu_instr": work_i[k],
+                     "achieved_T_slots": work[k] / (ms / 1e3) / 1e12, "frac": work[k] / (ms / 1e3) / INT32_PEAK,
+                     "instr_frac": work_i[k] / (ms / 1e3) / INT32_PEAK}
+    return rl
+
+
+def roofline_line(rl, dom, work_text):
+    ach = rl[dom]["achieved_T_slots"]
+    return {"bound": "valu-issue", "kernel": dom, "achieved": ach, "peak": INT32_PEAK / 1e12,
+            "unit": "T VALU issue slots/s", "frac": ach / (INT32_PEAK / 1e12), "instr_frac": rl[dom]["instr_frac"],
+            "traffic": None, "work": work_text, "all_kernels": rl}
 
 
 PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
@@ -132,8 +157,8 @@ def _naf(m):
     return digits
 
 
-def algorithmic_valu(n, t, rnd=2, U=1):
-    """Closed-form VALU instruction count of one verification round over all n dealers as
+def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS):
+    """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round over all n dealers as
     implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces of L = ceil((t+1)/U)
     coefficients, stepping, recombination by y_j = j^L (U > 1), fixed-base check."""
     L_ = -(-(t + 1) // U)
@@ -177,11 +202,11 @@ def algorithmic_valu(n, t, rnd=2, U=1):
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
-def fused_valu(n, t, U=1):
+def fused_valu(n, t, U=1, VALU=SLOTS):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
     recombination; one check kernel computing g*s once (32 radix-256 comb windows), h*s' (32 more) and both
     equalities per pair."""
-    w2, w4 = algorithmic_valu(n, t, 2, U), algorithmic_valu(n, t, 4, U)
+    w2, w4 = algorithmic_valu(n, t, 2, U, VALU), algorithmic_valu(n, t, 4, U, VALU)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
     out["check"] = n * n * (2 * 32 * VALU["comb8_window"] + 2 * VALU["eq"])
     return out
@@ -468,6 +493,7 @@ def main():
         out["config"]["degree_split"] = U
         w2, w4 = algorithmic_valu(n, t, 2, U), algorithmic_valu(n, t, 4, U)
         work = fused_valu(n, t, U) if ov else w2
+        work_i = fused_valu(n, t, U, INSTR) if ov else algorithmic_valu(n, t, 2, U, INSTR)
         # per-kernel device times need the serialised schedule (one chunk stream): one extra,
         # untimed ceremony in the same round order as the timed ones
         be.set_streams(1)
@@ -481,22 +507,13 @@ def main():
         vms = res.ms["round2"] + res.ms["round3"] + res.ms["round4"]
         wall = work if ov else {k: w2[k] + w4[k] for k in w2}
         out["checks_valu_frac"] = sum(wall.values()) / (vms / 1e3) / INT32_PEAK
-        rl = {}
-        for k in ("binomial", "stepping", "combine", "check"):
-            ms = ph.get(k, 0.0)
-            if ms > 0:
-                rl[k] = {"ms_per_pass": round(ms, 3), "valu_instr": work[k],
-                         "achieved_Tops": work[k] / (ms / 1e3) / 1e12,
-                         "frac": work[k] / (ms / 1e3) / INT32_PEAK}
+        rl = kernel_rooflines(ph, work, work_i)
         dom = max(rl, key=lambda k: rl[k]["ms_per_pass"]) if rl else None
         if dom:
-            ach = rl[dom]["achieved_Tops"]
             what = "rounds 2+4 (fused pipeline)" if ov else "round 2"
-            out["roofline"] = {"bound": "valu-int32", "kernel": dom, "achieved": ach, "peak": INT32_PEAK / 1e12,
-                               "unit": "T int32 VALU instr/s", "frac": ach / (INT32_PEAK / 1e12), "traffic": None,
-                               "work": f"{work[dom]:.4g} VALU instructions per pass over {what} (closed form); "
-                                       f"device time of the kernel's launches (HIP events) in a serialised pass",
-                               "all_kernels": rl}
+            out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} "
+                                            f"instructions) per pass over {what} (closed form); device time of "
+                                            f"the kernel's launches (HIP events) in a serialised pass")
             alg, launches = algorithmic_bytes(dom, n, t, U) if ov else (None, None)
             pmc = pmc_traffic(dom, n, t, U) if ov else None
             if alg is not None:
@@ -538,23 +555,14 @@ def main():
         ph = be.phase_times("r24" if not args.no_overlap else "r2")
         U = be.last_split()
         D = ((rank + 1) * n) // ws - (rank * n) // ws
-        work = fused_valu(n, t, U)
-        rl = {}
-        for k in ("binomial", "stepping", "combine", "check"):
-            ms = ph.get(k, 0.0)
-            if ms > 0:
-                w = work[k] * D / n
-                rl[k] = {"ms_per_pass": round(ms, 3), "valu_instr": w, "achieved_Tops": w / (ms / 1e3) / 1e12,
-                         "frac": w / (ms / 1e3) / INT32_PEAK}
+        work = {k: v * D / n for k, v in fused_valu(n, t, U).items()}
+        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR).items()}
+        rl = kernel_rooflines(ph, work, work_i)
         out["config"]["degree_split"] = U
         if rl:
             dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
-            ach = rl[dom]["achieved_Tops"]
-            out["roofline"] = {"bound": "valu-int32", "kernel": dom, "achieved": ach, "peak": INT32_PEAK / 1e12,
-                               "unit": "T int32 VALU instr/s", "frac": ach / (INT32_PEAK / 1e12), "traffic": None,
-                               "work": f"rank 0's shard ({D} dealers): {rl[dom]['valu_instr']:.4g} VALU instructions "
-                                       f"per pass (closed form); device time in a serialised pass",
-                               "all_kernels": rl}
+            out["roofline"] = roofline_line(rl, dom, f"rank 0's shard ({D} dealers): {work[dom]:.4g} VALU issue "
+                                                     f"slots per pass (closed form); device time in a serialised pass")
     if rank == 0:
         print(json.dumps(out), flush=True)
     be.close()

@@ -54,13 +54,11 @@ DKG_DEV void ge_identity(ge_p3& p) {
 }
 
 DKG_DEV void ge_to_cached(ge_cached& c, const ge_p3& p) {
-  fe t;
-  fe_add(t, p.Y, p.X);
-  fe_carry(c.YpX, t);
-  fe_sub(t, p.Y, p.X);
-  fe_carry(c.YmX, t);
-  fe_add(t, p.Z, p.Z);
-  fe_carry(c.Z2, t);
+  // Y+X <= 2^27, Y-X+2p <= 2^27.585 and 2Z <= 2^27 are left uncarried: a cached value is only
+  // ever the second (x19) operand of fe_mul, which takes them (tools/fe_bounds.py)
+  fe_add(c.YpX, p.Y, p.X);
+  fe_sub(c.YmX, p.Y, p.X);
+  fe_add(c.Z2, p.Z, p.Z);
   fe d2;
   fe_ld(d2, ge_const::D2);
   fe_mul(c.T2d, p.T, d2);
@@ -230,9 +228,8 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
   fe_mul(a, p.T, q.T2d);    // c  (the term whose sign flips with q)
   fe_mul(b, p.Z, q.Z2);     // d
   fe na;
-  fe_neg(na, a);            // -c <= 2^27
+  fe_neg(na, a);            // -c = 2p - c <= 2p limbwise: a valid fe_sub subtrahend as is
   fe_cmov(a, na, neg);      // a = +/-c (limbs <= 2^27)
-  fe_carry(a, a);           // tight again (fe_sub needs a tight subtrahend)
   fe_sub(t, b, a);          // f = d - (+/-c) <= 1.5*2^27
   fe_add(b, b, a);          // g <= 2^27
   fe_mul(r.X, e, t);

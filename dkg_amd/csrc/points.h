@@ -220,10 +220,7 @@ DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
   fe_add(h, b, a);          // <= 2^27
   lds_get_fe(qv, q, 3, stride);
   fe_mul(a, p.T, qv);       // c
-  if (neg) {
-    fe_neg(a, a);
-    fe_carry(a, a);
-  }
+  if (neg) fe_neg(a, a);    // 2p - c <= 2p limbwise: a valid fe_sub subtrahend, no carry needed
   lds_get_fe(qv, q, 2, stride);
   fe_mul(b, p.Z, qv);       // d
   fe_sub(t, b, a);          // f

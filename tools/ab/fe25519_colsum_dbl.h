@@ -78,45 +78,32 @@ DKG_DEV void fe_carry(fe& r, const fe& a) {
 }
 
 DKG_DEV uint64_t mul32(uint32_t a, uint32_t b) { return (uint64_t)a * (uint64_t)b; }
-
-// 2x as a full-rate v_add_u32: the compiler turns x + x into v_lshlrev_b32, which issues at half
-// rate on gfx950 like every shift (profiles/r02_ubench_intrate3.txt); non-volatile, so it CSEs.
 DKG_DEV uint32_t dbl32(uint32_t x) {
   uint32_t r;
   asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
   return r;
 }
 
-// One v_mad_u64_u32 (h = a * b + h) the compiler cannot reassociate.  The products are summed
-// column by column ("product scanning") and each column's chain STARTS from the carry out of the
-// previous column, so the carry costs no separate 64-bit add: per column one v_and (full rate) and
-// one v_lshrrev_b64 (half rate) besides the ten half-rate mads (profiles/r02_ubench_intrate3.txt:
-// shifts and 64-bit adds issue at half rate on gfx950, only add/sub/and/or at full rate).  The
-// serial chain costs no issue slots: a wave issues a mad only every ~9.5 cycles anyway
-// (tools/ubench/ilp.hip) and the SIMD interleaves the 4 resident waves and the independent
-// multiplications of each group formula.  The carry-out SGPR pair is unused.
-DKG_DEV void mad_acc(uint64_t& h, uint32_t a, uint32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(h), "=s"(cc) : "v"(a), "v"(b));
+// Carry the ten 64-bit column sums into a tight element.
+DKG_DEV void fe_carry64(fe& r, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4,
+                        uint64_t h5, uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+  uint64_t c;
+  c = h0 >> 26; h1 += c; h0 &= 0x3ffffff;
+  c = h4 >> 26; h5 += c; h4 &= 0x3ffffff;
+  c = h1 >> 25; h2 += c; h1 &= 0x1ffffff;
+  c = h5 >> 25; h6 += c; h5 &= 0x1ffffff;
+  c = h2 >> 26; h3 += c; h2 &= 0x3ffffff;
+  c = h6 >> 26; h7 += c; h6 &= 0x3ffffff;
+  c = h3 >> 25; h4 += c; h3 &= 0x1ffffff;
+  c = h7 >> 25; h8 += c; h7 &= 0x1ffffff;
+  c = h4 >> 26; h5 += c; h4 &= 0x3ffffff;
+  c = h8 >> 26; h9 += c; h8 &= 0x3ffffff;
+  c = h9 >> 25; h0 += c * 19; h9 &= 0x1ffffff;
+  c = h0 >> 26; h1 += c; h0 &= 0x3ffffff;
+  r.v[0] = (uint32_t)h0; r.v[1] = (uint32_t)h1; r.v[2] = (uint32_t)h2; r.v[3] = (uint32_t)h3;
+  r.v[4] = (uint32_t)h4; r.v[5] = (uint32_t)h5; r.v[6] = (uint32_t)h6; r.v[7] = (uint32_t)h7;
+  r.v[8] = (uint32_t)h8; r.v[9] = (uint32_t)h9;
 }
-DKG_DEV uint64_t mad_first(uint32_t a, uint32_t b) {
-  uint64_t h, cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(h), "=s"(cc) : "v"(a), "v"(b));
-  return h;
-}
-// limb k of the result from the column in h, carry left in h
-#define FE_LIMB(r, k, h)                                             \
-  r.v[k] = (uint32_t)h & ((k) & 1 ? 0x1ffffffu : 0x3ffffffu);        \
-  h >>= ((k) & 1 ? 25 : 26);
-// fold of the carry out of limb 9 (< 2^38): 19 h into limb 0, its carry into limb 1
-#define FE_FOLD(r, h)                                                \
-  {                                                                  \
-    uint64_t t_ = (uint64_t)r.v[0];                                  \
-    mad_acc(t_, (uint32_t)h, 19u);                                   \
-    t_ += (uint64_t)(19u * (uint32_t)(h >> 32)) << 32;               \
-    r.v[0] = (uint32_t)t_ & 0x3ffffffu;                              \
-    r.v[1] += (uint32_t)(t_ >> 26);                                  \
-  }
 
 DKG_DEV void fe_mul(fe& r, const fe& f, const fe& g) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
@@ -127,43 +114,35 @@ DKG_DEV void fe_mul(fe& r, const fe& f, const fe& g) {
   const uint32_t g5_19 = 19u * g5, g6_19 = 19u * g6, g7_19 = 19u * g7, g8_19 = 19u * g8;
   const uint32_t g9_19 = 19u * g9;
   const uint32_t f1_2 = dbl32(f1), f3_2 = dbl32(f3), f5_2 = dbl32(f5), f7_2 = dbl32(f7), f9_2 = dbl32(f9);
-  // column k: sum of f_i g_j over i + j = k, and 19 f_i g_j over i + j = k + 10; odd x odd doubled
-  uint64_t h = mad_first(f0, g0);
-  mad_acc(h, f1_2, g9_19); mad_acc(h, f2, g8_19); mad_acc(h, f3_2, g7_19); mad_acc(h, f4, g6_19);
-  mad_acc(h, f5_2, g5_19); mad_acc(h, f6, g4_19); mad_acc(h, f7_2, g3_19); mad_acc(h, f8, g2_19);
-  mad_acc(h, f9_2, g1_19);
-  FE_LIMB(r, 0, h)
-  mad_acc(h, f0, g1); mad_acc(h, f1, g0); mad_acc(h, f2, g9_19); mad_acc(h, f3, g8_19); mad_acc(h, f4, g7_19);
-  mad_acc(h, f5, g6_19); mad_acc(h, f6, g5_19); mad_acc(h, f7, g4_19); mad_acc(h, f8, g3_19); mad_acc(h, f9, g2_19);
-  FE_LIMB(r, 1, h)
-  mad_acc(h, f0, g2); mad_acc(h, f1_2, g1); mad_acc(h, f2, g0); mad_acc(h, f3_2, g9_19); mad_acc(h, f4, g8_19);
-  mad_acc(h, f5_2, g7_19); mad_acc(h, f6, g6_19); mad_acc(h, f7_2, g5_19); mad_acc(h, f8, g4_19);
-  mad_acc(h, f9_2, g3_19);
-  FE_LIMB(r, 2, h)
-  mad_acc(h, f0, g3); mad_acc(h, f1, g2); mad_acc(h, f2, g1); mad_acc(h, f3, g0); mad_acc(h, f4, g9_19);
-  mad_acc(h, f5, g8_19); mad_acc(h, f6, g7_19); mad_acc(h, f7, g6_19); mad_acc(h, f8, g5_19); mad_acc(h, f9, g4_19);
-  FE_LIMB(r, 3, h)
-  mad_acc(h, f0, g4); mad_acc(h, f1_2, g3); mad_acc(h, f2, g2); mad_acc(h, f3_2, g1); mad_acc(h, f4, g0);
-  mad_acc(h, f5_2, g9_19); mad_acc(h, f6, g8_19); mad_acc(h, f7_2, g7_19); mad_acc(h, f8, g6_19);
-  mad_acc(h, f9_2, g5_19);
-  FE_LIMB(r, 4, h)
-  mad_acc(h, f0, g5); mad_acc(h, f1, g4); mad_acc(h, f2, g3); mad_acc(h, f3, g2); mad_acc(h, f4, g1);
-  mad_acc(h, f5, g0); mad_acc(h, f6, g9_19); mad_acc(h, f7, g8_19); mad_acc(h, f8, g7_19); mad_acc(h, f9, g6_19);
-  FE_LIMB(r, 5, h)
-  mad_acc(h, f0, g6); mad_acc(h, f1_2, g5); mad_acc(h, f2, g4); mad_acc(h, f3_2, g3); mad_acc(h, f4, g2);
-  mad_acc(h, f5_2, g1); mad_acc(h, f6, g0); mad_acc(h, f7_2, g9_19); mad_acc(h, f8, g8_19);
-  mad_acc(h, f9_2, g7_19);
-  FE_LIMB(r, 6, h)
-  mad_acc(h, f0, g7); mad_acc(h, f1, g6); mad_acc(h, f2, g5); mad_acc(h, f3, g4); mad_acc(h, f4, g3);
-  mad_acc(h, f5, g2); mad_acc(h, f6, g1); mad_acc(h, f7, g0); mad_acc(h, f8, g9_19); mad_acc(h, f9, g8_19);
-  FE_LIMB(r, 7, h)
-  mad_acc(h, f0, g8); mad_acc(h, f1_2, g7); mad_acc(h, f2, g6); mad_acc(h, f3_2, g5); mad_acc(h, f4, g4);
-  mad_acc(h, f5_2, g3); mad_acc(h, f6, g2); mad_acc(h, f7_2, g1); mad_acc(h, f8, g0); mad_acc(h, f9_2, g9_19);
-  FE_LIMB(r, 8, h)
-  mad_acc(h, f0, g9); mad_acc(h, f1, g8); mad_acc(h, f2, g7); mad_acc(h, f3, g6); mad_acc(h, f4, g5);
-  mad_acc(h, f5, g4); mad_acc(h, f6, g3); mad_acc(h, f7, g2); mad_acc(h, f8, g1); mad_acc(h, f9, g0);
-  FE_LIMB(r, 9, h)
-  FE_FOLD(r, h)
+  uint64_t h0 = mul32(f0, g0) + mul32(f1_2, g9_19) + mul32(f2, g8_19) + mul32(f3_2, g7_19) +
+                mul32(f4, g6_19) + mul32(f5_2, g5_19) + mul32(f6, g4_19) + mul32(f7_2, g3_19) +
+                mul32(f8, g2_19) + mul32(f9_2, g1_19);
+  uint64_t h1 = mul32(f0, g1) + mul32(f1, g0) + mul32(f2, g9_19) + mul32(f3, g8_19) +
+                mul32(f4, g7_19) + mul32(f5, g6_19) + mul32(f6, g5_19) + mul32(f7, g4_19) +
+                mul32(f8, g3_19) + mul32(f9, g2_19);
+  uint64_t h2 = mul32(f0, g2) + mul32(f1_2, g1) + mul32(f2, g0) + mul32(f3_2, g9_19) +
+                mul32(f4, g8_19) + mul32(f5_2, g7_19) + mul32(f6, g6_19) + mul32(f7_2, g5_19) +
+                mul32(f8, g4_19) + mul32(f9_2, g3_19);
+  uint64_t h3 = mul32(f0, g3) + mul32(f1, g2) + mul32(f2, g1) + mul32(f3, g0) + mul32(f4, g9_19) +
+                mul32(f5, g8_19) + mul32(f6, g7_19) + mul32(f7, g6_19) + mul32(f8, g5_19) +
+                mul32(f9, g4_19);
+  uint64_t h4 = mul32(f0, g4) + mul32(f1_2, g3) + mul32(f2, g2) + mul32(f3_2, g1) + mul32(f4, g0) +
+                mul32(f5_2, g9_19) + mul32(f6, g8_19) + mul32(f7_2, g7_19) + mul32(f8, g6_19) +
+                mul32(f9_2, g5_19);
+  uint64_t h5 = mul32(f0, g5) + mul32(f1, g4) + mul32(f2, g3) + mul32(f3, g2) + mul32(f4, g1) +
+                mul32(f5, g0) + mul32(f6, g9_19) + mul32(f7, g8_19) + mul32(f8, g7_19) +
+                mul32(f9, g6_19);
+  uint64_t h6 = mul32(f0, g6) + mul32(f1_2, g5) + mul32(f2, g4) + mul32(f3_2, g3) + mul32(f4, g2) +
+                mul32(f5_2, g1) + mul32(f6, g0) + mul32(f7_2, g9_19) + mul32(f8, g8_19) +
+                mul32(f9_2, g7_19);
+  uint64_t h7 = mul32(f0, g7) + mul32(f1, g6) + mul32(f2, g5) + mul32(f3, g4) + mul32(f4, g3) +
+                mul32(f5, g2) + mul32(f6, g1) + mul32(f7, g0) + mul32(f8, g9_19) + mul32(f9, g8_19);
+  uint64_t h8 = mul32(f0, g8) + mul32(f1_2, g7) + mul32(f2, g6) + mul32(f3_2, g5) + mul32(f4, g4) +
+                mul32(f5_2, g3) + mul32(f6, g2) + mul32(f7_2, g1) + mul32(f8, g0) +
+                mul32(f9_2, g9_19);
+  uint64_t h9 = mul32(f0, g9) + mul32(f1, g8) + mul32(f2, g7) + mul32(f3, g6) + mul32(f4, g5) +
+                mul32(f5, g4) + mul32(f6, g3) + mul32(f7, g2) + mul32(f8, g1) + mul32(f9, g0);
+  fe_carry64(r, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
 }
 
 DKG_DEV void fe_sq(fe& r, const fe& f) {
@@ -176,54 +155,35 @@ DKG_DEV void fe_sq(fe& r, const fe& f) {
   const uint32_t f1_4 = dbl32(f1_2), f3_4 = dbl32(f3_2), f5_4 = dbl32(f5_2), f7_4 = dbl32(f7_2);
   const uint32_t f5_19 = 19u * f5, f6_19 = 19u * f6, f7_19 = 19u * f7, f8_19 = 19u * f8;
   const uint32_t f9_19 = 19u * f9;
-  uint64_t h = mad_first(f0, f0);
-  mad_acc(h, f1_4, f9_19); mad_acc(h, f2_2, f8_19); mad_acc(h, f3_4, f7_19); mad_acc(h, f4_2, f6_19);
-  mad_acc(h, f5_2, f5_19);
-  FE_LIMB(r, 0, h)
-  mad_acc(h, f0_2, f1); mad_acc(h, f2_2, f9_19); mad_acc(h, f3_2, f8_19); mad_acc(h, f4_2, f7_19);
-  mad_acc(h, f5_2, f6_19);
-  FE_LIMB(r, 1, h)
-  mad_acc(h, f0_2, f2); mad_acc(h, f1_2, f1); mad_acc(h, f3_4, f9_19); mad_acc(h, f4_2, f8_19);
-  mad_acc(h, f5_4, f7_19); mad_acc(h, f6, f6_19);
-  FE_LIMB(r, 2, h)
-  mad_acc(h, f0_2, f3); mad_acc(h, f1_2, f2); mad_acc(h, f4_2, f9_19); mad_acc(h, f5_2, f8_19);
-  mad_acc(h, f6_2, f7_19);
-  FE_LIMB(r, 3, h)
-  mad_acc(h, f0_2, f4); mad_acc(h, f1_2, f3_2); mad_acc(h, f2, f2); mad_acc(h, f5_4, f9_19);
-  mad_acc(h, f6_2, f8_19); mad_acc(h, f7_2, f7_19);
-  FE_LIMB(r, 4, h)
-  mad_acc(h, f0_2, f5); mad_acc(h, f1_2, f4); mad_acc(h, f2_2, f3); mad_acc(h, f6_2, f9_19);
-  mad_acc(h, f7_2, f8_19);
-  FE_LIMB(r, 5, h)
-  mad_acc(h, f0_2, f6); mad_acc(h, f1_2, f5_2); mad_acc(h, f2_2, f4); mad_acc(h, f3_2, f3);
-  mad_acc(h, f7_4, f9_19); mad_acc(h, f8, f8_19);
-  FE_LIMB(r, 6, h)
-  mad_acc(h, f0_2, f7); mad_acc(h, f1_2, f6); mad_acc(h, f2_2, f5); mad_acc(h, f3_2, f4);
-  mad_acc(h, f8_2, f9_19);
-  FE_LIMB(r, 7, h)
-  mad_acc(h, f0_2, f8); mad_acc(h, f1_2, f7_2); mad_acc(h, f2_2, f6); mad_acc(h, f3_2, f5_2);
-  mad_acc(h, f4, f4); mad_acc(h, f9_2, f9_19);
-  FE_LIMB(r, 8, h)
-  mad_acc(h, f0_2, f9); mad_acc(h, f1_2, f8); mad_acc(h, f2_2, f7); mad_acc(h, f3_2, f6);
-  mad_acc(h, f4_2, f5);
-  FE_LIMB(r, 9, h)
-  FE_FOLD(r, h)
+  uint64_t h0 = mul32(f0, f0) + mul32(f1_4, f9_19) + mul32(f2_2, f8_19) + mul32(f3_4, f7_19) +
+                mul32(f4_2, f6_19) + mul32(f5_2, f5_19);
+  uint64_t h1 = mul32(f0_2, f1) + mul32(f2_2, f9_19) + mul32(f3_2, f8_19) + mul32(f4_2, f7_19) +
+                mul32(f5_2, f6_19);
+  uint64_t h2 = mul32(f0_2, f2) + mul32(f1_2, f1) + mul32(f3_4, f9_19) + mul32(f4_2, f8_19) +
+                mul32(f5_4, f7_19) + mul32(f6, f6_19);
+  uint64_t h3 = mul32(f0_2, f3) + mul32(f1_2, f2) + mul32(f4_2, f9_19) + mul32(f5_2, f8_19) +
+                mul32(f6_2, f7_19);
+  uint64_t h4 = mul32(f0_2, f4) + mul32(f1_2, f3_2) + mul32(f2, f2) + mul32(f5_4, f9_19) +
+                mul32(f6_2, f8_19) + mul32(f7_2, f7_19);
+  uint64_t h5 = mul32(f0_2, f5) + mul32(f1_2, f4) + mul32(f2_2, f3) + mul32(f6_2, f9_19) +
+                mul32(f7_2, f8_19);
+  uint64_t h6 = mul32(f0_2, f6) + mul32(f1_2, f5_2) + mul32(f2_2, f4) + mul32(f3_2, f3) +
+                mul32(f7_4, f9_19) + mul32(f8, f8_19);
+  uint64_t h7 = mul32(f0_2, f7) + mul32(f1_2, f6) + mul32(f2_2, f5) + mul32(f3_2, f4) +
+                mul32(f8_2, f9_19);
+  uint64_t h8 = mul32(f0_2, f8) + mul32(f1_2, f7_2) + mul32(f2_2, f6) + mul32(f3_2, f5_2) +
+                mul32(f4, f4) + mul32(f9_2, f9_19);
+  uint64_t h9 = mul32(f0_2, f9) + mul32(f1_2, f8) + mul32(f2_2, f7) + mul32(f3_2, f6) +
+                mul32(f4_2, f5);
+  fe_carry64(r, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
 }
 
 // r = a * k for a small constant k < 2^12 (a tight).
 DKG_DEV void fe_mul_small(fe& r, const fe& a, uint32_t k) {
-  uint64_t h = mad_first(a.v[0], k);
-  FE_LIMB(r, 0, h)
-  mad_acc(h, a.v[1], k); FE_LIMB(r, 1, h)
-  mad_acc(h, a.v[2], k); FE_LIMB(r, 2, h)
-  mad_acc(h, a.v[3], k); FE_LIMB(r, 3, h)
-  mad_acc(h, a.v[4], k); FE_LIMB(r, 4, h)
-  mad_acc(h, a.v[5], k); FE_LIMB(r, 5, h)
-  mad_acc(h, a.v[6], k); FE_LIMB(r, 6, h)
-  mad_acc(h, a.v[7], k); FE_LIMB(r, 7, h)
-  mad_acc(h, a.v[8], k); FE_LIMB(r, 8, h)
-  mad_acc(h, a.v[9], k); FE_LIMB(r, 9, h)
-  FE_FOLD(r, h)
+  uint64_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = mul32(a.v[i], k);
+  fe_carry64(r, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
 }
 
 DKG_DEV void fe_sqn(fe& r, const fe& a, int n) {

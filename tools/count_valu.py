@@ -27,6 +27,8 @@ PRIMS = {
                     "comb_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
     "comb8_window": ("ge_p3 p; LDP(p, 0); sc x; for (int i_ = 0; i_ < 8; i_++) x.v[i_] = o[9000 + i_];",
                      "comb8_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
+    "eq": ("ge_p3 p, q; LDP(p, 0); LDP(q, 2560);", "if (ristretto_eq(p, q)) p.X.v[0] ^= 1; else q.Y.v[1] ^= 3;",
+           "STP(p); STP(q);"),
     "ge_to_cached": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached(q, p); p.X = q.T2d; p.Y = q.YpX;",
                      "STP(p);"),
 }
@@ -37,6 +39,20 @@ HDR = r'''
 #define LDP(p, off) { uint32_t* w_ = (uint32_t*)&(p); for (int i_ = 0; i_ < 40; i_++) w_[i_] = o[(off) + i_ * 64 + threadIdx.x]; }
 #define STP(p) { uint32_t* w_ = (uint32_t*)&(p); for (int i_ = 0; i_ < 40; i_++) o[i_ * 64 + threadIdx.x] = w_[i_]; }
 ''' % ROOT
+
+
+# gfx950 VALU issue cost in units of a full-rate wave64 instruction (2 cycles on a SIMD32), measured
+# by tools/ubench/intrate*.hip (profiles/r01_ubench_intrate*.txt, profiles/r02_ubench_intrate3.txt):
+# only plain 32-bit add/sub/logic/move/select issue at full rate; v_mad_u64_u32, v_mul_lo_u32,
+# every shift, the 3-operand fused ops (v_add3, v_lshl_add, v_lshl_or, v_and_or, v_bfe, v_alignbit)
+# and the carry-chain adds issue at half rate.
+FULL_RATE = ("v_add_u32", "v_sub_u32", "v_subrev_u32", "v_and_b32", "v_or_b32", "v_xor_b32",
+             "v_mov_b32", "v_cndmask_b32", "v_not_b32")
+
+
+def issue_slots(ins):
+    op = ins.split()[0].replace("_e32", "").replace("_e64", "").replace("_sdwa", "")
+    return 1 if op in FULL_RATE else 2
 
 
 def main():
@@ -56,7 +72,8 @@ def main():
         blocks = re.split(r"\n\.LBB\d+_\d+:", body)
         best = max(blocks, key=lambda b: sum(1 for l in b.split("\n") if l.strip().startswith("v_")))
         ins = [l.strip() for l in best.split("\n") if l.strip().startswith("v_")]
-        out[name] = {"valu": len(ins), "mad_u64": sum(1 for i in ins if i.startswith("v_mad_u64_u32"))}
+        out[name] = {"valu": len(ins), "slots": sum(issue_slots(i) for i in ins),
+                     "mad_u64": sum(1 for i in ins if i.startswith("v_mad_u64_u32"))}
     print(json.dumps(out))
 
 

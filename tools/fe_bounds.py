@@ -8,8 +8,8 @@ fe_sq take their product terms (which limb pairs, which operand carries the x19 
 weights) straight from the header text, so the checker cannot drift from the code.  It asserts:
   * every 32-bit limb result (fe_add, fe_sub, fe_neg, fe_carry, the x19 / x2 / x4 pre-multiplies
     of fe_mul / fe_sq) stays below 2^32, and fe_sub / fe_neg never wrap (subtrahend <= 2p limbwise);
-  * every 64-bit column sum of fe_mul / fe_sq, and every intermediate of the carry pass
-    fe_carry64, stays below 2^64, and the carried limbs fit 32 bits before the final truncation;
+  * every 64-bit column sum of fe_mul / fe_sq (on top of the carry out of the previous column,
+    product scanning), and the x19 fold of the top carry, stay below 2^64 / 2^32 as computed;
   * fe_tobytes32's canonical reduction sees a value below 2p (one conditional subtraction suffices).
 The group formulas (ge_to_cached, ge_add, ge_sub, ge_madd, ge_msub, ge_dbl / _rt / _lean,
 ge_add_signed, ge_add_lds incl. its negated path, the comb entry selection of comb8_mul_add,
@@ -92,40 +92,41 @@ def fe_carry(a, where="fe_carry"):
     return r
 
 
-def fe_carry64(h, where):
-    """fe_carry64 of fe25519.h, statement by statement, on 64-bit upper bounds."""
-    h = list(h)
-    for x in h:
-        check(f"{where} column", x, U64)
-
-    def step(i, j, fold=1):
-        c = h[i] >> W[i]
-        h[j] += c * fold
-        check(f"{where} carry into h{j}", h[j], U64)
-        h[i] = min(h[i], MASK[i])
-
-    for i, j in [(0, 1), (4, 5), (1, 2), (5, 6), (2, 3), (6, 7), (3, 4), (7, 8), (4, 5), (8, 9)]:
-        step(i, j)
-    step(9, 0, 19)
-    step(0, 1)
-    for i in range(10):
-        check(f"{where} carried limb fits u32", h[i], U32)
-    return h
+def fe_scan(cols, where):
+    """The product-scanning reduction of fe25519.h (FE_LIMB / FE_FOLD): column k is accumulated on
+    top of the carry out of column k-1 (one 64-bit register, v_mad_u64_u32 chains), limb k is its
+    low W[k] bits; the carry out of limb 9 is folded x19 into limb 0 and that carry into limb 1."""
+    r, h = [0] * 10, 0
+    for k in range(10):
+        h += cols[k]
+        check(f"{where} column + carry", h, U64)
+        r[k] = min(h, MASK[k])
+        h >>= W[k]
+    check(f"{where} 19 * (carry >> 32) (32-bit product)", 19 * (h >> 32), U32)
+    t = r[0] + 19 * h
+    check(f"{where} fold", t, U64)
+    r[0] = min(t, MASK[0])
+    r[1] += t >> W[0]
+    check(f"{where} limb 1 after fold", r[1], U32)
+    return r
 
 
 _MUL_TERMS = {}
 
 
 def _parse_terms(func):
-    """Column k of `func` (fe_mul / fe_sq in fe25519.h) as a list of (operand, operand) names."""
+    """Column k of `func` (fe_mul / fe_sq / fe_mul_small in fe25519.h) as a list of (operand,
+    operand) names: the mad_first / mad_acc calls before FE_LIMB(r, k, h)."""
     if func in _MUL_TERMS:
         return _MUL_TERMS[func]
     src = open(FE_H).read()
     body = src[src.index(f"DKG_DEV void {func}("):]
-    body = body[:body.index("fe_carry64(")]
-    cols = {}
-    for m in re.finditer(r"uint64_t h(\d) = (.*?);", body, re.S):
-        cols[int(m.group(1))] = re.findall(r"mul32\((\w+), (\w+)\)", m.group(2))
+    body = body[:body.index("FE_FOLD(")]
+    cols, last = {}, 0
+    for m in re.finditer(r"FE_LIMB\(r, (\d), h\)", body):
+        seg = body[last:m.start()]
+        cols[int(m.group(1))] = re.findall(r"mad_(?:first\(|acc\(h, )([\w.\[\]]+), ([\w.\[\]]+)\)", seg)
+        last = m.end()
     assert sorted(cols) == list(range(10)), f"{func}: could not parse the ten columns"
     _MUL_TERMS[func] = cols
     return cols
@@ -145,18 +146,20 @@ def _operand(name, f, g, where):
 
 def fe_mul(f, g, where="fe_mul"):
     cols = _parse_terms("fe_mul")
-    h = [sum(_operand(x, f, g, where) * _operand(y, f, g, where) for x, y in cols[k]) for k in range(10)]
-    return fe_carry64(h, where)
+    return fe_scan([sum(_operand(x, f, g, where) * _operand(y, f, g, where) for x, y in cols[k])
+                    for k in range(10)], where)
 
 
 def fe_sq(f, where="fe_sq"):
     cols = _parse_terms("fe_sq")
-    h = [sum(_operand(x, f, f, where) * _operand(y, f, f, where) for x, y in cols[k]) for k in range(10)]
-    return fe_carry64(h, where)
+    return fe_scan([sum(_operand(x, f, f, where) * _operand(y, f, f, where) for x, y in cols[k])
+                    for k in range(10)], where)
 
 
 def fe_mul_small(a, k, where="fe_mul_small"):
-    return fe_carry64([a[i] * k for i in range(10)], where)
+    cols = _parse_terms("fe_mul_small")
+    assert all(c == [(f"a.v[{i}]", "k")] for i, c in cols.items()), "fe_mul_small: unexpected terms"
+    return fe_scan([a[i] * k for i in range(10)], where)
 
 
 def fe_tobytes32(a, where="fe_tobytes32"):
@@ -183,9 +186,9 @@ ZERO = [0] * 10
 # ---------------- ge25519.h formulas (as written) ----------------
 def ge_to_cached(p):
     X, Y, Z, T = p
-    ypx = fe_carry(fe_add(Y, X, "to_cached Y+X"), "to_cached")
-    ymx = fe_carry(fe_sub(Y, X, "to_cached Y-X"), "to_cached")
-    z2 = fe_carry(fe_add(Z, Z, "to_cached 2Z"), "to_cached")
+    ypx = fe_add(Y, X, "to_cached Y+X")               # left uncarried (fe_mul's g operand only)
+    ymx = fe_sub(Y, X, "to_cached Y-X")
+    z2 = fe_add(Z, Z, "to_cached 2Z")
     t2d = fe_mul(T, D2, "to_cached T*2d")
     return (ypx, ymx, z2, t2d)
 
@@ -276,7 +279,7 @@ def ge_add_signed(p, q, where="ge_add_signed"):
     a = fe_mul(T, T2d, where)
     b = fe_mul(Z, Z2, where)
     na = fe_neg(a, where)
-    a = fe_carry(vmax(a, na), where)                # fe_cmov then fe_carry
+    a = vmax(a, na)                                 # fe_cmov (no carry: 2p - c <= 2p)
     t = fe_sub(b, a, where)
     b = fe_add(b, a, where)
     return (fe_mul(e, t, where), fe_mul(b, h, where), fe_mul(t, b, where), fe_mul(e, h, where))
@@ -294,7 +297,7 @@ def ge_add_lds(p, q, where="ge_add_lds"):
     e = fe_sub(b, a, where)
     h = fe_add(b, a, where)
     a = fe_mul(T, T2d, where)
-    a = vmax(a, fe_carry(fe_neg(a, where), where))  # if (neg) { fe_neg; fe_carry }
+    a = vmax(a, fe_neg(a, where))                   # if (neg) fe_neg (no carry)
     b = fe_mul(Z, Z2, where)
     t = fe_sub(b, a, where)
     b = fe_add(b, a, where)
