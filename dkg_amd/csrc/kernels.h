@@ -54,8 +54,10 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 // dealer columns starting at the given pointers (a dealer chunk: pass C + c0, e0 + c0, e1 + c0).
 // Returns the buffer holding e_m = Delta^m P_i(0), m = 0..t.
 // pieces > 1: the same for the columns [u * pstride, u * pstride + width) of every piece u
+// last_len (0: N): the last piece's length when it is shorter (its coefficients >= last_len are the
+// identity); its positions >= last_len are then left unwritten (never read by the stepping).
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
-                   hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
+                   hipStream_t stream, size_t pieces = 1, size_t pstride = 0, size_t last_len = 0);
 // Position-major [40][N][npad] -> column-major [40][npad][N] (element c * N + m) for the columns
 // [u * pstride, u * pstride + width) of each of `pieces` pieces (the stepping's input layout).
 void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uint32_t* eT, size_t pieces,
@@ -65,13 +67,20 @@ void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uin
 // word stride N * npad).  stream_a / stream_b: scratch for the inter-block boundary streams, each
 // >= ndealers*nrecv*160 B (unused when N <= 512).
 // How k_stepping covers an N-position table: nblk blocks of P positions on bs lanes (nblk > 1), or
-// `per` tables of P = N lanes each per bs-lane workgroup; maxbs = the LDS variant (256 or 512).
+// `per` tables of P = N lanes each per bs-lane workgroup; maxbs = the LDS variant (192, 256 or 512).
 struct StepShape {
   size_t nblk, P, per, bs, maxbs;
 };
 StepShape stepping_shape(size_t N);
+// relative issue rate of a bs-lane workgroup in the maxbs LDS variant (resident waves per SIMD)
+double step_occupancy(size_t bs, size_t maxbs);
+// true when every piece of a split column fits one workgroup slot ((pieces-1) L + last_len <= 512):
+// the stepping then runs one slot per column over all pieces
+bool stepping_whole_columns(size_t L, size_t pieces, size_t last_len);
+// last_len (0: N): length of a shorter last piece (its table positions >= last_len are not read)
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
-              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces = 1, size_t pstride = 0);
+              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces = 1, size_t pstride = 0,
+              size_t last_len = 0);
 // Degree-split recombination: R[c][j] = sum_u y_j^u R[u * pstride + c][j] (pairwise Horner in y^2
 // with joint NAF chains; digits [n][2][256] = NAF of y_j and y_j^2, top [n][2])
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,

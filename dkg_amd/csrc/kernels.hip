@@ -7,6 +7,9 @@
 // See DESIGN.md for the algorithm (exact finite-difference evaluation of the committed
 // polynomial in the exponent) and the roofline of each kernel.
 #include "kernels.h"
+
+#include <algorithm>
+#include <cmath>
 #include "points.h"
 
 namespace dkgk {
@@ -375,16 +378,18 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 
 // One Horner step in the binomial basis: e'_0 = C_k, e'_m = m (e_{m-1} + e_m), m = 1..r.
 // Lanes = dealers (so m is uniform per wave: no divergence in the m-chain); one wave per
-// (position, 64 dealers); position 0 just copies the next coefficient C_k.  Grid (dealer groups,
-// r+1) with m = r - blockIdx.y: workgroups are dispatched x-fastest, so the longest NAF chains
-// (largest m) start first and the launch tail is made of the short ones.
+// (position, 64 dealers); position 0 just copies the next coefficient C_k.  Grid (dealer groups x
+// pieces, r+1) with m = r - blockIdx.y: workgroups are dispatched x-fastest, so the longest NAF
+// chains (largest m) of EVERY piece start first and the launch tail is made of the short ones.
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
-                                                    size_t pstride) {
+                                                    size_t pstride, unsigned gx, unsigned last_piece,
+                                                    int last_off) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
-  const size_t d = blockIdx.z * pstride + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
+  const size_t d = piece * pstride + (size_t)grp * blockDim.x + threadIdx.x;
   const size_t S = N * npad;
   const int m = r - (int)blockIdx.y;
   if (m == 0) {
@@ -392,12 +397,17 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
     for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
     return;
   }
+  // A short last piece (last_off = L - its length) holds the identity in its top last_off
+  // coefficients: its polynomial has degree re = r - last_off after step r, and positions above
+  // re are never read (later steps mask position re, the stepping stops at the piece's length).
+  const int re = r - (piece == last_piece ? last_off : 0);
+  if (m > re) return;
   {
     ge_p3 cur;
     pt_load(cur, ein, S, (size_t)m * npad + d);
-    // degree r-1 input: position r is zero.  Branch-free, opaque select (a visible branch lets the
+    // degree re-1 input: position re is zero.  Branch-free, opaque select (a visible branch lets the
     // compiler specialise the identity path and doubles the register footprint).
-    uint32_t keep = (m == r) ? 0u : 0xffffffffu;
+    uint32_t keep = (m == re) ? 0u : 0xffffffffu;
     asm volatile("" : "+v"(keep));
     uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
 #pragma unroll
@@ -415,7 +425,8 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
 }
 
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
-                   hipStream_t stream, size_t pieces, size_t pstride) {
+                   hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
+  const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   const size_t t = N - 1;
   hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,
                      npad, N, C, t, e0, pstride);
@@ -424,8 +435,9 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
   for (size_t r = 1; r <= t; r++) {
     const size_t k = t - r;
     // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
-    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64), (unsigned)(r + 1), (unsigned)pieces), dim3(64), 0,
-                       stream, (int)r, (int)k, npad, N, C, in, out, pstride);
+    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64 * pieces), (unsigned)(r + 1)), dim3(64), 0,
+                       stream, (int)r, (int)k, npad, N, C, in, out, pstride, (unsigned)(width / 64),
+                       (unsigned)(pieces - 1), last_off);
     uint32_t* tmp = in;
     in = out;
     out = tmp;
@@ -478,46 +490,45 @@ void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uin
                      dim3(256), 0, stream, width, npad, N, e, eT, pstride);
 }
 
-__device__ __forceinline__ void cached_identity(ge_cached& c) {
-  fe_one(c.YpX);
-  fe_one(c.YmX);
-  fe_zero(c.Z2);
-  c.Z2.v[0] = 2;
-  fe_zero(c.T2d);
-}
-
-// One launch covers position block [pos0, pos0 + P) of every dealer.  Lanes are cut into segments
-// of P lanes, one dealer each (P = N when the whole table fits one block: a t = 31 table packs 8
-// dealers into a 256-lane workgroup instead of idling half of a 64-lane one).
+// One launch covers position block [pos0, pos0 + P) of every dealer.  Lanes are cut into column
+// slots of Ncol = (nseg - 1) P + Plast lanes, one dealer column each, holding nseg segments: pieces
+// piece0 + blockIdx.y + s of a degree-split table, P lanes each except the last (Plast).  nseg = 1:
+// one piece per launch (P = N when the whole table fits one block: a t = 31 table packs 8 dealers
+// into a 256-lane workgroup instead of idling half of a 64-lane one).  nseg = U: every piece of a
+// column in one slot (N = 512 split 192 + 192 + 128: one 512-lane workgroup per column).
 template <int MAXBS>
 __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_stepping(
     size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ e, size_t nrecv, size_t pos0, int P,
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
-    uint32_t* __restrict__ R, size_t pstride) {
+    uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast) {
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
   // segment position q adds column q + 1 of its segment.  Column q = 0 is never read inside a
   // segment (its value leaves through `down` / R), so the segment's top lane parks the upstream
-  // value there: position q reads segment column (q + 1) mod P.  160 B of LDS per lane (a
+  // value there: position q reads segment column (q + 1) mod Pseg.  160 B of LDS per lane (a
   // compile-time stride keeps the address arithmetic out of the VGPR budget); the addend never
   // occupies VGPRs.
   __shared__ uint32_t cols[PT_WORDS * MAXBS];
   const int l = threadIdx.x, bs = blockDim.x;
-  const int seg = l / P, q = l - seg * P;
-  const size_t dl = (size_t)blockIdx.x * (bs / P) + seg;
-  const bool live = seg < bs / P && dl < ndealers;
-  const size_t d = blockIdx.y * pstride + dl;  // piece blockIdx.y of a degree-split table
+  const int Ncol = (nseg - 1) * P + Plast;
+  const int slot = l / Ncol, p = l - slot * Ncol;
+  const int sg = min(p / P, nseg - 1), q = p - sg * P;
+  const int Pseg = sg == nseg - 1 ? Plast : P;
+  const size_t dl = (size_t)blockIdx.x * (bs / Ncol) + slot;
+  const bool live = slot < bs / Ncol && dl < ndealers;
+  const size_t d = (blockIdx.y + piece0 + sg) * pstride + dl;  // piece of a degree-split table
   const size_t S = N * npad;
   const size_t pos = pos0 + q;
   ge_p3 D;
-  if (live && pos < N) pt_load(D, e, S, d * N + pos);  // column-major table: a segment reads contiguously
+  // positions >= Nlive (a short last piece) are the identity whatever the table holds there
+  if (live && pos < Nlive) pt_load(D, e, S, d * N + pos);  // column-major: a segment reads contiguously
   else ge_identity(D);
-  const bool top_lane = live && (q == P - 1);
+  const bool top_lane = live && (q == Pseg - 1);
   const uint4* upd = (up && live) ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
   uint4* downd = (down && live) ? reinterpret_cast<uint4*>(down + d * nrecv * PT_WORDS) : nullptr;
   uint32_t* mine = cols + l;
-  uint32_t* base = cols + seg * P;
-  const uint32_t* nbr = base + ((q + 1) % P);
+  uint32_t* base = cols + (l - q);
+  const uint32_t* nbr = base + ((q + 1) % Pseg);
   for (size_t j = 0; j < nrecv; j++) {
     {
       ge_cached c0;
@@ -532,27 +543,30 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
         lds_put_cached(mine, c0, MAXBS);
       }
     }
-    if (top_lane) {
+    if (top_lane && upd) {  // the block above's lowest position, parked in column 0
       ge_cached u;
-      if (upd) {
-        uint4* u4 = reinterpret_cast<uint4*>(&u);
+      uint4* u4 = reinterpret_cast<uint4*>(&u);
 #pragma unroll
-        for (int k = 0; k < PT_WORDS / 4; k++) u4[k] = upd[j * (PT_WORDS / 4) + k];
-      } else {
-        cached_identity(u);
-      }
+      for (int k = 0; k < PT_WORDS / 4; k++) u4[k] = upd[j * (PT_WORDS / 4) + k];
       lds_put_cached(base, u, MAXBS);
     }
     __syncthreads();
-    if (live && pos + 1 < N) ge_add_lds(D, D, nbr, false, MAXBS);
+    if (live && pos + 1 < Nlive && (q + 1 < Pseg || up)) ge_add_lds(D, D, nbr, false, MAXBS);
     __syncthreads();  // every column read before the next step overwrites it
     if (live && q == 0 && R) pt_store_aos(R, d * nrecv + j, D);
   }
 }
 
 // Lanes given to an N-position table: 512-lane blocks (balanced when N > 512), or P = N lanes per
-// segment with floor(MAXBS / N) segments per workgroup; the variant wasting the fewest lanes wins
-// (ties to the 256-lane one: half the LDS per workgroup).
+// segment with floor(MAXBS / N) segments per workgroup.  MAXBS (the LDS variant: 160 B per lane)
+// is picked for the most useful lanes x resident waves: a 192-lane table in the 256 variant leaves
+// 4 workgroups = 12 waves per CU (LDS-bound), in the 192 variant 5 = 15 waves.
+double step_occupancy(size_t bs, size_t maxbs) {
+  const double wgs = std::min(std::floor(160.0 * 1024 / (160.0 * maxbs)), std::floor(16.0 / (bs / 64.0)));
+  const double wps = wgs * (bs / 64.0) / 4.0;  // waves per SIMD (VGPRs cap it at 4)
+  return wps >= 4 ? 1.0 : (wps >= 3 ? 0.85 + 0.15 * (wps - 3) : 0.7);
+}
+
 StepShape stepping_shape(size_t N) {
   StepShape sh;
   if (N > 512) {
@@ -563,44 +577,84 @@ StepShape stepping_shape(size_t N) {
     sh.maxbs = 512;
     return sh;
   }
-  auto fit = [&](size_t maxbs, StepShape& o) {
+  double best = -1;
+  for (size_t maxbs : {256, 192, 512}) {
+    if (maxbs < N) continue;
+    StepShape o;
     o.nblk = 1;
     o.P = N;
     o.per = maxbs / N;
     o.bs = (o.per * N + 63) / 64 * 64;
     o.maxbs = maxbs;
-    return (double)(o.per * N) / o.bs;
-  };
-  StepShape a, b;
-  const double ea = N <= 256 ? fit(256, a) : 0.0, eb = fit(512, b);
-  return ea >= eb - 0.02 ? a : b;
+    const double score = (double)(o.per * N) / o.bs * step_occupancy(o.bs, maxbs);
+    if (score > best + 0.02) {
+      best = score;
+      sh = o;
+    }
+  }
+  return sh;
+}
+
+// Every piece of a column in one slot: usable when the whole split table has <= 512 positions.
+bool stepping_whole_columns(size_t L, size_t pieces, size_t last_len) {
+  return pieces > 1 && (pieces - 1) * L + last_len <= 512;
 }
 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
-              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride) {
+              uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
+              size_t last_len) {
   if (!ndealers || !nrecv) return;
+  if (!last_len || last_len > N) last_len = N;
+  auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
+    const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), (unsigned)np), block((unsigned)s.bs);
+    if (s.maxbs == 192)
+      hipLaunchKernelGGL(k_stepping<192>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
+                         (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
+    else if (s.maxbs == 256)
+      hipLaunchKernelGGL(k_stepping<256>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
+                         (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
+    else
+      hipLaunchKernelGGL(k_stepping<512>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
+                         (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
+  };
+  if (stepping_whole_columns(N, pieces, last_len)) {
+    // one slot of (pieces - 1) N + last_len lanes per column: every workgroup does the same work
+    // (a column), so a launch of ndealers columns has no tail of lone pieces
+    StepShape s = stepping_shape((pieces - 1) * N + last_len);
+    s.P = N;
+    launch(s, N, 0u, 1, (int)pieces, (int)last_len);
+    return;
+  }
   const StepShape sh = stepping_shape(N);
   if (sh.nblk > 1) {  // one dealer per workgroup, top block first, block values streamed down
-    uint32_t* up = nullptr;
-    for (size_t b = sh.nblk; b-- > 0;) {
-      uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
-      hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)pieces), dim3((unsigned)sh.bs), 0,
-                         stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down, b ? nullptr : R,
-                         pstride);
-      up = down;
+    auto blocks = [&](size_t Nlive, unsigned piece0, size_t np) {
+      uint32_t* up = nullptr;
+      for (size_t b = sh.nblk; b-- > 0;) {
+        uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
+        hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)np), dim3((unsigned)sh.bs), 0,
+                           stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down, b ? nullptr : R,
+                           pstride, Nlive, piece0, 1, (int)sh.P);
+        up = down;
+      }
+    };
+    // a short last piece runs the same blocks with its positions >= last_len as the identity
+    if (last_len == N || pieces == 1) {
+      blocks(last_len, 0u, pieces);
+    } else {
+      blocks(N, 0u, pieces - 1);
+      blocks(last_len, (unsigned)(pieces - 1), 1);
     }
     return;
   }
-  // whole table in one segment of N lanes, sh.per tables per workgroup
-  const size_t grid = (ndealers + sh.per - 1) / sh.per;
-  if (sh.maxbs == 256)
-    hipLaunchKernelGGL(k_stepping<256>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)sh.bs), 0, stream,
-                       ndealers, npad, N, e, nrecv, (size_t)0, (int)sh.P, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                       R, pstride);
-  else
-    hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)grid, (unsigned)pieces), dim3((unsigned)sh.bs), 0, stream,
-                       ndealers, npad, N, e, nrecv, (size_t)0, (int)sh.P, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                       R, pstride);
+  // whole table in one segment of N lanes, sh.per tables per workgroup; a short last piece in its
+  // own launch with segments of last_len lanes (the same column-major stride N)
+  if (last_len == N) {
+    launch(sh, N, 0u, pieces, 1, (int)sh.P);
+    return;
+  }
+  if (pieces > 1) launch(sh, N, 0u, pieces - 1, 1, (int)sh.P);
+  const StepShape sl = stepping_shape(last_len);
+  launch(sl, last_len, (unsigned)(pieces - 1), 1, 1, (int)sl.P);
 }
 
 // Degree split: P(x) = sum_u x^(uL) Q_u(x).  With the stepped values Q_u(j) of

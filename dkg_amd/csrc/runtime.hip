@@ -184,9 +184,9 @@ struct VerifySeg {
 // kernels; the check does not depend on U) in SIMD
 // cycles: a SIMD retires one wave instruction per ~4.5 cycles of this mix when it has >= 2 waves,
 // one per ~8 when a lone wave runs a dependent chain (tools/ubench/ilp.hip); 1024 SIMDs.
-double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
+double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
   const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAUNCH = 3e-3 * 2.4e6;
-  const size_t L = (N + U - 1) / U;
+  const size_t Lr = N - (U - 1) * L, off = L - Lr;  // the last piece: Lr positions, starts at step off
   auto cost = [&](size_t m) {  // one binomial position-step: add + NAF multiplication by m
     int len = 0, nz = 0;  // NAF length and weight of m (as mul_small_lds recodes it)
     for (size_t v = m; v; v >>= 1, len++) {
@@ -200,10 +200,11 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
   };
   std::vector<double> pre(L + 1, 0.0);
   for (size_t m = 1; m <= L; m++) pre[m] = pre[m - 1] + cost(m);
-  const double waves_col = (double)cols * U / 64;
+  const double waves_col = (double)cols / 64;
   double cyc = 0;
   for (size_t r = 1; r < L; r++) {
-    const double work = waves_col * pre[r] * THR / SIMDS;  // wave-instructions of step r
+    // wave-instructions of step r: U-1 full pieces, the last one from step off on
+    const double work = waves_col * ((U - 1) * pre[r] + (r > off ? pre[r - off] : 0.0)) * THR / SIMDS;
     // a step pays its issue work AND its longest chain: the last waves of a launch run their chains
     // on partly idle SIMDs (the sum fits the measured shards within 5 %: 1-, 2-, 4-, 8-way n=1024,
     // one-GPU n=4096; the max alone picked U=2 for a 4-way n=1024 shard, 3 % slower than U=4)
@@ -214,23 +215,38 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
     // additions), then (ceil(U/2) - 1) joint y^2 / y steps (253 doublings + ~170 additions)
     const double per = (U % 2 == 0 ? 253 * 950 + 85 * ADD : 0.0) + ((U + 1) / 2 - 1) * (253 * 950 + 170 * ADD);
     const double waves = (double)cols / 64 * n;
-    const double occ = U > 2 ? 0.85 : 1.0;  // two LDS addend slots: 2 waves per SIMD
-    cyc += std::max(waves * per * THR / SIMDS / occ, per * LAT);
+    cyc += std::max(waves * per * THR / SIMDS, per * LAT);  // the 2-slot variant runs at 2 waves/SIMD as fast
   }
-  // stepping: n dependent additions per lane on the lanes k_stepping allocates to an L-position
-  // table (512-lane blocks above 256 positions, else floor(256/L) tables per 256-lane group),
-  // slower when a group leaves a SIMD fewer than 4 waves
-  {
-    const dkgk::StepShape sh = dkgk::stepping_shape(L);
+  // stepping: n dependent additions per lane on the lanes k_stepping allocates to each piece's
+  // table, or to a whole column's pieces (dkgk::stepping_shape), slower when a workgroup leaves a
+  // SIMD fewer than 4 waves, and when the last round of long-running workgroups leaves CUs idle
+  auto step_cyc = [&](size_t len, double pieces) {
+    const dkgk::StepShape sh = dkgk::stepping_shape(len);
     const double lanes = (double)sh.nblk * sh.bs / sh.per;
-    // resident waves per SIMD: LDS (160 B per lane of maxbs) and 16 waves per CU
-    const double wgs = std::min(160.0 * 1024 / (160.0 * sh.maxbs), 16.0 / (sh.bs / 64.0));
-    const double wps = std::floor(wgs) * sh.bs / 64 / 4;
-    const double occ = wps >= 4 ? 1.0 : (wps >= 3 ? 0.85 : 0.7);
-    const double waves = (double)cols * U * lanes / 64;
-    cyc += std::max(waves * n * ADD * THR / SIMDS / occ, n * ADD * LAT);
-  }
+    const double waves = (double)cols * pieces * lanes / 64;
+    const double per_cu = std::min(std::floor(1024.0 / sh.maxbs), std::floor(16.0 / (sh.bs / 64.0)));
+    const double wgs = std::ceil((double)cols / sh.per) * pieces, rounds = std::ceil(wgs / (256 * per_cu));
+    const double tail = wgs / (rounds * 256 * per_cu);
+    return std::max(waves * n * ADD * THR / SIMDS / dkgk::step_occupancy(sh.bs, sh.maxbs) / tail, n * ADD * LAT);
+  };
+  if (dkgk::stepping_whole_columns(L, U, Lr)) cyc += step_cyc(N, 1.0);
+  else cyc += Lr == L ? step_cyc(L, (double)U) : step_cyc(L, (double)(U - 1)) + step_cyc(Lr, 1.0);
   return cyc / 2.4e6;
+}
+
+// Piece length of a U-way split: ceil(N / U), or that rounded up to a multiple of 64 when the
+// model prefers it -- whole 64-lane waves for the stepping's tables and a shorter last piece
+// (N = 512, U = 3: pieces of 192, 192, 128 instead of 171, 171, 170).
+size_t split_len(size_t cols, size_t n, size_t N, size_t U) {
+  const size_t L1 = (N + U - 1) / U;
+  if (U == 1) return L1;
+  const size_t L64 = (L1 + 63) / 64 * 64;
+  if (L64 == L1 || (U - 1) * L64 >= N) return L1;
+  return split_model_ms(cols, n, N, U, L64) < split_model_ms(cols, n, N, U, L1) ? L64 : L1;
+}
+
+double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
+  return split_model_ms(cols, n, N, U, split_len(cols, n, N, U));
 }
 
 size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
@@ -324,7 +340,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const size_t groups = (D + 63) / 64, gw = 64 * nseg;  // columns per dealer group
   const size_t npad = groups * gw;
   // degree split: U pieces of L positions; piece u of column c is table column u * npad + c
-  const size_t U = choose_split(ctx, npad, n, N), L = (N + U - 1) / U, W = U * npad;
+  const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U), W = U * npad;
+  const size_t Lr = N - (U - 1) * L;  // the last piece's length (L or shorter)
   ctx->last_split = (int)U;
   hipStream_t home = ctx->stream;
   uint8_t* pok = buf<uint8_t>(ctx, "v.pok", npad * N);
@@ -372,11 +389,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    const uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad);
+    const uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad, Lr);
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
     dkgk::stepping(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad);
+                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));

@@ -2,10 +2,11 @@
 
 The oracle (tests/oracle_lib.py: dalek-3's algorithms, a vartime MSM per pair, committee.rs:287-305,
 532-548) recomputes WHOLE decision rows of the tampered dealers; the honest rows are checked by
-properties.  Sizes: n=256 (t=127), n=1024 (t=511, the headline schedule: cost-model split U=2, two
-dealer-chunk streams, rounds 2 and 4 fused), n=1100 (t=549) and n=4096 (t=2047) with splits whose
-pieces exceed 512 positions, i.e. the block-chained stepping (kernels.hip k_stepping<512> with its
-up/down boundary streams), and the 10,000-ceremony batch of config 5.
+properties.  Sizes: n=256 (t=127), n=1024 (t=511, the headline schedule: cost-model split U=3 with
+pieces of 192 + 192 + 128 positions, two dealer-chunk streams, rounds 2 and 4 fused; and forced
+U=2 / U=4), n=1100 (t=549) and n=4096 (t=2047) with splits whose pieces exceed 512 positions, i.e.
+the block-chained stepping (kernels.hip k_stepping<512> with its up/down boundary streams) or end
+in a short last piece, and the 10,000-ceremony batch of config 5.
 """
 import random
 
@@ -106,10 +107,12 @@ def _check_rows(n, dec2, dec4, qualified, exp, ctx):
             assert r2 == row and r4 == row, (ctx, i)
 
 
-@pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0)])
+@pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0), (1024, 511, 2), (1024, 511, 4)])
 def test_faults_baseline_sizes(be, n, t, split):
-    """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=2 from the cost
-    model, two dealer-chunk streams, rounds 2 and 4 fused): tampered shares, randomness, E and A
+    """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=3 from the cost
+    model with pieces of 192, 192 and 128 positions, every piece of a column in one stepping
+    workgroup, two dealer-chunk streams, rounds 2 and 4 fused), and forced U=2 / U=4 (pieces of one
+    stepping workgroup each): tampered shares, randomness, E and A
     coefficients, an undecodable E row and a tampered self-share.  Whole rows of every tampered
     dealer equal the oracle's per-pair MSM checks; qualification, reconstruction, final shares and
     the final parties' mpk follow the reference's rules (committee.rs:311-398, 454-467, 660-805)."""
@@ -125,8 +128,10 @@ def test_faults_baseline_sizes(be, n, t, split):
         U = be.last_split()
     finally:
         be.set_split(0)
-    if n == 1024:
-        assert U == 2, "the headline schedule uses the cost model's U=2 at n=1024"
+    if split:
+        assert U == split
+    elif n == 1024:
+        assert U == 3, "the headline schedule uses the cost model's U=3 at n=1024"
     assert sorted(faulty) == [0, 1, 2, 3, 4]
     exp = _expected_rows(n, t, h, E, A, s, sp)
     qualified = [0 if i in (0, 1, 3, 4) else 1 for i in range(n)]
@@ -177,11 +182,13 @@ def _shard_verify_all(be, n, t, tE, tA, ts, tsp):
     return o2.view(n, n), o4.view(n, n)
 
 
-@pytest.mark.parametrize("n,t,splits", [(1100, 549, (1,)), (4096, 2047, (2, 1))])
+@pytest.mark.parametrize("n,t,splits", [(1100, 549, (1, 3)), (4096, 2047, (2, 1, 3))])
 def test_faults_multiblock_stepping(be, golden, n, t, splits):
     """Pieces longer than 512 positions take the block-chained stepping (k_stepping<512>, the top
     block streaming its per-step values down): n=1100, t=549 unsplit (2 blocks of 275) and n=4096,
-    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks).  The committee is built on the
+    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks); U=3 gives a short last piece
+    (n=1100: 192 + 192 + 166 positions, the last piece in its own stepping launch; n=4096: pieces
+    of 704, 704 and 640 in 2 blocks each, the last one's top positions the identity).  The committee is built on the
     device (dkg_share_gen_device), tampered there, and verified as one shard of all dealers; whole
     rows of the tampered dealers equal the oracle's (MSM over t+1 = 550 / 2048 points, Pippenger
     w=7 / w=8).  At n=4096 the committee uses the seed of tests/golden/spot_n4096_t2047.json, whose
@@ -221,7 +228,7 @@ def test_faults_multiblock_stepping(be, golden, n, t, splits):
             assert be.last_split() == U
         finally:
             be.set_split(0)
-        assert -(-N // U) > 512  # pieces longer than one 512-lane block: the block-chained stepping ran
+        assert -(-N // U) > 512 or U == 3  # pieces longer than one 512-lane block: block-chained stepping
         h2 = d2[:D5].cpu().numpy()
         h4 = d4[:D5].cpu().numpy()
         # shard rows carry the raw decisions (SKIPPED is applied by the combine step)
