@@ -64,26 +64,29 @@ def roofline_line(rl, dom, work_text):
 
 
 PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
-def algorithmic_bytes(kernel, n, t, U):
+def algorithmic_bytes(kernel, n, t, U, plen=None):
     """(bytes per launch, launches per pass) of a check-pipeline kernel in the serialised fused pass:
-    columns = 2n (E and A rows) x U pieces of L = ceil((t+1)/U) positions (DESIGN.md sections 3-4)."""
-    L = -(-(t + 1) // U)
-    cols = 2 * n * U
-    if kernel == "binomial":  # step r: position 0 copies C_k (load+store), positions 1..r load 2, store 1
-        per_pass = sum(cols * (2 * PT_BYTES + r * 3 * PT_BYTES) for r in range(1, L))
-        return per_pass / max(L - 1, 1), max(L - 1, 1)
-    if kernel == "stepping":  # the table once, then D_0 out per receiver (one launch while L <= 512)
-        nblk = -(-L // 512)
-        return cols * (L + n) * PT_BYTES / nblk, nblk
+    2n columns (E and A rows) x U pieces (split_pieces: L positions, a shorter last one; DESIGN.md
+    sections 3-4)."""
+    pieces, Lp0 = split_pieces(t, U, plen)
+    cols = 2 * n
+    if kernel == "binomial":  # step r: position 0 copies C_k (load+store), positions 1..r' load 2, store 1
+        # (r' = r for full pieces, r - (L - Lp) for a short last piece, which starts late)
+        per_pass = sum(cols * (2 * PT_BYTES + max(r - (Lp0 - Lp), 0) * 3 * PT_BYTES)
+                       for r in range(1, Lp0) for Lp in pieces)
+        return per_pass / max(Lp0 - 1, 1), max(Lp0 - 1, 1)
+    if kernel == "stepping":  # the table once, then D_0 out per (piece, receiver)
+        nblk = -(-Lp0 // 512)
+        return cols * (t + 1 + U * n) * PT_BYTES / nblk, nblk
     if kernel == "combine":  # U piece values in, P(j) out per (column, receiver)
         return 2 * n * n * (U + 1) * PT_BYTES, 1
     return None, None
 
 
-def pmc_traffic(kernel, n, t, U):
+def pmc_traffic(kernel, n, t, U, plen=None):
     """HBM-side bytes per launch of `kernel` from the committed PMC passes (tools/profile.sh ->
     tools/pmc_summary.py), when they were taken on this workload; else None."""
     try:
@@ -92,6 +95,8 @@ def pmc_traffic(kernel, n, t, U):
     except (OSError, ValueError):
         return None
     if (doc.get("n"), doc.get("t"), doc.get("split")) != (n, t, U) or kernel not in doc.get("kernels", {}):
+        return None
+    if plen is not None and doc.get("split_len", split_pieces(t, U)[1]) != plen:
         return None
     return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
 
@@ -157,11 +162,20 @@ def _naf(m):
     return digits
 
 
-def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS):
-    """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round over all n dealers as
-    implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces of L = ceil((t+1)/U)
-    coefficients, stepping, recombination by y_j = j^L (U > 1), fixed-base check."""
-    L_ = -(-(t + 1) // U)
+def split_pieces(t, U, plen=None):
+    """Piece lengths of a U-way degree split with piece length plen (runtime.hip split_len:
+    ceil((t+1)/U), or that rounded up to a multiple of 64; the last piece holds the rest)."""
+    N = t + 1
+    plen = plen or -(-N // U)
+    return [plen] * (U - 1) + [N - (U - 1) * plen], plen
+
+
+def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None):
+    """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round
+    over all n dealers as implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces
+    (split_pieces: L coefficients each but a shorter last one), stepping, recombination by
+    y_j = j^L (U > 1), fixed-base check."""
+    pieces, L_ = split_pieces(t, U, plen)
     cost_m = {}
     for m in range(1, L_):
         ds = _naf(m)
@@ -174,9 +188,9 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS):
                 if nz:
                     c += VALU["ge_add_signed"]
         cost_m[m] = c
-    # position m of a piece is live for L-m steps
-    binom = U * sum(cost_m[m] * (L_ - m) for m in range(1, L_))
-    stepping = U * n * (L_ * VALU["ge_to_cached"] + (L_ - 1) * VALU["ge_add"])
+    # position m of a piece of length Lp is live for Lp-m steps (a short last piece starts late)
+    binom = sum(sum(cost_m[m] * (Lp - m) for m in range(1, Lp)) for Lp in pieces)
+    stepping = n * sum(Lp * VALU["ge_to_cached"] + (Lp - 1) * VALU["ge_add"] for Lp in pieces)
     combine = 0
     if U > 1:  # k_combine: pairwise Horner in y^2 with joint NAF chains (kernels.hip)
         for j in range(1, n + 1):
@@ -202,11 +216,11 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS):
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
-def fused_valu(n, t, U=1, VALU=SLOTS):
+def fused_valu(n, t, U=1, VALU=SLOTS, plen=None):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
     recombination; one check kernel computing g*s once (32 radix-256 comb windows), h*s' (32 more) and both
     equalities per pair."""
-    w2, w4 = algorithmic_valu(n, t, 2, U, VALU), algorithmic_valu(n, t, 4, U, VALU)
+    w2, w4 = algorithmic_valu(n, t, 2, U, VALU, plen), algorithmic_valu(n, t, 4, U, VALU, plen)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
     out["check"] = n * n * (2 * 32 * VALU["comb8_window"] + 2 * VALU["eq"])
     return out
@@ -489,11 +503,12 @@ def main():
         out["config"]["verify_streams"] = args.streams
         out["config"]["rounds_2_4_fused"] = not args.no_overlap
         ov = not args.no_overlap
-        U = be.last_split()
+        U, Ls = be.last_split(), be.last_split_len()
         out["config"]["degree_split"] = U
-        w2, w4 = algorithmic_valu(n, t, 2, U), algorithmic_valu(n, t, 4, U)
-        work = fused_valu(n, t, U) if ov else w2
-        work_i = fused_valu(n, t, U, INSTR) if ov else algorithmic_valu(n, t, 2, U, INSTR)
+        out["config"]["split_pieces"] = split_pieces(t, U, Ls)[0]
+        w2, w4 = algorithmic_valu(n, t, 2, U, plen=Ls), algorithmic_valu(n, t, 4, U, plen=Ls)
+        work = fused_valu(n, t, U, plen=Ls) if ov else w2
+        work_i = fused_valu(n, t, U, INSTR, Ls) if ov else algorithmic_valu(n, t, 2, U, INSTR, Ls)
         # per-kernel device times need the serialised schedule (one chunk stream): one extra,
         # untimed ceremony in the same round order as the timed ones
         be.set_streams(1)
@@ -514,8 +529,8 @@ def main():
             out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} "
                                             f"instructions) per pass over {what} (closed form); device time of "
                                             f"the kernel's launches (HIP events) in a serialised pass")
-            alg, launches = algorithmic_bytes(dom, n, t, U) if ov else (None, None)
-            pmc = pmc_traffic(dom, n, t, U) if ov else None
+            alg, launches = algorithmic_bytes(dom, n, t, U, Ls) if ov else (None, None)
+            pmc = pmc_traffic(dom, n, t, U, Ls) if ov else None
             if alg is not None:
                 ms_launch = rl[dom]["ms_per_pass"] / launches
                 out["roofline"]["algorithmic_bytes_per_launch"] = alg
@@ -553,10 +568,10 @@ def main():
         torch.cuda.synchronize()
         be.set_streams(args.streams)
         ph = be.phase_times("r24" if not args.no_overlap else "r2")
-        U = be.last_split()
+        U, Ls = be.last_split(), be.last_split_len()
         D = ((rank + 1) * n) // ws - (rank * n) // ws
-        work = {k: v * D / n for k, v in fused_valu(n, t, U).items()}
-        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR).items()}
+        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls).items()}
+        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls).items()}
         rl = kernel_rooflines(ph, work, work_i)
         out["config"]["degree_split"] = U
         if rl:

@@ -134,6 +134,10 @@ class Backend:
     def last_split(self) -> int:
         return _lib.lib().dkg_ctx_last_split(self._ctx)
 
+    def last_split_len(self) -> int:
+        """Piece length L of the last split (the last piece holds t + 1 - (U - 1) L coefficients)."""
+        return _lib.lib().dkg_ctx_last_split_len(self._ctx)
+
     def set_overlap(self, on: bool):
         """Verify rounds 2 and 4 as one fused pipeline (default) or in protocol order."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_overlap(self._ctx, 1 if on else 0))

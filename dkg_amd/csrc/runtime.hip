@@ -38,6 +38,7 @@ struct dkg_ctx {
   size_t vinv_N = 0;                    // key of the cached inverse Vandermonde (v.vinv)
   size_t fallback_rows = 0;             // interpolation mode: rows re-verified the general way
   int last_split = 1;                   // U used by the last verify_device
+  size_t last_split_len = 0;            // and its piece length L
   size_t ydig_n = 0, ydig_L = 0;        // key of the cached combine multipliers (v.ydig)
   // round-1 commitments of the ceremony being verified, in extended form on this device (set by
   // the drivers that generate them, ExtScope): verify_device places them instead of decoding the
@@ -235,8 +236,10 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
 }
 
 // Piece length of a U-way split: ceil(N / U), or that rounded up to a multiple of 64 when the
-// model prefers it -- whole 64-lane waves for the stepping's tables and a shorter last piece
-// (N = 512, U = 3: pieces of 192, 192, 128 instead of 171, 171, 170).
+// model prefers it -- whole 64-lane waves for the stepping's per-piece tables and a shorter last
+// piece (N = 550, U = 2: 320 + 230 instead of 275 + 275, two tables of 5 and 4 waves instead of
+// 5 + 5 with 45 idle lanes each).  When all pieces of a column fit one stepping workgroup
+// (N <= 512) ceil(N / U) always wins: N = 512, U = 3 runs 171 + 171 + 170 on 512 lanes.
 size_t split_len(size_t cols, size_t n, size_t N, size_t U) {
   const size_t L1 = (N + U - 1) / U;
   if (U == 1) return L1;
@@ -343,6 +346,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U), W = U * npad;
   const size_t Lr = N - (U - 1) * L;  // the last piece's length (L or shorter)
   ctx->last_split = (int)U;
+  ctx->last_split_len = L;
   hipStream_t home = ctx->stream;
   uint8_t* pok = buf<uint8_t>(ctx, "v.pok", npad * N);
   uint8_t* dok = buf<uint8_t>(ctx, "v.dok", npad);
@@ -1215,10 +1219,16 @@ int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
 }
 
 int dkg_ctx_last_split(const dkg_ctx* ctx) { return ctx ? ctx->last_split : 0; }
+size_t dkg_ctx_last_split_len(const dkg_ctx* ctx) { return ctx ? ctx->last_split_len : 0; }
 
 double dkg_split_model_ms(size_t columns, size_t n, size_t t, int pieces) {
   if (pieces < 1 || t + 1 < (size_t)pieces) return -1;
   return split_model_ms(columns, n, t + 1, (size_t)pieces);
+}
+
+size_t dkg_split_len(size_t columns, size_t n, size_t t, int pieces) {
+  if (pieces < 1 || t + 1 < (size_t)pieces) return 0;
+  return split_len(columns, n, t + 1, (size_t)pieces);
 }
 
 int dkg_ctx_set_overlap(dkg_ctx* ctx, int on) {

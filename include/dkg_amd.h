@@ -78,8 +78,12 @@ int dkg_ctx_set_verify_mode(dkg_ctx *ctx, int mode);
 size_t dkg_ctx_fallback_rows(const dkg_ctx *ctx);
 /* U used by the last ceremony's checks on this ctx. */
 int dkg_ctx_last_split(const dkg_ctx *ctx);
+/* Piece length L of that split: pieces 0..U-2 hold L coefficients, the last one t+1-(U-1)L. */
+size_t dkg_ctx_last_split_len(const dkg_ctx *ctx);
 /* The cost model's estimate (ms) of binomial + recombination for `columns` difference tables. */
 double dkg_split_model_ms(size_t columns, size_t n, size_t t, int pieces);
+/* The piece length L the runtime uses for a `pieces`-way split of such tables (0 on bad input). */
+size_t dkg_split_len(size_t columns, size_t n, size_t t, int pieces);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
 int dkg_device_count(void);
 

@@ -76,9 +76,13 @@ def test_split_cost_model():
     L = _lib.lib()
     ms = lambda cols, n, t, U: L.dkg_split_model_ms(cols, n, t, U)  # noqa: E731
     assert ms(2048, 1024, 511, 2) < 0.9 * ms(2048, 1024, 511, 1)
-    # n=1024: U=3 (pieces 192 + 192 + 128, one stepping workgroup per column) measured 3 % faster
-    # than U=2 (profiles/r02_split_ab.txt)
+    # n=1024: U=3 (pieces 171 + 171 + 170, one 512-lane stepping workgroup per column) measured 6 %
+    # faster than U=2 (profiles/r02_split_ab.txt)
     assert min(range(1, 9), key=lambda U: ms(2048, 1024, 511, U)) == 3
+    assert L.dkg_split_len(2048, 1024, 511, 3) == 171 and L.dkg_split_len(2048, 1024, 511, 2) == 256
+    # n=1100, U=2: 275 + 275 would leave 45 idle lanes per 320-lane stepping table: 320 + 230
+    assert L.dkg_split_len(2304, 1100, 549, 2) == 320 and L.dkg_split_len(2304, 1100, 549, 3) == 184
+    assert L.dkg_split_len(64, 10, 4, 6) == 0
     assert min(range(1, 17), key=lambda U: ms(8192, 4096, 2047, U)) == 4
     # dealer shards of n=1024 (2 rows per dealer): smaller shards split more (a shorter dependent
     # binomial chain; measured profiles/r01_shard_scaling_n1024_v13.txt for U in 1, 2, 4, 8)

@@ -31,17 +31,19 @@ def test_algorithmic_bytes_stepping_and_combine():
 
 
 def test_pmc_traffic_matches_workload():
-    """The committed traffic file belongs to the n=1024, t=511, U=2 pipeline; other workloads get
-    None (their traffic was not measured), and the binomial's measured bytes are within 10 % of
-    its algorithmic bytes (no re-reads)."""
-    got = bench.pmc_traffic("binomial", 1024, 511, 2)
-    assert got is not None
-    measured, source = got
-    alg, _ = bench.algorithmic_bytes("binomial", 1024, 511, 2)
-    assert 0.9 < measured / alg < 1.1
+    """The committed traffic file belongs to the n=1024, t=511, U=3 (L=171) pipeline; other
+    workloads get None (their traffic was not measured), and every check-pipeline kernel's
+    measured bytes are within 10 % of its algorithmic bytes (no re-reads)."""
+    for k in ("binomial", "stepping", "combine"):
+        got = bench.pmc_traffic(k, 1024, 511, 3, 171)
+        assert got is not None, k
+        measured, source = got
+        alg, _ = bench.algorithmic_bytes(k, 1024, 511, 3, 171)
+        assert 0.9 < measured / alg < 1.1, (k, measured / alg)
     assert "FETCH_SIZE" in source and "WRITE_SIZE" in source
     assert bench.pmc_traffic("binomial", 4096, 2047, 4) is None
-    assert bench.pmc_traffic("binomial", 1024, 511, 4) is None
+    assert bench.pmc_traffic("binomial", 1024, 511, 2) is None
+    assert bench.pmc_traffic("binomial", 1024, 511, 3, 192) is None
 
 
 def test_closed_form_work_per_pair():
@@ -68,3 +70,20 @@ def test_valu_table_matches_count_tool_format():
     """bench.VALU holds (instructions, issue slots) per primitive; slots between 1x and 2x."""
     for k, (ins, sl) in bench.VALU.items():
         assert ins <= sl <= 2 * ins, k
+
+
+def test_split_pieces_and_bytes():
+    """Uneven pieces (runtime.hip split_len): n=1100, t=549, U=2 with L=320 -> 320 + 230; the short
+    last piece joins the binomial 90 steps late (fewer bytes and slots than two pieces of 320)."""
+    assert bench.split_pieces(549, 2, 320) == ([320, 230], 320)
+    assert bench.split_pieces(511, 3) == ([171, 171, 170], 171)
+    assert bench.split_pieces(511, 2) == ([256, 256], 256)
+    per, nl = bench.algorithmic_bytes("binomial", 1100, 549, 2, 320)
+    assert nl == 319
+    cols = 2 * 1100
+    total = sum(cols * 160 * (2 + 3 * r) + cols * 160 * (2 + 3 * max(r - 90, 0)) for r in range(1, 320))
+    assert per * nl == pytest.approx(total)
+    w = bench.algorithmic_valu(1100, 549, 2, 2, plen=320)
+    w_even = bench.algorithmic_valu(1100, 549, 2, 2)
+    assert w["stepping"] == pytest.approx(w_even["stepping"], rel=0.01)  # the same 550 positions
+    assert w_even["binomial"] < w["binomial"] < 1.1 * w_even["binomial"]

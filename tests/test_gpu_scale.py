@@ -3,7 +3,7 @@
 The oracle (tests/oracle_lib.py: dalek-3's algorithms, a vartime MSM per pair, committee.rs:287-305,
 532-548) recomputes WHOLE decision rows of the tampered dealers; the honest rows are checked by
 properties.  Sizes: n=256 (t=127), n=1024 (t=511, the headline schedule: cost-model split U=3 with
-pieces of 192 + 192 + 128 positions, two dealer-chunk streams, rounds 2 and 4 fused; and forced
+pieces of 171 + 171 + 170 positions, two dealer-chunk streams, rounds 2 and 4 fused; and forced
 U=2 / U=4), n=1100 (t=549) and n=4096 (t=2047) with splits whose pieces exceed 512 positions, i.e.
 the block-chained stepping (kernels.hip k_stepping<512> with its up/down boundary streams) or end
 in a short last piece, and the 10,000-ceremony batch of config 5.
@@ -110,9 +110,9 @@ def _check_rows(n, dec2, dec4, qualified, exp, ctx):
 @pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0), (1024, 511, 2), (1024, 511, 4)])
 def test_faults_baseline_sizes(be, n, t, split):
     """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=3 from the cost
-    model with pieces of 192, 192 and 128 positions, every piece of a column in one stepping
-    workgroup, two dealer-chunk streams, rounds 2 and 4 fused), and forced U=2 / U=4 (pieces of one
-    stepping workgroup each): tampered shares, randomness, E and A
+    model with pieces of 171, 171 and 170 positions, the last one joining the binomial a step late,
+    every piece of a column in one 512-lane stepping workgroup, two dealer-chunk streams, rounds 2
+    and 4 fused), and forced U=2 / U=4: tampered shares, randomness, E and A
     coefficients, an undecodable E row and a tampered self-share.  Whole rows of every tampered
     dealer equal the oracle's per-pair MSM checks; qualification, reconstruction, final shares and
     the final parties' mpk follow the reference's rules (committee.rs:311-398, 454-467, 660-805)."""
@@ -182,13 +182,16 @@ def _shard_verify_all(be, n, t, tE, tA, ts, tsp):
     return o2.view(n, n), o4.view(n, n)
 
 
-@pytest.mark.parametrize("n,t,splits", [(1100, 549, (1, 3)), (4096, 2047, (2, 1, 3))])
+# (U, piece length L) per run; the last piece holds t + 1 - (U - 1) L coefficients
+@pytest.mark.parametrize("n,t,splits", [(1100, 549, ((1, 550), (3, 184), (2, 320))),
+                                        (4096, 2047, ((2, 1024), (1, 2048), (3, 683)))])
 def test_faults_multiblock_stepping(be, golden, n, t, splits):
     """Pieces longer than 512 positions take the block-chained stepping (k_stepping<512>, the top
     block streaming its per-step values down): n=1100, t=549 unsplit (2 blocks of 275) and n=4096,
-    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks); U=3 gives a short last piece
-    (n=1100: 192 + 192 + 166 positions, the last piece in its own stepping launch; n=4096: pieces
-    of 704, 704 and 640 in 2 blocks each, the last one's top positions the identity).  The committee is built on the
+    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks).  Short last pieces: n=1100
+    at U=3 (184 + 184 + 182, per-piece stepping tables, the last one in its own launch) and U=2
+    (320 + 230: the piece length rounded up to whole waves, the last piece joining the binomial 90
+    steps late), n=4096 at U=3 (683 + 683 + 682 in 2 blocks each).  The committee is built on the
     device (dkg_share_gen_device), tampered there, and verified as one shard of all dealers; whole
     rows of the tampered dealers equal the oracle's (MSM over t+1 = 550 / 2048 points, Pippenger
     w=7 / w=8).  At n=4096 the committee uses the seed of tests/golden/spot_n4096_t2047.json, whose
@@ -221,14 +224,13 @@ def test_faults_multiblock_stepping(be, golden, n, t, splits):
         t_[:len(b_)] = torch.frombuffer(bytearray(b_), dtype=torch.uint8).to(t_.device)
     sample = [7, n - 3] + random.Random(n).sample(range(8, n - 3), 30) if n > 2000 else None
     exp = _expected_rows(n, t, h, E, A, s, sp, sample=sample)
-    for U in splits:
+    for U, plen in splits:
         be.set_split(U)
         try:
             d2, d4 = _shard_verify_all(be, n, t, tE, tA, ts, tsp)
-            assert be.last_split() == U
+            assert be.last_split() == U and be.last_split_len() == plen
         finally:
             be.set_split(0)
-        assert -(-N // U) > 512 or U == 3  # pieces longer than one 512-lane block: block-chained stepping
         h2 = d2[:D5].cpu().numpy()
         h4 = d4[:D5].cpu().numpy()
         # shard rows carry the raw decisions (SKIPPED is applied by the combine step)

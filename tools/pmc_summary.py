@@ -1,6 +1,6 @@
 """Summarise rocprofv3 CSV output of tools/profile.sh per kernel (sums over dispatches).
 
-usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag> [traffic.json n t U]
+usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag> [traffic.json n t U [L]]
 Prints kernel-trace stats (calls, total/avg ms) and, per kernel, the SQ issue/wait split,
 VALU instructions (wave-level x 64 lanes) and HBM-side bytes: FETCH_SIZE doubled (gfx950 counts
 half the bytes of wide coalesced reads, MI355X_MICROARCH.md "HBM") and WRITE_SIZE, both in KB.
@@ -54,11 +54,12 @@ def main(d):
               f"{2 * fe[k].get('FETCH_SIZE', 0) / 1e3:12.1f} {wr[k].get('WRITE_SIZE', 0) / 1e3:10.1f}")
 
 
-PHASE = {"k_binom_step": "binomial", "void k_stepping<256>": "stepping", "void k_stepping<512>": "stepping",
+PHASE = {"k_binom_step": "binomial", "void k_stepping<192>": "stepping", "void k_stepping<256>": "stepping",
+         "void k_stepping<512>": "stepping",
          "void k_combine<1>": "combine", "void k_combine<2>": "combine", "k_check_both": "check", "k_check": "check"}
 
 
-def write_traffic(d, out, n, t, U):
+def write_traffic(d, out, n, t, U, split_len=None):
     """Per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, counted in separate --pmc passes) of the
     check-pipeline kernels, summed over every dispatch the profiled run made."""
     fe, fcalls = load_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
@@ -78,6 +79,8 @@ def write_traffic(d, out, n, t, U):
     doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
                      f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
            "n": n, "t": t, "split": U, "kernels": kern}
+    if split_len:
+        doc["split_len"] = split_len
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
 
@@ -85,4 +88,5 @@ def write_traffic(d, out, n, t, U):
 if __name__ == "__main__":
     main(sys.argv[1])
     if len(sys.argv) > 2:
-        write_traffic(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
+        write_traffic(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]),
+                      int(sys.argv[6]) if len(sys.argv) > 6 else None)
