@@ -77,10 +77,14 @@ double step_occupancy(size_t bs, size_t maxbs);
 // true when every piece of a split column fits one workgroup slot ((pieces-1) L + last_len <= 512):
 // the stepping then runs one slot per column over all pieces
 bool stepping_whole_columns(size_t L, size_t pieces, size_t last_len);
+// cost model of stepping()'s launches over `cols` columns: SIMD cycles per (receiver step x
+// instruction of one addition); compare modes / splits with it
+double stepping_cycles(size_t cols, size_t N, size_t pieces, size_t last_len, bool whole);
 // last_len (0: N): length of a shorter last piece (its table positions >= last_len are not read)
+// whole: run the pieces of a column in one slot when they fit (stepping_whole_columns)
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces = 1, size_t pstride = 0,
-              size_t last_len = 0);
+              size_t last_len = 0, bool whole = true);
 // Degree-split recombination: R[c][j] = sum_u y_j^u R[u * pstride + c][j] (pairwise Horner in y^2
 // with joint NAF chains; digits [n][2][256] = NAF of y_j and y_j^2, top [n][2])
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,

@@ -600,9 +600,32 @@ bool stepping_whole_columns(size_t L, size_t pieces, size_t last_len) {
   return pieces > 1 && (pieces - 1) * L + last_len <= 512;
 }
 
+// Model of stepping()'s launches in SIMD cycles per receiver step and addition instruction: each
+// launch runs ceil(workgroups / resident) rounds of its long-lived workgroups; a round costs one
+// wave's chain of n additions at max(w * THR / occ(w), LAT) cycles per instruction with w the
+// waves per SIMD of that round: issue-shared, at a rate that still grows from 2 to 4 resident
+// waves (occ 0.7 .. 1: n=4096 at U=5 runs 448-lane tables at 3.5 waves per SIMD 16 % slower
+// than U=4's 512-lane ones at 4, profiles/r02_split_ab.txt), latency-bound below.
+double stepping_cycles(size_t cols, size_t N, size_t pieces, size_t last_len, bool whole) {
+  const double THR = 4.5, LAT = 8, SIMDS = 1024;
+  if (!last_len || last_len > N) last_len = N;
+  auto launch = [&](const StepShape& s, double np) {
+    const double per_cu = std::min(std::floor(1024.0 / s.maxbs), std::floor(16.0 / (s.bs / 64.0)));
+    const double wgs = std::ceil((double)cols / s.per) * np * s.nblk, cap = 256 * per_cu;
+    const double rounds = std::ceil(wgs / cap), in_round = wgs / rounds;
+    const double w = in_round * (s.bs / 64.0) / SIMDS;
+    const double occ = std::min(1.0, std::max(0.7, 0.7 + 0.15 * (w - 2)));
+    return rounds * std::max(w * THR / occ, LAT);
+  };
+  if (whole && stepping_whole_columns(N, pieces, last_len)) return launch(stepping_shape((pieces - 1) * N + last_len), 1);
+  const StepShape sh = stepping_shape(N);
+  if (sh.nblk > 1 || last_len == N) return launch(sh, (double)pieces);
+  return (pieces > 1 ? launch(sh, (double)(pieces - 1)) : 0.0) + launch(stepping_shape(last_len), 1);
+}
+
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
-              size_t last_len) {
+              size_t last_len, bool whole) {
   if (!ndealers || !nrecv) return;
   if (!last_len || last_len > N) last_len = N;
   auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
@@ -617,7 +640,7 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
       hipLaunchKernelGGL(k_stepping<512>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
                          (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
   };
-  if (stepping_whole_columns(N, pieces, last_len)) {
+  if (whole && stepping_whole_columns(N, pieces, last_len)) {
     // one slot of (pieces - 1) N + last_len lanes per column: every workgroup does the same work
     // (a column), so a launch of ndealers columns has no tail of lone pieces
     StepShape s = stepping_shape((pieces - 1) * N + last_len);

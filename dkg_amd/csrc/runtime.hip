@@ -34,6 +34,7 @@ struct dkg_ctx {
   hipEvent_t fork = nullptr, join[MAX_SUB] = {};
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
+  int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece
   int verify_mode = 0;                  // 0: difference tables (every P_i(j) in the group); 1: interpolation
   size_t vinv_N = 0;                    // key of the cached inverse Vandermonde (v.vinv)
   size_t fallback_rows = 0;             // interpolation mode: rows re-verified the general way
@@ -176,6 +177,14 @@ struct VerifySeg {
   size_t self_mod = 0;                // self = (dealer + dealer_base) mod self_mod == j; 0: n
 };
 
+// Whole-column stepping slots (all U pieces of a column in one workgroup slot) when they fit and
+// the launch model says so (ties to per-piece slots: more, smaller workgroups; measured on the
+// 8-way n=1024 shard at U=4, 19.8 vs 20.9 ms, profiles/r02_shard_stepping_ab.txt).
+bool stepping_whole_pays(size_t cols, size_t U, size_t L, size_t Lr) {
+  return dkgk::stepping_whole_columns(L, U, Lr) &&
+         dkgk::stepping_cycles(cols, L, U, Lr, true) < 0.98 * dkgk::stepping_cycles(cols, L, U, Lr, false);
+}
+
 // ---- degree split ----
 // P(x) = sum_{u<U} x^(uL) Q_u(x), deg Q_u < L = ceil(N / U): the binomial-basis Horner runs on the
 // U pieces (quadratic in the degree: ~1/U of the work, and ~1/U of the dependent chain), the
@@ -218,20 +227,8 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
     const double waves = (double)cols / 64 * n;
     cyc += std::max(waves * per * THR / SIMDS, per * LAT);  // the 2-slot variant runs at 2 waves/SIMD as fast
   }
-  // stepping: n dependent additions per lane on the lanes k_stepping allocates to each piece's
-  // table, or to a whole column's pieces (dkgk::stepping_shape), slower when a workgroup leaves a
-  // SIMD fewer than 4 waves, and when the last round of long-running workgroups leaves CUs idle
-  auto step_cyc = [&](size_t len, double pieces) {
-    const dkgk::StepShape sh = dkgk::stepping_shape(len);
-    const double lanes = (double)sh.nblk * sh.bs / sh.per;
-    const double waves = (double)cols * pieces * lanes / 64;
-    const double per_cu = std::min(std::floor(1024.0 / sh.maxbs), std::floor(16.0 / (sh.bs / 64.0)));
-    const double wgs = std::ceil((double)cols / sh.per) * pieces, rounds = std::ceil(wgs / (256 * per_cu));
-    const double tail = wgs / (rounds * 256 * per_cu);
-    return std::max(waves * n * ADD * THR / SIMDS / dkgk::step_occupancy(sh.bs, sh.maxbs) / tail, n * ADD * LAT);
-  };
-  if (dkgk::stepping_whole_columns(L, U, Lr)) cyc += step_cyc(N, 1.0);
-  else cyc += Lr == L ? step_cyc(L, (double)U) : step_cyc(L, (double)(U - 1)) + step_cyc(Lr, 1.0);
+  // stepping: n dependent additions per lane, in the launches k_stepping gets (dkgk::stepping_cycles)
+  cyc += n * ADD * dkgk::stepping_cycles(cols, L, U, Lr, stepping_whole_pays(cols, U, L, Lr));
   return cyc / 2.4e6;
 }
 
@@ -345,6 +342,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // degree split: U pieces of L positions; piece u of column c is table column u * npad + c
   const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U), W = U * npad;
   const size_t Lr = N - (U - 1) * L;  // the last piece's length (L or shorter)
+  const bool whole = ctx->step_mode == 1 || (ctx->step_mode == 0 && stepping_whole_pays(npad, U, L, Lr));
   ctx->last_split = (int)U;
   ctx->last_split_len = L;
   hipStream_t home = ctx->stream;
@@ -397,7 +395,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
     dkgk::stepping(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr);
+                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));
@@ -1215,6 +1213,12 @@ size_t dkg_ctx_fallback_rows(const dkg_ctx* ctx) { return ctx ? ctx->fallback_ro
 int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
   if (!ctx || pieces < 0 || pieces > 16) return DKG_E_ARG;
   ctx->split = pieces;
+  return DKG_OK;
+}
+
+int dkg_ctx_set_stepping(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return DKG_E_ARG;
+  ctx->step_mode = mode;
   return DKG_OK;
 }
 

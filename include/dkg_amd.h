@@ -63,6 +63,10 @@ int dkg_ctx_set_overlap(dkg_ctx *ctx, int on);
  * multiplications by j^L; 0 (default) picks U with the cost model dkg_split_model_ms; 1 disables.
  * Decisions and outputs do not depend on it. */
 int dkg_ctx_set_split(dkg_ctx *ctx, int pieces);
+/* How the stepping covers a split table whose pieces fit one 512-lane workgroup together:
+ * 0 (default) by the cost model, 1 one workgroup slot per column holding all its pieces, 2 one
+ * slot per piece.  Outputs do not depend on it. */
+int dkg_ctx_set_stepping(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and
  *                 compared with g s_ij + h s'_ij, as each receiver of the reference does;

@@ -81,7 +81,7 @@ def test_split_cost_model():
     assert min(range(1, 9), key=lambda U: ms(2048, 1024, 511, U)) == 3
     assert L.dkg_split_len(2048, 1024, 511, 3) == 171 and L.dkg_split_len(2048, 1024, 511, 2) == 256
     # n=1100, U=2: 275 + 275 would leave 45 idle lanes per 320-lane stepping table: 320 + 230
-    assert L.dkg_split_len(2304, 1100, 549, 2) == 320 and L.dkg_split_len(2304, 1100, 549, 3) == 184
+    assert L.dkg_split_len(2304, 1100, 549, 2) == 320 and L.dkg_split_len(2304, 1100, 549, 3) == 192
     assert L.dkg_split_len(64, 10, 4, 6) == 0
     assert min(range(1, 17), key=lambda U: ms(8192, 4096, 2047, U)) == 4
     # dealer shards of n=1024 (2 rows per dealer): smaller shards split more (a shorter dependent

@@ -183,15 +183,15 @@ def _shard_verify_all(be, n, t, tE, tA, ts, tsp):
 
 
 # (U, piece length L) per run; the last piece holds t + 1 - (U - 1) L coefficients
-@pytest.mark.parametrize("n,t,splits", [(1100, 549, ((1, 550), (3, 184), (2, 320))),
+@pytest.mark.parametrize("n,t,splits", [(1100, 549, ((1, 550), (3, 192), (2, 320))),
                                         (4096, 2047, ((2, 1024), (1, 2048), (3, 683)))])
 def test_faults_multiblock_stepping(be, golden, n, t, splits):
     """Pieces longer than 512 positions take the block-chained stepping (k_stepping<512>, the top
     block streaming its per-step values down): n=1100, t=549 unsplit (2 blocks of 275) and n=4096,
-    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks).  Short last pieces: n=1100
-    at U=3 (184 + 184 + 182, per-piece stepping tables, the last one in its own launch) and U=2
-    (320 + 230: the piece length rounded up to whole waves, the last piece joining the binomial 90
-    steps late), n=4096 at U=3 (683 + 683 + 682 in 2 blocks each).  The committee is built on the
+    t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks).  Short last pieces, the piece
+    length rounded up to whole waves: n=1100 at U=3 (192 + 192 + 166, per-piece stepping tables,
+    the last one in its own launch, joining the binomial 26 steps late) and U=2 (320 + 230, 90 steps
+    late), n=4096 at U=3 (683 + 683 + 682 in 2 blocks each).  The committee is built on the
     device (dkg_share_gen_device), tampered there, and verified as one shard of all dealers; whole
     rows of the tampered dealers equal the oracle's (MSM over t+1 = 550 / 2048 points, Pippenger
     w=7 / w=8).  At n=4096 the committee uses the seed of tests/golden/spot_n4096_t2047.json, whose
