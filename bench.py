@@ -392,6 +392,8 @@ def main():
                     help="group: every P_i(j) computed in the group (default); interp: committee verification "
                          "by interpolation (identical decisions, DESIGN.md section 2)")
     ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
+    ap.add_argument("--field", type=int, default=0,
+                    help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")
@@ -416,6 +418,7 @@ def main():
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
     be.set_split(args.split)
+    be.set_field_mode(args.field)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1

@@ -131,6 +131,11 @@ class Backend:
         """Degree split of the difference tables (0 = cost model, 1 = off); results are identical."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_split(self._ctx, pieces))
 
+    def set_field_mode(self, mode: int):
+        """Field multiplication of the verification kernels: 0 by occupancy, 1 product scanning,
+        2 column sums; results are identical."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_field_mode(self._ctx, mode))
+
     def set_stepping(self, mode: int):
         """Stepping slots of a split table: 0 cost model, 1 one per column (all pieces), 2 one per
         piece; results are identical."""

@@ -2,21 +2,22 @@
 //
 // Representation: ten unsigned 32-bit limbs in radix 2^25.5 (limb i holds 26 bits for even i,
 // 25 bits for odd i; bit offsets 0,26,51,77,102,128,153,179,204,230).  A product limb pair is
-// one v_mad_u64_u32 (32x32 -> 64 plus a 64-bit addend), which the microbenchmark in
-// tools/ubench/intrate2.hip measured at the same issue cost as v_mul_lo_u32 / v_mul_hi_u32, so a
-// field multiply is 100 MADs + 9 x19 pre-multiplies + one 64-bit carry pass (a square is 55 MADs).
-// The pseudo-Mersenne fold 2^255 = 19 is applied inside the product (no Montgomery form: the
-// x19 fold is cheaper for this prime than a Montgomery reduction; see DESIGN.md "field").
+// one v_mad_u64_u32 (32x32 -> 64 plus a 64-bit addend), so a field multiply is 100 MADs + 9 x19
+// pre-multiplies + the carries (a square is 55 MADs).  The pseudo-Mersenne fold 2^255 = 19 is
+// applied inside the product (no Montgomery form).  Two flavours of the multiply, fixed per
+// translation unit: product scanning (default; fewest issue slots) and column sums (DKG_FE_ILP;
+// ten independent chains, for latency-bound launches) -- see fe_mul below and DESIGN.md section 5.
 //
-// Bounds (machine-checked: tools/fe_bounds.py propagates worst-case limb bounds through every
-// primitive and every formula of ge25519.h / points.h as written, and tests/test_bounds.py runs it).
-// TIGHT = every fe_mul / fe_sq / fe_carry output and every stored point coordinate: limbs below
-// 2^26 + 2^6 (even) / 2^25 + 2^12 (odd).  fe_mul(f, g) is overflow-free for uniform limb bounds up to
-// (f, g) = (2^28, 2^27.75), (2^28.32, 2^27.585) or (2^29, 2^26) -- g carries the x19 fold (19 g
-// < 2^32), f the x2 weight, and every 64-bit column sum stays below 2^64.  The formulas hand it at
-// most f = (h - t) + 2p <= 2^28 (doubling) and g = (d - c) + 2p <= 1.5 * 2^27 = 2^27.585 (additions)
-// or 2p - xy2d <= 2^27 (comb entries).  fe_sub(a, b) = a + 2p - b needs b <= 2p limbwise (a TIGHT b
-// always is); anything looser goes through fe_carry first.
+// Bounds (machine-checked: tools/fe_bounds.py propagates worst-case limb bounds through both
+// flavours of every primitive and every formula of ge25519.h / points.h as written, and
+// tests/test_bounds.py runs it).  TIGHT = every fe_mul / fe_sq / fe_carry output and every stored
+// point coordinate: limbs below 2^26 + 2^6 (even) / 2^25 + 2^12 (odd).  fe_mul(f, g) is
+// overflow-free for uniform limb bounds up to (f, g) = (2^28, 2^27.75), (2^28.32, 2^27.585) or
+// (2^29, 2^26) -- g carries the x19 fold (19 g < 2^32), f the x2 weight, and every 64-bit column
+// sum stays below 2^64.  The formulas hand it at most f = (h - t) + 2p <= 2^28 (doubling) and
+// g = (d - c) + 2p <= 1.5 * 2^27 = 2^27.585 (additions) or 2p - xy2d <= 2^27 (comb entries).
+// fe_sub(a, b) = a + 2p - b needs b <= 2p limbwise (a TIGHT b always is); anything looser goes
+// through fe_carry first.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -118,7 +119,7 @@ DKG_DEV uint64_t mad_first(uint32_t a, uint32_t b) {
     r.v[1] += (uint32_t)(t_ >> 26);                                  \
   }
 
-DKG_DEV void fe_mul(fe& r, const fe& f, const fe& g) {
+DKG_DEV void fe_mul_ps(fe& r, const fe& f, const fe& g) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
   const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
   const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
@@ -166,7 +167,7 @@ DKG_DEV void fe_mul(fe& r, const fe& f, const fe& g) {
   FE_FOLD(r, h)
 }
 
-DKG_DEV void fe_sq(fe& r, const fe& f) {
+DKG_DEV void fe_sq_ps(fe& r, const fe& f) {
   // Symmetric products counted once; x19 factors kept on limbs 5..9 (19 * 2^27.585 < 2^32) and
   // the extra 2 / 4 weights moved onto the partner limb so every operand fits in 32 bits.
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
@@ -210,8 +211,7 @@ DKG_DEV void fe_sq(fe& r, const fe& f) {
   FE_FOLD(r, h)
 }
 
-// r = a * k for a small constant k < 2^12 (a tight).
-DKG_DEV void fe_mul_small(fe& r, const fe& a, uint32_t k) {
+DKG_DEV void fe_mul_small_ps(fe& r, const fe& a, uint32_t k) {
   uint64_t h = mad_first(a.v[0], k);
   FE_LIMB(r, 0, h)
   mad_acc(h, a.v[1], k); FE_LIMB(r, 1, h)
@@ -224,6 +224,138 @@ DKG_DEV void fe_mul_small(fe& r, const fe& a, uint32_t k) {
   mad_acc(h, a.v[8], k); FE_LIMB(r, 8, h)
   mad_acc(h, a.v[9], k); FE_LIMB(r, 9, h)
   FE_FOLD(r, h)
+}
+
+// ---- the same three functions as ten independent column sums ("operand scanning") and one
+// parallel 64-bit carry pass afterwards: 12 % more issue slots than product scanning, but ten
+// independent mad chains per multiplication instead of one, which pays where a SIMD holds too few
+// waves to hide the chain (small multi-GPU shards, the first binomial steps).  Compiled into the
+// dkgk_ilp copy of the kernels (kernels.hip with DKG_FE_ILP); the runtime picks the copy per
+// launch by occupancy.
+// Carry the ten 64-bit column sums into a tight element.
+DKG_DEV void fe_carry64(fe& r, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4,
+                        uint64_t h5, uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+  uint64_t c;
+  c = h0 >> 26; h1 += c; h0 &= 0x3ffffff;
+  c = h4 >> 26; h5 += c; h4 &= 0x3ffffff;
+  c = h1 >> 25; h2 += c; h1 &= 0x1ffffff;
+  c = h5 >> 25; h6 += c; h5 &= 0x1ffffff;
+  c = h2 >> 26; h3 += c; h2 &= 0x3ffffff;
+  c = h6 >> 26; h7 += c; h6 &= 0x3ffffff;
+  c = h3 >> 25; h4 += c; h3 &= 0x1ffffff;
+  c = h7 >> 25; h8 += c; h7 &= 0x1ffffff;
+  c = h4 >> 26; h5 += c; h4 &= 0x3ffffff;
+  c = h8 >> 26; h9 += c; h8 &= 0x3ffffff;
+  c = h9 >> 25; h0 += c * 19; h9 &= 0x1ffffff;
+  c = h0 >> 26; h1 += c; h0 &= 0x3ffffff;
+  r.v[0] = (uint32_t)h0; r.v[1] = (uint32_t)h1; r.v[2] = (uint32_t)h2; r.v[3] = (uint32_t)h3;
+  r.v[4] = (uint32_t)h4; r.v[5] = (uint32_t)h5; r.v[6] = (uint32_t)h6; r.v[7] = (uint32_t)h7;
+  r.v[8] = (uint32_t)h8; r.v[9] = (uint32_t)h9;
+}
+
+DKG_DEV void fe_mul_cs(fe& r, const fe& f, const fe& g) {
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
+  const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
+  const uint32_t g1_19 = 19u * g1, g2_19 = 19u * g2, g3_19 = 19u * g3, g4_19 = 19u * g4;
+  const uint32_t g5_19 = 19u * g5, g6_19 = 19u * g6, g7_19 = 19u * g7, g8_19 = 19u * g8;
+  const uint32_t g9_19 = 19u * g9;
+  const uint32_t f1_2 = dbl32(f1), f3_2 = dbl32(f3), f5_2 = dbl32(f5), f7_2 = dbl32(f7), f9_2 = dbl32(f9);
+  uint64_t h0 = mul32(f0, g0) + mul32(f1_2, g9_19) + mul32(f2, g8_19) + mul32(f3_2, g7_19) +
+                mul32(f4, g6_19) + mul32(f5_2, g5_19) + mul32(f6, g4_19) + mul32(f7_2, g3_19) +
+                mul32(f8, g2_19) + mul32(f9_2, g1_19);
+  uint64_t h1 = mul32(f0, g1) + mul32(f1, g0) + mul32(f2, g9_19) + mul32(f3, g8_19) +
+                mul32(f4, g7_19) + mul32(f5, g6_19) + mul32(f6, g5_19) + mul32(f7, g4_19) +
+                mul32(f8, g3_19) + mul32(f9, g2_19);
+  uint64_t h2 = mul32(f0, g2) + mul32(f1_2, g1) + mul32(f2, g0) + mul32(f3_2, g9_19) +
+                mul32(f4, g8_19) + mul32(f5_2, g7_19) + mul32(f6, g6_19) + mul32(f7_2, g5_19) +
+                mul32(f8, g4_19) + mul32(f9_2, g3_19);
+  uint64_t h3 = mul32(f0, g3) + mul32(f1, g2) + mul32(f2, g1) + mul32(f3, g0) + mul32(f4, g9_19) +
+                mul32(f5, g8_19) + mul32(f6, g7_19) + mul32(f7, g6_19) + mul32(f8, g5_19) +
+                mul32(f9, g4_19);
+  uint64_t h4 = mul32(f0, g4) + mul32(f1_2, g3) + mul32(f2, g2) + mul32(f3_2, g1) + mul32(f4, g0) +
+                mul32(f5_2, g9_19) + mul32(f6, g8_19) + mul32(f7_2, g7_19) + mul32(f8, g6_19) +
+                mul32(f9_2, g5_19);
+  uint64_t h5 = mul32(f0, g5) + mul32(f1, g4) + mul32(f2, g3) + mul32(f3, g2) + mul32(f4, g1) +
+                mul32(f5, g0) + mul32(f6, g9_19) + mul32(f7, g8_19) + mul32(f8, g7_19) +
+                mul32(f9, g6_19);
+  uint64_t h6 = mul32(f0, g6) + mul32(f1_2, g5) + mul32(f2, g4) + mul32(f3_2, g3) + mul32(f4, g2) +
+                mul32(f5_2, g1) + mul32(f6, g0) + mul32(f7_2, g9_19) + mul32(f8, g8_19) +
+                mul32(f9_2, g7_19);
+  uint64_t h7 = mul32(f0, g7) + mul32(f1, g6) + mul32(f2, g5) + mul32(f3, g4) + mul32(f4, g3) +
+                mul32(f5, g2) + mul32(f6, g1) + mul32(f7, g0) + mul32(f8, g9_19) + mul32(f9, g8_19);
+  uint64_t h8 = mul32(f0, g8) + mul32(f1_2, g7) + mul32(f2, g6) + mul32(f3_2, g5) + mul32(f4, g4) +
+                mul32(f5_2, g3) + mul32(f6, g2) + mul32(f7_2, g1) + mul32(f8, g0) +
+                mul32(f9_2, g9_19);
+  uint64_t h9 = mul32(f0, g9) + mul32(f1, g8) + mul32(f2, g7) + mul32(f3, g6) + mul32(f4, g5) +
+                mul32(f5, g4) + mul32(f6, g3) + mul32(f7, g2) + mul32(f8, g1) + mul32(f9, g0);
+  fe_carry64(r, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+DKG_DEV void fe_sq_cs(fe& r, const fe& f) {
+  // Symmetric products counted once; x19 factors kept on limbs 5..9 (19 * 2^27.585 < 2^32) and
+  // the extra 2 / 4 weights moved onto the partner limb so every operand fits in 32 bits.
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t f0_2 = dbl32(f0), f1_2 = dbl32(f1), f2_2 = dbl32(f2), f3_2 = dbl32(f3), f4_2 = dbl32(f4);
+  const uint32_t f5_2 = dbl32(f5), f6_2 = dbl32(f6), f7_2 = dbl32(f7), f8_2 = dbl32(f8), f9_2 = dbl32(f9);
+  const uint32_t f1_4 = dbl32(f1_2), f3_4 = dbl32(f3_2), f5_4 = dbl32(f5_2), f7_4 = dbl32(f7_2);
+  const uint32_t f5_19 = 19u * f5, f6_19 = 19u * f6, f7_19 = 19u * f7, f8_19 = 19u * f8;
+  const uint32_t f9_19 = 19u * f9;
+  uint64_t h0 = mul32(f0, f0) + mul32(f1_4, f9_19) + mul32(f2_2, f8_19) + mul32(f3_4, f7_19) +
+                mul32(f4_2, f6_19) + mul32(f5_2, f5_19);
+  uint64_t h1 = mul32(f0_2, f1) + mul32(f2_2, f9_19) + mul32(f3_2, f8_19) + mul32(f4_2, f7_19) +
+                mul32(f5_2, f6_19);
+  uint64_t h2 = mul32(f0_2, f2) + mul32(f1_2, f1) + mul32(f3_4, f9_19) + mul32(f4_2, f8_19) +
+                mul32(f5_4, f7_19) + mul32(f6, f6_19);
+  uint64_t h3 = mul32(f0_2, f3) + mul32(f1_2, f2) + mul32(f4_2, f9_19) + mul32(f5_2, f8_19) +
+                mul32(f6_2, f7_19);
+  uint64_t h4 = mul32(f0_2, f4) + mul32(f1_2, f3_2) + mul32(f2, f2) + mul32(f5_4, f9_19) +
+                mul32(f6_2, f8_19) + mul32(f7_2, f7_19);
+  uint64_t h5 = mul32(f0_2, f5) + mul32(f1_2, f4) + mul32(f2_2, f3) + mul32(f6_2, f9_19) +
+                mul32(f7_2, f8_19);
+  uint64_t h6 = mul32(f0_2, f6) + mul32(f1_2, f5_2) + mul32(f2_2, f4) + mul32(f3_2, f3) +
+                mul32(f7_4, f9_19) + mul32(f8, f8_19);
+  uint64_t h7 = mul32(f0_2, f7) + mul32(f1_2, f6) + mul32(f2_2, f5) + mul32(f3_2, f4) +
+                mul32(f8_2, f9_19);
+  uint64_t h8 = mul32(f0_2, f8) + mul32(f1_2, f7_2) + mul32(f2_2, f6) + mul32(f3_2, f5_2) +
+                mul32(f4, f4) + mul32(f9_2, f9_19);
+  uint64_t h9 = mul32(f0_2, f9) + mul32(f1_2, f8) + mul32(f2_2, f7) + mul32(f3_2, f6) +
+                mul32(f4_2, f5);
+  fe_carry64(r, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+// r = a * k for a small constant k < 2^12 (a tight).
+DKG_DEV void fe_mul_small_cs(fe& r, const fe& a, uint32_t k) {
+  uint64_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = mul32(a.v[i], k);
+  fe_carry64(r, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+}
+
+// r = f * g, r = f^2, r = a * k (k < 2^12): all inputs tight or as bounded in tools/fe_bounds.py,
+// outputs tight.  The flavour is fixed per translation unit.
+DKG_DEV void fe_mul(fe& r, const fe& f, const fe& g) {
+#ifdef DKG_FE_ILP
+  fe_mul_cs(r, f, g);
+#else
+  fe_mul_ps(r, f, g);
+#endif
+}
+DKG_DEV void fe_sq(fe& r, const fe& f) {
+#ifdef DKG_FE_ILP
+  fe_sq_cs(r, f);
+#else
+  fe_sq_ps(r, f);
+#endif
+}
+DKG_DEV void fe_mul_small(fe& r, const fe& a, uint32_t k) {
+#ifdef DKG_FE_ILP
+  fe_mul_small_cs(r, a, k);
+#else
+  fe_mul_small_ps(r, a, k);
+#endif
 }
 
 DKG_DEV void fe_sqn(fe& r, const fe& a, int n) {

@@ -6,6 +6,11 @@
 //   K5 decode / encode              <- groups.rs:72-81
 // See DESIGN.md for the algorithm (exact finite-difference evaluation of the committed
 // polynomial in the exponent) and the roofline of each kernel.
+// Built twice (dkg_amd/Makefile): as namespace dkgk with the product-scanning field
+// multiplication, and with DKG_FE_ILP as namespace dkgk_ilp with the column-sum one.
+#ifdef DKG_FE_ILP
+#define dkgk dkgk_ilp
+#endif
 #include "kernels.h"
 
 #include <algorithm>
@@ -424,23 +429,29 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
   pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
+void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, hipStream_t stream,
+                size_t pieces, size_t pstride) {
+  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,
+                     npad, N, C, N - 1, e0, pstride);
+}
+
+void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
+                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
+  const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
+  // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
+  hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64 * pieces), (unsigned)(r + 1)), dim3(64), 0, stream,
+                     (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 64),
+                     (unsigned)(pieces - 1), last_off);
+}
+
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
                    hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
-  const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
-  const size_t t = N - 1;
-  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,
-                     npad, N, C, t, e0, pstride);
+  binom_init(width, npad, N, C, e0, stream, pieces, pstride);
   uint32_t* in = e0;
   uint32_t* out = e1;
-  for (size_t r = 1; r <= t; r++) {
-    const size_t k = t - r;
-    // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
-    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64 * pieces), (unsigned)(r + 1)), dim3(64), 0,
-                       stream, (int)r, (int)k, npad, N, C, in, out, pstride, (unsigned)(width / 64),
-                       (unsigned)(pieces - 1), last_off);
-    uint32_t* tmp = in;
-    in = out;
-    out = tmp;
+  for (size_t r = 1; r < N; r++) {
+    binom_step(r, width, npad, N, C, in, out, stream, pieces, pstride, last_len);
+    std::swap(in, out);
   }
   return in;
 }
@@ -621,6 +632,16 @@ double stepping_cycles(size_t cols, size_t N, size_t pieces, size_t last_len, bo
   const StepShape sh = stepping_shape(N);
   if (sh.nblk > 1 || last_len == N) return launch(sh, (double)pieces);
   return (pieces > 1 ? launch(sh, (double)(pieces - 1)) : 0.0) + launch(stepping_shape(last_len), 1);
+}
+
+double stepping_waves_per_simd(size_t cols, size_t N, size_t pieces, size_t last_len, bool whole) {
+  if (!last_len || last_len > N) last_len = N;
+  const bool wc = whole && stepping_whole_columns(N, pieces, last_len);
+  const StepShape s = stepping_shape(wc ? (pieces - 1) * N + last_len : N);
+  const double np = wc ? 1.0 : (last_len == N || s.nblk > 1 ? (double)pieces : (double)(pieces - 1));
+  const double per_cu = std::min(std::floor(1024.0 / s.maxbs), std::floor(16.0 / (s.bs / 64.0)));
+  const double wgs = std::ceil((double)cols / s.per) * np * s.nblk, cap = 256 * per_cu;
+  return wgs / std::ceil(wgs / cap) * (s.bs / 64.0) / 1024;
 }
 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,

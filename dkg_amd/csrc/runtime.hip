@@ -13,6 +13,7 @@
 #include "../../include/dkg_amd.h"
 #include "host_crypto.h"
 #include "kernels.h"
+#include "kernels_ilp.h"
 
 struct dkg_ctx {
   int device = 0;
@@ -35,6 +36,8 @@ struct dkg_ctx {
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
   int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece
+  int fe_mode = 0;                      // field multiplication per launch: 0 by occupancy, 1 product
+                                        // scanning (dkgk), 2 column sums (dkgk_ilp)
   int verify_mode = 0;                  // 0: difference tables (every P_i(j) in the group); 1: interpolation
   size_t vinv_N = 0;                    // key of the cached inverse Vandermonde (v.vinv)
   size_t fallback_rows = 0;             // interpolation mode: rows re-verified the general way
@@ -176,6 +179,13 @@ struct VerifySeg {
   const uint8_t* extra_ok = nullptr;  // [D] device: 0 = the dealer's other broadcast data is missing
   size_t self_mod = 0;                // self = (dealer + dealer_base) mod self_mod == j; 0: n
 };
+
+// Which copy of a kernel runs a launch: product scanning (dkgk, fewer issue slots) or column sums
+// (dkgk_ilp, ten independent chains per multiplication) when the launch leaves too few waves per
+// SIMD to hide the serial chain (`latency_bound`), unless dkg_ctx_set_field_mode forces one.
+bool use_ilp(const dkg_ctx* ctx, bool latency_bound) {
+  return ctx->fe_mode == 2 || (ctx->fe_mode == 0 && latency_bound);
+}
 
 // Whole-column stepping slots (all U pieces of a column in one workgroup slot) when they fit and
 // the launch model says so (ties to per-piece slots: more, smaller workgroups; measured on the
@@ -343,6 +353,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U), W = U * npad;
   const size_t Lr = N - (U - 1) * L;  // the last piece's length (L or shorter)
   const bool whole = ctx->step_mode == 1 || (ctx->step_mode == 0 && stepping_whole_pays(npad, U, L, Lr));
+  // the stepping keeps product scanning even at 2 waves per SIMD (8-way n=1024 shard, one stream:
+  // 6.07 vs 6.12 ms with column sums, profiles/r02_shard_stepping_ab.txt); only a forced mode 2
+  // switches it
+  const bool step_ilp = use_ilp(ctx, false);
   ctx->last_split = (int)U;
   ctx->last_split_len = L;
   hipStream_t home = ctx->stream;
@@ -391,10 +405,18 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    const uint32_t* e = dkgk::binomial(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad, Lr);
+    dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
+    uint32_t *bin = e0 + c0, *bout = e1 + c0;
+    for (size_t r = 1; r < L; r++) {
+      // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
+      const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (r + 1) / 1024 < 1.5);
+      (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+      std::swap(bin, bout);
+    }
+    const uint32_t* e = bin;
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
-    dkgk::stepping(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
+    (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
@@ -407,11 +429,13 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // that the chunks' phases drift apart and one chunk's recombination and checks run beside the
   // other's stepping.  A small ceremony or shard is latency-bound -- every binomial step is one
   // dependent NAF chain long whatever its width -- and two half-width pipelines only double its
-  // launches.  Measured (tools/shard_time.py): chunks gain 1.2-2.4 ms on n=1024 4- and 8-way
-  // shards and n=512 1- and 2-way (>= 6.7e7 lane-steps) and lose 0.9-2.5 ms on n=512 4-way and
-  // n=256 (<= 3.4e7).
+  // launches.  Measured (tools/shard_time.py): chunks gain 1.2-2.4 ms on n=512 1- and 2-way (>= 6.7e7
+  // lane-steps) and 0.3-0.8 ms on n=1024 1- to 4-way, and lose 0.9-2.5 ms on n=512 4-way and n=256
+  // (<= 3.4e7) -- and 2 ms on the 8-way n=1024 shard (256 columns: two half-width stepping launches
+  // of 128 workgroups each, 18.1 vs 20.2 ms, profiles/r02_shard_stepping_ab.txt), so a long stepping
+  // needs at least 512 columns too.
   const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
-  const bool long_stepping = (double)W * (double)L * (double)n >= 5e7;
+  const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
   const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
   ctx->timed_tag.clear();
   if (nsub <= 1) {
@@ -1213,6 +1237,12 @@ size_t dkg_ctx_fallback_rows(const dkg_ctx* ctx) { return ctx ? ctx->fallback_ro
 int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
   if (!ctx || pieces < 0 || pieces > 16) return DKG_E_ARG;
   ctx->split = pieces;
+  return DKG_OK;
+}
+
+int dkg_ctx_set_field_mode(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return DKG_E_ARG;
+  ctx->fe_mode = mode;
   return DKG_OK;
 }
 

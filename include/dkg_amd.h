@@ -67,6 +67,10 @@ int dkg_ctx_set_split(dkg_ctx *ctx, int pieces);
  * 0 (default) by the cost model, 1 one workgroup slot per column holding all its pieces, 2 one
  * slot per piece.  Outputs do not depend on it. */
 int dkg_ctx_set_stepping(dkg_ctx *ctx, int mode);
+/* Field multiplication of the verification kernels: 0 (default) per launch by occupancy, 1 always
+ * product scanning (fewest issue slots), 2 always column sums (most independent chains; for
+ * latency-bound launches).  Outputs do not depend on it. */
+int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and
  *                 compared with g s_ij + h s'_ij, as each receiver of the reference does;

@@ -11,9 +11,19 @@ import fe_bounds as F  # noqa: E402
 
 
 def test_terms_follow_the_header():
-    """fe_mul has 10 x 10 products, fe_sq the 55 distinct ones, read from fe25519.h."""
-    assert sum(len(v) for v in F._parse_terms("fe_mul").values()) == 100
-    assert sum(len(v) for v in F._parse_terms("fe_sq").values()) == 55
+    """fe_mul has 10 x 10 products, fe_sq the 55 distinct ones, read from fe25519.h, in both
+    flavours, and the two flavours sum the same products into each column."""
+    import random
+
+    for fl in ("ps", "cs"):
+        assert sum(len(v) for v in F._parse_terms(f"fe_mul_{fl}").values()) == 100
+        assert sum(len(v) for v in F._parse_terms(f"fe_sq_{fl}").values()) == 55
+    rng = random.Random(5)
+    for _ in range(50):
+        f = [rng.getrandbits(26) for _ in range(10)]
+        g = [rng.getrandbits(26) for _ in range(10)]
+        assert F._columns("fe_mul_ps", f, g, "x") == F._columns("fe_mul_cs", f, g, "x")
+        assert F._columns("fe_sq_ps", f, f, "x") == F._columns("fe_sq_cs", f, f, "x")
 
 
 def test_no_overflow_anywhere():

@@ -743,6 +743,26 @@ def test_degree_split_goldens(be, golden, name, pieces):
         be.set_overlap(True)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n16_t7.json", "ceremony_n64_t31.json"])
+def test_field_modes_goldens(be, golden, name, mode):
+    """Both copies of the verification kernels (dkgk: product-scanning field multiplication, dkgk_ilp:
+    column sums; dkg_ctx_set_field_mode) forced for every launch, with and without a degree split:
+    every output bit-exact against the fixture."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    try:
+        be.set_field_mode(mode)
+        for pieces in (1, min(3, t + 1)):
+            be.set_split(pieces)
+            r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+            _check_ceremony(c, r, n)
+    finally:
+        be.set_field_mode(0)
+        be.set_split(0)
+
+
 @pytest.mark.parametrize("pieces", [1, 2, 3])
 def test_degree_split_n256_matches_unsplit(be, pieces):
     """n = 256, t = 127 (BASELINE config 2) from device coefficients with one E row made undecodable

@@ -8,8 +8,9 @@ fe_sq take their product terms (which limb pairs, which operand carries the x19 
 weights) straight from the header text, so the checker cannot drift from the code.  It asserts:
   * every 32-bit limb result (fe_add, fe_sub, fe_neg, fe_carry, the x19 / x2 / x4 pre-multiplies
     of fe_mul / fe_sq) stays below 2^32, and fe_sub / fe_neg never wrap (subtrahend <= 2p limbwise);
-  * every 64-bit column sum of fe_mul / fe_sq (on top of the carry out of the previous column,
-    product scanning), and the x19 fold of the top carry, stay below 2^64 / 2^32 as computed;
+  * every 64-bit column sum of fe_mul / fe_sq in both flavours (product scanning: on top of the
+    carry out of the previous column, and the x19 fold of the top carry; column sums: every
+    intermediate of the carry pass fe_carry64) stays below 2^64, every 32-bit value below 2^32;
   * fe_tobytes32's canonical reduction sees a value below 2p (one conditional subtraction suffices).
 The group formulas (ge_to_cached, ge_add, ge_sub, ge_madd, ge_msub, ge_dbl / _rt / _lean,
 ge_add_signed, ge_add_lds incl. its negated path, the comb entry selection of comb8_mul_add,
@@ -111,22 +112,53 @@ def fe_scan(cols, where):
     return r
 
 
+def fe_carry64(h, where):
+    """fe_carry64 of fe25519.h (the column-sum flavour's carry pass), statement by statement."""
+    h = list(h)
+    for x in h:
+        check(f"{where} column", x, U64)
+
+    def step(i, j, fold=1):
+        c = h[i] >> W[i]
+        h[j] += c * fold
+        check(f"{where} carry into h{j}", h[j], U64)
+        h[i] = min(h[i], MASK[i])
+
+    for i, j in [(0, 1), (4, 5), (1, 2), (5, 6), (2, 3), (6, 7), (3, 4), (7, 8), (4, 5), (8, 9)]:
+        step(i, j)
+    step(9, 0, 19)
+    step(0, 1)
+    for i in range(10):
+        check(f"{where} carried limb fits u32", h[i], U32)
+    return h
+
+
 _MUL_TERMS = {}
 
 
-def _parse_terms(func):
-    """Column k of `func` (fe_mul / fe_sq / fe_mul_small in fe25519.h) as a list of (operand,
-    operand) names: the mad_first / mad_acc calls before FE_LIMB(r, k, h)."""
-    if func in _MUL_TERMS:
-        return _MUL_TERMS[func]
+def _body(func, end):
     src = open(FE_H).read()
     body = src[src.index(f"DKG_DEV void {func}("):]
-    body = body[:body.index("FE_FOLD(")]
-    cols, last = {}, 0
-    for m in re.finditer(r"FE_LIMB\(r, (\d), h\)", body):
-        seg = body[last:m.start()]
-        cols[int(m.group(1))] = re.findall(r"mad_(?:first\(|acc\(h, )([\w.\[\]]+), ([\w.\[\]]+)\)", seg)
-        last = m.end()
+    return body[:body.index(end)]
+
+
+def _parse_terms(func):
+    """Column k of `func` in fe25519.h as a list of (operand, operand) names: for the
+    product-scanning flavour (fe_mul_ps / fe_sq_ps / fe_mul_small_ps) the mad_first / mad_acc calls
+    before FE_LIMB(r, k, h); for the column-sum flavour (fe_mul_cs / fe_sq_cs) the mul32 terms of
+    `uint64_t hk = ...`."""
+    if func in _MUL_TERMS:
+        return _MUL_TERMS[func]
+    cols = {}
+    if func.endswith("_cs"):
+        for m in re.finditer(r"uint64_t h(\d) = (.*?);", _body(func, "fe_carry64("), re.S):
+            cols[int(m.group(1))] = re.findall(r"mul32\((\w+), (\w+)\)", m.group(2))
+    else:
+        body, last = _body(func, "FE_FOLD("), 0
+        for m in re.finditer(r"FE_LIMB\(r, (\d), h\)", body):
+            cols[int(m.group(1))] = re.findall(r"mad_(?:first\(|acc\(h, )([\w.\[\]]+), ([\w.\[\]]+)\)",
+                                               body[last:m.start()])
+            last = m.end()
     assert sorted(cols) == list(range(10)), f"{func}: could not parse the ten columns"
     _MUL_TERMS[func] = cols
     return cols
@@ -144,22 +176,27 @@ def _operand(name, f, g, where):
     return base * k
 
 
+def _columns(func, f, g, where):
+    cols = _parse_terms(func)
+    return [sum(_operand(x, f, g, where) * _operand(y, f, g, where) for x, y in cols[k]) for k in range(10)]
+
+
 def fe_mul(f, g, where="fe_mul"):
-    cols = _parse_terms("fe_mul")
-    return fe_scan([sum(_operand(x, f, g, where) * _operand(y, f, g, where) for x, y in cols[k])
-                    for k in range(10)], where)
+    """Both flavours of fe25519.h (dkgk: product scanning, dkgk_ilp: column sums) on the same
+    inputs; the result bound is the larger of the two."""
+    return vmax(fe_scan(_columns("fe_mul_ps", f, g, where), where),
+                fe_carry64(_columns("fe_mul_cs", f, g, where), where))
 
 
 def fe_sq(f, where="fe_sq"):
-    cols = _parse_terms("fe_sq")
-    return fe_scan([sum(_operand(x, f, f, where) * _operand(y, f, f, where) for x, y in cols[k])
-                    for k in range(10)], where)
+    return vmax(fe_scan(_columns("fe_sq_ps", f, f, where), where),
+                fe_carry64(_columns("fe_sq_cs", f, f, where), where))
 
 
 def fe_mul_small(a, k, where="fe_mul_small"):
-    cols = _parse_terms("fe_mul_small")
+    cols = _parse_terms("fe_mul_small_ps")
     assert all(c == [(f"a.v[{i}]", "k")] for i, c in cols.items()), "fe_mul_small: unexpected terms"
-    return fe_scan([a[i] * k for i in range(10)], where)
+    return vmax(fe_scan([a[i] * k for i in range(10)], where), fe_carry64([a[i] * k for i in range(10)], where))
 
 
 def fe_tobytes32(a, where="fe_tobytes32"):

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--split", type=int, default=0, help="degree split (0: cost model)")
     ap.add_argument("--stepping", type=int, default=0, help="stepping slots: 0 model, 1 per column, 2 per piece")
+    ap.add_argument("--field", type=int, default=0, help="field multiply: 0 by occupancy, 1 product scanning, 2 column sums")
     args = ap.parse_args()
     import torch
 
@@ -36,6 +37,7 @@ def main():
     be.set_streams(args.streams)
     be.set_split(args.split)
     be.set_stepping(args.stepping)
+    be.set_field_mode(args.field)
     be.env_init(t, n)
     dev = torch.device("cuda", 0)
     res = {}
@@ -63,7 +65,7 @@ def main():
         ph = be.phase_times("r24" if not args.no_overlap else "r4")
         print(json.dumps({"n": n, "t": t, "ws": ws, "dealers": D, "ms_wall": res[ws],
                           "overlap": not args.no_overlap, "streams": args.streams, "split": be.last_split(),
-                          "split_len": be.last_split_len(), "stepping": args.stepping,
+                          "split_len": be.last_split_len(), "stepping": args.stepping, "field": args.field,
                           "phases_ms_if_serialised": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     base = res.get(1)
     if base:
