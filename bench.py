@@ -10,9 +10,11 @@ N GPUs (torchrun, one process per GPU): the SAME ceremony is sharded by dealer; 
 generates and verifies its dealers' rows for all receivers, then RCCL all-gathers (over xGMI) the
 decision rows, the A_i0 commitments and the final-share partial sums (strong scaling).
 
-Also printed in the same JSON line: the roofline of the dominant kernel (INT32-VALU bound; see
-DESIGN.md "Measurement") and the CPU baseline: the dalek-algorithm-matched C oracle timed on a
-bounded sample of round-2 checks on this host's cores.
+Also printed in the same JSON line: the roofline of the dominant kernel (VALU issue slots, with the
+PMC-measured HBM bytes per launch) and the CPU baseline: the
+dalek-algorithm-matched C oracle timed on a bounded sample of the same ceremony (share generation
+and round-2 and round-4 checks of a subset of dealers against all receivers) on every host thread
+this process may use, extrapolated to the whole ceremony.
 """
 import argparse
 import ctypes
