@@ -1226,12 +1226,15 @@ void sum_shares(size_t D, size_t n, const uint32_t* s, const uint8_t* mask, uint
 // ceremonies): row_reject[i] = some receiver rejected dealer i or its data is missing (it is not
 // qualified); complaints[g][j] = number of dealers of group g rejected (REJECT only, MISSING is no
 // complaint) by receiver j (committee.rs:311-316, 331-335, 340-347).
-__global__ void k_row_reject(size_t rows, size_t n, const uint8_t* __restrict__ dec, uint8_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows) return;
-  uint8_t r = 0;
-  for (size_t j = 0; j < n; j++) r |= dec[i * n + j] == 0 || dec[i * n + j] == 4;  // REJECT or MISSING
-  out[i] = r;
+// One wave per row: the lanes read the row's bytes coalesced, a ballot reduces.
+__global__ __launch_bounds__(256) void k_row_reject(size_t rows, size_t n, const uint8_t* __restrict__ dec,
+                                                    uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows) return;  // wave-uniform
+  bool r = false;
+  for (size_t j = threadIdx.x & 63; j < n; j += 64) r |= dec[i * n + j] == 0 || dec[i * n + j] == 4;  // REJECT / MISSING
+  const bool any = __ballot(r) != 0;
+  if ((threadIdx.x & 63) == 0) out[i] = any;
 }
 
 __global__ void k_col_complaints(size_t groups, size_t n, const uint8_t* __restrict__ dec, int32_t* __restrict__ out) {
@@ -1268,7 +1271,7 @@ void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_
   const size_t rows = groups * n;
   if (!rows) return;
   if (row_reject)
-    hipLaunchKernelGGL(k_row_reject, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, rows, n, dec,
+    hipLaunchKernelGGL(k_row_reject, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, rows, n, dec,
                        row_reject);
   if (complaints)
     hipLaunchKernelGGL(k_col_complaints, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, groups, n, dec,

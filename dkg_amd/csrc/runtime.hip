@@ -33,6 +33,11 @@ struct dkg_ctx {
   int nsub = 2;                         // dealer-chunk streams of verify_device
   hipStream_t sub[MAX_SUB] = {};
   hipEvent_t fork = nullptr, join[MAX_SUB] = {};
+  // round-1 share evaluation on a low-priority side stream beside the first binomial steps
+  // (round1_device with overlap_shares): the checks and round 3 wait for shares_done
+  hipStream_t side = nullptr;
+  hipEvent_t side_fork = nullptr, shares_done = nullptr;
+  bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
   int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece
@@ -185,6 +190,11 @@ struct VerifySeg {
 // SIMD to hide the serial chain (`latency_bound`), unless dkg_ctx_set_field_mode forces one.
 bool use_ilp(const dkg_ctx* ctx, bool latency_bound) {
   return ctx->fe_mode == 2 || (ctx->fe_mode == 0 && latency_bound);
+}
+
+// Work on `st` that reads the shares waits for an overlapped share evaluation (round1_device).
+void wait_shares(dkg_ctx* ctx, hipStream_t st) {
+  if (ctx->shares_pending) HCK(hipStreamWaitEvent(st, ctx->shares_done, 0));
 }
 
 // Whole-column stepping slots (all U pieces of a column in one workgroup slot) when they fit and
@@ -391,6 +401,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // checks of dealers [d0, d1) on stream st
   auto checks = [&](size_t d0, size_t d1, hipStream_t st) {
     if (d1 <= d0) return;
+    wait_shares(ctx, st);
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
       dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
@@ -752,25 +763,26 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
   // ---- rounds 2 and 4 (committee.rs:260-366, :508-580), fused or in protocol order (verify_rounds)
-  std::vector<uint8_t> h2(n * n), h4(n * n);
+  std::vector<uint8_t> h4(copy_big && out->dec4 ? n * n : 0);
   std::vector<uint8_t> qualified(n, 1), r2err(n, 0);
   std::vector<int32_t> complaints(n, 0);
   uint32_t* fs = buf<uint32_t>(ctx, "final_share", 32 * n);
   uint32_t* pubc = buf<uint32_t>(ctx, "pub_comp", 32 * n);
+  uint8_t* rej = buf<uint8_t>(ctx, "rej", n);
+  int32_t* cnt = buf<int32_t>(ctx, "cnt", 4 * n);
+  uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
   auto round3 = [&] {
-    d2h(ctx, h2.data(), dec2, n * n);
+    wait_shares(ctx, ctx->stream);
+    // on the device: rows with a REJECT (a valid complaint disqualifies dealer i for everyone,
+    // committee.rs:311-316, 370-398) or MISSING (no decodable broadcast: disqualified without a
+    // complaint, :331-335), and the REJECTs of each receiver's column (its complaints)
+    dkgk::decision_summary(1, n, dec2, rej, cnt, ctx->stream);
+    d2h(ctx, qualified.data(), rej, n);
+    d2h(ctx, complaints.data(), cnt, 4 * n);
     sync(ctx);
-    for (size_t i = 0; i < n; i++)
-      for (size_t j = 0; j < n; j++)
-        if (h2[i * n + j] == DKG_REJECT) {
-          complaints[j]++;     // receiver j accuses dealer i (committee.rs:311-316)
-          qualified[i] = 0;    // a valid complaint disqualifies i for everyone (:370-398)
-        } else if (h2[i * n + j] == DKG_MISSING) {
-          qualified[i] = 0;    // no (decodable) broadcast: disqualified, no complaint (:331-335)
-        }
+    for (size_t i = 0; i < n; i++) qualified[i] = !qualified[i];
     for (size_t j = 0; j < n; j++) r2err[j] = complaints[j] > (int32_t)t;  // :340-347
     // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
-    uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
     h2d(ctx, qmask, qualified.data(), n);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
     uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
@@ -779,18 +791,20 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
   verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok, a_ok);
-  d2h(ctx, h4.data(), dec4, n * n);
+  wait_shares(ctx, ctx->stream);
+  ctx->shares_pending = false;
+  // round-4 outcome on the device: a qualified dealer some receiver rejects is reconstructed
+  // (committee.rs:660-670); receiver j's round-4 error (:515-516, 567-569) counts itself and the
+  // qualified dealers it accepted
+  std::vector<uint8_t> recon(n, 0), r4e(n, 0);
+  uint8_t* r4ed = buf<uint8_t>(ctx, "r4err", n);
+  dkgk::decision_summary(1, n, dec4, rej, nullptr, ctx->stream);
+  dkgk::r4_error(1, n, t, dec4, qmask, r4ed, ctx->stream);
+  d2h(ctx, recon.data(), rej, n);
+  d2h(ctx, r4e.data(), r4ed, n);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   sync(ctx);
-  std::vector<uint8_t> recon(n, 0);
-  std::vector<size_t> honest4(n, 1);  // round-4 honest count of receiver j, itself included (:515-516)
-  for (size_t i = 0; i < n; i++)
-    for (size_t j = 0; j < n; j++) {
-      if (i == j) continue;
-      if (!qualified[i]) h4[i * n + j] = DKG_SKIPPED;  // disqualified dealers are skipped (:522)
-      else if (h4[i * n + j] == DKG_REJECT) recon[i] = 1;  // -> reconstructable set (:660-670)
-      else if (h4[i * n + j] == DKG_ACCEPT) honest4[j]++;
-    }
+  for (size_t i = 0; i < n; i++) recon[i] = qualified[i] && recon[i];
   // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
   std::vector<uint8_t> honest_mask = final_parties(n, qualified.data(), recon.data());
   size_t nrecon = 0;
@@ -846,37 +860,58 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   // ---- outputs
   if (out->qualified) memcpy(out->qualified, qualified.data(), n);
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), n);
-  if (out->r4_error)
-    for (size_t j = 0; j < n; j++) out->r4_error[j] = honest4[j] < t + 1;  // :567-569
+  if (out->r4_error) memcpy(out->r4_error, r4e.data(), n);
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * n);
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
   out->n_qualified = nq;
   out->phase4_error = phase4_error;  // committee.rs:673-677
   if (copy_big) {
-    if (out->dec2) memcpy(out->dec2, h2.data(), n * n);
-    if (out->dec4) memcpy(out->dec4, h4.data(), n * n);
+    if (out->dec2) d2h(ctx, out->dec2, dec2, n * n);
+    if (out->dec4) d2h(ctx, h4.data(), dec4, n * n);
     if (out->final_share) d2h(ctx, out->final_share, fs, 32 * n);
     if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * n);
   }
   sync(ctx);
+  if (copy_big && out->dec4) {
+    for (size_t i = 0; i < n; i++)
+      if (!qualified[i])
+        for (size_t j = 0; j < n; j++)
+          if (j != i) h4[i * n + j] = DKG_SKIPPED;  // disqualified dealers are skipped (:522)
+    memcpy(out->dec4, h4.data(), n * n);
+  }
 }
 
 // Round 1 for D dealers on device: a, b canonical [D][N][8] -> Ecomp, Acomp [D][N][8], s, sp [D][n][8].
 // Round 1 on device.  encode = false: the commitments stay group elements (Ecomp / Acomp are not
 // written; the caller verifies through an ExtScope, as the reference's in-memory broadcasts).
+// overlap_shares: the share evaluation runs on ctx->side (lowest priority) beside what follows on
+// ctx->stream -- the verification's first binomial steps, which occupy few CUs -- and the
+// verification's checks and round 3 wait for it (ctx->shares_pending, wait_shares).
 void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a, const uint32_t* b,
-                   uint32_t* Ecomp, uint32_t* Acomp, uint32_t* s, uint32_t* sp, bool encode = true) {
+                   uint32_t* Ecomp, uint32_t* Acomp, uint32_t* s, uint32_t* sp, bool encode = true,
+                   bool overlap_shares = false) {
   const size_t N = t + 1;
   uint32_t* Aext = buf<uint32_t>(ctx, "Aext", PTB * D * N);
   uint32_t* Eext = buf<uint32_t>(ctx, "Eext", PTB * D * N);
+  if (overlap_shares) {  // the side stream starts where ctx->stream is (a, b written)
+    HCK(hipEventRecord(ctx->side_fork, ctx->stream));
+    HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
+  }
   dkgk::commit(D * N, a, b, ctx->tab_g8, ctx->tab_h8, Aext, Eext, ctx->stream);  // K2 (committee.rs:151-159)
   if (encode) {
     dkgk::encode_points(Eext, D * N, D * N, Ecomp, ctx->stream);                  // broadcast encodings
     dkgk::encode_points(Aext, D * N, D * N, Acomp, ctx->stream);
   }
-  dkgk::share_eval(D, n, N, a, b, s, sp, ctx->stream);                            // K1 (:164-167)
+  if (overlap_shares) {
+    dkgk::share_eval(D, n, N, a, b, s, sp, ctx->side);                             // K1 (:164-167)
+    HCK(hipEventRecord(ctx->shares_done, ctx->side));
+    ctx->shares_pending = true;
+  } else {
+    dkgk::share_eval(D, n, N, a, b, s, sp, ctx->stream);
+  }
   check_launch(ctx);
 }
+
 
 // Verify what round1_device just generated from its extended-form commitments (no encode/decode
 // round trip); restores the ctx on exit.
@@ -1163,10 +1198,17 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
   dkg_ctx* ctx = new dkg_ctx();
   ctx->device = device;
   int rc = guarded(ctx, [&] {
-    HCK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    // the ceremony's own streams at the highest priority, the side stream at the lowest: a
+    // latency-bound binomial step must not queue behind the side stream's share evaluation
+    int least = 0, greatest = 0;
+    HCK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HCK(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, greatest));
     for (auto& e : ctx->ev) HCK(hipEventCreate(&e));
     for (auto& e : ctx->pev) HCK(hipEventCreate(&e));
-    for (auto& st : ctx->sub) HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (auto& st : ctx->sub) HCK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+    HCK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
+    HCK(hipEventCreateWithFlags(&ctx->side_fork, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&ctx->shares_done, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
@@ -1209,6 +1251,9 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   for (auto& st : ctx->sub)
     if (st) (void)hipStreamDestroy(st);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
+  if (ctx->shares_done) (void)hipEventDestroy(ctx->shares_done);
   delete ctx;
 }
 
@@ -1506,7 +1551,12 @@ int dkg_ceremony_run_device(dkg_ctx* ctx, size_t n, size_t t, const void* d_a, c
     uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
     uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
+#ifdef DKG_NO_R1_OVERLAP
     round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
+#else
+    // with one stream (the bench's serialised roofline pass) the phases stay back to back
+    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false, ctx->nsub > 1);
+#endif
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     ExtScope ext(ctx, n, N);
     receivers_rounds(ctx, n, t, Ec, Ac, ds, dsp, out, false);  // small outputs only
