@@ -169,7 +169,8 @@ def split_pieces(t, U, plen=None):
     ceil((t+1)/U), or that rounded up to a multiple of 64; the last piece holds the rest)."""
     N = t + 1
     plen = plen or -(-N // U)
-    return [plen] * (U - 1) + [N - (U - 1) * plen], plen
+    last = N - (U - 1) * plen
+    return [plen] * (U - 1) + [last if last > 0 else plen], plen  # runtime.hip last_piece_len
 
 
 def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None):

@@ -197,6 +197,13 @@ void wait_shares(dkg_ctx* ctx, hipStream_t st) {
   if (ctx->shares_pending) HCK(hipStreamWaitEvent(st, ctx->shares_done, 0));
 }
 
+// Coefficients held by the last of U pieces of length L (N = t + 1).  A forced split can leave the
+// last pieces without any (N = 6, U = 5: L = 2, pieces 2 + 2 + 2 + 0 + 0); such a piece is a
+// full-length table of identities, as are the positions past t of a ragged one.
+size_t last_piece_len(size_t N, size_t U, size_t L) {
+  return (U - 1) * L < N ? N - (U - 1) * L : L;
+}
+
 // Whole-column stepping slots (all U pieces of a column in one workgroup slot) when they fit and
 // the launch model says so (ties to per-piece slots: more, smaller workgroups; measured on the
 // 8-way n=1024 shard at U=4, 19.8 vs 20.9 ms, profiles/r02_shard_stepping_ab.txt).
@@ -216,7 +223,7 @@ bool stepping_whole_pays(size_t cols, size_t U, size_t L, size_t Lr) {
 // one per ~8 when a lone wave runs a dependent chain (tools/ubench/ilp.hip); 1024 SIMDs.
 double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
   const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAUNCH = 3e-3 * 2.4e6;
-  const size_t Lr = N - (U - 1) * L, off = L - Lr;  // the last piece: Lr positions, starts at step off
+  const size_t Lr = last_piece_len(N, U, L), off = L - Lr;  // the last piece: Lr positions, starts at step off
   auto cost = [&](size_t m) {  // one binomial position-step: add + NAF multiplication by m
     int len = 0, nz = 0;  // NAF length and weight of m (as mul_small_lds recodes it)
     for (size_t v = m; v; v >>= 1, len++) {
@@ -361,7 +368,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const size_t npad = groups * gw;
   // degree split: U pieces of L positions; piece u of column c is table column u * npad + c
   const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U), W = U * npad;
-  const size_t Lr = N - (U - 1) * L;  // the last piece's length (L or shorter)
+  const size_t Lr = last_piece_len(N, U, L);  // the last piece's length (L or shorter)
   const bool whole = ctx->step_mode == 1 || (ctx->step_mode == 0 && stepping_whole_pays(npad, U, L, Lr));
   // the stepping keeps product scanning even at 2 waves per SIMD (8-way n=1024 shard, one stream:
   // 6.07 vs 6.12 ms with column sums, profiles/r02_shard_stepping_ab.txt); only a forced mode 2
