@@ -1237,33 +1237,56 @@ __global__ __launch_bounds__(256) void k_row_reject(size_t rows, size_t n, const
   if ((threadIdx.x & 63) == 0) out[i] = any;
 }
 
-__global__ void k_col_complaints(size_t groups, size_t n, const uint8_t* __restrict__ dec, int32_t* __restrict__ out) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = g * n + j
-  if (e >= groups * n) return;
-  const size_t g = e / n, j = e % n;
+// Column counts of a stacked decision matrix: 64 columns (lanes) x 16 row slices (waves) per
+// workgroup, the slices summed through LDS -- one thread per column alone leaves a 1024-party
+// ceremony with 16 waves walking 1024 rows each.
+constexpr int COL_SLICES = 16;
+template <typename Pred>
+__device__ __forceinline__ int32_t column_count(size_t groups, size_t n, const uint8_t* __restrict__ dec, Pred pred,
+                                                size_t& e_out) {
+  __shared__ int32_t part[COL_SLICES][64];
+  const int lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const size_t e = (size_t)blockIdx.x * 64 + lane;  // e = g * n + j
+  const bool live = e < groups * n;
+  const size_t g = live ? e / n : 0, j = live ? e % n : 0;
   int32_t c = 0;
-  for (size_t i = 0; i < n; i++) c += dec[(g * n + i) * n + j] == 0;
-  out[e] = c;
+  if (live)
+    for (size_t i = slice; i < n; i += COL_SLICES) c += pred(g * n + i, dec[(g * n + i) * n + j]);
+  part[slice][lane] = c;
+  __syncthreads();
+  int32_t s = 0;
+  if (slice == 0)
+    for (int k = 0; k < COL_SLICES; k++) s += part[k][lane];
+  e_out = live && slice == 0 ? e : SIZE_MAX;
+  return s;
+}
+
+__global__ __launch_bounds__(64 * COL_SLICES) void k_col_complaints(size_t groups, size_t n,
+                                                                   const uint8_t* __restrict__ dec,
+                                                                   int32_t* __restrict__ out) {
+  size_t e;
+  const int32_t c = column_count(groups, n, dec, [](size_t, uint8_t d) { return (int32_t)(d == 0); }, e);  // REJECT
+  if (e != SIZE_MAX) out[e] = c;
 }
 
 // Round-4 error of receiver j (committee.rs:515-516, 567-569): itself plus the qualified dealers
 // whose check it accepted are fewer than t+1.
-__global__ void k_r4_error(size_t groups, size_t n, size_t t, const uint8_t* __restrict__ dec,
-                           const uint8_t* __restrict__ qmask, uint8_t* __restrict__ out) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // e = g * n + j
-  if (e >= groups * n) return;
-  const size_t g = e / n, j = e % n;
-  size_t honest = 1;
-  for (size_t i = 0; i < n; i++) honest += qmask[g * n + i] && dec[(g * n + i) * n + j] == 1;  // ACCEPT
-  out[e] = honest < t + 1;
+__global__ __launch_bounds__(64 * COL_SLICES) void k_r4_error(size_t groups, size_t n, size_t t,
+                                                             const uint8_t* __restrict__ dec,
+                                                             const uint8_t* __restrict__ qmask,
+                                                             uint8_t* __restrict__ out) {
+  size_t e;
+  const int32_t c = column_count(
+      groups, n, dec, [qmask](size_t row, uint8_t d) { return (int32_t)(qmask[row] && d == 1); }, e);  // ACCEPT
+  if (e != SIZE_MAX) out[e] = (size_t)(1 + c) < t + 1;
 }
 
 void r4_error(size_t groups, size_t n, size_t t, const uint8_t* dec, const uint8_t* qmask, uint8_t* out,
               hipStream_t stream) {
   const size_t rows = groups * n;
   if (!rows) return;
-  hipLaunchKernelGGL(k_r4_error, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, groups, n, t, dec, qmask,
-                     out);
+  hipLaunchKernelGGL(k_r4_error, dim3((unsigned)((rows + 63) / 64)), dim3(64 * COL_SLICES), 0, stream, groups, n, t,
+                     dec, qmask, out);
 }
 
 void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
@@ -1274,8 +1297,8 @@ void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_
     hipLaunchKernelGGL(k_row_reject, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, rows, n, dec,
                        row_reject);
   if (complaints)
-    hipLaunchKernelGGL(k_col_complaints, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, stream, groups, n, dec,
-                       complaints);
+    hipLaunchKernelGGL(k_col_complaints, dim3((unsigned)((rows + 63) / 64)), dim3(64 * COL_SLICES), 0, stream, groups,
+                       n, dec, complaints);
 }
 
 }  // namespace dkgk

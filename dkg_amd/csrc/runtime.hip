@@ -36,7 +36,7 @@ struct dkg_ctx {
   // round-1 share evaluation on a low-priority side stream beside the first binomial steps
   // (round1_device with overlap_shares): the checks and round 3 wait for shares_done
   hipStream_t side = nullptr;
-  hipEvent_t side_fork = nullptr, shares_done = nullptr;
+  hipEvent_t side_fork = nullptr, shares_done = nullptr, pub_done = nullptr;
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
@@ -792,9 +792,14 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
     h2d(ctx, qmask, qualified.data(), n);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
+    // the public shares g s_j are an output only: computed on the side stream, off the path to
+    // round 4 and finalise (joined before the outputs are read)
     uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
-    dkgk::fixed_base(n, fs, ctx->tab_g8, pub, ctx->stream);
-    dkgk::encode_points(pub, n, n, pubc, ctx->stream);
+    HCK(hipEventRecord(ctx->side_fork, ctx->stream));
+    HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
+    dkgk::fixed_base(n, fs, ctx->tab_g8, pub, ctx->side);
+    dkgk::encode_points(pub, n, n, pubc, ctx->side);
+    HCK(hipEventRecord(ctx->pub_done, ctx->side));
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
   verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok, a_ok);
@@ -872,6 +877,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
   out->n_qualified = nq;
   out->phase4_error = phase4_error;  // committee.rs:673-677
+  HCK(hipStreamWaitEvent(ctx->stream, ctx->pub_done, 0));  // public shares (round 3, side stream)
   if (copy_big) {
     if (out->dec2) d2h(ctx, out->dec2, dec2, n * n);
     if (out->dec4) d2h(ctx, h4.data(), dec4, n * n);
@@ -1216,6 +1222,7 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     HCK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
     HCK(hipEventCreateWithFlags(&ctx->side_fork, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->shares_done, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&ctx->pub_done, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
@@ -1261,6 +1268,7 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
   if (ctx->shares_done) (void)hipEventDestroy(ctx->shares_done);
+  if (ctx->pub_done) (void)hipEventDestroy(ctx->pub_done);
   delete ctx;
 }
 
