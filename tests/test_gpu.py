@@ -763,6 +763,25 @@ def test_field_modes_goldens(be, golden, name, mode):
         be.set_split(0)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json"])
+def test_stepping_modes_goldens(be, golden, name, mode):
+    """Stepping workgroup slots forced per column (1: all pieces of a column in one slot) or per
+    piece (2), on split tables with ragged and short last pieces: every output bit-exact."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    try:
+        be.set_stepping(mode)
+        for pieces in {2, min(3, t + 1), min(5, t + 1)}:
+            be.set_split(pieces)
+            r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+            _check_ceremony(c, r, n)
+    finally:
+        be.set_stepping(0)
+        be.set_split(0)
+
+
 @pytest.mark.parametrize("pieces", [1, 2, 3])
 def test_degree_split_n256_matches_unsplit(be, pieces):
     """n = 256, t = 127 (BASELINE config 2) from device coefficients with one E row made undecodable
