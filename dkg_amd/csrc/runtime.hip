@@ -222,7 +222,7 @@ bool stepping_whole_pays(size_t cols, size_t U, size_t L, size_t Lr) {
 // cycles: a SIMD retires one wave instruction per ~4.5 cycles of this mix when it has >= 2 waves,
 // one per ~8 when a lone wave runs a dependent chain (tools/ubench/ilp.hip); 1024 SIMDs.
 double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
-  const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAUNCH = 3e-3 * 2.4e6;
+  const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAT_ILP = 6, LAUNCH = 3e-3 * 2.4e6;
   const size_t Lr = last_piece_len(N, U, L), off = L - Lr;  // the last piece: Lr positions, starts at step off
   auto cost = [&](size_t m) {  // one binomial position-step: add + NAF multiplication by m
     int len = 0, nz = 0;  // NAF length and weight of m (as mul_small_lds recodes it)
@@ -244,8 +244,12 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
     const double work = waves_col * ((U - 1) * pre[r] + (r > off ? pre[r - off] : 0.0)) * THR / SIMDS;
     // a step pays its issue work AND its longest chain: the last waves of a launch run their chains
     // on partly idle SIMDs (the sum fits the measured shards within 5 %: 1-, 2-, 4-, 8-way n=1024,
-    // one-GPU n=4096; the max alone picked U=2 for a 4-way n=1024 shard, 3 % slower than U=4)
-    cyc += work + cost(r) * LAT + LAUNCH;
+    // one-GPU n=4096; the max alone picked U=2 for a 4-way n=1024 shard, 3 % slower than U=4).
+    // Steps with under 1.5 waves per SIMD run the column-sum copy (verify_device), whose ten
+    // independent chains per multiplication shorten the latency-bound chain (8-way n=1024 shard:
+    // binomial 6.78 -> 6.26 ms at U=3, profiles/r02_shard_stepping_ab.txt).
+    const double lat = waves_col * U * (r + 1) / SIMDS < 1.5 ? LAT_ILP : LAT;
+    cyc += work + cost(r) * lat + LAUNCH;
   }
   if (U > 1) {
     // pairwise joint chains: an even U starts with one product (253 doublings + ~85 NAF
@@ -278,18 +282,23 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
 
 size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
   if (ctx->split > 0) return std::min<size_t>((size_t)ctx->split, N);
-  size_t best = 1;
   const double base = split_model_ms(cols, n, N, 1);
+  std::vector<double> ms(17, 0.0);
   double best_ms = base;
+  size_t umax = 1;
   for (size_t U = 2; U <= 16; U++) {
     if (N < 64 * U) break;  // pieces of degree < 63: the binomial is cheap already
-    const double ms = split_model_ms(cols, n, N, U);
-    if (ms < best_ms) {
-      best_ms = ms;
-      best = U;
-    }
+    ms[U] = split_model_ms(cols, n, N, U);
+    best_ms = std::min(best_ms, ms[U]);
+    umax = U;
   }
-  return best_ms < 0.9 * base ? best : 1;  // only for a clear win
+  if (!(best_ms < 0.9 * base)) return 1;  // only for a clear win
+  // the fewest pieces within 1 % of the best (the model's resolution; fewer pieces = less
+  // recombination work, which it prices exactly): the 8-way n=1024 shard measured U=3 17.2 ms
+  // against the model's U=5 18.2 (profiles/r02_shard_stepping_ab.txt)
+  for (size_t U = 2; U <= umax; U++)
+    if (ms[U] <= 1.01 * best_ms) return U;
+  return 1;
 }
 
 // NAF of y = (j+1)^L mod l and of y^2 for receivers j = 0..n-1 (k_combine's wave-uniform
