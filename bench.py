@@ -39,8 +39,8 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 #            is the roofline's work: frac = 1 means every issue cycle of every SIMD was used.
 #   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
-VALU = {"fe_mul": (140, 256), "ge_add": (1199, 2177), "ge_add_signed": (1242, 2223), "ge_dbl_t": (1082, 1898),
-        "ge_dbl_not": (943, 1643), "comb_window": (1195, 2107), "comb8_window": (1167, 2051),
+VALU = {"fe_mul": (140, 256), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200), "ge_dbl_t": (1057, 1864),
+        "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "comb8_window": (1154, 2030),
         "ge_to_cached": (143, 259), "eq": (633, 1151)}
 INSTR = {k: v[0] for k, v in VALU.items()}
 SLOTS = {k: v[1] for k, v in VALU.items()}

@@ -89,7 +89,7 @@ DKG_DEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
   fe_add(b, b, a);          // g = d + c <= 2^27
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
-  fe_mul(r.Z, t, b);
+  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
   fe_mul(r.T, e, h);
 }
 
@@ -108,7 +108,7 @@ DKG_DEV void ge_sub(ge_p3& r, const ge_p3& p, const ge_cached& q) {
   fe_sub(b, b, a);          // g = d - c
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
-  fe_mul(r.Z, t, b);
+  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
   fe_mul(r.T, e, h);
 }
 
@@ -126,9 +126,9 @@ DKG_DEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_aff& q) {
   fe_sub(t, b, a);          // f = d - c <= 2^27 + 2^27
   fe_add(b, b, a);          // g = d + c <= 1.5*2^27
   fe_mul(r.X, t, e);        // f <= 2^28 as first operand
-  fe_mul(r.Y, b, h);
+  fe_mul(r.Y, h, b);        // x19 operands E (X, T) and G (Y, Z), computed once each
   fe_mul(r.Z, t, b);
-  fe_mul(r.T, e, h);
+  fe_mul(r.T, h, e);
 }
 
 DKG_DEV void ge_msub(ge_p3& r, const ge_p3& p, const ge_aff& q) {
@@ -143,7 +143,7 @@ DKG_DEV void ge_msub(ge_p3& r, const ge_p3& p, const ge_aff& q) {
   fe_add(b, p.Z, p.Z);      // d
   fe_add(t, b, a);          // f = d + c <= 1.5*2^27
   fe_sub(b, b, a);          // g = d - c <= 2^28
-  fe_mul(r.X, t, e);
+  fe_mul(r.X, e, t);        // x19 operands F (X, Z) and H (Y, T), computed once each
   fe_mul(r.Y, b, h);        // g <= 2^28 first operand
   fe_mul(r.Z, b, t);
   fe_mul(r.T, e, h);
@@ -166,7 +166,7 @@ DKG_DEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe_carry(f, f);           // tight               (= -F_std)
   fe_mul(r.X, e, f);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
+  fe_mul(r.Z, g, f);        // x19 operands f (X, Z) and h (Y, T), computed once each
   if (with_t) fe_mul(r.T, e, h);
 }
 
@@ -186,7 +186,7 @@ DKG_DEV void ge_dbl_rt(ge_p3& r, const ge_p3& p, bool with_t) {
   fe_carry(c, c);           // tight               (= -F_std)
   fe_mul(r.X, e, c);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, c, g);
+  fe_mul(r.Z, g, c);        // x19 operands f (X, Z) and h (Y, T), computed once each
   if (with_t) fe_mul(r.T, e, h);
 }
 
@@ -206,7 +206,7 @@ DKG_DEV void ge_dbl_lean(ge_p3& r, const ge_p3& p, bool with_t) {
   fe_sub(b, h, a);          // e <= 2^28           (= -E_std)
   fe_mul(r.X, b, t);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, t, g);
+  fe_mul(r.Z, g, t);        // x19 operands f (X, Z) and h (Y, T), computed once each
   if (with_t) fe_mul(r.T, b, h);
 }
 
@@ -234,7 +234,7 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
   fe_add(b, b, a);          // g <= 2^27
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
-  fe_mul(r.Z, t, b);
+  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
   fe_mul(r.T, e, h);
 }
 

@@ -227,7 +227,7 @@ DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
   fe_add(b, b, a);          // g
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
-  fe_mul(r.Z, t, b);
+  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
   fe_mul(r.T, e, h);
 }
 
