@@ -129,6 +129,14 @@ class ShardedCeremony:
         self.g_part = torch.empty(self.ws * n * 32, **u8)
         self.D, self.R = D, R
 
+    def _fence(self):
+        """The library runs on its own HIP streams: before it reads buffers torch produced (the
+        gathered rows, concatenations, uploads) or overwrites buffers a collective may still read,
+        the work queued on torch's stream -- including an RCCL collective, which torch's current
+        stream waits for -- must have completed."""
+        if getattr(self.dev, "type", str(self.dev)) == "cuda":
+            self.torch.cuda.current_stream(self.dev).synchronize()
+
     def _all_gather(self, out, inp):
         if self.staged:  # gloo with device buffers: through host memory (rehearsal / CPU runs)
             o = out.cpu()
@@ -160,6 +168,7 @@ class ShardedCeremony:
         coefficients), exchange, combine.  With finalise, also the round-3 final shares (sum of the
         gathered partials) and the master public key (sum of the qualified dealers' terms), both on
         the GPU."""
+        self._fence()
         ms = self.be.ceremony_shard_device(self.n, self.t, self.d0, self.d1, d_a, d_b, self.dec2.data_ptr(),
                                            self.dec4.data_ptr(), self.A0.data_ptr(), self.part.data_ptr())
         return self._finish(ms, finalise)
@@ -167,6 +176,7 @@ class ShardedCeremony:
     def run_verify(self, d_E: int, d_A: int, d_s: int, d_sp: int, finalise: bool = True) -> ShardResult:
         """Rounds 2-5 on received broadcasts: this rank's dealers' commitments d_E, d_A [D][t+1][32]
         (compressed, as broadcast in phases 1 and 3) and their shares d_s, d_sp [D][n][32]."""
+        self._fence()
         ms = self.be.ceremony_shard_verify_device(self.n, self.t, self.d0, self.d1, d_E, d_A, d_s, d_sp,
                                                   self.dec2.data_ptr(), self.dec4.data_ptr(),
                                                   self.A0.data_ptr(), self.part.data_ptr())
@@ -180,12 +190,14 @@ class ShardedCeremony:
         if finalise:
             torch = self.torch
             fs_t = torch.empty(n * 32, dtype=torch.uint8, device=self.dev)
+            self._fence()
             self.be.scalar_sum_device(self.ws, n, parts.data_ptr(), None, fs_t.data_ptr())
             fs = bytes(fs_t.cpu().numpy())
             if dec.reconstruct.any() and not dec.phase4_error:
                 # a dealer accused in round 4 (committee.rs:660-670) enters mpk as g * a_i0 over the
                 # final parties' shares (:747-789): the owning rank replaces its term and the terms
                 # are gathered again (the interpolation points depend on every rank's rows)
+                self._fence()
                 self.be.ceremony_shard_recon_device(n, t, self.d0, self.d1, dec.qualified, dec.reconstruct, d_s,
                                                     self.A0.data_ptr())
                 self._all_gather(self.g_A0, self.A0)
@@ -196,6 +208,7 @@ class ShardedCeremony:
                 # the sum runs over the qualified set
                 mask = torch.from_numpy(dec.qualified).to(self.dev)
                 mpk_t = torch.empty(32, dtype=torch.uint8, device=self.dev)
+                self._fence()
                 self.be.point_sum_device(n, A0.data_ptr(), mask.data_ptr(), mpk_t.data_ptr())
                 mpk = bytes(mpk_t.cpu().numpy())
         return ShardResult(dec, fs, mpk, ms)
