@@ -40,9 +40,10 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 #   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
 VALU = {"fe_mul": (140, 256), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200), "ge_dbl_t": (1057, 1864),
-        "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "comb8_window": (1154, 2030),
+        "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "combw_window": (1171, 2047),
         "ge_to_cached": (143, 259), "eq": (633, 1151)}
 INSTR = {k: v[0] for k, v in VALU.items()}
+COMBW_WINDOWS = 26  # points.h: radix-2^10 fixed-base comb, one mixed addition per window
 SLOTS = {k: v[1] for k, v in VALU.items()}
 
 
@@ -215,7 +216,7 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None):
                 joint += VALU["ge_add_signed"] * ((e1 != 0) + (e2 != 0))
             c += ((U + 1) // 2 - 1) * joint
             combine += c
-    check = n * ((2 if rnd == 2 else 1) * 32 * VALU["comb8_window"] + VALU["eq"])  # radix-256 combs
+    check = n * ((2 if rnd == 2 else 1) * COMBW_WINDOWS * VALU["combw_window"] + VALU["eq"])  # radix-2^10 combs
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
@@ -225,7 +226,7 @@ def fused_valu(n, t, U=1, VALU=SLOTS, plen=None):
     equalities per pair."""
     w2, w4 = algorithmic_valu(n, t, 2, U, VALU, plen), algorithmic_valu(n, t, 4, U, VALU, plen)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
-    out["check"] = n * n * (2 * 32 * VALU["comb8_window"] + 2 * VALU["eq"])
+    out["check"] = n * n * (2 * COMBW_WINDOWS * VALU["combw_window"] + 2 * VALU["eq"])
     return out
 
 

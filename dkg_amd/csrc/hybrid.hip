@@ -21,9 +21,9 @@ namespace dkgk {
 constexpr int HY_COMB_WORDS = AFF_WORDS * COMB_ENTRIES;
 
 // grid (ceil(2D / 1024), n): recipient q = blockIdx.y; the recipient's comb table in LDS (60 KB),
-// the generator's radix-256 comb (32 mixed additions instead of 64) from global memory / L2.
+// the generator's radix-2^10 comb (26 mixed additions instead of 64) from global memory / L2.
 __global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
-                                                  const uint32_t* __restrict__ tab_g8,
+                                                  const uint32_t* __restrict__ tab_gw,
                                                   const uint32_t* __restrict__ tabs_pk, uint32_t* __restrict__ R_ext,
                                                   uint32_t* __restrict__ K_ext) {
   extern __shared__ uint4 lds4[];
@@ -43,18 +43,18 @@ __global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint
   sc_load(x, r + 8 * idx);
   ge_p3 acc;
   ge_identity(acc);
-  comb8_mul_add(acc, x, tab_g8);               // e1 = G::generator() * r      (elgamal.rs:141)
+  combw_mul_add(acc, x, tab_gw);               // e1 = G::generator() * r      (elgamal.rs:141)
   pt_store(R_ext, count, idx, acc);
   ge_identity(acc);
   comb_mul_add(acc, x, lds);                   // symmetric key = pk * r       (elgamal.rs:138-140)
   pt_store(K_ext, count, idx, acc);
 }
 
-void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_g8, const uint32_t* tabs_pk, uint32_t* R_ext,
+void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_gw, const uint32_t* tabs_pk, uint32_t* R_ext,
              uint32_t* K_ext, hipStream_t stream) {
   if (!D || !n) return;
   hipLaunchKernelGGL(k_enc_mul, dim3((unsigned)((2 * D + 1023) / 1024), (unsigned)n), dim3(1024),
-                     HY_COMB_WORDS * 4, stream, D, n, r, tab_g8, tabs_pk, R_ext, K_ext);
+                     HY_COMB_WORDS * 4, stream, D, n, r, tab_gw, tabs_pk, R_ext, K_ext);
 }
 
 // grid (ceil(D / 64), n, 2): recipient q = blockIdx.y, w = blockIdx.z; lanes = dealers.

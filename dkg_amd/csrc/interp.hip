@@ -158,11 +158,11 @@ __global__ __launch_bounds__(256, 4) void k_coef_check(size_t count, const uint3
   ge_p3 acc, c;
   ge_identity(acc);
   sc_load(x, F + 8 * e);
-  comb8_mul_add(acc, x, tab_g);
+  combw_mul_add(acc, x, tab_g);
   pt_load(c, Aext, cstride, e);
   okA[e] = ristretto_eq(acc, c) ? 1 : 0;
   sc_load(x, Fp + 8 * e);
-  comb8_mul_add(acc, x, tab_h);
+  combw_mul_add(acc, x, tab_h);
   pt_load(c, Eext, cstride, e);
   okE[e] = ristretto_eq(acc, c) ? 1 : 0;
 }
@@ -243,8 +243,8 @@ __global__ __launch_bounds__(256, 4) void k_interp_decide(size_t D, size_t nrecv
       sc_sub(b, spj, fpx);
       ge_p3 acc, id;
       ge_identity(acc);
-      comb8_mul_add(acc, a, tab_g);
-      comb8_mul_add(acc, b, tab_h);
+      combw_mul_add(acc, a, tab_g);
+      combw_mul_add(acc, b, tab_h);
       ge_identity(id);
       v2 = ristretto_eq(acc, id) ? 1 : 0;
     }

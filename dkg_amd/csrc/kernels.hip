@@ -189,9 +189,9 @@ __global__ __launch_bounds__(256, 4) void k_commit(size_t count, const uint32_t*
   sc_load(sb, b + 8 * e);
   ge_p3 acc;
   ge_identity(acc);
-  comb8_mul_add(acc, sa, tab_g);               // apub = G::generator() * a   (committee.rs:155)
+  combw_mul_add(acc, sa, tab_g);               // apub = G::generator() * a   (committee.rs:155)
   pt_store(A_ext, count, e, acc);
-  comb8_mul_add(acc, sb, tab_h);               // coeff_comm = h * b + apub   (committee.rs:156)
+  combw_mul_add(acc, sb, tab_h);               // coeff_comm = h * b + apub   (committee.rs:156)
   pt_store(E_ext, count, e, acc);
 }
 
@@ -333,22 +333,22 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
   }
 }
 
-// Radix-256 comb of point e0 + blockIdx.y of ext: block (window w = blockIdx.x, 128 threads),
-// thread d-1 writes d * 256^w B in affine Niels form (points.h comb8_mul_add).
-__global__ __launch_bounds__(128) void k_build_comb8(const uint32_t* __restrict__ ext, size_t stride, size_t e0,
-                                                   uint32_t* __restrict__ tab) {
+// Radix-2^10 comb of point e0 + blockIdx.y of ext: block (window w = blockIdx.x, 512 threads),
+// thread d-1 writes d * 2^(10 w) B in affine Niels form (points.h combw_mul_add).
+__global__ __launch_bounds__(COMBW_ENTRIES) void k_build_combw(const uint32_t* __restrict__ ext, size_t stride,
+                                                               size_t e0, uint32_t* __restrict__ tab) {
   const int w = blockIdx.x, d = threadIdx.x + 1;
-  tab += (size_t)blockIdx.y * COMB8_WORDS;
+  tab += (size_t)blockIdx.y * COMBW_WORDS;
   ge_p3 b, m;
   pt_load(b, ext, stride, e0 + blockIdx.y);
-  for (int i = 0; i < 8 * w; i++) ge_dbl<true>(b, b);
+  for (int i = 0; i < COMBW_BITS * w; i++) ge_dbl<true>(b, b);
   mul_small_uniform(m, b, (uint32_t)d);
   fe zi, x, y, t, d2;
   fe_ld(d2, ge_const::D2);
   fe_invert(zi, m.Z);
   fe_mul(x, m.X, zi);
   fe_mul(y, m.Y, zi);
-  uint32_t* out = tab + ((size_t)w * COMB8_ENTRIES + (d - 1)) * COMB8_STRIDE;
+  uint32_t* out = tab + ((size_t)w * COMBW_ENTRIES + (d - 1)) * COMBW_STRIDE;
   fe_add(t, y, x);
   fe_carry(t, t);
 #pragma unroll
@@ -365,9 +365,11 @@ __global__ __launch_bounds__(128) void k_build_comb8(const uint32_t* __restrict_
   out[31] = 0;
 }
 
-void build_comb8(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
+static_assert(COMBW_WORDS * 4 == (size_t)26 * 512 * 32 * 4, "runtime.hip COMBW_BYTES must match points.h");
+
+void build_combw(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
   if (!count) return;
-  hipLaunchKernelGGL(k_build_comb8, dim3((unsigned)COMB8_WINDOWS, (unsigned)count), dim3(COMB8_ENTRIES), 0, stream,
+  hipLaunchKernelGGL(k_build_combw, dim3((unsigned)COMBW_WINDOWS, (unsigned)count), dim3(COMBW_ENTRIES), 0, stream,
                      ext, stride, e0, tab);
 }
 
@@ -794,10 +796,10 @@ __global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv,
   ge_identity(acc);
   sc x;
   sc_load(x, s + 8 * p);
-  comb8_mul_add(acc, x, tab_g);                    // G::generator() * s       (committee.rs:294, :537)
+  combw_mul_add(acc, x, tab_g);                    // G::generator() * s       (committee.rs:294, :537)
   if (round == 2) {
     sc_load(x, sp + 8 * p);
-    comb8_mul_add(acc, x, tab_h);                  // + h * s'                 (committee.rs:292-293)
+    combw_mul_add(acc, x, tab_h);                  // + h * s'                 (committee.rs:292-293)
   }
   pt_load_aos(r, R, p);
   const bool eq = ristretto_eq(acc, r);            // check_element != multi_scalar (:305, :541)
@@ -839,12 +841,12 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
   ge_identity(acc);
   sc x;
   sc_load(x, s + 8 * q);
-  comb8_mul_add(acc, x, tab_g);                    // G::generator() * s   (committee.rs:294, :537)
+  combw_mul_add(acc, x, tab_g);                    // G::generator() * s   (committee.rs:294, :537)
   pt_load_aos(r, R, cA * nrecv + j);
   bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
   dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
   sc_load(x, sp + 8 * q);
-  comb8_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
+  combw_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
   pt_load_aos(r, R, cE * nrecv + j);
   eq = ristretto_eq(acc, r);                       // round 2 (:305)
   dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)
@@ -1124,11 +1126,11 @@ __global__ __launch_bounds__(256, 4) void k_fixed_base(size_t count, const uint3
   sc_load(x, scalars + 8 * e);
   ge_p3 acc;
   ge_identity(acc);
-  comb8_mul_add(acc, x, tab);
+  combw_mul_add(acc, x, tab);
   pt_store(out, count, e, acc);
 }
 
-// tab: a radix-256 comb (build_comb8)
+// tab: a radix-2^10 comb (build_combw)
 void fixed_base(size_t count, const uint32_t* scalars, const uint32_t* tab, uint32_t* out_ext, hipStream_t stream) {
   if (!count) return;
   hipLaunchKernelGGL(k_fixed_base, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, scalars, tab,

@@ -124,28 +124,37 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
   }
 }
 
-// Radix-256 comb in global memory (L2-resident, 512 KB per base): 32 windows B_w = 256^w B of
-// 128 affine Niels entries d B_w (d = 1..128), entry-major, 32 words per entry (ypx | ymx |
-// xy2d | 2 pad).  Signed digits in [-128, 127]: one mixed addition per 8 scalar bits, half the
-// additions of the LDS radix-16 comb, for the bases every kernel shares (g, h).
-constexpr int COMB8_WINDOWS = 32;
-constexpr int COMB8_ENTRIES = 128;
-constexpr int COMB8_STRIDE = 32;
-constexpr size_t COMB8_WORDS = (size_t)COMB8_WINDOWS * COMB8_ENTRIES * COMB8_STRIDE;
+// Radix-2^10 comb in global memory (L2-resident: 1.7 MB per base, both of g and h fit one XCD's
+// 4 MB L2): 26 windows B_w = 2^(10 w) B of 512 affine Niels entries d B_w (d = 1..512),
+// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-512, 511]: one
+// mixed addition per 10 scalar bits (26 per 253-bit scalar; radix 2^8 took 32, the LDS radix-16
+// comb 64), for the bases every kernel shares (g, h).
+constexpr int COMBW_BITS = 10;
+constexpr int COMBW_WINDOWS = (256 + COMBW_BITS - 1) / COMBW_BITS;  // 26: bits 250..259 absorb the top carry
+constexpr int COMBW_ENTRIES = 1 << (COMBW_BITS - 1);
+constexpr int COMBW_STRIDE = 32;
+constexpr size_t COMBW_WORDS = (size_t)COMBW_WINDOWS * COMBW_ENTRIES * COMBW_STRIDE;
+static_assert(COMBW_WINDOWS * COMBW_BITS > 256 && (1 << (256 - (COMBW_WINDOWS - 1) * COMBW_BITS)) < COMBW_ENTRIES,
+              "the top window must absorb the signed recoding's carry for any 256-bit scalar");
 
-DKG_DEV void comb8_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
+DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
   int carry = 0;
 #pragma unroll 1
-  for (int w = 0; w < COMB8_WINDOWS; w++) {
-    const int wi = w >> 2;
-    uint32_t word = s.v[0];
+  for (int w = 0; w < COMBW_WINDOWS; w++) {
+    // bits [10 w, 10 w + 10) of the scalar: words wi and wi + 1 (wave-uniform selects)
+    const int bit = COMBW_BITS * w, wi = bit >> 5, sh = bit & 31;
+    uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int k = 1; k < 8; k++) word = (wi == k) ? s.v[k] : word;
-    int d = (int)((word >> (8 * (w & 3))) & 255u) + carry;
-    carry = (d + 128) >> 8;
-    d -= carry << 8;
+    for (int k = 0; k < 8; k++) {
+      lo = (wi == k) ? s.v[k] : lo;
+      hi = (wi + 1 == k) ? s.v[k] : hi;
+    }
+    const uint32_t raw = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh) & ((1u << COMBW_BITS) - 1);
+    int d = (int)raw + carry;
+    carry = (d + COMBW_ENTRIES) >> COMBW_BITS;
+    d -= carry << COMBW_BITS;
     const int ad = d < 0 ? -d : d;
-    const uint32_t* ep = tab + ((size_t)w * COMB8_ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMB8_STRIDE;
+    const uint32_t* ep = tab + ((size_t)w * COMBW_ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMBW_STRIDE;
     const bool neg = d < 0, zero = ad == 0;
     // the entry's 30 words, selected as they arrive: -Q = (y-x, y+x, -2dxy), 0 = (1, 1, 0)
     ge_aff r;

@@ -22,8 +22,8 @@ struct dkg_ctx {
   std::map<std::string, std::pair<void*, size_t>> bufs;
   uint32_t* tab_g = nullptr;  // comb table of the generator (15360 words)
   uint32_t* tab_h = nullptr;  // comb table of the commitment key h
-  uint32_t* tab_g8 = nullptr;  // radix-256 combs (global, L2-resident) of g and h: commit, check,
-  uint32_t* tab_h8 = nullptr;  // fixed-base products
+  uint32_t* tab_gw = nullptr;  // radix-2^10 combs (global, L2-resident) of g and h: commit, check,
+  uint32_t* tab_hw = nullptr;  // fixed-base products
   uint8_t h[32] = {0};
   bool have_h = false;
   size_t threshold = 0, nr_members = 0;
@@ -68,7 +68,7 @@ namespace {
 constexpr size_t PTB = 160;  // bytes of one extended point (40 words)
 constexpr size_t PT_WORDS_H = 40;
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
-constexpr size_t COMB8_BYTES = 32 * 128 * 32 * 4;  // points.h COMB8_WORDS
+constexpr size_t COMBW_BYTES = 26 * 512 * 32 * 4;  // points.h COMBW_WORDS (radix 2^10)
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
                                0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
                                0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
@@ -133,7 +133,7 @@ int guarded(dkg_ctx* ctx, F&& f) {
 }
 
 // Decode one 32-byte point and build its comb table into `tab`.
-// Comb tables of one point: radix-16 (LDS kernels; may be null) and radix-256 (may be null).
+// Comb tables of one point: radix-16 (LDS kernels; may be null) and radix-2^10 (may be null).
 void comb_for_point(dkg_ctx* ctx, const uint8_t p[32], uint32_t* tab, bool* ok, uint32_t* tab8 = nullptr) {
   uint32_t* comp = buf<uint32_t>(ctx, "comb_in", 32);
   uint32_t* ext = buf<uint32_t>(ctx, "comb_ext", PTB);
@@ -141,7 +141,7 @@ void comb_for_point(dkg_ctx* ctx, const uint8_t p[32], uint32_t* tab, bool* ok, 
   h2d(ctx, comp, p, 32);
   dkgk::decode_points(comp, 1, ext, 1, okd, ctx->stream);
   if (tab) dkgk::build_comb(ext, 1, 0, tab, ctx->stream);
-  if (tab8) dkgk::build_comb8(ext, 1, 0, tab8, ctx->stream);
+  if (tab8) dkgk::build_combw(ext, 1, 0, tab8, ctx->stream);
   check_launch(ctx);
   uint8_t v = 0;
   d2h(ctx, &v, okd, 1);
@@ -421,10 +421,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
       dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
-                       ctx->tab_g8, ctx->tab_h8, dok, g.dec, segs[1].dec, st);
+                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st);
     } else {
       dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, g.self_mod ? g.self_mod : n, g.round, g.s + d0 * n * 8,
-                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n * PT_WORDS_H, ctx->tab_g8, ctx->tab_h8,
+                  g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n * PT_WORDS_H, ctx->tab_gw, ctx->tab_hw,
                   dok + d0, g.dec + d0 * n, st);
     }
   };
@@ -603,13 +603,13 @@ void verify_rounds_interp(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dea
     HCK(hipEventRecord(ctx->pev[1], st));
     uint8_t* okE = buf<uint8_t>(ctx, "i.okE", D * N);
     uint8_t* okA = buf<uint8_t>(ctx, "i.okA", D * N);
-    dkgk::coef_check(D, N, Fa, Fb, Ee, Ae, cs, ctx->tab_g8, ctx->tab_h8, okE, okA, st);
+    dkgk::coef_check(D, N, Fa, Fb, Ee, Ae, cs, ctx->tab_gw, ctx->tab_hw, okE, okA, st);
     uint8_t* cE = buf<uint8_t>(ctx, "i.cE", D);
     uint8_t* cA = buf<uint8_t>(ctx, "i.cA", D);
     dkgk::dealer_ok(D, N, okE, cE, st);
     dkgk::dealer_ok(D, N, okA, cA, st);
     HCK(hipEventRecord(ctx->pev[2], st));
-    dkgk::interp_decide(D, n, N, dealer_base, n, s, sp, Fa, Fb, dokE, dokA, cE, cA, ctx->tab_g8, ctx->tab_h8, dec2,
+    dkgk::interp_decide(D, n, N, dealer_base, n, s, sp, Fa, Fb, dokE, dokA, cE, cA, ctx->tab_gw, ctx->tab_hw, dec2,
                         dec4, st);
     HCK(hipEventRecord(ctx->pev[3], st));
     check_launch(ctx);
@@ -806,7 +806,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     uint32_t* pub = buf<uint32_t>(ctx, "pub_ext", PTB * n);
     HCK(hipEventRecord(ctx->side_fork, ctx->stream));
     HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
-    dkgk::fixed_base(n, fs, ctx->tab_g8, pub, ctx->side);
+    dkgk::fixed_base(n, fs, ctx->tab_gw, pub, ctx->side);
     dkgk::encode_points(pub, n, n, pubc, ctx->side);
     HCK(hipEventRecord(ctx->pub_done, ctx->side));
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
@@ -865,7 +865,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
       uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
       h2d(ctx, sec, secrets.data(), secrets.size());
       uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
-      dkgk::fixed_base(nrecon, sec, ctx->tab_g8, gsec, ctx->stream);
+      dkgk::fixed_base(nrecon, sec, ctx->tab_gw, gsec, ctx->stream);
       dkgk::sum_points(nrecon, gsec, nrecon, nullptr, parts, 2, 1, ctx->stream);
     } else {
       dkgk::sum_points(0, A0, n, nullptr, parts, 2, 1, ctx->stream);  // identity
@@ -919,7 +919,7 @@ void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a
     HCK(hipEventRecord(ctx->side_fork, ctx->stream));
     HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
   }
-  dkgk::commit(D * N, a, b, ctx->tab_g8, ctx->tab_h8, Aext, Eext, ctx->stream);  // K2 (committee.rs:151-159)
+  dkgk::commit(D * N, a, b, ctx->tab_gw, ctx->tab_hw, Aext, Eext, ctx->stream);  // K2 (committee.rs:151-159)
   if (encode) {
     dkgk::encode_points(Eext, D * N, D * N, Ecomp, ctx->stream);                  // broadcast encodings
     dkgk::encode_points(Aext, D * N, D * N, Acomp, ctx->stream);
@@ -982,7 +982,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
     // round 3 (committee.rs:433-476) per ceremony
     h2d(ctx, qmask, qualified.data(), V);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
-    dkgk::fixed_base(V, fs, ctx->tab_g8, pub, ctx->stream);
+    dkgk::fixed_base(V, fs, ctx->tab_gw, pub, ctx->stream);
     dkgk::encode_points(pub, V, V, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
@@ -1036,7 +1036,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
       uint32_t* sec = buf<uint32_t>(ctx, "b.recon_sec", 32 * nr);
       h2d(ctx, sec, secrets.data(), secrets.size());
       uint32_t* gsec = buf<uint32_t>(ctx, "b.recon_ext", PTB * nr);
-      dkgk::fixed_base(nr, sec, ctx->tab_g8, gsec, ctx->stream);
+      dkgk::fixed_base(nr, sec, ctx->tab_gw, gsec, ctx->stream);
       dkgk::sum_points(nr, gsec, nr, nullptr, extra, B, c, ctx->stream);
       dkgk::add_points(1, mpk_ext + c, extra + c, B, mpk_ext + c, ctx->stream);
       sync(ctx);  // sec / gsec are reused by the next ceremony
@@ -1106,7 +1106,7 @@ void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
   uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
   uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
-  dkgk::enc_mul(D, n, r, ctx->tab_g8, tabs, R, K, st);
+  dkgk::enc_mul(D, n, r, ctx->tab_gw, tabs, R, K, st);
   dkgk::encode_points(R, items, items, e1, st);
   dkgk::encode_points(K, items, items, Kc, st);
   dkgk::sym_xor(D, n, Kc, false, ct, const_cast<uint32_t*>(s), const_cast<uint32_t*>(sp), st);
@@ -1236,10 +1236,10 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
-    HCK(hipMalloc(&ctx->tab_g8, COMB8_BYTES));
-    HCK(hipMalloc(&ctx->tab_h8, COMB8_BYTES));
+    HCK(hipMalloc(&ctx->tab_gw, COMBW_BYTES));
+    HCK(hipMalloc(&ctx->tab_hw, COMBW_BYTES));
     bool ok = false;
-    comb_for_point(ctx, BASEPOINT, ctx->tab_g, &ok, ctx->tab_g8);
+    comb_for_point(ctx, BASEPOINT, ctx->tab_g, &ok, ctx->tab_gw);
     if (!ok) {
       ctx->err = "basepoint failed to decode on device";
       return DKG_E_DEVICE;
@@ -1262,8 +1262,8 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   for (auto& kv : ctx->bufs) (void)hipFree(kv.second.first);
   if (ctx->tab_g) (void)hipFree(ctx->tab_g);
   if (ctx->tab_h) (void)hipFree(ctx->tab_h);
-  if (ctx->tab_g8) (void)hipFree(ctx->tab_g8);
-  if (ctx->tab_h8) (void)hipFree(ctx->tab_h8);
+  if (ctx->tab_gw) (void)hipFree(ctx->tab_gw);
+  if (ctx->tab_hw) (void)hipFree(ctx->tab_hw);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->pev)
@@ -1367,7 +1367,7 @@ int dkg_env_init(dkg_ctx* ctx, size_t threshold, size_t nr_members, const uint8_
     d2h(ctx, ctx->h, comp, 32);
     sync(ctx);
     bool ok = false;
-    comb_for_point(ctx, ctx->h, ctx->tab_h, &ok, ctx->tab_h8);
+    comb_for_point(ctx, ctx->h, ctx->tab_h, &ok, ctx->tab_hw);
     if (!ok) return DKG_E_DEVICE;
     ctx->have_h = true;
     ctx->threshold = threshold;
@@ -1408,9 +1408,9 @@ int dkg_msm_batch(dkg_ctx* ctx, size_t B, size_t N, const uint8_t* scalars, cons
 int dkg_fixed_base_batch(dkg_ctx* ctx, const uint8_t base[32], size_t count, const uint8_t* scalars, uint8_t* out) {
   return guarded(ctx, [&] {
     if (count == 0) return DKG_OK;
-    const uint32_t* tab = ctx->tab_g8;
+    const uint32_t* tab = ctx->tab_gw;
     if (base) {
-      uint32_t* t = buf<uint32_t>(ctx, "fb_tab8", COMB8_BYTES);
+      uint32_t* t = buf<uint32_t>(ctx, "fb_tabw", COMBW_BYTES);
       bool ok = false;
       comb_for_point(ctx, base, nullptr, &ok, t);
       if (!ok) {
@@ -1555,7 +1555,7 @@ int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, c
     uint32_t* ds = upload_scalars(ctx, "vr_s", s, n);
     uint32_t* dsp = round == 2 ? upload_scalars(ctx, "vr_sp", s_prime, n) : nullptr;
     uint8_t* dec = buf<uint8_t>(ctx, "vr_dec", n);
-    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, ctx->tab_g8, ctx->tab_h8, dok, dec, ctx->stream);
+    dkgk::check(n, 1, 0, j, n, round, ds, dsp, R, ctx->tab_gw, ctx->tab_hw, dok, dec, ctx->stream);
     check_launch(ctx);
     d2h(ctx, decision, dec, n);
     sync(ctx);
@@ -1812,7 +1812,7 @@ int dkg_ceremony_shard_recon_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0,
     uint32_t* gsec = buf<uint32_t>(ctx, "sh_rext", PTB * R);
     uint32_t* gc = buf<uint32_t>(ctx, "sh_rcomp", 32 * R);
     h2d(ctx, sec, secrets.data(), secrets.size());
-    dkgk::fixed_base(R, sec, ctx->tab_g8, gsec, ctx->stream);  // G::generator() * recovered (:789)
+    dkgk::fixed_base(R, sec, ctx->tab_gw, gsec, ctx->stream);  // G::generator() * recovered (:789)
     dkgk::encode_points(gsec, R, R, gc, ctx->stream);
     for (size_t r = 0; r < R; r++)
       HCK(hipMemcpyAsync((uint8_t*)d_terms + 32 * rows[r], gc + 8 * r, 32, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1937,7 +1937,7 @@ int dkg_finalise_parties(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* qualif
     // a finalising disqualified party (the only disqualified dealer) also adds its own A_p0
     for (size_t p = 0; p < n; p++)
       if (ok[p] && !qualified[p]) dkgk::add_points(1, hrep + p, a0e + p, n, hrep + p, ctx->stream);
-    dkgk::fixed_base(n, sd, ctx->tab_g8, ge, ctx->stream);
+    dkgk::fixed_base(n, sd, ctx->tab_gw, ge, ctx->stream);
     dkgk::add_points(n, ge, hrep, n, ge, ctx->stream);
     dkgk::encode_points(ge, n, n, oc, ctx->stream);
     check_launch(ctx);
@@ -2076,7 +2076,7 @@ int dkg_member_keys(dkg_ctx* ctx, const uint8_t master[32], uint32_t ceremony, s
     uint32_t* dpe = buf<uint32_t>(ctx, "mk_pk_ext", PTB * n);
     uint32_t* dpc = buf<uint32_t>(ctx, "mk_pk", 32 * n);
     h2d(ctx, dsk, sk.data(), 32 * n);
-    dkgk::fixed_base(n, dsk, ctx->tab_g8, dpe, ctx->stream);  // to_public (procedure_keys.rs:78-82)
+    dkgk::fixed_base(n, dsk, ctx->tab_gw, dpe, ctx->stream);  // to_public (procedure_keys.rs:78-82)
     dkgk::encode_points(dpe, n, n, dpc, ctx->stream);
     check_launch(ctx);
     d2h(ctx, pk.data(), dpc, 32 * n);

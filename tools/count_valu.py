@@ -25,8 +25,8 @@ PRIMS = {
                 "ge_madd(p, p, q);", "STP(p);"),
     "comb_window": ("ge_p3 p; LDP(p, 0); sc x; for (int i_ = 0; i_ < 8; i_++) x.v[i_] = o[9000 + i_];",
                     "comb_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
-    "comb8_window": ("ge_p3 p; LDP(p, 0); sc x; for (int i_ = 0; i_ < 8; i_++) x.v[i_] = o[9000 + i_];",
-                     "comb8_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
+    "combw_window": ("ge_p3 p; LDP(p, 0); sc x; for (int i_ = 0; i_ < 8; i_++) x.v[i_] = o[9000 + i_];",
+                     "combw_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
     "eq": ("ge_p3 p, q; LDP(p, 0); LDP(q, 2560);", "if (ristretto_eq(p, q)) p.X.v[0] ^= 1; else q.Y.v[1] ^= 3;",
            "STP(p); STP(q);"),
     "ge_to_cached": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached(q, p); p.X = q.T2d; p.Y = q.YpX;",

@@ -13,7 +13,7 @@ weights) straight from the header text, so the checker cannot drift from the cod
     intermediate of the carry pass fe_carry64) stays below 2^64, every 32-bit value below 2^32;
   * fe_tobytes32's canonical reduction sees a value below 2p (one conditional subtraction suffices).
 The group formulas (ge_to_cached, ge_add, ge_sub, ge_madd, ge_msub, ge_dbl / _rt / _lean,
-ge_add_signed, ge_add_lds incl. its negated path, the comb entry selection of comb8_mul_add,
+ge_add_signed, ge_add_lds incl. its negated path, the comb entry selection of combw_mul_add,
 ristretto_eq, decode / encode) are run on the bounds; point coordinates are iterated to a fixpoint
 (every stored coordinate is again an input), so the invariant "a coordinate is TIGHT" is closed.
 
@@ -342,7 +342,7 @@ def ge_add_lds(p, q, where="ge_add_lds"):
 
 
 def comb8_entry(tab_ypx, tab_ymx, tab_xy2d):
-    """points.h comb8_mul_add: the selected affine entry, incl. identity (1, 1, 0) and -Q =
+    """points.h combw_mul_add: the selected affine entry, incl. identity (1, 1, 0) and -Q =
     (y-x, y+x, 2p - xy2d) -- the negated xy2d is NOT carried."""
     sel = vmax(tab_ypx, tab_ymx, ONE)
     for i in range(10):
