@@ -41,7 +41,7 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
 VALU = {"fe_mul": (140, 256), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200), "ge_dbl_t": (1057, 1864),
         "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "combw_window": (1171, 2047),
-        "ge_to_cached": (143, 259), "eq": (633, 1151)}
+        "ge_to_cached": (143, 259), "eq": (633, 1151), "sc_mont_mul": (580, 834)}
 INSTR = {k: v[0] for k, v in VALU.items()}
 COMBW_WINDOWS = 26  # points.h: radix-2^10 fixed-base comb, one mixed addition per window
 SLOTS = {k: v[1] for k, v in VALU.items()}
@@ -174,11 +174,31 @@ def split_pieces(t, U, plen=None):
     return [plen] * (U - 1) + [last if last > 0 else plen], plen  # runtime.hip last_piece_len
 
 
-def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None):
+def short_combine_valu(mults, VALU=SLOTS):
+    """k_combine_short per (column, receiver row of `mults`): U cached addends (the first KL in LDS:
+    ge_add, the rest in VGPRs: ge_add_signed), one joint chain over the U NAFs of the short vector."""
+    total = 0
+    for row in mults:
+        U = len(row)
+        KL = 1 if U == 2 else 2
+        ds = [_naf(abs(v)) for v in row]
+        top = max(len(d) for d in ds) - 1
+        c = U * VALU["ge_to_cached"]
+        for i in range(top, -1, -1):
+            nz = [u for u in range(U) if i < len(ds[u]) and ds[u][i] != 0]
+            if i != top:
+                c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
+            c += sum(VALU["ge_add"] if u < KL else VALU["ge_add_signed"] for u in nz)
+        total += c
+    return total
+
+
+def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None):
     """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round
     over all n dealers as implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces
     (split_pieces: L coefficients each but a shorter last one), stepping, recombination by
-    y_j = j^L (U > 1), fixed-base check."""
+    y_j = j^L (U > 1; with `mults`, the short multipliers of api.split_multipliers), fixed-base
+    check (with `mults`, of b_j s: one more Montgomery product per scalar)."""
     pieces, L_ = split_pieces(t, U, plen)
     cost_m = {}
     for m in range(1, L_):
@@ -196,7 +216,9 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None):
     binom = sum(sum(cost_m[m] * (Lp - m) for m in range(1, Lp)) for Lp in pieces)
     stepping = n * sum(Lp * VALU["ge_to_cached"] + (Lp - 1) * VALU["ge_add"] for Lp in pieces)
     combine = 0
-    if U > 1:  # k_combine: pairwise Horner in y^2 with joint NAF chains (kernels.hip)
+    if U > 1 and mults is not None:
+        combine = short_combine_valu(mults, VALU)
+    elif U > 1:  # k_combine: pairwise Horner in y^2 with joint NAF chains (kernels.hip)
         for j in range(1, n + 1):
             y = pow(j, L_, L)
             d1, d2 = _naf(y), _naf(y * y % L)
@@ -216,17 +238,21 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None):
                 joint += VALU["ge_add_signed"] * ((e1 != 0) + (e2 != 0))
             c += ((U + 1) // 2 - 1) * joint
             combine += c
-    check = n * ((2 if rnd == 2 else 1) * COMBW_WINDOWS * VALU["combw_window"] + VALU["eq"])  # radix-2^10 combs
+    nsc = 2 if rnd == 2 else 1
+    scale = nsc * VALU["sc_mont_mul"] if mults is not None else 0
+    check = n * (nsc * COMBW_WINDOWS * VALU["combw_window"] + VALU["eq"] + scale)  # radix-2^10 combs
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
-def fused_valu(n, t, U=1, VALU=SLOTS, plen=None):
+def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
-    recombination; one check kernel computing g*s once (32 radix-256 comb windows), h*s' (32 more) and both
-    equalities per pair."""
-    w2, w4 = algorithmic_valu(n, t, 2, U, VALU, plen), algorithmic_valu(n, t, 4, U, VALU, plen)
+    recombination; one check kernel computing g*s once (26 radix-2^10 comb windows), h*s' (26 more)
+    and both equalities per pair (with `mults`: s and s' scaled by b_j first)."""
+    w2 = algorithmic_valu(n, t, 2, U, VALU, plen, mults)
+    w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
-    out["check"] = n * n * (2 * COMBW_WINDOWS * VALU["combw_window"] + 2 * VALU["eq"])
+    scale = 2 * VALU["sc_mont_mul"] if mults is not None else 0
+    out["check"] = n * n * (2 * COMBW_WINDOWS * VALU["combw_window"] + 2 * VALU["eq"] + scale)
     return out
 
 
@@ -396,6 +422,8 @@ def main():
                     help="group: every P_i(j) computed in the group (default); interp: committee verification "
                          "by interpolation (identical decisions, DESIGN.md section 2)")
     ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
+    ap.add_argument("--combine", type=int, default=0,
+                    help="recombination of a degree split: 0 short lattice multipliers (U <= 4), 1 powers of j^L")
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
@@ -423,6 +451,7 @@ def main():
     be.set_overlap(not args.no_overlap)
     be.set_split(args.split)
     be.set_field_mode(args.field)
+    be.set_combine(args.combine)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1
@@ -511,11 +540,13 @@ def main():
         out["config"]["rounds_2_4_fused"] = not args.no_overlap
         ov = not args.no_overlap
         U, Ls = be.last_split(), be.last_split_len()
+        mults = dkg_amd.split_multipliers(n, Ls, U) if be.last_combine() == 2 else None
         out["config"]["degree_split"] = U
         out["config"]["split_pieces"] = split_pieces(t, U, Ls)[0]
-        w2, w4 = algorithmic_valu(n, t, 2, U, plen=Ls), algorithmic_valu(n, t, 4, U, plen=Ls)
-        work = fused_valu(n, t, U, plen=Ls) if ov else w2
-        work_i = fused_valu(n, t, U, INSTR, Ls) if ov else algorithmic_valu(n, t, 2, U, INSTR, Ls)
+        out["config"]["recombination"] = {0: "none", 1: "powers of j^L", 2: "short lattice multipliers"}[be.last_combine()]
+        w2, w4 = algorithmic_valu(n, t, 2, U, plen=Ls, mults=mults), algorithmic_valu(n, t, 4, U, plen=Ls, mults=mults)
+        work = fused_valu(n, t, U, plen=Ls, mults=mults) if ov else w2
+        work_i = fused_valu(n, t, U, INSTR, Ls, mults) if ov else algorithmic_valu(n, t, 2, U, INSTR, Ls, mults)
         # per-kernel device times need the serialised schedule (one chunk stream): one extra,
         # untimed ceremony in the same round order as the timed ones
         be.set_streams(1)
@@ -576,9 +607,10 @@ def main():
         be.set_streams(args.streams)
         ph = be.phase_times("r24" if not args.no_overlap else "r2")
         U, Ls = be.last_split(), be.last_split_len()
+        mults = dkg_amd.split_multipliers(n, Ls, U) if be.last_combine() == 2 else None
         D = ((rank + 1) * n) // ws - (rank * n) // ws
-        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls).items()}
-        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls).items()}
+        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls, mults=mults).items()}
+        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls, mults).items()}
         rl = kernel_rooflines(ph, work, work_i)
         out["config"]["degree_split"] = U
         if rl:

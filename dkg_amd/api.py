@@ -55,6 +55,19 @@ def enc_randomness(master: bytes, ceremony: int, d0: int, D: int, n: int, t: int
     return r.raw[:64 * D * n]
 
 
+def split_multipliers(n: int, L: int, pieces: int):
+    """Short recombination vectors [(b_j, a_j1, ..)] of receivers j = 1..n for a `pieces`-way split
+    of piece length L (a_ju = b_j j^(uL) mod l; dkg_split_multipliers, host-only)."""
+    mag = ctypes.create_string_buffer(32 * n * pieces)
+    sign = ctypes.create_string_buffer(n * pieces)
+    rc = _lib.lib().dkg_split_multipliers(n, L, pieces, mag, sign)
+    if rc != _lib.DKG_OK:
+        raise DkgError(rc, "split_multipliers")
+    sg = [1 if b < 128 else -1 for b in sign.raw]
+    return [[sg[j * pieces + u] * int.from_bytes(mag.raw[(j * pieces + u) * 32:(j * pieces + u + 1) * 32], "little")
+             for u in range(pieces)] for j in range(n)]
+
+
 @dataclass
 class CeremonyResult:
     n: int
@@ -140,6 +153,15 @@ class Backend:
         """Stepping slots of a split table: 0 cost model, 1 one per column (all pieces), 2 one per
         piece; results are identical."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_stepping(self._ctx, mode))
+
+    def set_combine(self, mode: int):
+        """Recombination of a degree split: 0 short lattice multipliers for 2..4 pieces (default),
+        1 powers of y = j^L; decisions are identical (dkg_ctx_set_combine)."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_combine(self._ctx, mode))
+
+    def last_combine(self) -> int:
+        """0 no split, 1 powers of y, 2 short multipliers (the last verification)."""
+        return _lib.lib().dkg_ctx_last_combine(self._ctx)
 
     def last_split(self) -> int:
         return _lib.lib().dkg_ctx_last_split(self._ctx)

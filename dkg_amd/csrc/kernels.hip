@@ -771,6 +771,77 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
   if (live) pt_store_aos(R, c * nrecv + j, acc);
 }
 
+// Recombination with short multipliers (lattice.cpp, U = K <= 4): b_j P(j) = sum_u v_ju Q_u(j) with
+// v_j = (b_j, a_j1, ..) entries of ~253 (K-1)/K bits, in ONE joint double-and-add chain over the K
+// NAFs (126 / 168 / 189 doublings for K = 2 / 3 / 4 instead of 253 per pair of pieces); the checks
+// compare b_j P(j) with g*(b_j s) + h*(b_j s').  The first KL addends' cached forms are parked in
+// LDS (10 KB each per wave), the others stay in VGPRs, so that K = 3 and 4 keep 2 waves per SIMD.
+// digits[j][b] packs the K signed digits of position b, one byte each; top[j] the highest position.
+// (Compile-time recursion over the pieces keeps the register-resident addends out of scratch.)
+template <int U, int K, int KL>
+DKG_DEV void short_addends(uint32_t* qs, ge_cached* qr, const uint32_t* R, size_t pstride, size_t cc, size_t nrecv,
+                           size_t j) {
+  if constexpr (U < K) {
+    ge_p3 q;
+    pt_load_aos(q, R, ((size_t)U * pstride + cc) * nrecv + j);
+    if constexpr (U < KL) {
+      ge_cached xc;
+      ge_to_cached(xc, q);
+      lds_put_cached(qs + U * PT_WORDS * 64 + threadIdx.x, xc);
+    } else {
+      ge_to_cached(qr[U - KL], q);
+    }
+    short_addends<U + 1, K, KL>(qs, qr, R, pstride, cc, nrecv, j);
+  }
+}
+template <int U, int K, int KL>
+DKG_DEV void short_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_cached* qr) {
+  if constexpr (U < K) {
+    const int e = (int8_t)(w >> (8 * U));
+    if (e != 0) {
+      if constexpr (U < KL) ge_add_lds(acc, acc, qs + U * PT_WORDS * 64 + threadIdx.x, e < 0);
+      else ge_add_signed(acc, acc, qr[U - KL], e < 0);
+    }
+    short_position<U + 1, K, KL>(acc, w, qs, qr);
+  }
+}
+
+template <int K, int KL>
+__global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_short(size_t width, size_t pstride, size_t nrecv,
+                                                        const uint32_t* __restrict__ digits,
+                                                        const int16_t* __restrict__ top, uint32_t* __restrict__ R) {
+  __shared__ uint32_t qs[KL * PT_WORDS * 64];
+  const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t j = blockIdx.y;
+  const bool live = c < width;
+  const size_t cc = live ? c : 0;
+  ge_cached qr[K - KL > 0 ? K - KL : 1];
+  short_addends<0, K, KL>(qs, qr, R, pstride, cc, nrecv, j);
+  const uint32_t* dw = digits + j * 256;
+  const int tp = top[j];
+  ge_p3 acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int b = tp; b >= 0; b--) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(dw[b]);
+    if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
+    short_position<0, K, KL>(acc, w, qs, qr);
+  }
+  if (live) pt_store_aos(R, c * nrecv + j, acc);
+}
+
+void combine_short(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* digits,
+                   const int16_t* top, uint32_t* R, hipStream_t stream) {
+  if (!width || !nrecv || pieces < 2 || pieces > 4) return;
+  const dim3 grid((unsigned)((width + 63) / 64), (unsigned)nrecv);
+  if (pieces == 2)
+    hipLaunchKernelGGL((k_combine_short<2, 1>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, R);
+  else if (pieces == 3)
+    hipLaunchKernelGGL((k_combine_short<3, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, R);
+  else
+    hipLaunchKernelGGL((k_combine_short<4, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, R);
+}
+
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
              uint32_t* R, hipStream_t stream) {
   if (!width || !nrecv || pieces < 2) return;
@@ -788,17 +859,21 @@ __global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv,
                                                const uint32_t* __restrict__ R,
                                                const uint32_t* __restrict__ tab_g,
                                                const uint32_t* __restrict__ tab_h,
-                                               const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec) {
+                                               const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec,
+                                               const uint32_t* __restrict__ scale) {
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ndealers * nrecv) return;
   const size_t i = p / nrecv, j = p % nrecv;
   ge_p3 acc, r;
   ge_identity(acc);
-  sc x;
+  sc x, f;
+  if (scale) sc_load(f, scale + 8 * j);            // R holds b_j P(j): compare with g*(b_j s) + h*(b_j s')
   sc_load(x, s + 8 * p);
+  if (scale) sc_mont_mul(x, x, f);
   combw_mul_add(acc, x, tab_g);                    // G::generator() * s       (committee.rs:294, :537)
   if (round == 2) {
     sc_load(x, sp + 8 * p);
+    if (scale) sc_mont_mul(x, x, f);
     combw_mul_add(acc, x, tab_h);                  // + h * s'                 (committee.rs:292-293)
   }
   pt_load_aos(r, R, p);
@@ -812,11 +887,11 @@ __global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv,
 
 void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, size_t nmod, int round,
            const uint32_t* s, const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g,
-           const uint32_t* tab_h, const uint8_t* dok, uint8_t* dec, hipStream_t stream) {
+           const uint32_t* tab_h, const uint8_t* dok, uint8_t* dec, hipStream_t stream, const uint32_t* scale) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
   hipLaunchKernelGGL(k_check, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
-                     dealer_base, recv_base, (uint32_t)nmod, round, s, sp, R, tab_g, tab_h, dok, dec);
+                     dealer_base, recv_base, (uint32_t)nmod, round, s, sp, R, tab_g, tab_h, dok, dec, scale);
 }
 
 // Fused round-2 + round-4 check of dealers [dealer0, dealer0 + ndealers) (local indices) whose E and A
@@ -830,7 +905,7 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
                                                     const uint32_t* __restrict__ tab_g,
                                                     const uint32_t* __restrict__ tab_h,
                                                     const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
-                                                    uint8_t* __restrict__ dec4) {
+                                                    uint8_t* __restrict__ dec4, const uint32_t* __restrict__ scale) {
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ndealers * nrecv) return;
   const size_t i = dealer0 + p / nrecv, j = p % nrecv;
@@ -839,13 +914,16 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
   const bool self = (uint32_t)((i + dealer_base) % nmod) == (uint32_t)j;
   ge_p3 acc, r;
   ge_identity(acc);
-  sc x;
+  sc x, f;
+  if (scale) sc_load(f, scale + 8 * j);            // R holds b_j P(j): compare with g*(b_j s) + h*(b_j s')
   sc_load(x, s + 8 * q);
+  if (scale) sc_mont_mul(x, x, f);
   combw_mul_add(acc, x, tab_g);                    // G::generator() * s   (committee.rs:294, :537)
   pt_load_aos(r, R, cA * nrecv + j);
   bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
   dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
   sc_load(x, sp + 8 * q);
+  if (scale) sc_mont_mul(x, x, f);
   combw_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
   pt_load_aos(r, R, cE * nrecv + j);
   eq = ristretto_eq(acc, r);                       // round 2 (:305)
@@ -854,11 +932,11 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
 
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
                 const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
-                const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream) {
+                const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream, const uint32_t* scale) {
   const size_t total = ndealers * nrecv;
   if (!total) return;
   hipLaunchKernelGGL(k_check_both, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
-                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4);
+                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale);
 }
 
 // Identity in every column of a position-major table [40][S] (S = N * npad words apart).

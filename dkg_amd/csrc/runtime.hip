@@ -49,6 +49,10 @@ struct dkg_ctx {
   int last_split = 1;                   // U used by the last verify_device
   size_t last_split_len = 0;            // and its piece length L
   size_t ydig_n = 0, ydig_L = 0;        // key of the cached combine multipliers (v.ydig)
+  int combine_mode = 0;                 // recombination: 0 short vectors for U <= 4, 1 powers of y,
+                                        // 2 short vectors (U <= 4)
+  int last_combine = 0;                 // 1: the last verify_device recombined with powers, 2: short vectors
+  size_t sdig_n = 0, sdig_L = 0, sdig_K = 0;  // key of the cached short multipliers (v.sdig)
   // round-1 commitments of the ceremony being verified, in extended form on this device (set by
   // the drivers that generate them, ExtScope): verify_device places them instead of decoding the
   // encodings, finalise reads A_i0 from them.  E/A [D][t+1] points, word stride ext_stride.
@@ -221,7 +225,7 @@ bool stepping_whole_pays(size_t cols, size_t U, size_t L, size_t Lr) {
 // kernels; the check does not depend on U) in SIMD
 // cycles: a SIMD retires one wave instruction per ~4.5 cycles of this mix when it has >= 2 waves,
 // one per ~8 when a lone wave runs a dependent chain (tools/ubench/ilp.hip); 1024 SIMDs.
-double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
+double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L, bool short_mult) {
   const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAT_ILP = 6, LAUNCH = 3e-3 * 2.4e6;
   const size_t Lr = last_piece_len(N, U, L), off = L - Lr;  // the last piece: Lr positions, starts at step off
   auto cost = [&](size_t m) {  // one binomial position-step: add + NAF multiplication by m
@@ -252,9 +256,14 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
     cyc += work + cost(r) * lat + LAUNCH;
   }
   if (U > 1) {
-    // pairwise joint chains: an even U starts with one product (253 doublings + ~85 NAF
-    // additions), then (ceil(U/2) - 1) joint y^2 / y steps (253 doublings + ~170 additions)
-    const double per = (U % 2 == 0 ? 253 * 950 + 85 * ADD : 0.0) + ((U + 1) / 2 - 1) * (253 * 950 + 170 * ADD);
+    // short multipliers (U <= 4): one joint chain of 253 (U-1)/U doublings over U NAFs of that
+    // length (~1/3 nonzero); powers of y: pairwise joint chains, an even U starting with one
+    // product (253 doublings + ~85 NAF additions), then (ceil(U/2) - 1) joint y^2 / y steps (253
+    // doublings + ~170 additions)
+    const double bits = 253.0 * (U - 1) / U;
+    const double per = short_mult && U <= 4 ? bits * 950 + U * bits / 3 * ADD
+                                            : (U % 2 == 0 ? 253 * 950 + 85 * ADD : 0.0) +
+                                                  ((U + 1) / 2 - 1) * (253 * 950 + 170 * ADD);
     const double waves = (double)cols / 64 * n;
     cyc += std::max(waves * per * THR / SIMDS, per * LAT);  // the 2-slot variant runs at 2 waves/SIMD as fast
   }
@@ -268,44 +277,43 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L) {
 // piece (N = 550, U = 2: 320 + 230 instead of 275 + 275, two tables of 5 and 4 waves instead of
 // 5 + 5 with 45 idle lanes each).  When all pieces of a column fit one stepping workgroup
 // (N <= 512) ceil(N / U) always wins: N = 512, U = 3 runs 171 + 171 + 170 on 512 lanes.
-size_t split_len(size_t cols, size_t n, size_t N, size_t U) {
+size_t split_len(size_t cols, size_t n, size_t N, size_t U, bool short_mult = true) {
   const size_t L1 = (N + U - 1) / U;
   if (U == 1) return L1;
   const size_t L64 = (L1 + 63) / 64 * 64;
   if (L64 == L1 || (U - 1) * L64 >= N) return L1;
-  return split_model_ms(cols, n, N, U, L64) < split_model_ms(cols, n, N, U, L1) ? L64 : L1;
+  return split_model_ms(cols, n, N, U, L64, short_mult) < split_model_ms(cols, n, N, U, L1, short_mult) ? L64 : L1;
 }
 
-double split_model_ms(size_t cols, size_t n, size_t N, size_t U) {
-  return split_model_ms(cols, n, N, U, split_len(cols, n, N, U));
+double split_model_ms(size_t cols, size_t n, size_t N, size_t U, bool short_mult = true) {
+  return split_model_ms(cols, n, N, U, split_len(cols, n, N, U, short_mult), short_mult);
 }
 
 size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
   if (ctx->split > 0) return std::min<size_t>((size_t)ctx->split, N);
-  const double base = split_model_ms(cols, n, N, 1);
+  const bool sm = ctx->combine_mode != 1;
+  const double base = split_model_ms(cols, n, N, 1, sm);
   std::vector<double> ms(17, 0.0);
   double best_ms = base;
   size_t umax = 1;
   for (size_t U = 2; U <= 16; U++) {
     if (N < 64 * U) break;  // pieces of degree < 63: the binomial is cheap already
-    ms[U] = split_model_ms(cols, n, N, U);
+    ms[U] = split_model_ms(cols, n, N, U, sm);
     best_ms = std::min(best_ms, ms[U]);
     umax = U;
   }
   if (!(best_ms < 0.9 * base)) return 1;  // only for a clear win
-  // the fewest pieces within 1 % of the best (the model's resolution; fewer pieces = less
-  // recombination work, which it prices exactly): the 8-way n=1024 shard measured U=3 17.2 ms
-  // against the model's U=5 18.2 (profiles/r02_shard_stepping_ab.txt)
+  // the model's best (with short multipliers it ranks the measured n=1024 shards right: U=4 ahead
+  // of U=3 by 0.3-0.5 ms per rank at 1-8 ranks, U=5 -- powers of y again -- far behind;
+  // profiles/r02_lattice_ab.txt)
   for (size_t U = 2; U <= umax; U++)
-    if (ms[U] <= 1.01 * best_ms) return U;
+    if (ms[U] <= best_ms) return U;
   return 1;
 }
 
 // NAF of y = (j+1)^L mod l and of y^2 for receivers j = 0..n-1 (k_combine's wave-uniform
 // multipliers), cached per (n, L) on the device: digits [n][2][256] int8, top [n][2] int16.
-void naf_digits(const dkgh::Zl& v, int8_t* d, int16_t* tp) {
-  uint8_t b[32];
-  dkgh::zl_to_bytes(b, v);
+void naf_digits(const uint8_t b[32], int8_t* d, int16_t* tp) {
   uint32_t k[9] = {0};
   for (int w = 0; w < 8; w++)
     k[w] = (uint32_t)b[4 * w] | (uint32_t)b[4 * w + 1] << 8 | (uint32_t)b[4 * w + 2] << 16 | (uint32_t)b[4 * w + 3] << 24;
@@ -344,13 +352,72 @@ void split_digits(dkg_ctx* ctx, size_t n, size_t L, const int8_t** digits, const
       if (e & 1) y = dkgh::zl_mul(y, x);
       x = dkgh::zl_mul(x, x);
     }
-    naf_digits(y, &hd[512 * j], &ht[2 * j]);
-    naf_digits(dkgh::zl_mul(y, y), &hd[512 * j + 256], &ht[2 * j + 1]);
+    uint8_t b[32];
+    dkgh::zl_to_bytes(b, y);
+    naf_digits(b, &hd[512 * j], &ht[2 * j]);
+    dkgh::zl_to_bytes(b, dkgh::zl_mul(y, y));
+    naf_digits(b, &hd[512 * j + 256], &ht[2 * j + 1]);
   }
   h2d(ctx, dd, hd.data(), hd.size());
   h2d(ctx, dt, ht.data(), 4 * n);
   ctx->ydig_n = n;
   ctx->ydig_L = L;
+}
+
+// Short recombination multipliers (lattice.cpp) of receivers j = 1..n for a K-way split, K <= 4
+// (k_combine_short): digits [n][256] u32, byte u of word b = the signed NAF digit at position b of
+// the scalar of piece u; top [n] int16 = the highest position with a nonzero digit; scale [n][8]
+// words = b_j 2^256 mod l, the checks' Montgomery factor taking s to b_j s.  Cached per (n, L, K).
+void short_vectors(size_t n, size_t L, size_t K, std::vector<uint8_t>& mag, std::vector<int8_t>& sign) {
+  mag.assign(n * K * 32, 0);
+  sign.assign(n * K, 1);
+  for (size_t j = 0; j < n; j++) {
+    dkgh::Zl x = dkgh::zl_from_u64(j + 1), y = dkgh::zl_from_u64(1);
+    for (size_t e = L; e; e >>= 1) {  // y = x^L
+      if (e & 1) y = dkgh::zl_mul(y, x);
+      x = dkgh::zl_mul(x, x);
+    }
+    dkgh::short_multipliers(y, (int)K, reinterpret_cast<uint8_t(*)[32]>(&mag[j * K * 32]), &sign[j * K]);
+  }
+}
+
+void split_short(dkg_ctx* ctx, size_t n, size_t L, size_t K, const uint32_t** digits, const int16_t** top,
+                 const uint32_t** scale) {
+  uint32_t* dd = buf<uint32_t>(ctx, "v.sdig", 4 * 256 * n);
+  int16_t* dt = buf<int16_t>(ctx, "v.stop", 2 * n);
+  uint32_t* ds = buf<uint32_t>(ctx, "v.sscale", 32 * n);
+  *digits = dd;
+  *top = dt;
+  *scale = ds;
+  if (ctx->sdig_n == n && ctx->sdig_L == L && ctx->sdig_K == K) return;
+  std::vector<uint8_t> mag;
+  std::vector<int8_t> sign;
+  short_vectors(n, L, K, mag, sign);
+  std::vector<uint32_t> hd(256 * n, 0), hs(8 * n, 0);
+  std::vector<int16_t> ht(n, -1);
+  uint8_t r256[33] = {0};
+  r256[32] = 1;
+  const dkgh::Zl R = dkgh::zl_from_bytes_wide(r256, 33);  // 2^256 mod l
+  for (size_t j = 0; j < n; j++) {
+    for (size_t u = 0; u < K; u++) {
+      int8_t d[256];
+      int16_t tp;
+      naf_digits(&mag[(j * K + u) * 32], d, &tp);
+      ht[j] = std::max(ht[j], tp);
+      for (int b = 0; b < 256; b++)
+        hd[256 * j + b] |= (uint32_t)(uint8_t)(int8_t)(d[b] * sign[j * K + u]) << (8 * u);
+    }
+    const dkgh::Zl b = dkgh::zl_from_bytes_wide(&mag[j * K * 32], 32);  // b > 0
+    uint8_t w[32];
+    dkgh::zl_to_bytes(w, dkgh::zl_mul(b, R));
+    memcpy(&hs[8 * j], w, 32);
+  }
+  h2d(ctx, dd, hd.data(), 4 * hd.size());
+  h2d(ctx, dt, ht.data(), 2 * n);
+  h2d(ctx, ds, hs.data(), 4 * hs.size());
+  ctx->sdig_n = n;
+  ctx->sdig_L = L;
+  ctx->sdig_K = K;
 }
 
 // One or two segments on device, as ONE pipeline over "virtual dealers" (table columns).  With two
@@ -376,7 +443,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const size_t groups = (D + 63) / 64, gw = 64 * nseg;  // columns per dealer group
   const size_t npad = groups * gw;
   // degree split: U pieces of L positions; piece u of column c is table column u * npad + c
-  const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U), W = U * npad;
+  const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U, ctx->combine_mode != 1), W = U * npad;
   const size_t Lr = last_piece_len(N, U, L);  // the last piece's length (L or shorter)
   const bool whole = ctx->step_mode == 1 || (ctx->step_mode == 0 && stepping_whole_pays(npad, U, L, Lr));
   // the stepping keeps product scanning even at 2 waves per SIMD (8-way n=1024 shard, one stream:
@@ -400,7 +467,12 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   }
   const int8_t* ydig = nullptr;
   const int16_t* ytop = nullptr;
-  if (U > 1) split_digits(ctx, n, L, &ydig, &ytop);
+  const uint32_t *sdig = nullptr, *sscale = nullptr;  // short multipliers: R holds b_j P(j)
+  const int16_t* stop = nullptr;
+  const bool short_mult = U > 1 && U <= 4 && ctx->combine_mode != 1;
+  if (short_mult) split_short(ctx, n, L, U, &sdig, &stop, &sscale);
+  else if (U > 1) split_digits(ctx, n, L, &ydig, &ytop);
+  ctx->last_combine = U > 1 ? (short_mult ? 2 : 1) : 0;
   // padding columns, and the positions past t of the last piece, are the identity
   if (npad != D * nseg || U * L != N) dkgk::fill_identity(L * W, Cpm, home);
   HCK(hipMemsetAsync(pok, 1, npad * N, home));
@@ -421,11 +493,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
       dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
-                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st);
+                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st, sscale);
     } else {
       dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, g.self_mod ? g.self_mod : n, g.round, g.s + d0 * n * 8,
                   g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n * PT_WORDS_H, ctx->tab_gw, ctx->tab_hw,
-                  dok + d0, g.dec + d0 * n, st);
+                  dok + d0, g.dec + d0 * n, st, sscale);
     }
   };
   // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
@@ -446,7 +518,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
-    dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
+    if (short_mult) dkgk::combine_short(w, npad, U, n, sdig, stop, R + c0 * n * PT_WORDS_H, st);
+    else dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));
     checks(g0 * 64, std::min(D, g1 * 64), st);
     if (tm) HCK(hipEventRecord(ctx->pev[4], st));
@@ -1323,6 +1396,25 @@ int dkg_ctx_set_stepping(dkg_ctx* ctx, int mode) {
 
 int dkg_ctx_last_split(const dkg_ctx* ctx) { return ctx ? ctx->last_split : 0; }
 size_t dkg_ctx_last_split_len(const dkg_ctx* ctx) { return ctx ? ctx->last_split_len : 0; }
+int dkg_ctx_set_combine(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return DKG_E_ARG;
+  ctx->combine_mode = mode;
+  return DKG_OK;
+}
+int dkg_ctx_last_combine(const dkg_ctx* ctx) { return ctx ? ctx->last_combine : 0; }
+int dkg_split_multipliers(size_t n, size_t L, int pieces, uint8_t* mag, int8_t* sign) {
+  if (!n || !L || pieces < 2 || pieces > 4 || !mag || !sign) return DKG_E_ARG;
+  try {
+    std::vector<uint8_t> m;
+    std::vector<int8_t> sg;
+    short_vectors(n, L, (size_t)pieces, m, sg);
+    memcpy(mag, m.data(), m.size());
+    memcpy(sign, sg.data(), sg.size());
+  } catch (const std::exception&) {
+    return DKG_E_NOMEM;
+  }
+  return DKG_OK;
+}
 
 double dkg_split_model_ms(size_t columns, size_t n, size_t t, int pieces) {
   if (pieces < 1 || t + 1 < (size_t)pieces) return -1;

@@ -70,16 +70,35 @@ def test_enc_randomness_golden(golden, name):
     assert r.hex() == c["enc_r"]
 
 
+def test_split_multipliers():
+    """Short recombination vectors (lattice.cpp): a_ju = b_j j^(uL) mod l exactly, b_j > 0, and
+    entries near l^((U-1)/U): <= 127 / 169 / 190 bits for 2 / 3 / 4 pieces (253 for the powers)."""
+    import dkg_amd
+
+    ell = 2**252 + 27742317777372353535851937790883648493
+    for U, Lp, bound in ((2, 256, 127), (3, 171, 169), (4, 128, 190), (3, 683, 169)):
+        rows = dkg_amd.split_multipliers(300, Lp, U)
+        assert len(rows) == 300
+        for j, row in enumerate(rows, 1):
+            y = pow(j, Lp, ell)
+            assert row[0] > 0
+            assert all((row[u] - row[0] * pow(y, u, ell)) % ell == 0 for u in range(U))
+            assert max(abs(v).bit_length() for v in row) <= bound
+    with pytest.raises(dkg_amd.DkgError):
+        dkg_amd.split_multipliers(10, 5, 5)
+
+
 def test_split_cost_model():
     """The degree-split cost model (runtime.hip choose_split) picks a split where the binomial
     dominates (n=1024, t=511 and n=4096, t=2047) and none for small tables (config 5)."""
     L = _lib.lib()
     ms = lambda cols, n, t, U: L.dkg_split_model_ms(cols, n, t, U)  # noqa: E731
     assert ms(2048, 1024, 511, 2) < 0.9 * ms(2048, 1024, 511, 1)
-    # n=1024: U=3 (pieces 171 + 171 + 170, one 512-lane stepping workgroup per column) measured 6 %
-    # faster than U=2 (profiles/r02_split_ab.txt)
-    assert min(range(1, 9), key=lambda U: ms(2048, 1024, 511, U)) == 3
+    # n=1024 with short recombination multipliers: U=4 (4 x 128) measured ahead of U=3 (171 + 171 +
+    # 170) and U=2 (profiles/r02_lattice_ab.txt)
+    assert min(range(1, 9), key=lambda U: ms(2048, 1024, 511, U)) == 4
     assert L.dkg_split_len(2048, 1024, 511, 3) == 171 and L.dkg_split_len(2048, 1024, 511, 2) == 256
+    assert L.dkg_split_len(2048, 1024, 511, 4) == 128
     # n=1100, U=2: 275 + 275 would leave 45 idle lanes per 320-lane stepping table: 320 + 230
     assert L.dkg_split_len(2304, 1100, 549, 2) == 320 and L.dkg_split_len(2304, 1100, 549, 3) == 192
     assert L.dkg_split_len(64, 10, 4, 6) == 0
@@ -87,6 +106,6 @@ def test_split_cost_model():
     # dealer shards of n=1024 (2 rows per dealer): smaller shards split more (a shorter dependent
     # binomial chain; measured profiles/r01_shard_scaling_n1024_v13.txt for U in 1, 2, 4, 8)
     picks = [min(range(1, 9), key=lambda U: ms(c, 1024, 511, U)) for c in (2048, 1024, 512, 256)]
-    assert picks == sorted(picks) and picks[0] == 3 and picks[-1] <= 5
+    assert picks == [4, 4, 4, 4]  # measured best at 1, 2, 4 and 8 ranks (profiles/r02_lattice_ab.txt)
     assert ms(16384, 64, 31, 1) < ms(16384, 64, 31, 2)
     assert ms(64, 10, 4, 6) == -1.0  # more pieces than coefficients

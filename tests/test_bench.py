@@ -31,19 +31,19 @@ def test_algorithmic_bytes_stepping_and_combine():
 
 
 def test_pmc_traffic_matches_workload():
-    """The committed traffic file belongs to the n=1024, t=511, U=3 (L=171) pipeline; other
-    workloads get None (their traffic was not measured), and every check-pipeline kernel's
-    measured bytes are within 10 % of its algorithmic bytes (no re-reads)."""
+    """The committed traffic file belongs to the n=1024, t=511, U=4 (L=128) pipeline (the headline
+    schedule); other workloads get None (their traffic was not measured), and every check-pipeline
+    kernel's measured bytes are within 10 % of its algorithmic bytes (no re-reads)."""
     for k in ("binomial", "stepping", "combine"):
-        got = bench.pmc_traffic(k, 1024, 511, 3, 171)
+        got = bench.pmc_traffic(k, 1024, 511, 4, 128)
         assert got is not None, k
         measured, source = got
-        alg, _ = bench.algorithmic_bytes(k, 1024, 511, 3, 171)
+        alg, _ = bench.algorithmic_bytes(k, 1024, 511, 4, 128)
         assert 0.9 < measured / alg < 1.1, (k, measured / alg)
     assert "FETCH_SIZE" in source and "WRITE_SIZE" in source
     assert bench.pmc_traffic("binomial", 4096, 2047, 4) is None
-    assert bench.pmc_traffic("binomial", 1024, 511, 2) is None
-    assert bench.pmc_traffic("binomial", 1024, 511, 3, 192) is None
+    assert bench.pmc_traffic("binomial", 1024, 511, 3) is None
+    assert bench.pmc_traffic("binomial", 1024, 511, 4, 192) is None
 
 
 def test_closed_form_work_per_pair():
@@ -64,6 +64,23 @@ def test_closed_form_work_per_pair():
     # the fused schedule carries both rounds' tables through binomial, stepping and recombination
     f = bench.fused_valu(n, t, 2)
     assert f["binomial"] == pytest.approx(2 * w["binomial"])
+
+
+def test_short_combine_work():
+    """Recombination with short lattice multipliers (k_combine_short): at U=3 one chain of ~169
+    doublings over three NAFs replaces 253 doublings over the NAFs of y and y^2 (~17 % less work);
+    at U=4 one chain of ~190 replaces two chains of 253.  The check pays one Montgomery product per
+    scalar for b_j s."""
+    import dkg_amd
+
+    n, t = 64, 511
+    for U, plen, lo, hi in ((3, 171, 0.78, 0.88), (4, 128, 0.58, 0.68)):
+        mults = dkg_amd.split_multipliers(n, plen, U)
+        short = bench.algorithmic_valu(n, t, 2, U, plen=plen, mults=mults)
+        powers = bench.algorithmic_valu(n, t, 2, U, plen=plen)
+        assert lo < short["combine"] / powers["combine"] < hi, (U, short["combine"] / powers["combine"])
+        assert short["check"] - powers["check"] == n * n * 2 * bench.VALU["sc_mont_mul"][1]
+        assert short["binomial"] == powers["binomial"] and short["stepping"] == powers["stepping"]
 
 
 def test_valu_table_matches_count_tool_format():

@@ -107,12 +107,14 @@ def _check_rows(n, dec2, dec4, qualified, exp, ctx):
             assert r2 == row and r4 == row, (ctx, i)
 
 
-@pytest.mark.parametrize("n,t,split", [(256, 127, 0), (1024, 511, 0), (1024, 511, 2), (1024, 511, 4)])
-def test_faults_baseline_sizes(be, n, t, split):
-    """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=3 from the cost
-    model with pieces of 171, 171 and 170 positions, the last one joining the binomial a step late,
-    every piece of a column in one 512-lane stepping workgroup, two dealer-chunk streams, rounds 2
-    and 4 fused), and forced U=2 / U=4: tampered shares, randomness, E and A
+@pytest.mark.parametrize("n,t,split,combine", [(256, 127, 0, 0), (1024, 511, 0, 0), (1024, 511, 2, 0),
+                                               (1024, 511, 3, 0), (1024, 511, 3, 1), (1024, 511, 5, 0)])
+def test_faults_baseline_sizes(be, n, t, split, combine):
+    """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=4 from the cost
+    model, pieces of 128 positions recombined with short lattice multipliers, every piece of a
+    column in one 512-lane stepping workgroup, two dealer-chunk streams, rounds 2 and 4 fused), and
+    forced U=2 / U=3 (171 + 171 + 170, the last piece a step late; short multipliers and powers of
+    j^L) / U=5 (powers, pairwise Horner in y^2): tampered shares, randomness, E and A
     coefficients, an undecodable E row and a tampered self-share.  Whole rows of every tampered
     dealer equal the oracle's per-pair MSM checks; qualification, reconstruction, final shares and
     the final parties' mpk follow the reference's rules (committee.rs:311-398, 454-467, 660-805)."""
@@ -123,15 +125,18 @@ def test_faults_baseline_sizes(be, n, t, split):
     rng = random.Random(n)
     faulty = _inject(rng, n, t, E, A, s, sp)
     be.set_split(split)
+    be.set_combine(combine)
     try:
         r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
-        U = be.last_split()
+        U, comb = be.last_split(), be.last_combine()
     finally:
         be.set_split(0)
+        be.set_combine(0)
     if split:
         assert U == split
     elif n == 1024:
-        assert U == 3, "the headline schedule uses the cost model's U=3 at n=1024"
+        assert U == 4, "the headline schedule uses the cost model's U=4 at n=1024"
+    assert comb == (0 if U == 1 else 1 if (combine == 1 or U > 4) else 2)
     assert sorted(faulty) == [0, 1, 2, 3, 4]
     exp = _expected_rows(n, t, h, E, A, s, sp)
     qualified = [0 if i in (0, 1, 3, 4) else 1 for i in range(n)]
@@ -184,14 +189,15 @@ def _shard_verify_all(be, n, t, tE, tA, ts, tsp):
 
 # (U, piece length L) per run; the last piece holds t + 1 - (U - 1) L coefficients
 @pytest.mark.parametrize("n,t,splits", [(1100, 549, ((1, 550), (3, 192), (2, 320))),
-                                        (4096, 2047, ((2, 1024), (1, 2048), (3, 683)))])
+                                        (4096, 2047, ((2, 1024), (1, 2048), (3, 683), (4, 512)))])
 def test_faults_multiblock_stepping(be, golden, n, t, splits):
     """Pieces longer than 512 positions take the block-chained stepping (k_stepping<512>, the top
     block streaming its per-step values down): n=1100, t=549 unsplit (2 blocks of 275) and n=4096,
     t=2047 at U=2 (2 blocks of 512 per piece) and unsplit (4 blocks).  Short last pieces, the piece
     length rounded up to whole waves: n=1100 at U=3 (192 + 192 + 166, per-piece stepping tables,
     the last one in its own launch, joining the binomial 26 steps late) and U=2 (320 + 230, 90 steps
-    late), n=4096 at U=3 (683 + 683 + 682 in 2 blocks each).  The committee is built on the
+    late), n=4096 at U=3 (683 + 683 + 682 in 2 blocks each) and U=4 (config E's split).  Split
+    runs recombine with short lattice multipliers (the default).  The committee is built on the
     device (dkg_share_gen_device), tampered there, and verified as one shard of all dealers; whole
     rows of the tampered dealers equal the oracle's (MSM over t+1 = 550 / 2048 points, Pippenger
     w=7 / w=8).  At n=4096 the committee uses the seed of tests/golden/spot_n4096_t2047.json, whose

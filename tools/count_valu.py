@@ -29,6 +29,9 @@ PRIMS = {
                      "combw_mul_add(p, x, o + 20000); x.v[0] ^= p.X.v[0];", "STP(p);"),
     "eq": ("ge_p3 p, q; LDP(p, 0); LDP(q, 2560);", "if (ristretto_eq(p, q)) p.X.v[0] ^= 1; else q.Y.v[1] ^= 3;",
            "STP(p); STP(q);"),
+    "sc_mont_mul": ("sc x, f; for (int i_ = 0; i_ < 8; i_++) { x.v[i_] = o[9000 + i_ * 64 + threadIdx.x]; "
+                    "f.v[i_] = o[9600 + i_ * 64 + threadIdx.x]; }",
+                    "sc_mont_mul(x, x, f);", "for (int i_ = 0; i_ < 8; i_++) o[i_ * 64 + threadIdx.x] = x.v[i_];"),
     "ge_to_cached": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached(q, p); p.X = q.T2d; p.Y = q.YpX;",
                      "STP(p);"),
 }

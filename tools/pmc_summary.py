@@ -56,7 +56,9 @@ def main(d):
 
 PHASE = {"k_binom_step": "binomial", "void k_stepping<192>": "stepping", "void k_stepping<256>": "stepping",
          "void k_stepping<512>": "stepping",
-         "void k_combine<1>": "combine", "void k_combine<2>": "combine", "k_check_both": "check", "k_check": "check"}
+         "void k_combine<1>": "combine", "void k_combine<2>": "combine", "void k_combine_short<2, 1>": "combine",
+         "void k_combine_short<3, 2>": "combine", "void k_combine_short<4, 2>": "combine",
+         "k_check_both": "check", "k_check": "check"}
 
 
 def write_traffic(d, out, n, t, U, split_len=None):
