@@ -72,11 +72,13 @@ def test_enc_randomness_golden(golden, name):
 
 def test_split_multipliers():
     """Short recombination vectors (lattice.cpp): a_ju = b_j j^(uL) mod l exactly, b_j > 0, and
-    entries near l^((U-1)/U): <= 127 / 169 / 190 bits for 2 / 3 / 4 pieces (253 for the powers)."""
+    entries near l^((U-1)/U) (the cheapest chain among small combinations of the reduced basis, a
+    few bits above the shortest row): <= 132 / 174 / 195 bits for 2 / 3 / 4 pieces (253 for the
+    powers)."""
     import dkg_amd
 
     ell = 2**252 + 27742317777372353535851937790883648493
-    for U, Lp, bound in ((2, 256, 127), (3, 171, 169), (4, 128, 190), (3, 683, 169)):
+    for U, Lp, bound in ((2, 256, 132), (3, 171, 174), (4, 128, 195), (3, 683, 174)):
         rows = dkg_amd.split_multipliers(300, Lp, U)
         assert len(rows) == 300
         for j, row in enumerate(rows, 1):
