@@ -248,10 +248,11 @@ bool short_multipliers(const Zl& y, int K, uint8_t (*mag)[32], int8_t* sign) {
     if (!any) continue;
     bool small = true;
     for (int u = 0; u < K && small; u++) small = i_bits(c[u]) < 253;
-    if (!small || i_bits(c[0]) == 0) continue;  // |b| < l: b != 0 mod l iff b != 0
+    if (!small) continue;
     const double cost = chain_cost(c, K);
     if (!(cost < best)) continue;
     const Zl b = zl_of(c[0]);
+    if (zl_is_zero(b)) continue;  // b must be invertible mod l (rows like (l, 0, .., 0) are not)
     bool ok = true;  // a_u == b y^u (mod l): exact in Z_l, whatever the reduction did
     for (int u = 1; u < K && ok; u++) ok = zl_is_zero(zl_sub(zl_of(c[u]), zl_mul(b, pw[u])));
     if (!ok) continue;
