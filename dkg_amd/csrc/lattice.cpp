@@ -89,11 +89,14 @@ int i_bits(const I512& a) {  // bit length of |a|
     if (m.w[i]) return 64 * i + 64 - __builtin_clzll(m.w[i]);
   return 0;
 }
-long double i_ld(const I512& a) {
+long double i_ld(const I512& a) {  // to 64 significant bits: the top two nonzero limbs
   const bool neg = i_neg_p(a);
   const I512 m = neg ? i_neg(a) : a;
-  long double v = 0;
-  for (int i = 7; i >= 0; i--) v = v * 18446744073709551616.0L + (long double)m.w[i];
+  static const long double P64[8] = {1.0L, 0x1p64L, 0x1p128L, 0x1p192L, 0x1p256L, 0x1p320L, 0x1p384L, 0x1p448L};
+  int t = 7;
+  while (t > 0 && !m.w[t]) t--;
+  const long double v = t > 0 ? ((long double)m.w[t] * P64[1] + (long double)m.w[t - 1]) * P64[t - 1]
+                              : (long double)m.w[0];
   return neg ? -v : v;
 }
 I512 i_add(const I512& a, const I512& b) {
@@ -228,37 +231,52 @@ bool short_multipliers(const Zl& y, int K, uint8_t (*mag)[32], int8_t* sign) {
       k = k > 1 ? k - 1 : 1;
     }
   }
-  // the cheapest chain among the small combinations of the reduced rows with b != 0 and every
-  // entry below 2^253 (the NAF digit arrays hold 256 positions)
+  // the cheapest chain among the small combinations of the reduced rows with every entry below
+  // 2^253 (the NAF digit arrays hold 256 positions); v and -v cost the same, so only combinations
+  // whose first nonzero coefficient is positive are priced.  Integer combinations of lattice rows
+  // are lattice rows: the Z_l check of the winner below is a safety net.
+  const int CR = 2;  // coefficients in {-2..2} (625 combinations at K = 4; {-1..1}: 0.9 % more work)
+  I512 mult[KMAX][5][KMAX];  // mult[i][c + 2] = c B_i, |c| <= CR
+  for (int i = 0; i < K; i++)
+    for (int c = -CR; c <= CR; c++)
+      for (int u = 0; u < K; u++) mult[i][c + 2][u] = i_mul_shift(B[i][u], c, 0);
   I512 v[KMAX];
   for (int u = 0; u < K; u++) v[u] = i_from_zl(pw[u]);  // fallback: the powers themselves
   double best = chain_cost(v, K);
+  I512 win[KMAX];
+  bool have = false;
   int ncomb = 1;
-  for (int i = 0; i < K; i++) ncomb *= 5;
+  for (int i = 0; i < K; i++) ncomb *= 2 * CR + 1;
   for (int code = 0; code < ncomb; code++) {
-    I512 c[KMAX];
-    for (int u = 0; u < K; u++) c[u] = i_zero();
-    bool any = false;
-    for (int i = 0, cd = code; i < K; i++, cd /= 5) {
-      const int64_t ci = cd % 5 - 2;
-      if (!ci) continue;
-      any = true;
-      for (int u = 0; u < K; u++) c[u] = i_add(c[u], i_mul_shift(B[i][u], ci, 0));
+    int cf[KMAX], first = 0;
+    for (int i = 0, cd = code; i < K; i++, cd /= 2 * CR + 1) {
+      cf[i] = cd % (2 * CR + 1) - CR;
+      if (!first && cf[i]) first = cf[i];
     }
-    if (!any) continue;
+    if (first <= 0) continue;  // zero, or the negation of a combination priced already
+    I512 c[KMAX];
     bool small = true;
-    for (int u = 0; u < K && small; u++) small = i_bits(c[u]) < 253;
+    for (int u = 0; u < K && small; u++) {
+      c[u] = i_zero();
+      for (int i = 0; i < K; i++)
+        if (cf[i]) c[u] = i_add(c[u], mult[i][cf[i] + 2][u]);
+      small = i_bits(c[u]) < 253;
+    }
     if (!small) continue;
     const double cost = chain_cost(c, K);
     if (!(cost < best)) continue;
-    const Zl b = zl_of(c[0]);
-    if (zl_is_zero(b)) continue;  // b must be invertible mod l (rows like (l, 0, .., 0) are not)
-    bool ok = true;  // a_u == b y^u (mod l): exact in Z_l, whatever the reduction did
-    for (int u = 1; u < K && ok; u++) ok = zl_is_zero(zl_sub(zl_of(c[u]), zl_mul(b, pw[u])));
-    if (!ok) continue;
+    if (zl_is_zero(zl_of(c[0]))) continue;  // b must be invertible mod l ((l, 0, .., 0) is not)
     best = cost;
-    const bool flip = i_neg_p(c[0]);  // b > 0
-    for (int u = 0; u < K; u++) v[u] = flip ? i_neg(c[u]) : c[u];
+    have = true;
+    for (int u = 0; u < K; u++) win[u] = c[u];
+  }
+  if (have) {
+    const Zl b = zl_of(win[0]);
+    bool ok = true;  // a_u == b y^u (mod l), exactly
+    for (int u = 1; u < K && ok; u++) ok = zl_is_zero(zl_sub(zl_of(win[u]), zl_mul(b, pw[u])));
+    const bool flip = i_neg_p(win[0]);  // b > 0
+    if (ok)
+      for (int u = 0; u < K; u++) v[u] = flip ? i_neg(win[u]) : win[u];
   }
   for (int u = 0; u < K; u++) {
     sign[u] = i_neg_p(v[u]) ? -1 : 1;

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dkg_amd.h"
@@ -368,17 +369,25 @@ void split_digits(dkg_ctx* ctx, size_t n, size_t L, const int8_t** digits, const
 // (k_combine_short): digits [n][256] u32, byte u of word b = the signed NAF digit at position b of
 // the scalar of piece u; top [n] int16 = the highest position with a nonzero digit; scale [n][8]
 // words = b_j 2^256 mod l, the checks' Montgomery factor taking s to b_j s.  Cached per (n, L, K).
+// (one LLL per receiver, ~1 ms at K = 4: spread over up to 16 host threads)
 void short_vectors(size_t n, size_t L, size_t K, std::vector<uint8_t>& mag, std::vector<int8_t>& sign) {
   mag.assign(n * K * 32, 0);
   sign.assign(n * K, 1);
-  for (size_t j = 0; j < n; j++) {
-    dkgh::Zl x = dkgh::zl_from_u64(j + 1), y = dkgh::zl_from_u64(1);
-    for (size_t e = L; e; e >>= 1) {  // y = x^L
-      if (e & 1) y = dkgh::zl_mul(y, x);
-      x = dkgh::zl_mul(x, x);
+  auto rows = [&](size_t j0, size_t j1) {
+    for (size_t j = j0; j < j1; j++) {
+      dkgh::Zl x = dkgh::zl_from_u64(j + 1), y = dkgh::zl_from_u64(1);
+      for (size_t e = L; e; e >>= 1) {  // y = x^L
+        if (e & 1) y = dkgh::zl_mul(y, x);
+        x = dkgh::zl_mul(x, x);
+      }
+      dkgh::short_multipliers(y, (int)K, reinterpret_cast<uint8_t(*)[32]>(&mag[j * K * 32]), &sign[j * K]);
     }
-    dkgh::short_multipliers(y, (int)K, reinterpret_cast<uint8_t(*)[32]>(&mag[j * K * 32]), &sign[j * K]);
-  }
+  };
+  const size_t nt = std::min<size_t>({(size_t)std::max(1u, std::thread::hardware_concurrency()), 16, (n + 63) / 64});
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < nt; i++) th.emplace_back(rows, n * i / nt, n * (i + 1) / nt);
+  rows(0, n / nt);
+  for (auto& t : th) t.join();
 }
 
 void split_short(dkg_ctx* ctx, size_t n, size_t L, size_t K, const uint32_t** digits, const int16_t** top,
