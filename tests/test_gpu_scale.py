@@ -309,3 +309,31 @@ def test_batch_faulty_members_at_scale(be, golden):
         assert d["final_share"].hex() == c["final_share"] and d["mpk"].hex() == c["mpk"], k
     hm = H(honest["mpk"])
     assert sum(1 for c in range(B) if r.mpk[c] == hm) == B - len(at)
+
+
+@pytest.mark.parametrize("n,t", [(130, 64), (300, 149), (517, 258)])
+def test_recombination_modes_agree_on_faults(be, n, t):
+    """Ragged sizes with tampered dealers (shares, E, A, an undecodable row, randomness): every split
+    U = 2..4 recombined with short lattice multipliers, U = 3..4 with powers of j^L and U = 5 give the
+    same decision matrices, qualification and mpk as the unsplit tables."""
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([t % 251]) * 32, 5, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
+    _inject(random.Random(n * 7 + t), n, t, E, A, s, sp)
+    runs = {}
+    try:
+        for split, comb in ((1, 0), (2, 0), (3, 0), (4, 0), (3, 1), (4, 1), (5, 0)):
+            be.set_split(split)
+            be.set_combine(comb)
+            r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            assert be.last_split() == split
+            assert be.last_combine() == (0 if split == 1 else 1 if (comb == 1 or split > 4) else 2)
+            runs[(split, comb)] = r
+    finally:
+        be.set_split(0)
+        be.set_combine(0)
+    ref = runs.pop((1, 0))
+    assert ref.qualified[:5] == [0, 0, 1, 0, 0] and all(ref.qualified[5:])
+    for key, r in runs.items():
+        assert r.dec2 == ref.dec2 and r.dec4 == ref.dec4, key
+        assert r.qualified == ref.qualified and r.reconstruct == ref.reconstruct and r.mpk == ref.mpk, key
