@@ -39,7 +39,8 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 #            is the roofline's work: frac = 1 means every issue cycle of every SIMD was used.
 #   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
-VALU = {"fe_mul": (140, 256), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200), "ge_dbl_t": (1057, 1864),
+VALU = {"fe_mul": (140, 256), "fe_sq": (109, 185), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200),
+        "ge_madd_signed": (1130, 2002), "ge_dbl_t": (1057, 1864),
         "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "combw_window": (1171, 2047),
         "ge_to_cached": (143, 259), "eq": (633, 1151), "sc_mont_mul": (580, 834)}
 INSTR = {k: v[0] for k, v in VALU.items()}
@@ -174,26 +175,37 @@ def split_pieces(t, U, plen=None):
     return [plen] * (U - 1) + [last if last > 0 else plen], plen  # runtime.hip last_piece_len
 
 
-def short_combine_valu(mults, VALU=SLOTS):
+def affine_point_valu(VALU=SLOTS):
+    """k_affine_pieces per stepped value: blocks of 4 points cost 31 fe_mul + 8 fe_add/fe_sub
+    (counted as ~1/10 of a product each), one inversion (254 fe_sq + 11 fe_mul) per 32 points."""
+    return (31 * VALU["fe_mul"] + 0.8 * VALU["fe_mul"]) / 4 + (254 * VALU["fe_sq"] + 11 * VALU["fe_mul"]) / 32
+
+
+def short_combine_valu(mults, VALU=SLOTS, affine=True):
     """k_combine_short per (column, receiver row of `mults`): U cached addends (the first KL in LDS:
-    ge_add, the rest in VGPRs: ge_add_signed), one joint chain over the U NAFs of the short vector."""
+    ge_add, the rest in VGPRs: ge_add_signed), one joint chain over the U NAFs of the short vector.
+    affine (k_combine_aff, the default addends): mixed additions (ge_madd_signed, LDS ones priced
+    the same), no cached conversion, and k_affine_pieces' normalisation of the U addends."""
     total = 0
     for row in mults:
         U = len(row)
         KL = 1 if U == 2 else 2
         ds = [_naf(abs(v)) for v in row]
         top = max(len(d) for d in ds) - 1
-        c = U * VALU["ge_to_cached"]
+        c = U * (affine_point_valu(VALU) if affine else VALU["ge_to_cached"])
         for i in range(top, -1, -1):
             nz = [u for u in range(U) if i < len(ds[u]) and ds[u][i] != 0]
             if i != top:
                 c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
-            c += sum(VALU["ge_add"] if u < KL else VALU["ge_add_signed"] for u in nz)
+            if affine:
+                c += len(nz) * VALU["ge_madd_signed"]
+            else:
+                c += sum(VALU["ge_add"] if u < KL else VALU["ge_add_signed"] for u in nz)
         total += c
     return total
 
 
-def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None):
+def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine=True):
     """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round
     over all n dealers as implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces
     (split_pieces: L coefficients each but a shorter last one), stepping, recombination by
@@ -214,10 +226,15 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None):
         cost_m[m] = c
     # position m of a piece of length Lp is live for Lp-m steps (a short last piece starts late)
     binom = sum(sum(cost_m[m] * (Lp - m) for m in range(1, Lp)) for Lp in pieces)
-    stepping = n * sum(Lp * VALU["ge_to_cached"] + (Lp - 1) * VALU["ge_add"] for Lp in pieces)
+    # stepping: every lane converts each step; position p adds at step j (0..n-1) only while
+    # p + j < n (k_stepping skips dead positions), so sum_j min(Lp - 1, n - j) additions
+    def adds(Lp):
+        m = min(Lp - 1, n)
+        return m * (m + 1) // 2 + (n - m) * m
+    stepping = sum(n * Lp * VALU["ge_to_cached"] + adds(Lp) * VALU["ge_add"] for Lp in pieces)
     combine = 0
     if U > 1 and mults is not None:
-        combine = short_combine_valu(mults, VALU)
+        combine = short_combine_valu(mults, VALU, affine)
     elif U > 1:  # k_combine: pairwise Horner in y^2 with joint NAF chains (kernels.hip)
         for j in range(1, n + 1):
             y = pow(j, L_, L)
@@ -244,12 +261,12 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None):
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
-def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None):
+def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None, affine=True):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
     recombination; one check kernel computing g*s once (26 radix-2^10 comb windows), h*s' (26 more)
     and both equalities per pair (with `mults`: s and s' scaled by b_j first)."""
-    w2 = algorithmic_valu(n, t, 2, U, VALU, plen, mults)
-    w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults)
+    w2 = algorithmic_valu(n, t, 2, U, VALU, plen, mults, affine)
+    w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults, affine)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
     scale = 2 * VALU["sc_mont_mul"] if mults is not None else 0
     out["check"] = n * n * (2 * COMBW_WINDOWS * VALU["combw_window"] + 2 * VALU["eq"] + scale)
@@ -424,6 +441,8 @@ def main():
     ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
     ap.add_argument("--combine", type=int, default=0,
                     help="recombination of a degree split: 0 short lattice multipliers (U <= 4), 1 powers of j^L")
+    ap.add_argument("--addends", type=int, default=0, choices=[0, 1],
+                    help="short-multiplier recombination addends: 0 affine Niels, 1 cached projective")
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
@@ -452,6 +471,7 @@ def main():
     be.set_split(args.split)
     be.set_field_mode(args.field)
     be.set_combine(args.combine)
+    be.set_addends(args.addends)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1
@@ -544,9 +564,13 @@ def main():
         out["config"]["degree_split"] = U
         out["config"]["split_pieces"] = split_pieces(t, U, Ls)[0]
         out["config"]["recombination"] = {0: "none", 1: "powers of j^L", 2: "short lattice multipliers"}[be.last_combine()]
-        w2, w4 = algorithmic_valu(n, t, 2, U, plen=Ls, mults=mults), algorithmic_valu(n, t, 4, U, plen=Ls, mults=mults)
-        work = fused_valu(n, t, U, plen=Ls, mults=mults) if ov else w2
-        work_i = fused_valu(n, t, U, INSTR, Ls, mults) if ov else algorithmic_valu(n, t, 2, U, INSTR, Ls, mults)
+        aff = args.addends == 0
+        out["config"]["recombination_addends"] = "affine Niels" if aff else "cached projective"
+        w2 = algorithmic_valu(n, t, 2, U, plen=Ls, mults=mults, affine=aff)
+        w4 = algorithmic_valu(n, t, 4, U, plen=Ls, mults=mults, affine=aff)
+        work = fused_valu(n, t, U, plen=Ls, mults=mults, affine=aff) if ov else w2
+        work_i = (fused_valu(n, t, U, INSTR, Ls, mults, aff) if ov
+                  else algorithmic_valu(n, t, 2, U, INSTR, Ls, mults, aff))
         # per-kernel device times need the serialised schedule (one chunk stream): one extra,
         # untimed ceremony in the same round order as the timed ones
         be.set_streams(1)
@@ -609,8 +633,9 @@ def main():
         U, Ls = be.last_split(), be.last_split_len()
         mults = dkg_amd.split_multipliers(n, Ls, U) if be.last_combine() == 2 else None
         D = ((rank + 1) * n) // ws - (rank * n) // ws
-        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls, mults=mults).items()}
-        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls, mults).items()}
+        aff = args.addends == 0
+        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls, mults=mults, affine=aff).items()}
+        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls, mults, aff).items()}
         rl = kernel_rooflines(ph, work, work_i)
         out["config"]["degree_split"] = U
         if rl:

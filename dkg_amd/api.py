@@ -159,6 +159,11 @@ class Backend:
         1 powers of y = j^L; decisions are identical (dkg_ctx_set_combine)."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_combine(self._ctx, mode))
 
+    def set_addends(self, mode: int):
+        """Addends of the short-multiplier recombination: 0 affine Niels (default), 1 cached
+        projective; decisions are identical (dkg_ctx_set_addends)."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_addends(self._ctx, mode))
+
     def last_combine(self) -> int:
         """0 no split, 1 powers of y, 2 short multipliers (the last verification)."""
         return _lib.lib().dkg_ctx_last_combine(self._ctx)

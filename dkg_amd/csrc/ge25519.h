@@ -238,6 +238,38 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
   fe_mul(r.T, e, h);
 }
 
+// r = p + q (neg = false) or p - q (neg = true), q affine Niels (Z = 1): 7M, one code path.  The
+// sign selects which of (y+x, y-x) multiplies which and the sign of c; d = 2Z is carried so that
+// f and g keep ge_add_signed's bounds whatever the sign.  q's fields are second operands only, so
+// they may carry the cached form's uncarried bounds (y+x <= 2^27, y-x <= 2^27.585;
+// tools/fe_bounds.py).
+DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg) {
+  fe a, b, e, h, t, qa, qb;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    qa.v[i] = neg ? q.ypx.v[i] : q.ymx.v[i];
+    qb.v[i] = neg ? q.ymx.v[i] : q.ypx.v[i];
+  }
+  fe_sub(t, p.Y, p.X);
+  fe_mul(a, t, qa);
+  fe_add(t, p.Y, p.X);
+  fe_mul(b, t, qb);
+  fe_sub(e, b, a);
+  fe_add(h, b, a);
+  fe_mul(a, p.T, q.xy2d);   // c
+  fe na;
+  fe_neg(na, a);            // -c = 2p - c <= 2p limbwise
+  fe_cmov(a, na, neg);      // a = +/-c
+  fe_add(b, p.Z, p.Z);
+  fe_carry(b, b);           // d = 2Z, tight
+  fe_sub(t, b, a);          // f = d - (+/-c)
+  fe_add(b, b, a);          // g = d + (+/-c)
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
+  fe_mul(r.T, e, h);
+}
+
 // ---- Ristretto255 (RFC 9496 section 4.3) ----
 
 // (was_square, r) = SQRT_RATIO_M1(u, v); u, v tight.

@@ -564,7 +564,10 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       lds_put_cached(base, u, MAXBS);
     }
     __syncthreads();
-    if (live && pos + 1 < Nlive && (q + 1 < Pseg || up)) ge_add_lds(D, D, nbr, false, MAXBS);
+    // D_pos after step j reaches an output only through D_0 after step j + pos, so positions with
+    // pos + j >= nrecv are dead for the rest of the launch: a wave whose lowest position is past
+    // that line skips its additions (the last 64 steps of every piece's upper wave at L = 128)
+    if (live && pos + 1 < Nlive && (q + 1 < Pseg || up) && pos + j < nrecv) ge_add_lds(D, D, nbr, false, MAXBS);
     __syncthreads();  // every column read before the next step overwrites it
     if (live && q == 0 && R) pt_store_aos(R, d * nrecv + j, D);
   }
@@ -840,6 +843,211 @@ void combine_short(size_t width, size_t pstride, size_t pieces, size_t nrecv, co
     hipLaunchKernelGGL((k_combine_short<3, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, R);
   else
     hipLaunchKernelGGL((k_combine_short<4, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, R);
+}
+
+// Affine addends.  Every addition of the recombination chain adds one of the U stepped values
+// Q_u(j); in affine Niels form (Z = 1) that addition is 7M instead of 8M (d = 2Z1 needs no product),
+// ~250 additions per (column, receiver) at U = 4.  Normalising needs 1/Z of every stepped value:
+// Montgomery's trick over AFF_RUN = 32 receivers per lane (one inversion, ~50 k slots, per 32
+// points).  Half a wave takes one (piece, column) and 1024 consecutive receivers, lane r the
+// receivers r, r + 32, .. so that every load instruction reads consecutive points.  Two levels keep
+// the prefixes out of memory: blocks of 4 points; pass 1 multiplies the block products into a
+// running product and parks the exclusive block prefix in the block's first output slot; after the
+// inversion, pass 2 walks the blocks backwards, rebuilds the 4 in-block prefixes in registers and
+// converts (x, y, 2dxy): ~7.75 M per point + 1/32 inversion.
+constexpr int AFFP_WORDS = 32;  // slot of an affine addend: y+x, y-x, 2dxy, 2 pad (128 B)
+constexpr int AFF_RUN = 32;     // points per lane
+constexpr int AFF_BLK = 4;      // points per block
+
+DKG_DEV void st_fe3(uint32_t* slot, const fe& a, const fe& b, const fe& c) {
+  uint4* s = reinterpret_cast<uint4*>(slot);
+  s[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  s[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  s[2] = make_uint4(a.v[8], a.v[9], b.v[0], b.v[1]);
+  s[3] = make_uint4(b.v[2], b.v[3], b.v[4], b.v[5]);
+  s[4] = make_uint4(b.v[6], b.v[7], b.v[8], b.v[9]);
+  s[5] = make_uint4(c.v[0], c.v[1], c.v[2], c.v[3]);
+  s[6] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
+  s[7] = make_uint4(c.v[8], c.v[9], 0u, 0u);
+}
+
+DKG_DEV void ld_z(fe& z, const uint32_t* R, size_t e) {  // Z of point e (words 20..29)
+  const uint4* p4 = reinterpret_cast<const uint4*>(R + e * PT_WORDS);
+  const uint4 z0 = p4[5], z1 = p4[6], z2 = p4[7];
+  z = fe{{z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w, z2.x, z2.y}};
+}
+
+__global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstride, size_t pieces, size_t nrecv,
+                                                       const uint32_t* __restrict__ R, uint32_t* __restrict__ A) {
+  const size_t span = 32 * AFF_RUN, runs = (nrecv + span - 1) / span;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t item = gid / 32;
+  if (item >= pieces * width * runs) return;
+  const size_t c = item % width, rest = item / width, run = rest % runs, u = rest / runs;
+  const size_t e0 = (u * pstride + c) * nrecv;
+  const size_t jb = run * span + (gid % 32);  // receivers jb + 32 i, i < cnt
+  const int cnt = jb < nrecv ? (int)min((size_t)AFF_RUN, (nrecv - jb + 31) / 32) : 0;
+  const int nblk = (cnt + AFF_BLK - 1) / AFF_BLK;
+  auto pt = [&](int i) { return e0 + jb + 32 * (size_t)i; };
+  // points past cnt in the last block count as Z = 1
+  fe acc;
+  fe_one(acc);
+#pragma unroll 1
+  for (int b = 0; b < nblk; b++) {
+    uint4* a4 = reinterpret_cast<uint4*>(A + pt(AFF_BLK * b) * AFFP_WORDS);
+    a4[0] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+    a4[1] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
+    a4[2] = make_uint4(acc.v[8], acc.v[9], 0u, 0u);
+#pragma unroll 1
+    for (int k = 0; k < AFF_BLK; k++) {
+      const int i = AFF_BLK * b + k;
+      if (i < cnt) {
+        fe z;
+        ld_z(z, R, pt(i));
+        fe_mul(acc, acc, z);
+      }
+    }
+  }
+  fe inv;
+  fe_invert(inv, acc);
+  fe d2;
+  fe_ld(d2, ge_const::D2);
+#pragma unroll 1
+  for (int b = nblk - 1; b >= 0; b--) {
+    fe z[AFF_BLK], q[AFF_BLK];  // q[k] = z[0] .. z[k-1] (q[0] = 1 is never formed)
+#pragma unroll
+    for (int k = 0; k < AFF_BLK; k++) {
+      if (AFF_BLK * b + k < cnt) ld_z(z[k], R, pt(AFF_BLK * b + k));
+      else fe_one(z[k]);
+    }
+    fe_copy(q[1], z[0]);
+#pragma unroll
+    for (int k = 2; k < AFF_BLK; k++) fe_mul(q[k], q[k - 1], z[k - 1]);
+    fe blk, ib;
+    fe_mul(blk, q[AFF_BLK - 1], z[AFF_BLK - 1]);  // the block's product
+    {
+      const uint4* a4 = reinterpret_cast<const uint4*>(A + pt(AFF_BLK * b) * AFFP_WORDS);
+      const uint4 q0 = a4[0], q1 = a4[1], q2 = a4[2];
+      const fe pre = {{q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y}};
+      fe_mul(ib, inv, pre);   // 1 / (this block's product)
+    }
+    fe_mul(inv, inv, blk);    // 1 / (the earlier blocks' product)
+    // the in-block points from the last down, each k a compile-time constant (q[k], z[k] in VGPRs)
+    auto point = [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int i = AFF_BLK * b + k;
+      fe zi;
+      if constexpr (k > 0) {
+        fe_mul(zi, ib, q[k]);   // 1 / Z_i
+        fe_mul(ib, ib, z[k]);
+      } else {
+        fe_copy(zi, ib);
+      }
+      if (i < cnt) {
+        ge_p3 p;
+        pt_load_aos(p, R, pt(i));
+        fe x, y;
+        fe_mul(x, p.X, zi);
+        fe_mul(y, p.Y, zi);
+        fe_mul(p.T, p.T, zi);   // xy
+        fe_mul(p.T, p.T, d2);   // 2dxy
+        fe_add(p.X, y, x);      // y + x <= 2^27
+        fe_sub(p.Y, y, x);      // y - x <= 2^27.585
+        st_fe3(A + pt(i) * AFFP_WORDS, p.X, p.Y, p.T);
+      }
+    };
+    static_assert(AFF_BLK == 4, "point() is spelled out for blocks of 4");
+    point(std::integral_constant<int, 3>{});
+    point(std::integral_constant<int, 2>{});
+    point(std::integral_constant<int, 1>{});
+    point(std::integral_constant<int, 0>{});
+  }
+}
+
+void affine_pieces(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* R, uint32_t* A,
+                   hipStream_t stream) {
+  if (!width || !nrecv || !pieces) return;
+  const size_t runs = (nrecv + 32 * AFF_RUN - 1) / (32 * AFF_RUN), lanes = pieces * width * runs * 32;
+  hipLaunchKernelGGL(k_affine_pieces, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, width, pstride,
+                     pieces, nrecv, R, A);
+}
+
+template <int U, int K, int KL>
+DKG_DEV void aff_addends(uint32_t* qs, ge_aff* qr, const uint32_t* A, size_t pstride, size_t cc, size_t nrecv,
+                         size_t j) {
+  if constexpr (U < K) {
+    const uint4* a4 = reinterpret_cast<const uint4*>(A + (((size_t)U * pstride + cc) * nrecv + j) * AFFP_WORDS);
+    uint32_t w[AFFP_WORDS];
+#pragma unroll
+    for (int k = 0; k < AFFP_WORDS / 4; k++) {
+      const uint4 v = a4[k];
+      w[4 * k] = v.x;
+      w[4 * k + 1] = v.y;
+      w[4 * k + 2] = v.z;
+      w[4 * k + 3] = v.w;
+    }
+    if constexpr (U < KL) {
+      uint32_t* s = qs + U * AFF_WORDS * 64 + threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < AFF_WORDS; k++) s[k * 64] = w[k];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        qr[U - KL].ypx.v[i] = w[i];
+        qr[U - KL].ymx.v[i] = w[10 + i];
+        qr[U - KL].xy2d.v[i] = w[20 + i];
+      }
+    }
+    aff_addends<U + 1, K, KL>(qs, qr, A, pstride, cc, nrecv, j);
+  }
+}
+template <int U, int K, int KL>
+DKG_DEV void aff_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_aff* qr) {
+  if constexpr (U < K) {
+    const int e = (int8_t)(w >> (8 * U));
+    if (e != 0) {
+      if constexpr (U < KL) ge_madd_lds(acc, acc, qs + U * AFF_WORDS * 64 + threadIdx.x, e < 0);
+      else ge_madd_signed(acc, acc, qr[U - KL], e < 0);
+    }
+    aff_position<U + 1, K, KL>(acc, w, qs, qr);
+  }
+}
+
+template <int K, int KL>
+__global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width, size_t pstride, size_t nrecv,
+                                                      const uint32_t* __restrict__ digits,
+                                                      const int16_t* __restrict__ top,
+                                                      const uint32_t* __restrict__ A, uint32_t* __restrict__ R) {
+  __shared__ uint32_t qs[KL * AFF_WORDS * 64];
+  const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t j = blockIdx.y;
+  const bool live = c < width;
+  const size_t cc = live ? c : 0;
+  ge_aff qr[K - KL > 0 ? K - KL : 1];
+  aff_addends<0, K, KL>(qs, qr, A, pstride, cc, nrecv, j);
+  const uint32_t* dw = digits + j * 256;
+  const int tp = top[j];
+  ge_p3 acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int b = tp; b >= 0; b--) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(dw[b]);
+    if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
+    aff_position<0, K, KL>(acc, w, qs, qr);
+  }
+  if (live) pt_store_aos(R, c * nrecv + j, acc);
+}
+
+void combine_short_aff(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* digits,
+                       const int16_t* top, const uint32_t* A, uint32_t* R, hipStream_t stream) {
+  if (!width || !nrecv || pieces < 2 || pieces > 4) return;
+  const dim3 grid((unsigned)((width + 63) / 64), (unsigned)nrecv);
+  if (pieces == 2)
+    hipLaunchKernelGGL((k_combine_aff<2, 1>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R);
+  else if (pieces == 3)
+    hipLaunchKernelGGL((k_combine_aff<3, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R);
+  else
+    hipLaunchKernelGGL((k_combine_aff<4, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R);
 }
 
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,

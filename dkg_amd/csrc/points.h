@@ -240,4 +240,28 @@ DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
   fe_mul(r.T, e, h);
 }
 
+// r = p +/- Q with Q affine Niels (y+x, y-x, 2dxy) in LDS, read like the cached form above (fields
+// 0, 1, 2): 7M, d = 2Z carried as in ge_madd_signed.  `neg` must be wave-uniform.
+DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64) {
+  fe a, b, e, h, t, qv;
+  fe_sub(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 0 : 1, stride);
+  fe_mul(a, t, qv);
+  fe_add(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 1 : 0, stride);
+  fe_mul(b, t, qv);
+  fe_sub(e, b, a);
+  fe_add(h, b, a);
+  lds_get_fe(qv, q, 2, stride);
+  fe_mul(a, p.T, qv);       // c
+  if (neg) fe_neg(a, a);    // 2p - c <= 2p limbwise
+  fe_add(b, p.Z, p.Z);
+  fe_carry(b, b);           // d = 2Z, tight
+  fe_sub(t, b, a);          // f
+  fe_add(b, b, a);          // g
+  fe_mul(r.X, e, t);
+  fe_mul(r.Y, b, h);
+  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
+  fe_mul(r.T, e, h);
+}
 

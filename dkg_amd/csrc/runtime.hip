@@ -53,6 +53,8 @@ struct dkg_ctx {
   int combine_mode = 0;                 // recombination: 0 short vectors for U <= 4, 1 powers of y,
                                         // 2 short vectors (U <= 4)
   int last_combine = 0;                 // 1: the last verify_device recombined with powers, 2: short vectors
+  int addend_mode = 0;                  // short vectors' addends: 0 affine Niels (affine_pieces, mixed
+                                        // additions), 1 cached projective (read from R)
   size_t sdig_n = 0, sdig_L = 0, sdig_K = 0;  // key of the cached short multipliers (v.sdig)
   // round-1 commitments of the ceremony being verified, in extended form on this device (set by
   // the drivers that generate them, ExtScope): verify_device places them instead of decoding the
@@ -72,6 +74,7 @@ namespace {
 
 constexpr size_t PTB = 160;  // bytes of one extended point (40 words)
 constexpr size_t PT_WORDS_H = 40;
+constexpr size_t AFFP_WORDS_H = 32;  // affine addend slot of kernels.hip affine_pieces
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
 constexpr size_t COMBW_BYTES = 26 * 512 * 32 * 4;  // points.h COMBW_WORDS (radix 2^10)
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
@@ -479,6 +482,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const uint32_t *sdig = nullptr, *sscale = nullptr;  // short multipliers: R holds b_j P(j)
   const int16_t* stop = nullptr;
   const bool short_mult = U > 1 && U <= 4 && ctx->combine_mode != 1;
+  // affine addends: one 128-B slot per (piece column, receiver), like R
+  uint32_t* Aff = short_mult && ctx->addend_mode == 0 ? buf<uint32_t>(ctx, "v.Aff", 4 * AFFP_WORDS_H * W * n) : nullptr;
   if (short_mult) split_short(ctx, n, L, U, &sdig, &stop, &sscale);
   else if (U > 1) split_digits(ctx, n, L, &ydig, &ytop);
   ctx->last_combine = U > 1 ? (short_mult ? 2 : 1) : 0;
@@ -527,7 +532,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
                    sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
-    if (short_mult) dkgk::combine_short(w, npad, U, n, sdig, stop, R + c0 * n * PT_WORDS_H, st);
+    if (short_mult && Aff) {
+      dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st);
+      dkgk::combine_short_aff(w, npad, U, n, sdig, stop, Aff + c0 * n * AFFP_WORDS_H, R + c0 * n * PT_WORDS_H, st);
+    } else if (short_mult) dkgk::combine_short(w, npad, U, n, sdig, stop, R + c0 * n * PT_WORDS_H, st);
     else dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
     if (tm) HCK(hipEventRecord(ctx->pev[3], st));
     checks(g0 * 64, std::min(D, g1 * 64), st);
@@ -1411,6 +1419,11 @@ int dkg_ctx_set_combine(dkg_ctx* ctx, int mode) {
   return DKG_OK;
 }
 int dkg_ctx_last_combine(const dkg_ctx* ctx) { return ctx ? ctx->last_combine : 0; }
+int dkg_ctx_set_addends(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
+  ctx->addend_mode = mode;
+  return DKG_OK;
+}
 int dkg_split_multipliers(size_t n, size_t L, int pieces, uint8_t* mag, int8_t* sign) {
   if (!n || !L || pieces < 2 || pieces > 4 || !mag || !sign) return DKG_E_ARG;
   try {

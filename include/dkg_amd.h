@@ -101,6 +101,10 @@ size_t dkg_split_len(size_t columns, size_t n, size_t t, int pieces);
 int dkg_ctx_set_combine(dkg_ctx *ctx, int mode);
 /* What the last verification recombined with: 0 no split, 1 powers of y, 2 short multipliers. */
 int dkg_ctx_last_combine(const dkg_ctx *ctx);
+/* Addends of the short-multiplier recombination: 0 (default) affine Niels (the stepped values
+ * normalised with one inversion per run of receivers; mixed additions, 7M instead of 8M), 1 cached
+ * projective.  Outputs do not depend on it. */
+int dkg_ctx_set_addends(dkg_ctx *ctx, int mode);
 /* The short multipliers (b_j, a_j1, .., a_j(U-1)) of receivers j = 1..n for a `pieces`-way split of
  * piece length L (2 <= pieces <= 4): magnitudes mag[n][pieces][32] (little-endian), signs
  * sign[n][pieces] (+1 / -1); a_ju = b_j j^(uL) mod l and b_j > 0.  DKG_E_ARG on bad input. */

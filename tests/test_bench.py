@@ -53,11 +53,12 @@ def test_closed_form_work_per_pair():
     pairs = n * n  # the closed form counts every (dealer, receiver) position
     w = bench.algorithmic_valu(n, t, 2, 2)
     assert w["binomial"] / pairs == pytest.approx(1.10e6, rel=0.05)
-    assert w["stepping"] / pairs == pytest.approx(1.24e6, rel=0.05)
+    # stepping: 2 x 256 positions, the additions of position p stop after step n - 1 - p
+    assert w["stepping"] / pairs == pytest.approx(1.094e6, rel=0.05)
     assert w["combine"] / pairs == pytest.approx(0.62e6, rel=0.05)
     wi = bench.algorithmic_valu(n, t, 2, 2, bench.INSTR)
     assert wi["binomial"] / pairs == pytest.approx(0.625e6, rel=0.05)
-    assert wi["stepping"] / pairs == pytest.approx(0.685e6, rel=0.05)
+    assert wi["stepping"] / pairs == pytest.approx(0.602e6, rel=0.05)
     assert wi["combine"] / pairs == pytest.approx(0.353e6, rel=0.05)
     for k in w:  # every primitive is mostly half-rate (v_mad_u64_u32) work
         assert 1.6 < w[k] / wi[k] < 2.0
@@ -76,9 +77,12 @@ def test_short_combine_work():
     n, t = 64, 511
     for U, plen, lo, hi in ((3, 171, 0.78, 0.88), (4, 128, 0.58, 0.68)):
         mults = dkg_amd.split_multipliers(n, plen, U)
-        short = bench.algorithmic_valu(n, t, 2, U, plen=plen, mults=mults)
+        short = bench.algorithmic_valu(n, t, 2, U, plen=plen, mults=mults, affine=False)
         powers = bench.algorithmic_valu(n, t, 2, U, plen=plen)
         assert lo < short["combine"] / powers["combine"] < hi, (U, short["combine"] / powers["combine"])
+        # affine addends (default): mixed additions pay for the normalisation (k_affine_pieces)
+        aff = bench.algorithmic_valu(n, t, 2, U, plen=plen, mults=mults)
+        assert 0.95 < aff["combine"] / short["combine"] < 0.99, (U, aff["combine"] / short["combine"])
         assert short["check"] - powers["check"] == n * n * 2 * bench.VALU["sc_mont_mul"][1]
         assert short["binomial"] == powers["binomial"] and short["stepping"] == powers["stepping"]
 

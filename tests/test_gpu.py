@@ -782,16 +782,18 @@ def test_stepping_modes_goldens(be, golden, name, mode):
         be.set_split(0)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode,addends", [(1, 0), (2, 0), (2, 1)])
 @pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json"])
-def test_combine_modes_goldens(be, golden, name, mode):
+def test_combine_modes_goldens(be, golden, name, mode, addends):
     """Recombination with powers of j^L (1) or with short lattice multipliers (2: R holds b_j P(j),
-    the checks scale the shares by b_j) for 2..5 pieces: every output bit-exact."""
+    the checks scale the shares by b_j; addends affine Niels (0) or cached projective (1)) for 2..5
+    pieces: every output bit-exact."""
     c = golden(name)
     n, t = c["n"], c["t"]
     be.env_init(t, n, CK)
     try:
         be.set_combine(mode)
+        be.set_addends(addends)
         for pieces in sorted({2, min(3, t + 1), min(4, t + 1), min(5, t + 1)}):
             be.set_split(pieces)
             r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
@@ -799,6 +801,7 @@ def test_combine_modes_goldens(be, golden, name, mode):
             assert be.last_combine() == (2 if mode == 2 and pieces <= 4 else 1) or pieces == 1
     finally:
         be.set_combine(0)
+        be.set_addends(0)
         be.set_split(0)
 
 

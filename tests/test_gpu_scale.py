@@ -322,17 +322,20 @@ def test_recombination_modes_agree_on_faults(be, n, t):
     _inject(random.Random(n * 7 + t), n, t, E, A, s, sp)
     runs = {}
     try:
-        for split, comb in ((1, 0), (2, 0), (3, 0), (4, 0), (3, 1), (4, 1), (5, 0)):
+        for split, comb, add in ((1, 0, 0), (2, 0, 0), (3, 0, 0), (4, 0, 0), (2, 0, 1), (3, 0, 1), (4, 0, 1),
+                                 (3, 1, 0), (4, 1, 0), (5, 0, 0)):
             be.set_split(split)
             be.set_combine(comb)
+            be.set_addends(add)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             assert be.last_split() == split
             assert be.last_combine() == (0 if split == 1 else 1 if (comb == 1 or split > 4) else 2)
-            runs[(split, comb)] = r
+            runs[(split, comb, add)] = r
     finally:
         be.set_split(0)
         be.set_combine(0)
-    ref = runs.pop((1, 0))
+        be.set_addends(0)
+    ref = runs.pop((1, 0, 0))
     assert ref.qualified[:5] == [0, 0, 1, 0, 0] and all(ref.qualified[5:])
     for key, r in runs.items():
         assert r.dec2 == ref.dec2 and r.dec4 == ref.dec4, key

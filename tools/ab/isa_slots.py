@@ -8,7 +8,7 @@ src, out = sys.argv[1], sys.argv[2]
 inc = sys.argv[3]
 subprocess.check_call(["/opt/rocm/bin/hipcc","--offload-arch=gfx950","-O3","-std=c++17","-S","--cuda-device-only","-I",inc,"-o",out,src], stderr=subprocess.DEVNULL)
 s = open(out).read()
-for m in re.finditer(r"\n(_Z\w*(k_binom_step|k_stepping|k_combine|k_check)\w*):[^\n]*\n", s):
+for m in re.finditer(r"\n(_Z\w*(k_binom_step|k_stepping|k_combine|k_check|k_affine)\w*):[^\n]*\n", s):
     name = m.group(1); body = s[m.end():]; body = body[:body.index("s_endpgm")]
     ops = [l.split()[0] for l in body.split("\n") if l.strip().startswith("v_")]
     tot = sum(slots(o) for o in ops)

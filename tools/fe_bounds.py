@@ -13,7 +13,8 @@ weights) straight from the header text, so the checker cannot drift from the cod
     intermediate of the carry pass fe_carry64) stays below 2^64, every 32-bit value below 2^32;
   * fe_tobytes32's canonical reduction sees a value below 2p (one conditional subtraction suffices).
 The group formulas (ge_to_cached, ge_add, ge_sub, ge_madd, ge_msub, ge_dbl / _rt / _lean,
-ge_add_signed, ge_add_lds incl. its negated path, the comb entry selection of combw_mul_add,
+ge_add_signed, ge_add_lds incl. its negated path, ge_madd_signed / ge_madd_lds and the affine
+addends of k_affine_pieces, the comb entry selection of combw_mul_add,
 ristretto_eq, decode / encode) are run on the bounds; point coordinates are iterated to a fixpoint
 (every stored coordinate is again an input), so the invariant "a coordinate is TIGHT" is closed.
 
@@ -341,6 +342,35 @@ def ge_add_lds(p, q, where="ge_add_lds"):
     return (fe_mul(e, t, where), fe_mul(b, h, where), fe_mul(t, b, where), fe_mul(e, h, where))
 
 
+def ge_madd_signed(p, q, where="ge_madd_signed"):
+    """ge25519.h ge_madd_signed and points.h ge_madd_lds, both signs: the two reads selected from
+    (y+x, y-x), a = +-c (fe_neg, no carry), d = 2Z carried."""
+    X, Y, Z, T = p
+    ypx, ymx, xy2d = q
+    sel = vmax(ypx, ymx)
+    t = fe_sub(Y, X, where)
+    a = fe_mul(t, sel, where)
+    t = fe_add(Y, X, where)
+    b = fe_mul(t, sel, where)
+    e = fe_sub(b, a, where)
+    h = fe_add(b, a, where)
+    a = fe_mul(T, xy2d, where)
+    a = vmax(a, fe_neg(a, where))
+    b = fe_carry(fe_add(Z, Z, where), where)
+    t = fe_sub(b, a, where)
+    b = fe_add(b, a, where)
+    return (fe_mul(e, t, where), fe_mul(b, h, where), fe_mul(t, b, where), fe_mul(e, h, where))
+
+
+def affine_addend(p, where="affine_pieces"):
+    """kernels.hip k_affine_pieces: zi = inv * prefix (products of Z), x = X zi, y = Y zi,
+    2dxy = (T zi) 2d; y+x and y-x left uncarried like the cached form."""
+    X, Y, Z, T = p
+    zi = fe_mul(fe_mul(Z, Z, where), Z, where)
+    x, y = fe_mul(X, zi, where), fe_mul(Y, zi, where)
+    return (fe_add(y, x, where), fe_sub(y, x, where), fe_mul(fe_mul(T, zi, where), D2, where))
+
+
 def comb8_entry(tab_ypx, tab_ymx, tab_xy2d):
     """points.h combw_mul_add: the selected affine entry, incl. identity (1, 1, 0) and -Q =
     (y-x, y+x, 2p - xy2d) -- the negated xy2d is NOT carried."""
@@ -471,6 +501,7 @@ def run():
                 ge_add_signed(pt, c), ge_add_lds(pt, c), ge_add(pt, ge_cached_neg(c), "ge_add(-q)")]
         aff = (fe_carry(fe_add(tight, tight)), fe_carry(fe_sub(tight, tight)), fe_mul(fe_mul(tight, tight), D2))
         outs += [ge_madd(pt, comb8_entry(*aff), "comb8 madd"), ge_madd(pt, aff, "ge_msub", minus=True)]
+        outs += [ge_madd_signed(pt, affine_addend(pt))]
         outs += [ristretto_decode(), ristretto_elligator()]
         ristretto_encode(pt)
         new = vmax(tight, *[x for o in outs for x in o])
