@@ -40,7 +40,8 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 #   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
 VALU = {"fe_mul": (140, 256), "fe_sq": (109, 185), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200),
-        "ge_madd_signed": (1130, 2002), "ge_dbl_t": (1057, 1864),
+        "ge_madd_signed": (1130, 2002), "ge_add_ded": (1198, 2180), "ge_to_cached_ded": (73, 95),
+        "fe_tight_zero": (16, 31), "ge_dbl_t": (1057, 1864),
         "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "combw_window": (1171, 2047),
         "ge_to_cached": (143, 259), "eq": (633, 1151), "sc_mont_mul": (580, 834)}
 INSTR = {k: v[0] for k, v in VALU.items()}
@@ -205,7 +206,7 @@ def short_combine_valu(mults, VALU=SLOTS, affine=True):
     return total
 
 
-def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine=True):
+def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine=True, ded=True):
     """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round
     over all n dealers as implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces
     (split_pieces: L coefficients each but a shorter last one), stepping, recombination by
@@ -231,7 +232,11 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
     def adds(Lp):
         m = min(Lp - 1, n)
         return m * (m + 1) // 2 + (n - m) * m
-    stepping = sum(n * Lp * VALU["ge_to_cached"] + adds(Lp) * VALU["ge_add"] for Lp in pieces)
+    # (ded: the dedicated addition + fe_tight_zero on its Z, and the product-free cached form; the
+    # complete redo of marked workgroups does not occur on honest tables)
+    cached, add = ((VALU["ge_to_cached_ded"], VALU["ge_add_ded"] + VALU["fe_tight_zero"]) if ded
+                   else (VALU["ge_to_cached"], VALU["ge_add"]))
+    stepping = sum(n * Lp * cached + adds(Lp) * add for Lp in pieces)
     combine = 0
     if U > 1 and mults is not None:
         combine = short_combine_valu(mults, VALU, affine)
@@ -261,12 +266,12 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
-def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None, affine=True):
+def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None, affine=True, ded=True):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
     recombination; one check kernel computing g*s once (26 radix-2^10 comb windows), h*s' (26 more)
     and both equalities per pair (with `mults`: s and s' scaled by b_j first)."""
-    w2 = algorithmic_valu(n, t, 2, U, VALU, plen, mults, affine)
-    w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults, affine)
+    w2 = algorithmic_valu(n, t, 2, U, VALU, plen, mults, affine, ded)
+    w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults, affine, ded)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
     scale = 2 * VALU["sc_mont_mul"] if mults is not None else 0
     out["check"] = n * n * (2 * COMBW_WINDOWS * VALU["combw_window"] + 2 * VALU["eq"] + scale)
@@ -441,6 +446,8 @@ def main():
     ap.add_argument("--split", type=int, default=0, help="degree split U of the difference tables (0: cost model)")
     ap.add_argument("--combine", type=int, default=0,
                     help="recombination of a degree split: 0 short lattice multipliers (U <= 4), 1 powers of j^L")
+    ap.add_argument("--step-formula", type=int, default=0, choices=[0, 1],
+                    help="stepping additions: 0 dedicated (complete redo where exceptional), 1 complete")
     ap.add_argument("--addends", type=int, default=0, choices=[0, 1],
                     help="short-multiplier recombination addends: 0 affine Niels, 1 cached projective")
     ap.add_argument("--field", type=int, default=0,
@@ -472,6 +479,7 @@ def main():
     be.set_field_mode(args.field)
     be.set_combine(args.combine)
     be.set_addends(args.addends)
+    be.set_stepping_formula(args.step_formula)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1
@@ -564,13 +572,15 @@ def main():
         out["config"]["degree_split"] = U
         out["config"]["split_pieces"] = split_pieces(t, U, Ls)[0]
         out["config"]["recombination"] = {0: "none", 1: "powers of j^L", 2: "short lattice multipliers"}[be.last_combine()]
-        aff = args.addends == 0
+        aff, ded = args.addends == 0, args.step_formula == 0
         out["config"]["recombination_addends"] = "affine Niels" if aff else "cached projective"
-        w2 = algorithmic_valu(n, t, 2, U, plen=Ls, mults=mults, affine=aff)
-        w4 = algorithmic_valu(n, t, 4, U, plen=Ls, mults=mults, affine=aff)
-        work = fused_valu(n, t, U, plen=Ls, mults=mults, affine=aff) if ov else w2
-        work_i = (fused_valu(n, t, U, INSTR, Ls, mults, aff) if ov
-                  else algorithmic_valu(n, t, 2, U, INSTR, Ls, mults, aff))
+        out["config"]["stepping_additions"] = "dedicated (complete redo where exceptional)" if ded else "complete"
+        out["stepping_redos"] = be.stepping_redos()
+        w2 = algorithmic_valu(n, t, 2, U, plen=Ls, mults=mults, affine=aff, ded=ded)
+        w4 = algorithmic_valu(n, t, 4, U, plen=Ls, mults=mults, affine=aff, ded=ded)
+        work = fused_valu(n, t, U, plen=Ls, mults=mults, affine=aff, ded=ded) if ov else w2
+        work_i = (fused_valu(n, t, U, INSTR, Ls, mults, aff, ded) if ov
+                  else algorithmic_valu(n, t, 2, U, INSTR, Ls, mults, aff, ded))
         # per-kernel device times need the serialised schedule (one chunk stream): one extra,
         # untimed ceremony in the same round order as the timed ones
         be.set_streams(1)
@@ -633,9 +643,9 @@ def main():
         U, Ls = be.last_split(), be.last_split_len()
         mults = dkg_amd.split_multipliers(n, Ls, U) if be.last_combine() == 2 else None
         D = ((rank + 1) * n) // ws - (rank * n) // ws
-        aff = args.addends == 0
-        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls, mults=mults, affine=aff).items()}
-        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls, mults, aff).items()}
+        aff, ded = args.addends == 0, args.step_formula == 0
+        work = {k: v * D / n for k, v in fused_valu(n, t, U, plen=Ls, mults=mults, affine=aff, ded=ded).items()}
+        work_i = {k: v * D / n for k, v in fused_valu(n, t, U, INSTR, Ls, mults, aff, ded).items()}
         rl = kernel_rooflines(ph, work, work_i)
         out["config"]["degree_split"] = U
         if rl:

@@ -159,6 +159,18 @@ class Backend:
         1 powers of y = j^L; decisions are identical (dkg_ctx_set_combine)."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_combine(self._ctx, mode))
 
+    def set_stepping_formula(self, mode: int):
+        """Stepping additions: 0 dedicated formula with complete redo of the workgroups that met an
+        exceptional pair (default), 1 complete formula only; decisions are identical."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_stepping_formula(self._ctx, mode))
+
+    def stepping_redos(self) -> int:
+        """Workgroups of the last verification's stepping redone by the complete formula."""
+        r = _lib.lib().dkg_ctx_stepping_redos(self._ctx)
+        if r < 0:
+            raise DkgError(_lib.DKG_E_DEVICE, "dkg_ctx_stepping_redos failed")
+        return r
+
     def set_addends(self, mode: int):
         """Addends of the short-multiplier recombination: 0 affine Niels (default), 1 cached
         projective; decisions are identical (dkg_ctx_set_addends)."""

@@ -484,6 +484,19 @@ DKG_DEV bool fe_iszero(const fe& a) {
   for (int i = 0; i < 8; i++) o |= s[i];
   return o == 0;
 }
+// a == 0 (mod p) for `a` an fe_mul / fe_sq output (either flavour): such a value is below 2p and
+// its limbs sit in their nominal widths except limbs 1 and 5, which can exceed 2^25 - 1 by a small
+// carry (< 2^11, far below another 2^25), so 0 and p each have exactly one representation: all limbs zero, or p's
+// canonical limbs (tools/fe_bounds.py asserts the output bounds this relies on).  ~30 full-rate ops.
+DKG_DEV bool fe_tight_zero(const fe& a) {
+  uint32_t z = a.v[0], q = a.v[0] ^ 0x3ffffedu;
+#pragma unroll
+  for (int i = 1; i < 10; i++) {
+    z |= a.v[i];
+    q |= a.v[i] ^ ((i & 1) ? 0x1ffffffu : 0x3ffffffu);
+  }
+  return (z == 0u) | (q == 0u);
+}
 DKG_DEV void fe_cmov(fe& r, const fe& a, bool c) {
 #pragma unroll
   for (int i = 0; i < 10; i++) r.v[i] = c ? a.v[i] : r.v[i];

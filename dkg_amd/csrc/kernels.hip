@@ -509,12 +509,21 @@ void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uin
 // one piece per launch (P = N when the whole table fits one block: a t = 31 table packs 8 dealers
 // into a 256-lane workgroup instead of idling half of a 64-lane one).  nseg = U: every piece of a
 // column in one slot (N = 512 split 192 + 192 + 128: one 512-lane workgroup per column).
-template <int MAXBS>
+//
+// DED: additions by the dedicated formula (ge_add_ded_lds: no product by d, one fewer per lane and
+// step); a lane whose sum comes out with Z = 0 (an exceptional pair, never for honest tables but
+// reachable by crafted commitments or identity padding) marks its workgroup in flags[wg].  !DED with
+// flags: the complete formula, only in the workgroups marked (the same grid is relaunched), which
+// recompute their tables from the start -- so every value is the complete formula's.
+template <int MAXBS, bool DED>
 __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_stepping(
     size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ e, size_t nrecv, size_t pos0, int P,
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
-    uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast) {
+    uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast,
+    uint32_t* __restrict__ flags) {
+  const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if (!DED && flags && !flags[wg]) return;  // a redo launch: this workgroup's tables were exact
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
   // segment position q adds column q + 1 of its segment.  Column q = 0 is never read inside a
   // segment (its value leaves through `down` / R), so the segment's top lane parks the upstream
@@ -542,10 +551,12 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   uint32_t* mine = cols + l;
   uint32_t* base = cols + (l - q);
   const uint32_t* nbr = base + ((q + 1) % Pseg);
+  bool bad = false;
   for (size_t j = 0; j < nrecv; j++) {
     {
       ge_cached c0;
-      ge_to_cached(c0, D);
+      if (DED) ge_to_cached_ded(c0, D);
+      else ge_to_cached(c0, D);
       if (q == 0) {
         if (downd) {
           const uint4* w4 = reinterpret_cast<const uint4*>(&c0);
@@ -567,10 +578,18 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     // D_pos after step j reaches an output only through D_0 after step j + pos, so positions with
     // pos + j >= nrecv are dead for the rest of the launch: a wave whose lowest position is past
     // that line skips its additions (the last 64 steps of every piece's upper wave at L = 128)
-    if (live && pos + 1 < Nlive && (q + 1 < Pseg || up) && pos + j < nrecv) ge_add_lds(D, D, nbr, false, MAXBS);
+    if (live && pos + 1 < Nlive && (q + 1 < Pseg || up) && pos + j < nrecv) {
+      if (DED) {
+        ge_add_ded_lds(D, D, nbr, MAXBS);
+        bad |= fe_tight_zero(D.Z);
+      } else {
+        ge_add_lds(D, D, nbr, false, MAXBS);
+      }
+    }
     __syncthreads();  // every column read before the next step overwrites it
     if (live && q == 0 && R) pt_store_aos(R, d * nrecv + j, D);
   }
+  if (DED && bad) flags[wg] = 1u;  // any lane: the same value
 }
 
 // Lanes given to an N-position table: 512-lane blocks (balanced when N > 512), or P = N lanes per
@@ -649,22 +668,45 @@ double stepping_waves_per_simd(size_t cols, size_t N, size_t pieces, size_t last
   return wgs / std::ceil(wgs / cap) * (s.bs / 64.0) / 1024;
 }
 
+size_t stepping_flag_words(size_t ndealers, size_t pieces) { return ndealers * (pieces + 1); }
+
+template <bool DED>
+void step_launch(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t ndealers, size_t npad, size_t N,
+                 const uint32_t* e, size_t nrecv, size_t pos0, int P, const uint32_t* up, uint32_t* down,
+                 uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags) {
+  if (maxbs == 192)
+    hipLaunchKernelGGL((k_stepping<192, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags);
+  else if (maxbs == 256)
+    hipLaunchKernelGGL((k_stepping<256, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags);
+  else
+    hipLaunchKernelGGL((k_stepping<512, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags);
+}
+
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
-              size_t last_len, bool whole) {
+              size_t last_len, bool whole, uint32_t* flags) {
   if (!ndealers || !nrecv) return;
   if (!last_len || last_len > N) last_len = N;
+  // with flags (stepping_flag_words zeroed words): every launch below runs dedicated, then again
+  // complete in its marked workgroups (its own flag words: a grid has at most ndealers x pieces)
+  size_t foff = 0;
+  auto run = [&](int maxbs, dim3 grid, dim3 block, size_t pos0, int P, const uint32_t* up, uint32_t* down,
+                 uint32_t* Rout, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* f) {
+    if (f) {
+      step_launch<true>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
+                        Nlive, piece0, nseg, Plast, f);
+    }
+    step_launch<false>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
+                       Nlive, piece0, nseg, Plast, f);
+  };
   auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
     const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), (unsigned)np), block((unsigned)s.bs);
-    if (s.maxbs == 192)
-      hipLaunchKernelGGL(k_stepping<192>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
-                         (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
-    else if (s.maxbs == 256)
-      hipLaunchKernelGGL(k_stepping<256>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
-                         (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
-    else
-      hipLaunchKernelGGL(k_stepping<512>, grid, block, 0, stream, ndealers, npad, N, e, nrecv, (size_t)0, (int)s.P,
-                         (const uint32_t*)nullptr, (uint32_t*)nullptr, R, pstride, Nlive, piece0, nseg, Plast);
+    uint32_t* f = flags ? flags + foff : nullptr;
+    foff += (size_t)grid.x * grid.y;
+    run((int)s.maxbs, grid, block, 0, (int)s.P, nullptr, nullptr, R, Nlive, piece0, nseg, Plast, f);
   };
   if (whole && stepping_whole_columns(N, pieces, last_len)) {
     // one slot of (pieces - 1) N + last_len lanes per column: every workgroup does the same work
@@ -676,14 +718,24 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
   }
   const StepShape sh = stepping_shape(N);
   if (sh.nblk > 1) {  // one dealer per workgroup, top block first, block values streamed down
+    // the blocks of a column share one flag word (same grid in every block launch): the dedicated
+    // pass runs all blocks top-down, then the complete pass redoes all blocks of marked columns
     auto blocks = [&](size_t Nlive, unsigned piece0, size_t np) {
-      uint32_t* up = nullptr;
-      for (size_t b = sh.nblk; b-- > 0;) {
-        uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
-        hipLaunchKernelGGL(k_stepping<512>, dim3((unsigned)ndealers, (unsigned)np), dim3((unsigned)sh.bs), 0,
-                           stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down, b ? nullptr : R,
-                           pstride, Nlive, piece0, 1, (int)sh.P);
-        up = down;
+      const dim3 grid((unsigned)ndealers, (unsigned)np), block((unsigned)sh.bs);
+      uint32_t* f = flags ? flags + foff : nullptr;
+      foff += (size_t)grid.x * grid.y;
+      for (int pass = f ? 0 : 1; pass < 2; pass++) {
+        uint32_t* up = nullptr;
+        for (size_t b = sh.nblk; b-- > 0;) {
+          uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
+          if (pass == 0)
+            step_launch<true>(512, grid, block, stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down,
+                              b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f);
+          else
+            step_launch<false>(512, grid, block, stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down,
+                               b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f);
+          up = down;
+        }
       }
     };
     // a short last piece runs the same blocks with its positions >= last_len as the identity

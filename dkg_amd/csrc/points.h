@@ -240,6 +240,41 @@ DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
   fe_mul(r.T, e, h);
 }
 
+// Dedicated addition (Hisil-Wong-Carter-Dawson 2008, "add-2008-hwcd-4", a = -1): r = p + Q with Q
+// prepared by ge_to_cached_ded as (Y+X, Y-X, 2Z, 2T) in LDS.  8M and no multiplication by d (the
+// cached form needs none either: the stepping saves one product per lane and step), but the formula
+// is not complete: F = 2(X1 Y2 - Y1 X2) vanishes when p - Q is 0 or the 2-torsion point, G = 2(Y1 Y2
+// - X1 X2) when p + Q meets the 4-torsion, and then the result has Z = F G = 0.  Whenever Z != 0 the
+// result is p + Q exactly (tools/ded_check.py checks both claims over every 8-torsion offset).
+// Callers test Z with fe_tight_zero and redo the work with the complete ge_add_lds.
+DKG_DEV void ge_to_cached_ded(ge_cached& c, const ge_p3& p) {
+  fe_add(c.YpX, p.Y, p.X);
+  fe_sub(c.YmX, p.Y, p.X);
+  fe_add(c.Z2, p.Z, p.Z);
+  fe_add(c.T2d, p.T, p.T);  // 2T in the 2dT slot
+}
+DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int stride = 64) {
+  fe a, b, e, h, t, qv;
+  fe_sub(t, p.Y, p.X);
+  lds_get_fe(qv, q, 0, stride);  // Y2 + X2
+  fe_mul(a, t, qv);              // A = (Y1 - X1)(Y2 + X2)
+  fe_add(t, p.Y, p.X);
+  lds_get_fe(qv, q, 1, stride);  // Y2 - X2
+  fe_mul(b, t, qv);              // B = (Y1 + X1)(Y2 - X2)
+  fe_sub(e, b, a);               // F = B - A <= 1.5*2^27
+  fe_add(h, b, a);               // G = B + A <= 2^27
+  lds_get_fe(qv, q, 3, stride);  // 2 T2
+  fe_mul(a, p.Z, qv);            // C = 2 Z1 T2
+  lds_get_fe(qv, q, 2, stride);  // 2 Z2
+  fe_mul(b, p.T, qv);            // D = 2 T1 Z2
+  fe_add(t, b, a);               // E = D + C <= 2^27
+  fe_sub(b, b, a);               // H = D - C <= 1.5*2^27
+  fe_mul(r.X, t, e);             // X3 = E F
+  fe_mul(r.Y, h, b);             // Y3 = G H
+  fe_mul(r.T, t, b);             // T3 = E H
+  fe_mul(r.Z, h, e);             // Z3 = F G  (x19 operands F and H, computed once each)
+}
+
 // r = p +/- Q with Q affine Niels (y+x, y-x, 2dxy) in LDS, read like the cached form above (fields
 // 0, 1, 2): 7M, d = 2Z carried as in ge_madd_signed.  `neg` must be wave-uniform.
 DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64) {

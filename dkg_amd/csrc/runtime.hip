@@ -53,6 +53,10 @@ struct dkg_ctx {
   int combine_mode = 0;                 // recombination: 0 short vectors for U <= 4, 1 powers of y,
                                         // 2 short vectors (U <= 4)
   int last_combine = 0;                 // 1: the last verify_device recombined with powers, 2: short vectors
+  int step_formula = 0;                 // stepping additions: 0 dedicated + complete redo of marked
+                                        // workgroups, 1 complete formula only
+  uint32_t* last_step_flags = nullptr;  // the last verify_device's stepping flags (dedicated mode)
+  size_t last_step_flag_words = 0;
   int addend_mode = 0;                  // short vectors' addends: 0 affine Niels (affine_pieces, mixed
                                         // additions), 1 cached projective (read from R)
   size_t sdig_n = 0, sdig_L = 0, sdig_K = 0;  // key of the cached short multipliers (v.sdig)
@@ -482,6 +486,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const uint32_t *sdig = nullptr, *sscale = nullptr;  // short multipliers: R holds b_j P(j)
   const int16_t* stop = nullptr;
   const bool short_mult = U > 1 && U <= 4 && ctx->combine_mode != 1;
+  // stepping flags of the dedicated additions: chunk c0's words start at stepping_flag_words(c0, U)
+  uint32_t* sflags = ctx->step_formula == 0
+                         ? buf<uint32_t>(ctx, "v.sflags", 4 * dkgk::stepping_flag_words(npad, U)) : nullptr;
+  ctx->last_step_flags = sflags;
+  ctx->last_step_flag_words = sflags ? dkgk::stepping_flag_words(npad, U) : 0;
   // affine addends: one 128-B slot per (piece column, receiver), like R
   uint32_t* Aff = short_mult && ctx->addend_mode == 0 ? buf<uint32_t>(ctx, "v.Aff", 4 * AFFP_WORDS_H * W * n) : nullptr;
   if (short_mult) split_short(ctx, n, L, U, &sdig, &stop, &sscale);
@@ -529,8 +538,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     const uint32_t* e = bin;
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
+    uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
+    if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole);
+                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     if (short_mult && Aff) {
       dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st);
@@ -1419,6 +1430,25 @@ int dkg_ctx_set_combine(dkg_ctx* ctx, int mode) {
   return DKG_OK;
 }
 int dkg_ctx_last_combine(const dkg_ctx* ctx) { return ctx ? ctx->last_combine : 0; }
+int dkg_ctx_set_stepping_formula(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
+  ctx->step_formula = mode;
+  return DKG_OK;
+}
+long long dkg_ctx_stepping_redos(dkg_ctx* ctx) {
+  if (!ctx) return -1;
+  if (!ctx->last_step_flags) return 0;
+  try {
+    std::vector<uint32_t> h(ctx->last_step_flag_words);
+    sync(ctx);
+    HCK(hipMemcpy(h.data(), ctx->last_step_flags, 4 * h.size(), hipMemcpyDeviceToHost));
+    long long c = 0;
+    for (uint32_t x : h) c += x != 0;
+    return c;
+  } catch (const Fail& f) {
+    return -1;
+  }
+}
 int dkg_ctx_set_addends(dkg_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
   ctx->addend_mode = mode;

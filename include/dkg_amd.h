@@ -105,6 +105,14 @@ int dkg_ctx_last_combine(const dkg_ctx *ctx);
  * normalised with one inversion per run of receivers; mixed additions, 7M instead of 8M), 1 cached
  * projective.  Outputs do not depend on it. */
 int dkg_ctx_set_addends(dkg_ctx *ctx, int mode);
+/* Additions of the finite-difference stepping: 0 (default) the dedicated formula (HWCD 2008, no
+ * product by d; not complete), with every workgroup that met an exceptional pair (a sum with Z = 0:
+ * equal or 2-/4-torsion-related points, which crafted commitments can reach) recomputed by the
+ * complete formula; 1 the complete formula only.  Outputs do not depend on it. */
+int dkg_ctx_set_stepping_formula(dkg_ctx *ctx, int mode);
+/* Workgroups of the last verification's stepping that were recomputed by the complete formula
+ * (synchronises the context's stream; 0 in mode 1; -1 on error). */
+long long dkg_ctx_stepping_redos(dkg_ctx *ctx);
 /* The short multipliers (b_j, a_j1, .., a_j(U-1)) of receivers j = 1..n for a `pieces`-way split of
  * piece length L (2 <= pieces <= 4): magnitudes mag[n][pieces][32] (little-endian), signs
  * sign[n][pieces] (+1 / -1); a_ju = b_j j^(uL) mod l and b_j > 0.  DKG_E_ARG on bad input. */

@@ -51,19 +51,22 @@ def test_closed_form_work_per_pair():
     issue slots (the roofline's unit: half-rate instructions count 2) and in instructions."""
     n, t = 1024, 511
     pairs = n * n  # the closed form counts every (dealer, receiver) position
-    w = bench.algorithmic_valu(n, t, 2, 2)
+    w = bench.algorithmic_valu(n, t, 2, 2, ded=False)
     assert w["binomial"] / pairs == pytest.approx(1.10e6, rel=0.05)
     # stepping: 2 x 256 positions, the additions of position p stop after step n - 1 - p
     assert w["stepping"] / pairs == pytest.approx(1.094e6, rel=0.05)
     assert w["combine"] / pairs == pytest.approx(0.62e6, rel=0.05)
-    wi = bench.algorithmic_valu(n, t, 2, 2, bench.INSTR)
+    wi = bench.algorithmic_valu(n, t, 2, 2, bench.INSTR, ded=False)
     assert wi["binomial"] / pairs == pytest.approx(0.625e6, rel=0.05)
     assert wi["stepping"] / pairs == pytest.approx(0.602e6, rel=0.05)
     assert wi["combine"] / pairs == pytest.approx(0.353e6, rel=0.05)
     for k in w:  # every primitive is mostly half-rate (v_mad_u64_u32) work
         assert 1.6 < w[k] / wi[k] < 2.0
+    # the dedicated stepping additions (default) drop the product of the cached form
+    wd = bench.algorithmic_valu(n, t, 2, 2)
+    assert 0.93 < wd["stepping"] / w["stepping"] < 0.97 and wd["binomial"] == w["binomial"]
     # the fused schedule carries both rounds' tables through binomial, stepping and recombination
-    f = bench.fused_valu(n, t, 2)
+    f = bench.fused_valu(n, t, 2, ded=False)
     assert f["binomial"] == pytest.approx(2 * w["binomial"])
 
 

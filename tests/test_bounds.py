@@ -50,3 +50,28 @@ def test_checker_detects_violations():
     F.fe_mul([int(2 ** 28.32)] * 10, [int(2 ** 27.585)] * 10, "probe")
     F.fe_mul([1 << 29] * 10, [1 << 26] * 10, "probe")
     assert F.violations == []
+
+
+def test_dedicated_addition_is_exact_or_flags():
+    """The stepping's dedicated addition (points.h ge_add_ded_lds) returns p + q or a point with
+    Z = 0, never a wrong point, over random pairs and every pair of 8-torsion offsets with equal,
+    opposite, doubled and random prime-order parts (tools/ded_check.py); random pairs never flag."""
+    import ded_check
+
+    stats, random_flags = ded_check.run(seed=2, nrand=32)
+    assert stats["wrong"] == 0 and random_flags == 0
+    assert stats["Z=0"] > 0  # the exceptional cases exist and are caught
+
+
+def test_tight_zero_representations():
+    """fe_tight_zero's rule on fe_mul / fe_sq outputs: with limbs bounded as tools/fe_bounds.py
+    derives (limbs 1 and 5 below 2 * 2^25 - 1, the rest in their widths), 0 and p have one
+    representation each (all zero / p's canonical limbs)."""
+    W = F.W
+    p_limbs = [(2**255 - 19 >> sum(W[:i])) & ((1 << W[i]) - 1) for i in range(10)]
+    assert p_limbs == [0x3ffffed] + [(1 << W[i]) - 1 for i in range(1, 10)]
+    # a representation of p (or 0) other than the canonical one needs some limb to hold at least
+    # one extra unit of its width: limb i >= 2^W[i] + canonical -- beyond every derived bound
+    z = F.fe_mul([F.MASK[i] for i in range(10)], [F.MASK[i] for i in range(10)], "x")
+    for i in range(10):
+        assert z[i] < (1 << W[i]) + p_limbs[i] if i in (1, 5) else z[i] <= F.MASK[i]

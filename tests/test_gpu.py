@@ -782,6 +782,47 @@ def test_stepping_modes_goldens(be, golden, name, mode):
         be.set_split(0)
 
 
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json"])
+def test_stepping_formulas_goldens(be, golden, name):
+    """The stepping's dedicated additions (default; workgroups that met an exceptional pair redone by
+    the complete formula) and the complete formula alone give every output bit-exact, unsplit and
+    split into 2..4 pieces.  An E row made the identity (committee.rs:1127) makes every addition of
+    its tables exceptional: the redo path runs; honest tables never need it."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    try:
+        for pieces in sorted({1, 2, min(3, t + 1), min(4, t + 1)}):
+            be.set_split(pieces)
+            redos = []
+            for formula in (0, 1):
+                be.set_stepping_formula(formula)
+                r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+                _check_ceremony(c, r, n)
+                redos.append(be.stepping_redos())
+            assert redos[1] == 0
+            if name.startswith("fault_e_identity"):
+                assert redos[0] > 0, "the identity row must take the complete-formula redo"
+            elif name.startswith("ceremony_"):  # n = 64: no identity padding columns either
+                assert redos[0] == 0, "an honest ceremony needs no redo"
+        if name.startswith("ceremony_"):
+            # dealer 5's E row made the identity (committee.rs:1127) in a table without padding:
+            # both formulas agree, and only the dedicated one needed the redo
+            E = bytearray(H(c["E"]))
+            E[5 * (t + 1) * 32:6 * (t + 1) * 32] = bytes(32 * (t + 1))
+            be.set_split(0)
+            out = []
+            for formula in (0, 1):
+                be.set_stepping_formula(formula)
+                r = be.ceremony_verify(bytes(E), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+                out.append((r.dec2, r.dec4, r.qualified, r.mpk, be.stepping_redos()))
+            assert out[0][:4] == out[1][:4] and out[0][4] > 0 and out[1][4] == 0
+            assert r.dec2[5 * n:6 * n].count(0) == n - 1  # every other receiver complains about dealer 5
+    finally:
+        be.set_stepping_formula(0)
+        be.set_split(0)
+
+
 @pytest.mark.parametrize("mode,addends", [(1, 0), (2, 0), (2, 1)])
 @pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json"])
 def test_combine_modes_goldens(be, golden, name, mode, addends):

@@ -21,6 +21,11 @@ PRIMS = {
                       "ge_add_signed(p, p, q, ng); ng = !ng;", "STP(p);"),
     "ge_dbl_t": ("ge_p3 p; LDP(p, 0);", "ge_dbl_rt(p, p, true);", "STP(p);"),
     "ge_dbl_not": ("ge_p3 p; LDP(p, 0);", "ge_dbl_rt(p, p, false);", "STP(p);"),
+    "ge_add_ded": ("ge_p3 p; LDP(p, 0);", "ge_add_ded_lds(p, p, o + 2560 + threadIdx.x, 64);", "STP(p);"),
+    "ge_to_cached_ded": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached_ded(q, p); p.X = q.T2d; p.Y = q.YpX;",
+                         "STP(p);"),
+    "fe_tight_zero": ("fe a; LD10(a.v, 0); uint32_t acc = 0;", "acc += fe_tight_zero(a) ? 1u : 0u; a.v[0] ^= acc;",
+                      "ST10(a.v);"),
     "ge_madd_signed": ("ge_p3 p; ge_aff q; LDP(p, 0); LD10(q.ypx.v, 3000); LD10(q.ymx.v, 3640); LD10(q.xy2d.v, 4280); "
                        "bool ng = o[9999] & 1;", "ge_madd_signed(p, p, q, ng); ng = !ng;", "STP(p);"),
     "ge_madd": ("ge_p3 p; ge_aff q; LDP(p, 0); LD10(q.ypx.v, 3000); LD10(q.ymx.v, 3640); LD10(q.xy2d.v, 4280);",

@@ -14,7 +14,7 @@ weights) straight from the header text, so the checker cannot drift from the cod
   * fe_tobytes32's canonical reduction sees a value below 2p (one conditional subtraction suffices).
 The group formulas (ge_to_cached, ge_add, ge_sub, ge_madd, ge_msub, ge_dbl / _rt / _lean,
 ge_add_signed, ge_add_lds incl. its negated path, ge_madd_signed / ge_madd_lds and the affine
-addends of k_affine_pieces, the comb entry selection of combw_mul_add,
+addends of k_affine_pieces, the stepping's dedicated ge_add_ded_lds (and fe_tight_zero's operand), the comb entry selection of combw_mul_add,
 ristretto_eq, decode / encode) are run on the bounds; point coordinates are iterated to a fixpoint
 (every stored coordinate is again an input), so the invariant "a coordinate is TIGHT" is closed.
 
@@ -371,6 +371,40 @@ def affine_addend(p, where="affine_pieces"):
     return (fe_add(y, x, where), fe_sub(y, x, where), fe_mul(fe_mul(T, zi, where), D2, where))
 
 
+def ge_to_cached_ded(p):
+    X, Y, Z, T = p
+    return (fe_add(Y, X, "to_cached_ded"), fe_sub(Y, X, "to_cached_ded"), fe_add(Z, Z, "to_cached_ded"),
+            fe_add(T, T, "to_cached_ded 2T"))
+
+
+def tight_zero_ok(z, where):
+    """fe25519.h fe_tight_zero: limbs within their widths except 1 and 5, which stay below
+    2 * 2^25 - 1 (so 0 and p each have one representation)."""
+    for i in range(10):
+        lim = (2 * (MASK[i] + 1) - 1) if i in (1, 5) else MASK[i] + 1
+        check(f"{where} fe_tight_zero operand limb {i}", z[i], lim)
+
+
+def ge_add_ded(p, q, where="ge_add_ded_lds"):
+    """points.h ge_add_ded_lds (dedicated addition, q = ge_to_cached_ded): X3 = E F, Y3 = G H,
+    T3 = E H, Z3 = G F with F, H the second operands; Z3 feeds fe_tight_zero."""
+    X, Y, Z, T = p
+    YpX, YmX, Z2, T2 = q
+    t = fe_sub(Y, X, where)
+    a = fe_mul(t, YpX, where)
+    t = fe_add(Y, X, where)
+    b = fe_mul(t, YmX, where)
+    f = fe_sub(b, a, where)
+    g = fe_add(b, a, where)
+    c = fe_mul(Z, T2, where)
+    d = fe_mul(T, Z2, where)
+    e = fe_add(d, c, where)
+    h = fe_sub(d, c, where)
+    z3 = fe_mul(g, f, where)
+    tight_zero_ok(z3, where)
+    return (fe_mul(e, f, where), fe_mul(g, h, where), z3, fe_mul(e, h, where))
+
+
 def comb8_entry(tab_ypx, tab_ymx, tab_xy2d):
     """points.h combw_mul_add: the selected affine entry, incl. identity (1, 1, 0) and -Q =
     (y-x, y+x, 2p - xy2d) -- the negated xy2d is NOT carried."""
@@ -501,7 +535,7 @@ def run():
                 ge_add_signed(pt, c), ge_add_lds(pt, c), ge_add(pt, ge_cached_neg(c), "ge_add(-q)")]
         aff = (fe_carry(fe_add(tight, tight)), fe_carry(fe_sub(tight, tight)), fe_mul(fe_mul(tight, tight), D2))
         outs += [ge_madd(pt, comb8_entry(*aff), "comb8 madd"), ge_madd(pt, aff, "ge_msub", minus=True)]
-        outs += [ge_madd_signed(pt, affine_addend(pt))]
+        outs += [ge_madd_signed(pt, affine_addend(pt)), ge_add_ded(pt, ge_to_cached_ded(pt))]
         outs += [ristretto_decode(), ristretto_elligator()]
         ristretto_encode(pt)
         new = vmax(tight, *[x for o in outs for x in o])
