@@ -69,6 +69,7 @@ def roofline_line(rl, dom, work_text):
 
 
 PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
+AFF_BYTES = 128  # kernels.hip AFFP_WORDS: one affine addend slot
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
@@ -86,8 +87,11 @@ def algorithmic_bytes(kernel, n, t, U, plen=None):
     if kernel == "stepping":  # the table once, then D_0 out per (piece, receiver)
         nblk = -(-Lp0 // 512)
         return cols * (t + 1 + U * n) * PT_BYTES / nblk, nblk
-    if kernel == "combine":  # U piece values in, P(j) out per (column, receiver)
-        return 2 * n * n * (U + 1) * PT_BYTES, 1
+    if kernel == "combine":  # U affine piece values (128-B slots) in, P(j) out per (column, receiver)
+        return 2 * n * n * (U * AFF_BYTES + PT_BYTES), 1
+    if kernel == "affine":  # per stepped value: Z twice (3 x 16 B each), the point, a block prefix
+        # (48 B written and read per 4 points), the 128-B affine slot out
+        return 2 * n * U * n * (2 * 48 + PT_BYTES + 2 * 12 + AFF_BYTES), 1
     return None, None
 
 

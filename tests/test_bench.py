@@ -26,7 +26,7 @@ def test_algorithmic_bytes_stepping_and_combine():
     step, nl = bench.algorithmic_bytes("stepping", n, t, U)
     assert nl == 1 and step == 2 * n * U * (256 + n) * 160  # the table once, D_0 out per receiver
     comb, nl = bench.algorithmic_bytes("combine", n, t, U)
-    assert nl == 1 and comb == 2 * n * n * 3 * 160  # two piece values in, P(j) out
+    assert nl == 1 and comb == 2 * n * n * (2 * 128 + 160)  # two affine piece values in, P(j) out
     assert bench.algorithmic_bytes("check", n, t, U) == (None, None)
 
 

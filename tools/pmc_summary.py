@@ -56,6 +56,13 @@ def main(d):
 
 PHASE = {"k_binom_step": "binomial", "void k_stepping<192>": "stepping", "void k_stepping<256>": "stepping",
          "void k_stepping<512>": "stepping",
+         # dedicated stepping, and its complete-formula redo launches (separate: near-empty when no
+         # workgroup was marked, they would halve the per-launch average)
+         "void k_stepping<192, true>": "stepping", "void k_stepping<256, true>": "stepping",
+         "void k_stepping<512, true>": "stepping", "void k_stepping<192, false>": "stepping_redo",
+         "void k_stepping<256, false>": "stepping_redo", "void k_stepping<512, false>": "stepping_redo",
+         "void k_combine_aff<2, 1>": "combine", "void k_combine_aff<3, 2>": "combine",
+         "void k_combine_aff<4, 2>": "combine", "k_affine_pieces": "affine",
          "void k_combine<1>": "combine", "void k_combine<2>": "combine", "void k_combine_short<2, 1>": "combine",
          "void k_combine_short<3, 2>": "combine", "void k_combine_short<4, 2>": "combine",
          "k_check_both": "check", "k_check": "check"}
