@@ -340,3 +340,37 @@ def test_recombination_modes_agree_on_faults(be, n, t):
     for key, r in runs.items():
         assert r.dec2 == ref.dec2 and r.dec4 == ref.dec4, key
         assert r.qualified == ref.qualified and r.reconstruct == ref.reconstruct and r.mpk == ref.mpk, key
+
+
+@pytest.mark.parametrize("n,t,split", [(1024, 511, 4), (1024, 511, 3), (1100, 549, 1)])
+def test_stepping_redo_at_scale(be, n, t, split):
+    """The stepping's exact fallback at the BASELINE size and in each stepping layout -- whole-column
+    slots (U=4), per-piece tables (U=3: 171-position pieces) and 512-lane blocks chained through
+    boundary streams (n=1100 unsplit: 550 positions): an E row made the identity (committee.rs:1127)
+    makes its dedicated additions exceptional; the marked workgroups are redone by the complete
+    formula, and every output equals the complete formula's run."""
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([split]) * 32, 3, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
+    N = t + 1
+    for d in (3, n - 2):  # dealers in the first and the last stepping workgroups
+        E[32 * d * N:32 * (d + 1) * N] = bytes(32 * N)
+    _bump(s, 32 * (5 * n + 9))  # and an ordinary fault beside them
+    out = []
+    try:
+        be.set_split(split)
+        for formula in (0, 1):
+            be.set_stepping_formula(formula)
+            r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            assert be.last_split() == split
+            out.append((r.dec2, r.dec4, r.qualified, r.reconstruct, r.mpk, r.final_share, be.stepping_redos()))
+    finally:
+        be.set_stepping_formula(0)
+        be.set_split(0)
+    assert out[0][:6] == out[1][:6]
+    assert out[0][6] > 0 and out[1][6] == 0
+    dec2 = out[0][0]
+    for d in (3, n - 2):
+        row = dec2[d * n:(d + 1) * n]
+        assert row.count(REJECT) == n - 1 and row[d] == SELF
+    assert dec2[5 * n + 9] == REJECT and dec2[5 * n:6 * n].count(REJECT) == 1
