@@ -87,6 +87,11 @@ DKG_DEV uint32_t dbl32(uint32_t x) {
   asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
   return r;
 }
+// r = 2a limb by limb with dbl32 (fe_add(r, a, a) compiles to half-rate shifts)
+DKG_DEV void fe_dbl(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = dbl32(a.v[i]);
+}
 
 // One v_mad_u64_u32 (h = a * b + h) the compiler cannot reassociate.  The products are summed
 // column by column ("product scanning") and each column's chain STARTS from the carry out of the

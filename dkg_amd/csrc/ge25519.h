@@ -58,7 +58,7 @@ DKG_DEV void ge_to_cached(ge_cached& c, const ge_p3& p) {
   // ever the second (x19) operand of fe_mul, which takes them (tools/fe_bounds.py)
   fe_add(c.YpX, p.Y, p.X);
   fe_sub(c.YmX, p.Y, p.X);
-  fe_add(c.Z2, p.Z, p.Z);
+  fe_dbl(c.Z2, p.Z);
   fe d2;
   fe_ld(d2, ge_const::D2);
   fe_mul(c.T2d, p.T, d2);
@@ -122,7 +122,7 @@ DKG_DEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_aff& q) {
   fe_sub(e, b, a);
   fe_add(h, b, a);
   fe_mul(a, p.T, q.xy2d);   // c
-  fe_add(b, p.Z, p.Z);      // d <= 2^27
+  fe_dbl(b, p.Z);           // d <= 2^27
   fe_sub(t, b, a);          // f = d - c <= 2^27 + 2^27
   fe_add(b, b, a);          // g = d + c <= 1.5*2^27
   fe_mul(r.X, t, e);        // f <= 2^28 as first operand
@@ -140,7 +140,7 @@ DKG_DEV void ge_msub(ge_p3& r, const ge_p3& p, const ge_aff& q) {
   fe_sub(e, b, a);
   fe_add(h, b, a);
   fe_mul(a, p.T, q.xy2d);   // c
-  fe_add(b, p.Z, p.Z);      // d
+  fe_dbl(b, p.Z);           // d
   fe_add(t, b, a);          // f = d + c <= 1.5*2^27
   fe_sub(b, b, a);          // g = d - c <= 2^28
   fe_mul(r.X, e, t);        // x19 operands F (X, Z) and H (Y, T), computed once each
@@ -156,7 +156,7 @@ DKG_DEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe_sq(a, p.X);
   fe_sq(b, p.Y);
   fe_sq(c, p.Z);
-  fe_add(c, c, c);          // <= 2^27
+  fe_dbl(c, c);             // <= 2^27
   fe_add(t, p.X, p.Y);      // <= 2^27
   fe_sq(t, t);
   fe_add(h, a, b);          // <= 2^27             (= -H_std)
@@ -176,7 +176,7 @@ DKG_DEV void ge_dbl_rt(ge_p3& r, const ge_p3& p, bool with_t) {
   fe_sq(a, p.X);
   fe_sq(b, p.Y);
   fe_sq(c, p.Z);
-  fe_add(c, c, c);          // <= 2^27
+  fe_dbl(c, c);             // <= 2^27
   fe_add(t, p.X, p.Y);      // <= 2^27
   fe_sq(t, t);              // (X+Y)^2
   fe_add(h, a, b);          // <= 2^27             (= -H_std)
@@ -198,7 +198,7 @@ DKG_DEV void ge_dbl_lean(ge_p3& r, const ge_p3& p, bool with_t) {
   fe_add(h, a, b);          // <= 2^27             (= -H_std)
   fe_sub(g, a, b);          // <= 1.5*2^27         (= -G_std)
   fe_sq(t, p.Z);
-  fe_add(t, t, t);          // 2Z^2 <= 2^27
+  fe_dbl(t, t);             // 2Z^2 <= 2^27
   fe_add(t, t, g);          // <= 2.5*2^27
   fe_carry(t, t);           // f, tight            (= -F_std)
   fe_add(a, p.X, p.Y);      // <= 2^27
@@ -260,7 +260,7 @@ DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg)
   fe na;
   fe_neg(na, a);            // -c = 2p - c <= 2p limbwise
   fe_cmov(a, na, neg);      // a = +/-c
-  fe_add(b, p.Z, p.Z);
+  fe_dbl(b, p.Z);
   fe_carry(b, b);           // d = 2Z, tight
   fe_sub(t, b, a);          // f = d - (+/-c)
   fe_add(b, b, a);          // g = d + (+/-c)

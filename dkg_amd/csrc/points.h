@@ -250,8 +250,8 @@ DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
 DKG_DEV void ge_to_cached_ded(ge_cached& c, const ge_p3& p) {
   fe_add(c.YpX, p.Y, p.X);
   fe_sub(c.YmX, p.Y, p.X);
-  fe_add(c.Z2, p.Z, p.Z);
-  fe_add(c.T2d, p.T, p.T);  // 2T in the 2dT slot
+  fe_dbl(c.Z2, p.Z);
+  fe_dbl(c.T2d, p.T);       // 2T in the 2dT slot
 }
 DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int stride = 64) {
   fe a, b, e, h, t, qv;
@@ -290,7 +290,7 @@ DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, 
   lds_get_fe(qv, q, 2, stride);
   fe_mul(a, p.T, qv);       // c
   if (neg) fe_neg(a, a);    // 2p - c <= 2p limbwise
-  fe_add(b, p.Z, p.Z);
+  fe_dbl(b, p.Z);
   fe_carry(b, b);           // d = 2Z, tight
   fe_sub(t, b, a);          // f
   fe_add(b, b, a);          // g
