@@ -40,10 +40,9 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 #   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
 VALU = {"fe_mul": (140, 256), "fe_sq": (109, 185), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200),
-        "ge_madd_signed": (1130, 2002), "ge_add_ded": (1198, 2180), "ge_to_cached_ded": (73, 95),
-        "fe_tight_zero": (16, 31), "ge_dbl_t": (1057, 1864),
-        "ge_dbl_not": (929, 1620), "comb_window": (1181, 2084), "combw_window": (1171, 2047),
-        "ge_to_cached": (143, 259), "eq": (633, 1151), "sc_mont_mul": (580, 834)}
+        "ge_madd_signed": (1130, 1992), "ge_add_ded": (1198, 2180), "ge_to_cached_ded": (70, 70),
+        "fe_tight_zero": (16, 31), "ge_dbl_t": (1058, 1855), "ge_dbl_not": (930, 1611), "comb_window": (1181, 2074),
+        "combw_window": (1171, 2037), "ge_to_cached": (193, 309), "eq": (633, 1151), "sc_mont_mul": (580, 834)}
 INSTR = {k: v[0] for k, v in VALU.items()}
 COMBW_WINDOWS = 26  # points.h: radix-2^10 fixed-base comb, one mixed addition per window
 SLOTS = {k: v[1] for k, v in VALU.items()}

@@ -22,7 +22,8 @@ PRIMS = {
     "ge_dbl_t": ("ge_p3 p; LDP(p, 0);", "ge_dbl_rt(p, p, true);", "STP(p);"),
     "ge_dbl_not": ("ge_p3 p; LDP(p, 0);", "ge_dbl_rt(p, p, false);", "STP(p);"),
     "ge_add_ded": ("ge_p3 p; LDP(p, 0);", "ge_add_ded_lds(p, p, o + 2560 + threadIdx.x, 64);", "STP(p);"),
-    "ge_to_cached_ded": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached_ded(q, p); p.X = q.T2d; p.Y = q.YpX;",
+    "ge_to_cached_ded": ("ge_p3 p; ge_cached q; LDP(p, 0);",
+                         "ge_to_cached_ded(q, p); p.X = q.T2d; p.Y = q.YpX; p.Z = q.Z2; p.T = q.YmX;",
                          "STP(p);"),
     "fe_tight_zero": ("fe a; LD10(a.v, 0); uint32_t acc = 0;", "acc += fe_tight_zero(a) ? 1u : 0u; a.v[0] ^= acc;",
                       "ST10(a.v);"),
@@ -39,7 +40,8 @@ PRIMS = {
     "sc_mont_mul": ("sc x, f; for (int i_ = 0; i_ < 8; i_++) { x.v[i_] = o[9000 + i_ * 64 + threadIdx.x]; "
                     "f.v[i_] = o[9600 + i_ * 64 + threadIdx.x]; }",
                     "sc_mont_mul(x, x, f);", "for (int i_ = 0; i_ < 8; i_++) o[i_ * 64 + threadIdx.x] = x.v[i_];"),
-    "ge_to_cached": ("ge_p3 p; ge_cached q; LDP(p, 0);", "ge_to_cached(q, p); p.X = q.T2d; p.Y = q.YpX;",
+    "ge_to_cached": ("ge_p3 p; ge_cached q; LDP(p, 0);",
+                     "ge_to_cached(q, p); p.X = q.T2d; p.Y = q.YpX; p.Z = q.Z2; p.T = q.YmX;",
                      "STP(p);"),
 }
 HDR = r'''
