@@ -923,6 +923,15 @@ DKG_DEV void st_fe3(uint32_t* slot, const fe& a, const fe& b, const fe& c) {
   s[7] = make_uint4(c.v[8], c.v[9], 0u, 0u);
 }
 
+// f(K-1), f(K-2), .., f(0) with compile-time arguments
+template <int K, typename F>
+DKG_DEV void for_desc(F&& f) {
+  if constexpr (K > 0) {
+    f(std::integral_constant<int, K - 1>{});
+    for_desc<K - 1>(f);
+  }
+}
+
 DKG_DEV void ld_z(fe& z, const uint32_t* R, size_t e) {  // Z of point e (words 20..29)
   const uint4* p4 = reinterpret_cast<const uint4*>(R + e * PT_WORDS);
   const uint4 z0 = p4[5], z1 = p4[6], z2 = p4[7];
@@ -967,6 +976,7 @@ __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstr
 #pragma unroll 1
   for (int b = nblk - 1; b >= 0; b--) {
     fe z[AFF_BLK], q[AFF_BLK];  // q[k] = z[0] .. z[k-1] (q[0] = 1 is never formed)
+    static_assert(AFF_BLK >= 2, "q[1] = z[0] below");
 #pragma unroll
     for (int k = 0; k < AFF_BLK; k++) {
       if (AFF_BLK * b + k < cnt) ld_z(z[k], R, pt(AFF_BLK * b + k));
@@ -1008,11 +1018,7 @@ __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstr
         st_fe3(A + pt(i) * AFFP_WORDS, p.X, p.Y, p.T);
       }
     };
-    static_assert(AFF_BLK == 4, "point() is spelled out for blocks of 4");
-    point(std::integral_constant<int, 3>{});
-    point(std::integral_constant<int, 2>{});
-    point(std::integral_constant<int, 1>{});
-    point(std::integral_constant<int, 0>{});
+    for_desc<AFF_BLK>(point);
   }
 }
 
