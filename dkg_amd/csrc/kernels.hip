@@ -55,26 +55,38 @@ __global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ com
 // Same placement as k_decode's position-major mode for points that are already in extended form
 // (round-1 commitments generated on this device: the reference's broadcasts carry group elements,
 // not encodings, so nothing is decoded).  src: [D][N] points, word stride sstride.
-__global__ __launch_bounds__(256) void k_place_pm(const uint32_t* __restrict__ src, size_t sstride, size_t count,
-                                                  uint32_t* __restrict__ out, size_t N, size_t npad, uint32_t nseg,
+// [D][N] dealer-major extended points -> the position-major table, one word (blockIdx.z) of a
+// 64-dealer x 64-coefficient tile per workgroup through LDS: the reads run along a dealer's
+// coefficients, the writes along 64 consecutive table columns (straight per-element placement wrote
+// one 4-B word per lane npad words apart: 0.33 ms per 1024 x 512 segment).
+__global__ __launch_bounds__(256) void k_place_pm(const uint32_t* __restrict__ src, size_t sstride, size_t D,
+                                                  size_t N, uint32_t* __restrict__ out, size_t npad, uint32_t nseg,
                                                   uint32_t seg, size_t L, size_t pstride) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= count) return;
-  const size_t i = e / N, k = e % N;
+  __shared__ uint32_t tile[64][65];
+  const size_t w = blockIdx.z, k0 = (size_t)blockIdx.x * 64, i0 = (size_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const size_t i = i0 + ty + 4 * r, k = k0 + tx;
+    if (i < D && k < N) tile[ty + 4 * r][tx] = src[w * sstride + i * N + k];
+  }
+  __syncthreads();
+  const size_t i = i0 + tx;
   const size_t col = (i / 64) * 64 * nseg + seg * 64 + i % 64;
-  const size_t idx = (k % L) * npad + (k / L) * pstride + col;
-  const size_t ostride = L * npad;
-#pragma unroll 8
-  for (int w = 0; w < PT_WORDS; w++) out[w * ostride + idx] = src[w * sstride + e];
+  uint32_t* o = out + w * L * npad + col;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const size_t k = k0 + ty + 4 * r;
+    if (i < D && k < N) o[(k % L) * npad + (k / L) * pstride] = tile[tx][ty + 4 * r];
+  }
 }
 
 void place_position_major(const uint32_t* src, size_t sstride, size_t D, size_t N, size_t npad, uint32_t* out,
                           hipStream_t stream, int nseg, int seg, size_t L, size_t pstride) {
-  const size_t count = D * N;
-  if (!count) return;
+  if (!D || !N) return;
   if (!L) L = N;
-  hipLaunchKernelGGL(k_place_pm, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, src, sstride, count, out,
-                     N, npad, (uint32_t)nseg, (uint32_t)seg, L, pstride);
+  hipLaunchKernelGGL(k_place_pm, dim3((unsigned)((N + 63) / 64), (unsigned)((D + 63) / 64), (unsigned)PT_WORDS),
+                     dim3(256), 0, stream, src, sstride, D, N, out, npad, (uint32_t)nseg, (uint32_t)seg, L, pstride);
 }
 
 // dst[i] = src[i * step + k0] for i < count (extended points; word strides sstride / dstride)
