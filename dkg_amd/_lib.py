@@ -5,6 +5,7 @@ or no GPU is visible, the calls below raise instead of silently computing someth
 """
 import ctypes
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DKG_AMD_LIB", os.path.join(HERE, "libdkg_amd.so"))
@@ -63,6 +64,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C dkg_amd` or __graft_entry__.build()")
+    # When torch shares the process, its HIP runtime must be the one the dynamic loader binds
+    # first: loading libdkg_amd.so (linked against /opt/rocm's libamdhip64) before torch leaves
+    # torch.cuda without a device.  Import torch first whenever it is importable.
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     sz, p, u8p = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
     L.dkg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(p)]

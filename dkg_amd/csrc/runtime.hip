@@ -1985,10 +1985,14 @@ int dkg_finalise_parties(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* qualif
     }
     const std::vector<uint8_t> fin = final_parties(n, qualified, reconstruct);
     const bool phase4 = nq - (int32_t)recon.size() <= (int32_t)t;  // committee.rs:673-677
-    // S: final parties whose phase-5 disclosures the finalising party fetched (committee.rs:763-775)
+    // S: final parties whose phase-5 disclosures the finalising party fetched (committee.rs:763-775).
+    // A party whose Phase1 or Phase3 proceed failed never reaches Phase4::proceed and so never
+    // broadcasts a BroadcastPhase5 (:340-347, :567-569, :684), whatever `disclosed` says.
     std::vector<uint8_t> S(n);
     size_t nS = 0;
-    for (size_t j = 0; j < n; j++) nS += S[j] = fin[j] && (!disclosed || disclosed[j]);
+    for (size_t j = 0; j < n; j++)
+      nS += S[j] = fin[j] && (!disclosed || disclosed[j]) && !(r2_error && r2_error[j]) &&
+                   !(r4_error && r4_error[j]);
     const Zl zero = zl_from_u64(0), one = zl_from_u64(1);
     std::vector<Zl> lamS, yrows;  // Lagrange coefficients over S; the reconstructed rows' shares
     if (!recon.empty() && !phase4) {

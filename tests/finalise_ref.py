@@ -58,7 +58,9 @@ def party_finalise(p, n, t, qualified, recon, A0, share, own_A0=None, disclosed=
         if recon[i] and qualified[i]:
             xs, ys = [p + 1], [share(i, p)]                   # own index and share (:754-761)
             for q in range(n):
-                if q != p and disclosed[q] and final[q]:      # :763-775
+                # :763-775; a party that failed Phase1/Phase3 never broadcasts phase 5 (:684)
+                if (q != p and disclosed[q] and final[q] and not (r2_error and r2_error[q])
+                        and not (r4_error and r4_error[q])):
                     xs.append(q + 1)
                     ys.append(share(i, q))
             if len(xs) < t:                                   # :779-781 (threshold, not t + 1)

@@ -285,7 +285,9 @@ def finalise_party(p, n, t, st, disclosed, r2_error=None, r4_error=None):
         if rec[i] and q[i]:
             xs, ys = [p + 1], [st["Sw"][i][p]]                # own index and share (:754-761)
             for s_ in range(n):
-                if s_ != p and disclosed[s_] and final[s_]:   # :763-775
+                # :763-775; a party whose Phase1/Phase3 proceed failed never broadcasts phase 5
+                if (s_ != p and disclosed[s_] and final[s_] and not (r2_error and r2_error[s_])
+                        and not (r4_error and r4_error[s_])):
                     xs.append(s_ + 1)
                     ys.append(st["Sw"][i][s_])
             if len(xs) < t:                                   # :779-781 (threshold, not t + 1)
@@ -762,7 +764,13 @@ def main():
         {"name": "all disclose"},
         {"name": "t points", "disclosed": [1 if j in (0, 1, 3, 4) else 0 for j in range(n10)]},
         {"name": "t-1 points", "disclosed": [1 if j in (0, 1, 4) else 0 for j in range(n10)]},
-        {"name": "one missing", "disclosed": [0 if j == 5 else 1 for j in range(n10)]}])}
+        {"name": "one missing", "disclosed": [0 if j == 5 else 1 for j in range(n10)]},
+        # four final parties stop at Phase3 (r4_error) and never disclose: the others are left with
+        # exactly t points although every disclosure flag is set (a wrong secret, as the reference)
+        {"name": "r4 errors leave t points", "r4_error": [1 if j in (0, 1, 3, 4) else 0 for j in range(n10)]},
+        {"name": "r2 and r4 errors leave t-1 points",
+         "r2_error": [1 if j in (0, 1) else 0 for j in range(n10)],
+         "r4_error": [1 if j in (3, 4, 5) else 0 for j in range(n10)]}])}
     files["spot_n4096_t2047.json"] = spot(4096, 2047, m, [5, 3000], [0, 1500, 4095])
     for obj in files.values():
         obj.pop("_state", None)
