@@ -45,6 +45,14 @@ class CeremonyOut(ctypes.Structure):
     ]
 
 
+class ShardOutcome(ctypes.Structure):
+    _fields_ = [
+        ("qualified", ctypes.c_void_p), ("complaints2", ctypes.c_void_p), ("r2_error", ctypes.c_void_p),
+        ("reconstruct", ctypes.c_void_p), ("r4_error", ctypes.c_void_p),
+        ("n_qualified", ctypes.c_int32), ("phase4_error", ctypes.c_int32),
+    ]
+
+
 class BatchOut(ctypes.Structure):
     _fields_ = [
         ("mpk", ctypes.c_void_p), ("n_qualified", ctypes.c_void_p), ("phase4_error", ctypes.c_void_p),
@@ -139,6 +147,12 @@ def lib():
     L.dkg_share_gen_device.argtypes = [p, sz, sz, sz, p, p, p, p, p, p]
     L.dkg_ceremony_shard_recon_device.argtypes = [p, sz, sz, sz, sz, u8p, u8p, p, p]
     L.dkg_finalise_parties.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, u8p, u8p, u8p, p, p, p]
+    L.dkg_shard_range.argtypes = [sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    L.dkg_shard_range.restype = None
+    L.dkg_shard_rows.argtypes = [sz, sz]
+    L.dkg_shard_rows.restype = sz
+    L.dkg_shard_combine_device.argtypes = [p, sz, sz, sz, p, p, p, p, ctypes.POINTER(ShardOutcome)]
+    L.dkg_shard_finalise_device.argtypes = [p, sz, sz, sz, p, p, u8p, ctypes.c_int, p, p, p]
     _lib = L
     return L
 
@@ -156,5 +170,6 @@ EXPORTED = [
     "dkg_enc_randomness_device", "dkg_encrypt_shares", "dkg_decrypt_shares", "dkg_ceremony_run_full_device",
     "dkg_ceremony_verify_full", "dkg_misbehaviour_prove", "dkg_complaint1_verify", "dkg_complaint3_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
     "dkg_scalar_sum_device", "dkg_point_sum_device", "dkg_ceremony_shard_recon_device", "dkg_finalise_parties",
-    "dkg_share_gen_device",
+    "dkg_share_gen_device", "dkg_shard_range", "dkg_shard_rows", "dkg_shard_combine_device",
+    "dkg_shard_finalise_device",
 ]

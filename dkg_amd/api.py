@@ -432,6 +432,33 @@ class Backend:
             A0, s, mpk, st, ri))
         return PartyFinalise([mpk.raw[32 * p:32 * p + 32] for p in range(n)], list(st)[:n], list(ri)[:n])
 
+    def shard_combine_device(self, n: int, t: int, world_size: int, d_dec2_g: int, d_dec4_g: int,
+                             d_dec2: Optional[int] = None, d_dec4: Optional[int] = None) -> "ShardOutcome":
+        """Combine step of the sharded run (dkg_shard_combine_device): the common round-2/4 outcome
+        from the all-gathered [ws][R][n] decision blocks (device pointers); d_dec2 / d_dec4 optionally
+        receive the compacted [n][n] matrices (dec4 with SKIPPED rows)."""
+        q, r2e, rc, r4e = (ctypes.create_string_buffer(max(n, 1)) for _ in range(4))
+        c = (ctypes.c_int32 * max(n, 1))()
+        o = _lib.ShardOutcome(ctypes.cast(q, ctypes.c_void_p), ctypes.cast(c, ctypes.c_void_p),
+                              ctypes.cast(r2e, ctypes.c_void_p), ctypes.cast(rc, ctypes.c_void_p),
+                              ctypes.cast(r4e, ctypes.c_void_p), 0, 0)
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_shard_combine_device(self._ctx, n, t, world_size, vp(d_dec2_g), vp(d_dec4_g),
+                                                               vp(d_dec2), vp(d_dec4), ctypes.byref(o)))
+        return ShardOutcome(list(q.raw[:n]), list(c)[:n], list(r2e.raw[:n]), list(rc.raw[:n]), list(r4e.raw[:n]),
+                            o.n_qualified, bool(o.phase4_error))
+
+    def shard_finalise_device(self, n: int, t: int, world_size: int, d_terms_g: int, d_partials_g: int, qualified,
+                              phase4_error: bool, d_final_share: int, d_public_share: Optional[int] = None) -> bytes:
+        """Finalise of the sharded run (dkg_shard_finalise_device): final shares (and public shares)
+        into device buffers; returns the mpk (zero when phase4_error)."""
+        mpk = ctypes.create_string_buffer(32)
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_shard_finalise_device(
+            self._ctx, n, t, world_size, vp(d_terms_g), vp(d_partials_g), bytes(bytearray(qualified)),
+            int(bool(phase4_error)), vp(d_final_share), vp(d_public_share), mpk))
+        return mpk.raw
+
     def scalar_sum_device(self, rows: int, n: int, d_in: int, d_mask: Optional[int], d_out: int):
         """out[j] = sum over rows r with mask[r] of in[r][j] mod l (device pointers)."""
         vp = ctypes.c_void_p
@@ -441,6 +468,30 @@ class Backend:
         """out = sum of the compressed points[c] with mask[c] (device pointers)."""
         vp = ctypes.c_void_p
         _check(self._ctx, _lib.lib().dkg_point_sum_device(self._ctx, count, vp(d_points), vp(d_mask), vp(d_out)))
+
+
+@dataclass
+class ShardOutcome:
+    """The common outcome of a sharded ceremony (dkg_shard_combine_device), identical on every rank."""
+    qualified: List[int]
+    complaints2: List[int]
+    r2_error: List[int]
+    reconstruct: List[int]
+    r4_error: List[int]
+    n_qualified: int
+    phase4_error: bool
+
+
+def shard_range(n: int, world_size: int, rank: int):
+    """Dealers [d0, d1) of `rank` (dkg_shard_range: contiguous, sizes differ by at most one)."""
+    d0, d1 = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.lib().dkg_shard_range(n, world_size, rank, ctypes.byref(d0), ctypes.byref(d1))
+    return d0.value, d1.value
+
+
+def shard_rows(n: int, world_size: int) -> int:
+    """Padded per-rank block height R of the all-gathers (dkg_shard_rows)."""
+    return _lib.lib().dkg_shard_rows(n, world_size)
 
 
 @dataclass

@@ -1647,6 +1647,56 @@ void r4_error(size_t groups, size_t n, size_t t, const uint8_t* dec, const uint8
                      dec, qmask, out);
 }
 
+// Round 4 skips the dealers round 2 disqualified (committee.rs:522): row i of a group whose
+// dealer is not qualified becomes SKIPPED except its SELF diagonal.  One wave per row.
+__global__ __launch_bounds__(256) void k_apply_skipped(size_t rows, size_t n, uint8_t* __restrict__ dec,
+                                                       const uint8_t* __restrict__ qmask) {
+  const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows || qmask[i]) return;  // wave-uniform
+  const size_t self = i % n;
+  for (size_t j = threadIdx.x & 63; j < n; j += 64)
+    if (j != self) dec[i * n + j] = 3;  // DKG_SKIPPED
+}
+
+void apply_skipped(size_t groups, size_t n, uint8_t* dec, const uint8_t* qmask, hipStream_t stream) {
+  const size_t rows = groups * n;
+  if (!rows) return;
+  hipLaunchKernelGGL(k_apply_skipped, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, rows, n, dec, qmask);
+}
+
+// Compaction of all-gathered per-rank blocks: rank r's block sits at in + r * R * width and holds
+// d1(r) - d0(r) valid rows of `width` bytes (dealer partition [r * n / ws, (r + 1) * n / ws));
+// out is the dense [n][width] matrix.  One thread per element of T (16, 4 or 1 bytes).
+template <typename T>
+__global__ __launch_bounds__(256) void k_compact_ranks(size_t n, size_t ws, size_t R, size_t q,
+                                                       const T* __restrict__ in, T* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * q) return;
+  const size_t i = e / q, w = e % q;
+  size_t r = (i * ws) / n;  // the rank owning row i: the largest r with r * n / ws <= i
+  while (r + 1 < ws && ((r + 1) * n) / ws <= i) r++;
+  while (r > 0 && (r * n) / ws > i) r--;
+  out[e] = in[(r * R + (i - (r * n) / ws)) * q + w];
+}
+
+void compact_ranks(size_t n, size_t ws, size_t R, size_t width, const void* in, void* out, hipStream_t stream) {
+  if (!n || !width) return;
+  const uintptr_t al = (uintptr_t)in | (uintptr_t)out | width;
+  if (al % 16 == 0) {
+    const size_t q = width / 16, total = n * q;
+    hipLaunchKernelGGL(k_compact_ranks<uint4>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, n, ws, R,
+                       q, (const uint4*)in, (uint4*)out);
+  } else if (al % 4 == 0) {
+    const size_t q = width / 4, total = n * q;
+    hipLaunchKernelGGL(k_compact_ranks<uint32_t>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, n, ws,
+                       R, q, (const uint32_t*)in, (uint32_t*)out);
+  } else {
+    const size_t total = n * width;
+    hipLaunchKernelGGL(k_compact_ranks<uint8_t>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, n, ws,
+                       R, width, (const uint8_t*)in, (uint8_t*)out);
+  }
+}
+
 void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
                       hipStream_t stream) {
   const size_t rows = groups * n;

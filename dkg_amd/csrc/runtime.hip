@@ -872,6 +872,48 @@ std::vector<uint8_t> recon_secrets(size_t n, const std::vector<uint8_t>& fin, co
   return secrets;
 }
 
+// Round-2 outcome of `groups` stacked ceremonies of n parties from the decision matrix
+// dec2 [groups*n][n] on the device, as every party derives it (committee.rs:311-347, 370-398): a
+// REJECT by receiver j is a complaint of j against dealer i, and a valid complaint disqualifies i for
+// everyone; MISSING (no decodable broadcast) disqualifies without a complaint (:331-335); more than t
+// complaints raise MisbehaviourHigherThreshold for j (:340-347).  Host outputs [groups*n]; qmask
+// (device [groups*n]) receives the qualified set.  The single-GPU drivers, the batches and the
+// sharded combine all decide through this function.
+void round2_outcome(dkg_ctx* ctx, size_t groups, size_t n, size_t t, const uint8_t* dec2, uint8_t* qmask,
+                    uint8_t* qualified, int32_t* complaints, uint8_t* r2err) {
+  const size_t V = groups * n;
+  uint8_t* rej = buf<uint8_t>(ctx, "o.rej2", V);
+  int32_t* cnt = buf<int32_t>(ctx, "o.cnt", 4 * V);
+  dkgk::decision_summary(groups, n, dec2, rej, cnt, ctx->stream);
+  d2h(ctx, qualified, rej, V);
+  d2h(ctx, complaints, cnt, 4 * V);
+  sync(ctx);
+  for (size_t i = 0; i < V; i++) {
+    qualified[i] = !qualified[i];
+    r2err[i] = complaints[i] > (int32_t)t;
+  }
+  h2d(ctx, qmask, qualified, V);
+}
+
+// Round-4 outcome (committee.rs:515-522, 567-569, 660-670) from dec4 [groups*n][n] on the device and
+// the round-2 qualified set (host `qualified`, device `qmask`): the rows of disqualified dealers
+// become SKIPPED in place (:522); a qualified dealer some receiver rejects is reconstructed; receiver
+// j's round-4 error (r4err, may be NULL) counts itself and the qualified dealers it accepted.
+void round4_outcome(dkg_ctx* ctx, size_t groups, size_t n, size_t t, uint8_t* dec4, const uint8_t* qmask,
+                    const uint8_t* qualified, uint8_t* recon, uint8_t* r4err) {
+  const size_t V = groups * n;
+  uint8_t* rej = buf<uint8_t>(ctx, "o.rej4", V);
+  uint8_t* r4d = buf<uint8_t>(ctx, "o.r4err", V);
+  dkgk::decision_summary(groups, n, dec4, rej, nullptr, ctx->stream);
+  if (r4err) dkgk::r4_error(groups, n, t, dec4, qmask, r4d, ctx->stream);
+  dkgk::apply_skipped(groups, n, dec4, qmask, ctx->stream);
+  check_launch(ctx);
+  d2h(ctx, recon, rej, V);
+  if (r4err) d2h(ctx, r4err, r4d, V);
+  sync(ctx);
+  for (size_t i = 0; i < V; i++) recon[i] = qualified[i] && recon[i];
+}
+
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
 void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
                       const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
@@ -880,27 +922,15 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
   // ---- rounds 2 and 4 (committee.rs:260-366, :508-580), fused or in protocol order (verify_rounds)
-  std::vector<uint8_t> h4(copy_big && out->dec4 ? n * n : 0);
   std::vector<uint8_t> qualified(n, 1), r2err(n, 0);
   std::vector<int32_t> complaints(n, 0);
   uint32_t* fs = buf<uint32_t>(ctx, "final_share", 32 * n);
   uint32_t* pubc = buf<uint32_t>(ctx, "pub_comp", 32 * n);
-  uint8_t* rej = buf<uint8_t>(ctx, "rej", n);
-  int32_t* cnt = buf<int32_t>(ctx, "cnt", 4 * n);
   uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
   auto round3 = [&] {
     wait_shares(ctx, ctx->stream);
-    // on the device: rows with a REJECT (a valid complaint disqualifies dealer i for everyone,
-    // committee.rs:311-316, 370-398) or MISSING (no decodable broadcast: disqualified without a
-    // complaint, :331-335), and the REJECTs of each receiver's column (its complaints)
-    dkgk::decision_summary(1, n, dec2, rej, cnt, ctx->stream);
-    d2h(ctx, qualified.data(), rej, n);
-    d2h(ctx, complaints.data(), cnt, 4 * n);
-    sync(ctx);
-    for (size_t i = 0; i < n; i++) qualified[i] = !qualified[i];
-    for (size_t j = 0; j < n; j++) r2err[j] = complaints[j] > (int32_t)t;  // :340-347
+    round2_outcome(ctx, 1, n, t, dec2, qmask, qualified.data(), complaints.data(), r2err.data());
     // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
-    h2d(ctx, qmask, qualified.data(), n);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
     // the public shares g s_j are an output only: computed on the side stream, off the path to
     // round 4 and finalise (joined before the outputs are read)
@@ -919,14 +949,8 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   // (committee.rs:660-670); receiver j's round-4 error (:515-516, 567-569) counts itself and the
   // qualified dealers it accepted
   std::vector<uint8_t> recon(n, 0), r4e(n, 0);
-  uint8_t* r4ed = buf<uint8_t>(ctx, "r4err", n);
-  dkgk::decision_summary(1, n, dec4, rej, nullptr, ctx->stream);
-  dkgk::r4_error(1, n, t, dec4, qmask, r4ed, ctx->stream);
-  d2h(ctx, recon.data(), rej, n);
-  d2h(ctx, r4e.data(), r4ed, n);
+  round4_outcome(ctx, 1, n, t, dec4, qmask, qualified.data(), recon.data(), r4e.data());
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
-  sync(ctx);
-  for (size_t i = 0; i < n; i++) recon[i] = qualified[i] && recon[i];
   // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
   std::vector<uint8_t> honest_mask = final_parties(n, qualified.data(), recon.data());
   size_t nrecon = 0;
@@ -990,18 +1014,11 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   HCK(hipStreamWaitEvent(ctx->stream, ctx->pub_done, 0));  // public shares (round 3, side stream)
   if (copy_big) {
     if (out->dec2) d2h(ctx, out->dec2, dec2, n * n);
-    if (out->dec4) d2h(ctx, h4.data(), dec4, n * n);
+    if (out->dec4) d2h(ctx, out->dec4, dec4, n * n);  // SKIPPED rows applied (round4_outcome)
     if (out->final_share) d2h(ctx, out->final_share, fs, 32 * n);
     if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * n);
   }
   sync(ctx);
-  if (copy_big && out->dec4) {
-    for (size_t i = 0; i < n; i++)
-      if (!qualified[i])
-        for (size_t j = 0; j < n; j++)
-          if (j != i) h4[i * n + j] = DKG_SKIPPED;  // disqualified dealers are skipped (:522)
-    memcpy(out->dec4, h4.data(), n * n);
-  }
 }
 
 // Round 1 for D dealers on device: a, b canonical [D][N][8] -> Ecomp, Acomp [D][N][8], s, sp [D][n][8].
@@ -1062,8 +1079,6 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   const size_t N = t + 1, V = B * n;
   uint8_t* dec2 = buf<uint8_t>(ctx, "b.dec2", V * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "b.dec4", V * n);
-  uint8_t* rej = buf<uint8_t>(ctx, "b.rej", V);
-  int32_t* cnt = buf<int32_t>(ctx, "b.cnt", 4 * V);
   uint8_t* qmask = buf<uint8_t>(ctx, "b.qmask", V);
   uint32_t* fs = buf<uint32_t>(ctx, "b.final", 32 * V);
   uint32_t* pub = buf<uint32_t>(ctx, "b.pub_ext", PTB * V);
@@ -1072,35 +1087,25 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   std::vector<int32_t> complaints(V);
   auto round3 = [&] {
     // round-2 outcome per ceremony (committee.rs:311-316, 340-347, 370-398)
-    dkgk::decision_summary(B, n, dec2, rej, cnt, ctx->stream);
-    d2h(ctx, qualified.data(), rej, V);
-    d2h(ctx, complaints.data(), cnt, 4 * V);
-    sync(ctx);
-    for (size_t i = 0; i < V; i++) {
-      qualified[i] = !qualified[i];
-      r2err[i] = complaints[i] > (int32_t)t;
-    }
+    round2_outcome(ctx, B, n, t, dec2, qmask, qualified.data(), complaints.data(), r2err.data());
     // round 3 (committee.rs:433-476) per ceremony
-    h2d(ctx, qmask, qualified.data(), V);
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
     dkgk::fixed_base(V, fs, ctx->tab_gw, pub, ctx->stream);
     dkgk::encode_points(pub, V, V, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
   verify_rounds(ctx, n, t, V, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3);
-  // round-4 outcome: a qualified dealer rejected by someone is reconstructed (committee.rs:660-670)
-  std::vector<uint8_t> rej4(V);
-  dkgk::decision_summary(B, n, dec4, rej, nullptr, ctx->stream);
-  d2h(ctx, rej4.data(), rej, V);
+  // round-4 outcome: a qualified dealer rejected by someone is reconstructed (committee.rs:660-670),
+  // disqualified dealers' rows SKIPPED (:522)
+  std::vector<uint8_t> r4e(out->r4_error ? V : 0);
+  round4_outcome(ctx, B, n, t, dec4, qmask, qualified.data(), recon.data(), out->r4_error ? r4e.data() : nullptr);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
-  sync(ctx);
   std::vector<size_t> recon_cer;
   std::vector<uint8_t> p4err(B, 0);
   for (size_t c = 0; c < B; c++) {
     bool any = false;
     int32_t h = 0;
     for (size_t i = c * n; i < (c + 1) * n; i++) {
-      recon[i] = qualified[i] && rej4[i];
       honest[i] = qualified[i] && !recon[i];
       any |= recon[i] != 0;
       h += honest[i];
@@ -1147,28 +1152,13 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
   check_launch(ctx);
   if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
-  if (out->r4_error) {  // qmask (the qualified set) is on the device since round 3
-    uint8_t* r4e = buf<uint8_t>(ctx, "b.r4err", V);
-    dkgk::r4_error(B, n, t, dec4, qmask, r4e, ctx->stream);
-    d2h(ctx, out->r4_error, r4e, V);
-  }
   if (out->final_share) d2h(ctx, out->final_share, fs, 32 * V);
   if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * V);
-  std::vector<uint8_t> h4;
   if (out->dec2) d2h(ctx, out->dec2, dec2, V * n);
-  if (out->dec4) {
-    h4.resize(V * n);
-    d2h(ctx, h4.data(), dec4, V * n);
-  }
+  if (out->dec4) d2h(ctx, out->dec4, dec4, V * n);  // SKIPPED rows applied (round4_outcome)
   HCK(hipEventRecord(ctx->ev[5], ctx->stream));
   sync(ctx);
-  if (out->dec4) {
-    for (size_t i = 0; i < V; i++)
-      if (!qualified[i])
-        for (size_t j = 0; j < n; j++)
-          if (j != i % n) h4[i * n + j] = DKG_SKIPPED;  // committee.rs:522
-    memcpy(out->dec4, h4.data(), V * n);
-  }
+  if (out->r4_error) memcpy(out->r4_error, r4e.data(), V);
   if (out->qualified) memcpy(out->qualified, qualified.data(), V);
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), V);
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * V);
@@ -2137,6 +2127,102 @@ int dkg_point_sum_device(dkg_ctx* ctx, size_t count, const void* d_points, const
         ctx->err = "point_sum: a selected point does not decode";
         return DKG_E_DECODE;
       }
+    return DKG_OK;
+  });
+}
+
+void dkg_shard_range(size_t n, size_t world_size, size_t rank, size_t* d0, size_t* d1) {
+  const size_t ws = world_size ? world_size : 1;
+  if (d0) *d0 = rank < ws ? (rank * n) / ws : n;
+  if (d1) *d1 = rank < ws ? ((rank + 1) * n) / ws : n;
+}
+
+size_t dkg_shard_rows(size_t n, size_t world_size) {
+  size_t R = 0;
+  for (size_t r = 0; r < world_size; r++) R = std::max(R, ((r + 1) * n) / world_size - (r * n) / world_size);
+  return R;
+}
+
+int dkg_shard_combine_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_size, const void* d_dec2_g,
+                             const void* d_dec4_g, void* d_dec2, void* d_dec4, dkg_shard_outcome* out) {
+  return guarded(ctx, [&] {
+    if (!out || !d_dec2_g || !d_dec4_g || !world_size || world_size > n || dkg_env_check(t, n) != DKG_OK)
+      return DKG_E_ARG;
+    const size_t R = dkg_shard_rows(n, world_size);
+    uint8_t* dec2 = d_dec2 ? (uint8_t*)d_dec2 : buf<uint8_t>(ctx, "sc.dec2", n * n);
+    uint8_t* dec4 = d_dec4 ? (uint8_t*)d_dec4 : buf<uint8_t>(ctx, "sc.dec4", n * n);
+    uint8_t* qmask = buf<uint8_t>(ctx, "sc.qmask", n);
+    dkgk::compact_ranks(n, world_size, R, n, d_dec2_g, dec2, ctx->stream);
+    dkgk::compact_ranks(n, world_size, R, n, d_dec4_g, dec4, ctx->stream);
+    check_launch(ctx);
+    std::vector<uint8_t> q(n), r2e(n), recon(n), r4e(n);
+    std::vector<int32_t> c(n);
+    round2_outcome(ctx, 1, n, t, dec2, qmask, q.data(), c.data(), r2e.data());
+    round4_outcome(ctx, 1, n, t, dec4, qmask, q.data(), recon.data(), r4e.data());
+    int32_t nq = 0, nr = 0;
+    for (size_t i = 0; i < n; i++) {
+      nq += q[i];
+      nr += recon[i];
+    }
+    if (out->qualified) memcpy(out->qualified, q.data(), n);
+    if (out->complaints2) memcpy(out->complaints2, c.data(), 4 * n);
+    if (out->r2_error) memcpy(out->r2_error, r2e.data(), n);
+    if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
+    if (out->r4_error) memcpy(out->r4_error, r4e.data(), n);
+    out->n_qualified = nq;
+    out->phase4_error = nq - nr <= (int32_t)t;  // committee.rs:673-677
+    return DKG_OK;
+  });
+}
+
+int dkg_shard_finalise_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_size, const void* d_terms_g,
+                              const void* d_partials_g, const uint8_t* qualified, int phase4_error,
+                              void* d_final_share, void* d_public_share, uint8_t* mpk) {
+  return guarded(ctx, [&] {
+    if (!d_terms_g || !d_partials_g || !qualified || !d_final_share || !mpk || !world_size || world_size > n ||
+        dkg_env_check(t, n) != DKG_OK)
+      return DKG_E_ARG;
+    int rc = need_env(ctx);
+    if (rc) return rc;
+    const size_t R = dkg_shard_rows(n, world_size);
+    // round 3 (committee.rs:454-467): s_j = sum over the ranks' partials, g * s_j
+    uint8_t* ones = buf<uint8_t>(ctx, "sf.ones", world_size);
+    HCK(hipMemsetAsync(ones, 1, world_size, ctx->stream));
+    dkgk::sum_shares(world_size, n, (const uint32_t*)d_partials_g, ones, (uint32_t*)d_final_share, ctx->stream);
+    if (d_public_share) {
+      uint32_t* pub = buf<uint32_t>(ctx, "sf.pub", PTB * n);
+      dkgk::fixed_base(n, (const uint32_t*)d_final_share, ctx->tab_gw, pub, ctx->stream);
+      dkgk::encode_points(pub, n, n, (uint32_t*)d_public_share, ctx->stream);
+    }
+    memset(mpk, 0, 32);
+    if (!phase4_error) {
+      // finalise (committee.rs:790-795): the qualified dealers' terms -- A_i0 for the final parties,
+      // g * a_i0 recovered over the final parties for the reconstructed ones
+      uint32_t* terms = buf<uint32_t>(ctx, "sf.terms", 32 * n);
+      uint32_t* ext = buf<uint32_t>(ctx, "sf.ext", PTB * n);
+      uint8_t* ok = buf<uint8_t>(ctx, "sf.ok", n);
+      uint8_t* qm = buf<uint8_t>(ctx, "sf.q", n);
+      uint32_t* sum = buf<uint32_t>(ctx, "sf.sum", PTB);
+      uint32_t* mc = buf<uint32_t>(ctx, "sf.mpk", 32);
+      dkgk::compact_ranks(n, world_size, R, 32, d_terms_g, terms, ctx->stream);
+      h2d(ctx, qm, qualified, n);
+      dkgk::decode_points(terms, n, ext, n, ok, ctx->stream);
+      dkgk::sum_points(n, ext, n, qm, sum, 1, 0, ctx->stream);
+      dkgk::encode_points(sum, 1, 1, mc, ctx->stream);
+      check_launch(ctx);
+      std::vector<uint8_t> okh(n);
+      d2h(ctx, okh.data(), ok, n);
+      d2h(ctx, mpk, mc, 32);
+      sync(ctx);
+      for (size_t i = 0; i < n; i++)
+        if (qualified[i] && !okh[i]) {
+          memset(mpk, 0, 32);
+          ctx->err = "shard_finalise: a qualified dealer's master-key term does not decode";
+          return DKG_E_DECODE;
+        }
+    }
+    check_launch(ctx);
+    sync(ctx);
     return DKG_OK;
   });
 }

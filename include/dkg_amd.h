@@ -260,6 +260,48 @@ int dkg_scalar_sum_device(dkg_ctx *ctx, size_t rows, size_t n, const void *d_in,
  * [count][32] compressed, out [32] compressed.  DKG_E_DECODE if a selected point does not decode. */
 int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const void *d_mask, void *d_out);
 
+/* ---- the sharded run's protocol layer (multi-GPU, one process per GPU) ----
+ * The reference has no transport (its broadcast channel is abstract, src/lib.rs:91-115); a
+ * multi-rank driver supplies the all-gathers (RCCL over xGMI) and calls, on every rank:
+ *   dkg_ceremony_shard_device / _shard_verify_device   this rank's dealers' rows
+ *   all-gather dec2, dec4 (each rank's [R][n] block), A0 ([R][32]), partials ([n][32])
+ *   dkg_shard_combine_device                           the common outcome (identical on every rank)
+ *   if reconstruct has any member and !phase4_error:
+ *     dkg_ceremony_shard_recon_device, all-gather the terms again
+ *   dkg_shard_finalise_device                          final shares, public shares, mpk
+ * Rank r of world_size owns dealers [r*n/ws, (r+1)*n/ws); R = dkg_shard_rows(n, ws) is the padded
+ * block height every rank gathers. */
+void dkg_shard_range(size_t n, size_t world_size, size_t rank, size_t *d0, size_t *d1);
+size_t dkg_shard_rows(size_t n, size_t world_size);
+
+typedef struct {
+  /* host arrays [n] (any may be NULL) */
+  uint8_t *qualified;     /* round 2: no REJECT and no MISSING in the dealer's row (committee.rs:311-335, 370-398) */
+  int32_t *complaints2;   /* REJECTs raised by receiver j */
+  uint8_t *r2_error;      /* complaints2[j] > t (:340-347) */
+  uint8_t *reconstruct;   /* qualified dealers some receiver rejected in round 4 (:660-670) */
+  uint8_t *r4_error;      /* receiver j: itself plus the qualified dealers it accepted < t+1 (:515-516, 567-569) */
+  int32_t n_qualified;
+  int32_t phase4_error;   /* qualified minus reconstructable <= t (:673-677) */
+} dkg_shard_outcome;
+
+/* Combine step after the decision all-gathers: d_dec2_g, d_dec4_g device [ws][R][n] (rank blocks as
+ * gathered, rows past a rank's dealer count ignored).  Derives the common outcome with the same code
+ * as the single-GPU drivers (runtime.hip round2_outcome / round4_outcome).  d_dec2, d_dec4 (device
+ * [n][n], may be NULL): the compacted decision matrices, dec4 with the SKIPPED rows of disqualified
+ * dealers applied (:522). */
+int dkg_shard_combine_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_size, const void *d_dec2_g,
+                             const void *d_dec4_g, void *d_dec2, void *d_dec4, dkg_shard_outcome *out);
+/* Finalise of the sharded run: d_terms_g device [ws][R][32] the gathered master-key terms (A_i0, or
+ * g * a_i0 for reconstructed dealers after dkg_ceremony_shard_recon_device), d_partials_g device
+ * [ws][n][32] the gathered partial final shares, qualified host [n] (the combine's).  Outputs:
+ * d_final_share device [n][32] s_j = sum of the partials (committee.rs:454-462), d_public_share device
+ * [n][32] g * s_j (:463-467; may be NULL), mpk host [32] = sum of the qualified dealers' terms
+ * (:790-795), zero when phase4_error (nobody finalises, :673-677). */
+int dkg_shard_finalise_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_size, const void *d_terms_g,
+                              const void *d_partials_g, const uint8_t *qualified, int phase4_error,
+                              void *d_final_share, void *d_public_share, uint8_t *mpk);
+
 /* ---- per-party finalise: Phases<Phase5>::finalise (committee.rs:726-805) as EVERY party p runs it ----
  * Inputs are the ceremony's common outcome (host arrays [n]): qualified, reconstruct (round 4,
  * committee.rs:660-670), r2_error / r4_error (may be NULL: a party whose Phase1 / Phase3 proceed failed

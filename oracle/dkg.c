@@ -83,9 +83,11 @@ void or_share_gen(size_t D, size_t n, size_t t, const uint8_t *a, const uint8_t 
   }
 }
 
-int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8_t h[32],
-                    const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
-                    uint8_t *accept, int nthreads) {
+/* or_verify_pairs on row-local arrays: C [d1-d0][N], s / sp [d1-d0][n] hold dealers d0..d1-1 only
+ * (one rank's block of a sharded run); dealer indices (the SELF diagonal) stay global. */
+int or_verify_pairs_rows(size_t n, size_t t, int round, const uint8_t *C, const uint8_t h[32],
+                         const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
+                         uint8_t *accept, int nthreads) {
   const size_t N = t + 1, nd = d1 - d0, nr = r1 - r0;
   ge_ext hp, g;
   ge_base_point(&g);
@@ -95,7 +97,7 @@ int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8
   int rc = 0;
   for (size_t i = 0; i < nd; i++)
     for (size_t k = 0; k < N; k++)
-      if (ge_decode(&pts[i * N + k], C + 32 * ((d0 + i) * N + k))) bad[i] = 1;
+      if (ge_decode(&pts[i * N + k], C + 32 * (i * N + k))) bad[i] = 1;
   for (size_t i = 0; i < nd; i++) rc |= bad[i] ? -1 : 0;
   set_threads(nthreads);
 #pragma omp parallel for schedule(dynamic)
@@ -123,12 +125,12 @@ int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8
     }
     ge_ext lhs, rhs, tmp;
     uint8_t sv[32];
-    or_sc_reduce(sv, s + 32 * (i * n + j));
+    or_sc_reduce(sv, s + 32 * (ii * n + j));
     ge_mul_vartime_base(&lhs, &g, sv);
     if (round == 2) {
       /* committee.rs:292-294: h * decrypted_randomness + G::generator() * decrypted_share */
       uint8_t spv[32];
-      or_sc_reduce(spv, sp + 32 * (i * n + j));
+      or_sc_reduce(spv, sp + 32 * (ii * n + j));
       ge_mul_vartime_base(&tmp, &hp, spv);
       ge_add_ext(&lhs, &tmp, &lhs);
     }
@@ -139,6 +141,14 @@ int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8
   free(pts);
   free(bad);
   return rc;
+}
+
+/* dealers d0..d1-1 of whole arrays C [n][N], s / sp [n][n] (committee.rs:287-305, 532-548) */
+int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8_t h[32],
+                    const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
+                    uint8_t *accept, int nthreads) {
+  return or_verify_pairs_rows(n, t, round, C + 32 * d0 * (t + 1), h, s + 32 * d0 * n,
+                              round == 2 ? sp + 32 * d0 * n : sp, d0, d1, r0, r1, accept, nthreads);
 }
 
 /* polynomial.rs:162-184 */

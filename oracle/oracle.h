@@ -76,6 +76,11 @@ void or_share_gen(size_t D, size_t n, size_t t, const uint8_t *a, const uint8_t 
 int or_verify_pairs(size_t n, size_t t, int round, const uint8_t *C, const uint8_t h[32],
                     const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
                     uint8_t *accept, int nthreads);
+/* The same on row-local arrays (one rank's block of a sharded run): C [d1-d0][t+1][32],
+ * s, sp [d1-d0][n][32]; dealer indices (the SELF diagonal i == j) stay global. */
+int or_verify_pairs_rows(size_t n, size_t t, int round, const uint8_t *C, const uint8_t h[32],
+                         const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
+                         uint8_t *accept, int nthreads);
 /* ---- full (encrypted-share) mode: hybrid.c (elgamal.rs, procedure_keys.rs) ---- */
 void or_chacha20_ietf_xor(uint8_t *out, const uint8_t *in, size_t len, const uint8_t key[32],
                           const uint8_t nonce[12]);

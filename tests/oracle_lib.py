@@ -28,6 +28,7 @@ def lib():
         _lib.or_verify_pairs.argtypes = [sz, sz, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
                                          ctypes.c_char_p, ctypes.c_char_p, sz, sz, sz, sz, ctypes.c_char_p,
                                          ctypes.c_int]
+        _lib.or_verify_pairs_rows.argtypes = _lib.or_verify_pairs.argtypes
         _lib.or_dealer_coeffs.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_char_p]
         _lib.or_dealer_seed.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
         _lib.or_lagrange.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz]
@@ -95,6 +96,14 @@ def share_gen(D, n, t, a, b, h, nthreads=0):
 def verify_pairs(n, t, rnd, C, h, s, sp, d0, d1, r0, r1, nthreads=0):
     acc = _b((d1 - d0) * (r1 - r0))
     rc = lib().or_verify_pairs(n, t, rnd, C, h, s, sp or b"", d0, d1, r0, r1, acc, nthreads)
+    return acc.raw, rc
+
+
+def verify_rows(n, t, rnd, C, h, s, sp, d0, d1, r0, r1, nthreads=0):
+    """verify_pairs on row-local arrays holding dealers d0..d1-1 only (C [d1-d0][t+1], s / sp
+    [d1-d0][n]); the SELF diagonal stays at the global dealer index."""
+    acc = _b((d1 - d0) * (r1 - r0))
+    rc = lib().or_verify_pairs_rows(n, t, rnd, C, h, s, sp or b"", d0, d1, r0, r1, acc, nthreads)
     return acc.raw, rc
 
 

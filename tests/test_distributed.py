@@ -1,8 +1,10 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the dealer-sharded exchange and combine
+"""Multi-process (world_size 2/3, gloo, CPU) tests of the dealer-sharded exchange
 (dkg_amd/distributed.py).  Each rank holds only its dealers' rows of a golden ceremony; after the
-all-gathers every rank must derive the golden qualified set, complaints, r2 errors, round-4 SKIPPED
-marks, reconstruction set and final shares.  The GPU half of the sharded path
-(dkg_ceremony_shard_device) is covered by tests/test_gpu.py::test_sharded_ceremony_matches_golden.
+all-gathers every rank must hold every rank's blocks, from which the combine rules
+(tests/combine_ref.py, the checker of the library's dkg_shard_combine_device) derive the golden
+qualified set, complaints, r2 errors, round-4 SKIPPED marks, reconstruction set and final shares.
+The GPU half of the sharded path (dkg_ceremony_shard_device, dkg_shard_combine_device,
+dkg_shard_finalise_device) is covered by tests/test_gpu.py and tests/test_gpu_dist.py.
 """
 import json
 import os
@@ -30,7 +32,8 @@ def _rank_main(rank, ws, port, names, errq):
     import torch
     import torch.distributed as dist
 
-    from dkg_amd.distributed import ShardedCeremony, combine_decisions, dealer_range
+    from dkg_amd.distributed import ShardedCeremony, dealer_range
+    from tests import combine_ref as CR
 
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
@@ -61,9 +64,11 @@ def _rank_main(rank, ws, port, names, errq):
                 sc.A0[:len(A0)] = torch.frombuffer(bytearray(A0), dtype=torch.uint8)
             sc.part[:] = torch.frombuffer(bytearray(part), dtype=torch.uint8)
             g2, g4, gA0, gpart = sc.exchange()
-            assert bytes(g2.numpy()) == bytes(int(x) for x in c["dec2"]), name
-            assert bytes(gA0.numpy()) == b"".join(A[32 * N * i:32 * N * i + 32] for i in range(n)), name
-            d = combine_decisions(g2.numpy(), g4.numpy(), n, t)
+            g2, g4 = CR.compact(g2.numpy(), ws, n, n), CR.compact(g4.numpy(), ws, n, n)
+            gA0 = CR.compact(gA0.numpy(), ws, n, 32)
+            assert bytes(g2) == bytes(int(x) for x in c["dec2"]), name
+            assert bytes(gA0) == b"".join(A[32 * N * i:32 * N * i + 32] for i in range(n)), name
+            d = CR.combine(g2, g4, n, t)
             assert d.qualified.tolist() == c["qualified"], name
             assert d.complaints2.tolist() == c["complaints2"], name
             assert d.r2_error.tolist() == [int(x) for x in c["r2_error"]], name
@@ -103,40 +108,39 @@ def test_sharded_exchange_gloo(ws):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
 
 
-def test_combine_single_process(golden):
-    """combine_decisions alone on every golden ceremony (no exchange)."""
-    from dkg_amd.distributed import combine_decisions
+def test_combine_ref_on_goldens(golden):
+    """The checker's combine rules (tests/combine_ref.py) reproduce every golden ceremony's outcome
+    from its raw decision matrices (round-4 SKIPPED marks replaced by arbitrary checks)."""
+    from tests import combine_ref as CR
 
     for name in NAMES + ["ceremony_n64_t31.json"]:
         c = golden(name)
         n, t = c["n"], c["t"]
         dec2 = np.frombuffer(bytes(int(x) for x in c["dec2"]), dtype=np.uint8)
         dec4 = np.frombuffer(bytes(1 if x == "3" else int(x) for x in c["dec4"]), dtype=np.uint8)
-        d = combine_decisions(dec2, dec4, n, t)
+        d = CR.combine(dec2, dec4, n, t)
         assert d.qualified.tolist() == c["qualified"]
+        assert d.complaints2.tolist() == c["complaints2"]
         assert d.reconstruct.tolist() == c["reconstruct"]
         assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
         assert d.phase4_error == c["phase4_error"]
         assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
 
 
-def test_combine_torch_matches_numpy(golden):
-    """The device-side combine (torch tensors, as ShardedCeremony hands over the gathered rows)
-    equals the numpy combine on every golden ceremony."""
-    import torch
+def test_shard_partition_matches_library():
+    """The padded gather layout the checker assumes is the library's partition (dkg_shard_range,
+    dkg_shard_rows: C entry points without a device)."""
+    import dkg_amd
+    from tests import combine_ref as CR
 
-    from dkg_amd.distributed import combine_decisions
-
-    for name in NAMES + ["ceremony_n64_t31.json"]:
-        c = golden(name)
-        n, t = c["n"], c["t"]
-        dec2 = np.frombuffer(bytes(int(x) for x in c["dec2"]), dtype=np.uint8).copy()
-        dec4 = np.frombuffer(bytes(1 if x == "3" else int(x) for x in c["dec4"]), dtype=np.uint8).copy()
-        a = combine_decisions(dec2, dec4, n, t)
-        b = combine_decisions(torch.from_numpy(dec2), torch.from_numpy(dec4), n, t)
-        for f in ("qualified", "complaints2", "r2_error", "reconstruct", "r4_error", "honest"):
-            assert getattr(a, f).tolist() == getattr(b, f).tolist(), (name, f)
-        assert a.dec4.reshape(-1).tolist() == b.dec4.reshape(-1).tolist() and a.phase4_error == b.phase4_error
+    for n in (2, 3, 10, 11, 64, 1024, 1100, 4096):
+        for ws in (1, 2, 3, 5, 8):
+            if ws > n:
+                continue
+            assert dkg_amd.shard_rows(n, ws) == CR.rows_per_rank(ws, n)
+            assert [dkg_amd.shard_range(n, ws, r) for r in range(ws)] == [CR.dealer_range(r, ws, n) for r in range(ws)]
+            rows = [dkg_amd.shard_range(n, ws, r) for r in range(ws)]
+            assert rows[0][0] == 0 and rows[-1][1] == n and all(rows[r][1] == rows[r + 1][0] for r in range(ws - 1))
 
 
 class OracleBackend:
@@ -190,15 +194,34 @@ class OracleBackend:
                 ys = [int.from_bytes(row[32 * (x - 1):32 * x], "little") for x in xs]
                 self._wr(d_terms + 32 * (i - d0), FR.g_mul(FR.lagrange_at_zero(ys, xs)))
 
-    def scalar_sum_device(self, rows, n, d_in, d_mask, d_out):
-        data = self._rd(d_in, 32 * rows * n)
-        self._wr(d_out, b"".join((sum(int.from_bytes(data[32 * (r * n + j):32 * (r * n + j) + 32], "little")
-                                      for r in range(rows)) % L).to_bytes(32, "little") for j in range(n)))
+    def shard_combine_device(self, n, t, ws, d_dec2_g, d_dec4_g, d_dec2=None, d_dec4=None):
+        from dkg_amd.api import ShardOutcome
+        from tests import combine_ref as CR
+        R = CR.rows_per_rank(ws, n)
+        g2 = CR.compact(np.frombuffer(self._rd(d_dec2_g, ws * R * n), dtype=np.uint8), ws, n, n)
+        g4 = CR.compact(np.frombuffer(self._rd(d_dec4_g, ws * R * n), dtype=np.uint8), ws, n, n)
+        d = CR.combine(g2, g4, n, t)
+        if d_dec2:
+            self._wr(d_dec2, bytes(d.dec2))
+        if d_dec4:
+            self._wr(d_dec4, bytes(d.dec4))
+        return ShardOutcome(d.qualified.tolist(), d.complaints2.tolist(), d.r2_error.tolist(), d.reconstruct.tolist(),
+                            d.r4_error.tolist(), int(d.qualified.sum()), d.phase4_error)
 
-    def point_sum_device(self, count, d_points, d_mask, d_out):
+    def shard_finalise_device(self, n, t, ws, d_terms_g, d_partials_g, qualified, phase4_error, d_fs, d_pub=None):
+        from tests import combine_ref as CR
         from tests import finalise_ref as FR
-        pts, mask = self._rd(d_points, 32 * count), self._rd(d_mask, count)
-        self._wr(d_out, FR.gsum([pts[32 * c:32 * c + 32] for c in range(count) if mask[c]]))
+        data = self._rd(d_partials_g, 32 * ws * n)
+        fs = [sum(int.from_bytes(data[32 * (r * n + j):32 * (r * n + j) + 32], "little") for r in range(ws)) % L
+              for j in range(n)]
+        self._wr(d_fs, b"".join(x.to_bytes(32, "little") for x in fs))
+        if d_pub:
+            self._wr(d_pub, b"".join(FR.g_mul(x) for x in fs))
+        R = CR.rows_per_rank(ws, n)
+        terms = bytes(CR.compact(np.frombuffer(self._rd(d_terms_g, 32 * ws * R), dtype=np.uint8), ws, n, 32))
+        if phase4_error:
+            return bytes(32)
+        return FR.gsum([terms[32 * i:32 * i + 32] for i in range(n) if qualified[i]])
 
 
 def _run_verify_main(rank, ws, port, names, errq):
@@ -225,6 +248,7 @@ def _run_verify_main(rank, ws, port, names, errq):
             d = res.decisions
             assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"], name
             assert res.final_share.hex() == c["final_share"], name
+            assert res.public_share.hex() == c["public_share"], name
             if c["phase4_error"]:
                 assert res.mpk is None, name
             else:

@@ -325,16 +325,37 @@ def test_chunked_streams_identical(be, round_, n, t):
         be.set_streams(2)
 
 
+def _check_played(p, c, n, ws):
+    """A played sharded run (tests/shard_play.py) against a golden ceremony, and the library's combine
+    against the checker's rules (tests/combine_ref.py) on the same gathered rows."""
+    from tests import combine_ref as CR
+
+    assert dec_str(p.dec2) == c["dec2"]
+    assert dec_str(p.dec4) == c["dec4"]
+    o = p.outcome
+    assert o.qualified == c["qualified"] and o.reconstruct == c["reconstruct"]
+    assert o.complaints2 == c["complaints2"]
+    assert o.r2_error == [int(x) for x in c["r2_error"]]
+    assert o.r4_error == [int(x) for x in c["r4_error"]]
+    assert o.phase4_error == c["phase4_error"] and o.n_qualified == sum(c["qualified"])
+    ref = CR.combine(p.dec2, p.raw4, n, int(c["t"]))
+    assert ref.qualified.tolist() == o.qualified and ref.reconstruct.tolist() == o.reconstruct
+    assert ref.r4_error.tolist() == o.r4_error and bytes(ref.dec4) == p.dec4
+    assert p.final_share.hex() == c["final_share"]
+    assert p.public_share.hex() == c["public_share"]
+    # Phases<Phase4>::proceed fails for everyone without a master key (committee.rs:673-677): zero
+    assert p.mpk.hex() == c["mpk"]
+
+
 @pytest.mark.parametrize("name,ws", [("ceremony_n16_t7.json", 2), ("ceremony_n64_t31.json", 3),
                                      ("ceremony_n11_t5.json", 4)])
 def test_sharded_ceremony_matches_golden(be, golden, name, ws):
-    """dkg_ceremony_shard_device for every rank of a ws-way dealer split (played in one process),
-    the host-side exchange (concatenation = what the all-gathers deliver) and the device combine
-    reproduce the single-GPU golden ceremony bit for bit."""
-    import numpy as np
+    """dkg_ceremony_shard_device for every rank of a ws-way dealer split (played in one process), the
+    gathered padded blocks, and the library's combine and finalise (dkg_shard_combine_device,
+    dkg_shard_finalise_device) reproduce the single-GPU golden ceremony bit for bit."""
     import torch
 
-    from dkg_amd.distributed import combine_decisions, dealer_range
+    from tests import shard_play
 
     c = golden(name)
     n, t = c["n"], c["t"]
@@ -342,50 +363,30 @@ def test_sharded_ceremony_matches_golden(be, golden, name, ws):
     be.env_init(t, n, CK)
     dev = torch.device("cuda", 0)
     a, b = dkg_amd.dealer_coefficients(H(c["master_seed"]), c["ceremony"], 0, n, t)
-    dec2, dec4, A0, parts = [], [], [], []
-    for r in range(ws):
-        d0, d1 = dealer_range(r, ws, n)
-        D = d1 - d0
+    keep = []
+
+    def call(r, d0, d1, o2, o4, oA, op):
         ta = torch.frombuffer(bytearray(a[32 * N * d0:32 * N * d1] or b"\0"), dtype=torch.uint8).to(dev)
         tb = torch.frombuffer(bytearray(b[32 * N * d0:32 * N * d1] or b"\0"), dtype=torch.uint8).to(dev)
-        o2 = torch.zeros(max(D * n, 1), dtype=torch.uint8, device=dev)
-        o4 = torch.zeros_like(o2)
-        oA = torch.zeros(max(D * 32, 1), dtype=torch.uint8, device=dev)
-        op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+        keep.extend((ta, tb))
         be.ceremony_shard_device(n, t, d0, d1, ta.data_ptr(), tb.data_ptr(), o2.data_ptr(), o4.data_ptr(),
                                  oA.data_ptr(), op.data_ptr())
-        dec2.append(o2[:D * n])
-        dec4.append(o4[:D * n])
-        A0.append(oA[:D * 32])
-        parts.append(op)
-    g2, g4, gA0, gp = (torch.cat(x) for x in (dec2, dec4, A0, parts))
-    assert dec_str(bytes(g2.cpu().numpy())) == c["dec2"]
-    assert bytes(gA0.cpu().numpy()) == b"".join(H(c["A"])[32 * N * i:32 * N * i + 32] for i in range(n))
-    d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
-    assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
-    assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
-    assert d.phase4_error == c["phase4_error"]
-    assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
-    fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-    be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
-    assert bytes(fs.cpu().numpy()).hex() == c["final_share"]
-    mask = torch.from_numpy(np.ascontiguousarray(d.qualified)).to(dev)
-    mpk = torch.empty(32, dtype=torch.uint8, device=dev)
-    be.point_sum_device(n, gA0.data_ptr(), mask.data_ptr(), mpk.data_ptr())
-    assert bytes(mpk.cpu().numpy()).hex() == c["mpk"]
+        return None
+
+    p = shard_play.play(be, n, t, ws, call, dev)
+    _check_played(p, c, n, ws)
 
 
 @pytest.mark.parametrize("ws", [1, 2, 3])
 @pytest.mark.parametrize("name", FAULTS + ["ceremony_n16_t7.json"])
 def test_sharded_verify_faults(be, golden, name, ws):
     """dkg_ceremony_shard_verify_device on the fixtures' broadcasts (faulty commitments / shares):
-    every rank's rows, the host exchange and combine, and the device finalise -- including a dealer
-    reconstructed on its owning rank (fault_a_generator: committee.rs:660-670, 747-783) -- give the
-    single-GPU golden decisions, final shares and mpk bit for bit."""
-    import numpy as np
+    every rank's rows, the library's combine, the reconstruction of a dealer accused in round 4 on its
+    owning rank (fault_a_generator: committee.rs:660-670, 747-783) and the library's finalise give the
+    single-GPU golden decisions, final shares, public shares and mpk bit for bit."""
     import torch
 
-    from dkg_amd.distributed import combine_decisions, dealer_range
+    from tests import shard_play
 
     c = golden(name)
     n, t = c["n"], c["t"]
@@ -393,53 +394,68 @@ def test_sharded_verify_faults(be, golden, name, ws):
     be.env_init(t, n, CK)
     dev = torch.device("cuda", 0)
     E, A, s, sp = (H(c[k]) for k in ("E", "A", "s", "s_prime"))
+    keep = []
 
     def put(x):
-        return torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)
+        v = torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)
+        keep.append(v)
+        return v
 
-    dec2, dec4, terms, parts, shares = [], [], [], [], []
-    for r in range(ws):
-        d0, d1 = dealer_range(r, ws, n)
-        D = d1 - d0
+    def call(r, d0, d1, o2, o4, oA, op):
         tE, tA = put(E[32 * N * d0:32 * N * d1]), put(A[32 * N * d0:32 * N * d1])
         ts, tsp = put(s[32 * n * d0:32 * n * d1]), put(sp[32 * n * d0:32 * n * d1])
-        o2 = torch.zeros(max(D * n, 1), dtype=torch.uint8, device=dev)
-        o4 = torch.zeros_like(o2)
-        oA = torch.zeros(max(D * 32, 1), dtype=torch.uint8, device=dev)
-        op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
         be.ceremony_shard_verify_device(n, t, d0, d1, tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr(),
                                         o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
-        dec2.append(o2[:D * n])
-        dec4.append(o4[:D * n])
-        terms.append(oA)
-        parts.append(op)
-        shares.append(ts)
-    g2, g4, gp = (torch.cat(x) for x in (dec2, dec4, parts))
-    assert dec_str(bytes(g2.cpu().numpy())) == c["dec2"]
-    d = combine_decisions(g2.cpu().numpy(), g4.cpu().numpy(), n, t)
-    assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"]
-    assert d.r4_error.tolist() == [int(x) for x in c["r4_error"]]
-    assert d.phase4_error == c["phase4_error"]
-    assert d.complaints2.tolist() == c["complaints2"]
-    assert "".join(str(x) for x in d.dec4.reshape(-1).tolist()) == c["dec4"]
-    fs = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-    be.scalar_sum_device(ws, n, gp.data_ptr(), None, fs.data_ptr())
-    assert bytes(fs.cpu().numpy()).hex() == c["final_share"]
-    if d.phase4_error:  # Phases<Phase4>::proceed fails for everyone: no master key (committee.rs:673-677)
-        assert c["mpk"] == "00" * 32
-        return
-    # after the exchange: the owning rank of a dealer accused in round 4 replaces its term by g * a_i0
-    # over the final parties' shares (committee.rs:747-789)
-    for r in range(ws):
-        d0, d1 = dealer_range(r, ws, n)
-        if d1 > d0:
-            be.ceremony_shard_recon_device(n, t, d0, d1, d.qualified, d.reconstruct, shares[r].data_ptr(),
-                                           terms[r].data_ptr())
-    gT = torch.cat([terms[r][:32 * (dealer_range(r, ws, n)[1] - dealer_range(r, ws, n)[0])] for r in range(ws)])
-    mask = torch.from_numpy(np.ascontiguousarray(d.qualified)).to(dev)
-    mpk = torch.empty(32, dtype=torch.uint8, device=dev)
-    be.point_sum_device(n, gT.data_ptr(), mask.data_ptr(), mpk.data_ptr())
-    assert bytes(mpk.cpu().numpy()).hex() == c["mpk"]
+        return ts
+
+    p = shard_play.play(be, n, t, ws, call, dev)
+    _check_played(p, c, n, ws)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_shard_combine_random_matrices(be, seed):
+    """dkg_shard_combine_device against the checker's rules (tests/combine_ref.py) on random decision
+    matrices in the padded gather layout: random REJECT densities (from none to over-threshold
+    columns), MISSING rows, random round-4 accusations (including rows of disqualified dealers, which
+    the combine must turn SKIPPED) and ragged rank partitions (ws up to 8, n not a multiple of ws)."""
+    import numpy as np
+    import torch
+
+    from tests import combine_ref as CR
+
+    rng = np.random.default_rng(seed)
+    n = int(rng.choice([3, 10, 33, 64, 257, 1024]))
+    t = int(rng.integers(0, (n + 1) // 2))
+    if 2 * t >= n + 1:
+        t = (n - 1) // 2
+    ws = int(rng.choice([w for w in (1, 2, 3, 5, 8) if w <= n]))
+    p2, p4 = float(rng.choice([0.0, 0.001, 0.02, 0.3])), float(rng.choice([0.0, 0.002, 0.05, 0.5]))
+    dec2 = np.where(rng.random((n, n)) < p2, REJECT, ACCEPT).astype(np.uint8)
+    for i in rng.choice(n, size=int(rng.integers(0, 4)), replace=False) if n > 3 else []:
+        dec2[i, :] = MISSING
+    dec4 = np.where(rng.random((n, n)) < p4, REJECT, ACCEPT).astype(np.uint8)
+    np.fill_diagonal(dec2, SELF)
+    np.fill_diagonal(dec4, SELF)
+    be.env_init(t, n, CK)
+    dev = torch.device("cuda", 0)
+    g2 = torch.from_numpy(CR.pad(dec2, ws, n, n)).to(dev)
+    g4 = torch.from_numpy(CR.pad(dec4, ws, n, n)).to(dev)
+    c2 = torch.empty(n * n, dtype=torch.uint8, device=dev)
+    c4 = torch.empty_like(c2)
+    o = be.shard_combine_device(n, t, ws, g2.data_ptr(), g4.data_ptr(), c2.data_ptr(), c4.data_ptr())
+    ref = CR.combine(dec2, dec4, n, t)
+    ctx = (seed, n, t, ws, p2, p4)
+    assert bytes(c2.cpu().numpy()) == bytes(dec2), ctx
+    assert bytes(c4.cpu().numpy()) == bytes(ref.dec4), ctx
+    assert o.qualified == ref.qualified.tolist(), ctx
+    assert o.complaints2 == ref.complaints2.tolist(), ctx
+    assert o.r2_error == ref.r2_error.tolist(), ctx
+    assert o.reconstruct == ref.reconstruct.tolist(), ctx
+    assert o.r4_error == ref.r4_error.tolist(), ctx
+    assert o.phase4_error == ref.phase4_error and o.n_qualified == int(ref.qualified.sum()), ctx
+    # the optional compacted outputs may be omitted
+    o2 = be.shard_combine_device(n, t, ws, g2.data_ptr(), g4.data_ptr())
+    assert (o2.qualified, o2.reconstruct, o2.r4_error) == (o.qualified, o.reconstruct, o.r4_error)
 
 
 def _check_batch_member(c, d, n):
@@ -1129,7 +1145,9 @@ def test_ceremony_n4096_device(be):
     op = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     be.ceremony_shard_device(n, t, 0, D, ta.data_ptr(), tb.data_ptr(), o2.data_ptr(), o4.data_ptr(), oA.data_ptr(),
                              op.data_ptr())
-    m2, m4 = o2.view(D, n).cpu().numpy(), o4.view(D, n).cpu().numpy()
-    for i in range(D):
-        assert m2[i, i] == SELF and m4[i, i] == SELF
-    assert (m2 != 0).all() and (m4 != 0).all() and int((m2 == ACCEPT).sum()) == D * (n - 1)
+    import numpy as np
+
+    honest = np.full((D, n), ACCEPT, dtype=np.uint8)
+    honest[np.arange(D), np.arange(D)] = SELF  # rank 0 owns dealers 0..D-1: SELF at j == i
+    assert np.array_equal(o2.view(D, n).cpu().numpy(), honest)
+    assert np.array_equal(o4.view(D, n).cpu().numpy(), honest)

@@ -40,10 +40,12 @@ def _bump(buf, off):
     buf[off:off + 32] = v.to_bytes(32, "little")
 
 
-def _inject(rng, n, t, E, A, s, sp):
-    """Tamper dealers 0..4 (rows of bytearrays E, A [n][t+1][32], s, sp [n][n][32]); returns
-    {dealer: description}.  Receivers and coefficient positions are chosen across the stepping
-    blocks (multiples of 512) and the degree-split pieces."""
+def _inject(rng, n, t, E, A, s, sp, base=0):
+    """Tamper dealers base..base+4: E, A [..][t+1][32], s, sp [..][n][32] are bytearrays whose row 0
+    is dealer `base` (a rank's block of a sharded run; base = 0: the whole committee).  Returns
+    {local dealer: description}.  Receivers and coefficient positions are chosen across the stepping
+    blocks (multiples of 512) and the degree-split pieces; dealer base+2's unchecked self-share sits
+    at the GLOBAL diagonal j = base + 2."""
     N = t + 1
     js = sorted({0, 1, min(511, n - 1), min(512, n - 1), n // 2, n - 1, rng.randrange(n)} - {0})
     for j in js:                                           # dealer 0: flipped shares
@@ -52,7 +54,7 @@ def _inject(rng, n, t, E, A, s, sp):
     for k in sorted({0, N // 2, N - 1}):                   # dealer 1: replaced E coefficients
         E[32 * (1 * N + k):32 * (1 * N + k) + 32] = _rand_point(rng)
     A[32 * (2 * N + N - 1):32 * (2 * N + N)] = _rand_point(rng)  # dealer 2: a replaced A coefficient
-    _bump(s, 32 * (2 * n + 2))                             # ... and its unchecked self-share
+    _bump(s, 32 * (2 * n + base + 2))                      # ... and its unchecked self-share
     E[32 * (3 * N + N // 3) + 31] |= 0x80                  # dealer 3: an undecodable E row (MISSING)
     for j in (7, n - 3):                                   # dealer 4: randomness only (round 2 only)
         _bump(sp, 32 * (4 * n + j))
@@ -64,31 +66,35 @@ def _inject(rng, n, t, E, A, s, sp):
 FULL_ROWS = [(0, 2), (0, 4), (1, 2), (2, 4), (4, 2)]
 
 
-def _expected_rows(n, t, h, E, A, s, sp, full=FULL_ROWS, sample=None):
-    """{(dealer, round): expected raw decision row} for dealers 0..4 (SKIPPED not applied).
-    Rows in `full` come from the oracle; with `sample` (a receiver list) the (4, 2) row is checked by
-    the oracle at those receivers only and completed analytically (large n)."""
+def _expected_rows(n, t, h, E, A, s, sp, full=FULL_ROWS, sample=None, base=0):
+    """{(local dealer, round): expected raw decision row} for dealers base..base+4 (SKIPPED not
+    applied; E, A, s, sp as _inject's, row 0 = dealer base).  Rows in `full` come from the oracle;
+    with `sample` (a receiver list) the (4, 2) row is checked by the oracle at those receivers only
+    and completed analytically (large n)."""
     N = t + 1
     exp = {}
     for i in range(5):
+        g = base + i
         for rnd in (2, 4):
-            row = bytearray(SELF if j == i else ACCEPT for j in range(n))
+            row = bytearray(SELF if j == g else ACCEPT for j in range(n))
             if (i, rnd) == (3, 2):
-                row = bytearray(SELF if j == i else MISSING for j in range(n))
+                row = bytearray(SELF if j == g else MISSING for j in range(n))
             exp[(i, rnd)] = row
     for j in (7, n - 3):
-        exp[(4, 2)][j] = REJECT
+        if j != base + 4:
+            exp[(4, 2)][j] = REJECT
+    rows = lambda buf, w, i: bytes(buf[w * i:w * (i + 1)])  # noqa: E731
     for (i, rnd) in full:
         if sample is not None and (i, rnd) == (4, 2):
             continue
         C = E if rnd == 2 else A
-        acc, _ = O.verify_pairs(n, t, rnd, bytes(C[:32 * N * (i + 1)]), h, bytes(s[:32 * n * (i + 1)]),
-                                bytes(sp[:32 * n * (i + 1)]) if rnd == 2 else None, i, i + 1, 0, n)
+        acc, _ = O.verify_rows(n, t, rnd, rows(C, 32 * N, i), h, rows(s, 32 * n, i),
+                               rows(sp, 32 * n, i) if rnd == 2 else None, base + i, base + i + 1, 0, n)
         exp[(i, rnd)] = bytearray(acc)
     if sample is not None:
         for j in sample:
-            acc, _ = O.verify_pairs(n, t, 2, bytes(E[:32 * N * 5]), h, bytes(s[:32 * n * 5]), bytes(sp[:32 * n * 5]),
-                                    4, 5, j, j + 1)
+            acc, _ = O.verify_rows(n, t, 2, rows(E, 32 * N, 4), h, rows(s, 32 * n, 4), rows(sp, 32 * n, 4),
+                                   base + 4, base + 5, j, j + 1)
             assert acc[0] == exp[(4, 2)][j], ("oracle disagrees with the injected fault", j)
     return {k: bytes(v) for k, v in exp.items()}
 
@@ -374,3 +380,120 @@ def test_stepping_redo_at_scale(be, n, t, split):
         row = dec2[d * n:(d + 1) * n]
         assert row.count(REJECT) == n - 1 and row[d] == SELF
     assert dec2[5 * n + 9] == REJECT and dec2[5 * n:6 * n].count(REJECT) == 1
+
+
+def _rank_rows(be, n, t, d0, d1, tE, tA, ts, tsp):
+    """Rank [d0, d1)'s rows through dkg_ceremony_shard_verify_device on views of the committee."""
+    import torch
+
+    N, D = t + 1, d1 - d0
+    dev = ts.device
+    o2 = torch.zeros(D * n, dtype=torch.uint8, device=dev)
+    o4 = torch.zeros_like(o2)
+    oA = torch.zeros(D * 32, dtype=torch.uint8, device=dev)
+    op = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    be.ceremony_shard_verify_device(n, t, d0, d1, tE[32 * N * d0:].data_ptr(), tA[32 * N * d0:].data_ptr(),
+                                    ts[32 * n * d0:].data_ptr(), tsp[32 * n * d0:].data_ptr(), o2.data_ptr(),
+                                    o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+    return o2.view(D, n), o4.view(D, n)
+
+
+def _tamper_rank(be, n, t, d0, tE, tA, ts, tsp, seed):
+    """_inject on the first five dealers of the rank starting at d0, written back to the device."""
+    import torch
+
+    N, D5 = t + 1, 5
+    E = bytearray(tE[32 * N * d0:32 * N * (d0 + D5)].cpu().numpy().tobytes())
+    A = bytearray(tA[32 * N * d0:32 * N * (d0 + D5)].cpu().numpy().tobytes())
+    s = bytearray(ts[32 * n * d0:32 * n * (d0 + D5)].cpu().numpy().tobytes())
+    sp = bytearray(tsp[32 * n * d0:32 * n * (d0 + D5)].cpu().numpy().tobytes())
+    _inject(random.Random(seed), n, t, E, A, s, sp, base=d0)
+    for t_, b_, w in ((tE, E, 32 * N), (tA, A, 32 * N), (ts, s, 32 * n), (tsp, sp, 32 * n)):
+        t_[w * d0:w * d0 + len(b_)] = torch.frombuffer(bytearray(b_), dtype=torch.uint8).to(t_.device)
+    return E, A, s, sp
+
+
+def _check_rank(n, d0, d2, d4, exp, ctx):
+    """Rank rows: the five tampered dealers equal `exp`; every other row ACCEPT with SELF at j == i."""
+    import torch
+
+    D = d2.shape[0]
+    h2, h4 = d2[:5].cpu().numpy(), d4[:5].cpu().numpy()
+    for i in range(5):
+        assert bytes(h2[i]) == exp[(i, 2)], (ctx, d0 + i, "round 2")
+        assert bytes(h4[i]) == exp[(i, 4)], (ctx, d0 + i, "round 4")
+    honest = torch.full((D - 5, n), ACCEPT, dtype=torch.uint8, device=d2.device)
+    idx = torch.arange(5, D, device=d2.device)
+    honest[idx - 5, d0 + idx] = SELF  # the GLOBAL diagonal j = d0 + i
+    assert torch.equal(d2[5:], honest) and torch.equal(d4[5:], honest), ctx
+
+
+@pytest.mark.parametrize("rank", [1, 4, 7])
+def test_shard_ranks_n4096(be, rank):
+    """BASELINE config 4's per-rank shape: rank r in {1, 4, 7} of the 8-way dealer split at n=4096,
+    t=2047 (512 dealers, d0 = 512 r) through dkg_ceremony_shard_verify_device, faults inside the
+    rank's range (tampered shares and randomness, replaced E and A coefficients, an undecodable E row,
+    a tampered self-share at the global diagonal j = d0 + 2).  Whole rows of the tampered dealers equal
+    the oracle's per-pair MSM checks (committee.rs:287-305, 532-548); the other 507 rows accept
+    everywhere except their global SELF diagonal."""
+    import torch
+
+    n, t, ws = 4096, 2047, 8
+    h = be.env_init(t, n, CK)
+    ta, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([41]) * 32, 0)
+    del ta
+    d0, d1 = dkg_amd.shard_range(n, ws, rank)
+    assert (d0, d1) == (512 * rank, 512 * (rank + 1))
+    E, A, s, sp = _tamper_rank(be, n, t, d0, tE, tA, ts, tsp, seed=rank)
+    d2, d4 = _rank_rows(be, n, t, d0, d1, tE, tA, ts, tsp)
+    U = be.last_split()
+    exp = _expected_rows(n, t, h, E, A, s, sp, sample=[7, n - 3] + random.Random(rank).sample(range(8, n - 3), 16),
+                         base=d0)
+    _check_rank(n, d0, d2, d4, exp, (n, rank, U))
+    torch.cuda.synchronize()
+
+
+def test_shard_ranks_n1024_all_match_single(be):
+    """BASELINE config 2 split 8 ways (128 dealers per rank: the latency-bound shard -- column-sum
+    binomial copy on every step, one stream, 2-waves-per-SIMD stepping), faults inside EVERY rank's
+    range (40 tampered dealers).  Per rank: whole rows of its tampered dealers equal the oracle's.
+    Then the eight ranks' blocks, gathered, through the library's combine, reconstruction and
+    finalise (tests/shard_play.py) equal the single-GPU ceremony on the same broadcasts bit for bit:
+    decision matrices, qualified / complaints / r2 and r4 errors / reconstruction set, final and
+    public shares, mpk (committee.rs:287-305, 311-398, 454-467, 532-569, 660-805)."""
+    import torch
+
+    from tests import shard_play
+
+    n, t, ws = 1024, 511, 8
+    N = t + 1
+    h = be.env_init(t, n, CK)
+    ta, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([43]) * 32, 2)
+    del ta
+    exps = {}
+    for r in range(ws):
+        d0, _ = dkg_amd.shard_range(n, ws, r)
+        E, A, s, sp = _tamper_rank(be, n, t, d0, tE, tA, ts, tsp, seed=100 + r)
+        exps[r] = _expected_rows(n, t, h, E, A, s, sp, base=d0)
+
+    def call(r, d0, d1, o2, o4, oA, op):
+        be.ceremony_shard_verify_device(n, t, d0, d1, tE[32 * N * d0:].data_ptr(), tA[32 * N * d0:].data_ptr(),
+                                        ts[32 * n * d0:].data_ptr(), tsp[32 * n * d0:].data_ptr(), o2.data_ptr(),
+                                        o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+        D = d1 - d0
+        _check_rank(n, d0, o2[:D * n].view(D, n), o4[:D * n].view(D, n), exps[r], (n, r, be.last_split()))
+        return ts[32 * n * d0:]
+
+    p = shard_play.play(be, n, t, ws, call, ts.device)
+    single = be.ceremony_verify(bytes(tE.cpu().numpy()), bytes(tA.cpu().numpy()), bytes(ts.cpu().numpy()),
+                                bytes(tsp.cpu().numpy()), n, t)
+    o = p.outcome
+    assert p.dec2 == bytes(single.dec2) and p.dec4 == bytes(single.dec4)
+    assert o.qualified == single.qualified and o.reconstruct == single.reconstruct
+    assert o.complaints2 == single.complaints2 and o.r2_error == single.r2_error and o.r4_error == single.r4_error
+    assert o.phase4_error == bool(single.phase4_error) and o.n_qualified == single.n_qualified
+    assert p.final_share == single.final_share and p.public_share == single.public_share
+    assert p.mpk == single.mpk and p.mpk != bytes(32)
+    bad = {dkg_amd.shard_range(n, ws, r)[0] + i for r in range(ws) for i in (0, 1, 3, 4)}
+    assert o.qualified == [int(i not in bad) for i in range(n)]
+    assert o.reconstruct == [int(i in {dkg_amd.shard_range(n, ws, r)[0] + 2 for r in range(ws)}) for i in range(n)]
