@@ -12,6 +12,13 @@ import numpy as np
 REJECT, ACCEPT, SELF, SKIPPED, MISSING = 0, 1, 2, 3, 4
 
 
+def _u8(x):
+    """uint8 array view of bytes / bytearray / arrays / tensors already on the host."""
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(x), dtype=np.uint8)
+    return np.asarray(x, dtype=np.uint8)
+
+
 def dealer_range(rank, ws, n):
     return (rank * n) // ws, ((rank + 1) * n) // ws
 
@@ -23,14 +30,14 @@ def rows_per_rank(ws, n):
 def compact(gathered, ws, n, width):
     """[ws][R][width] padded blocks (flat) -> dense [n][width] (numpy uint8)."""
     R = rows_per_rank(ws, n)
-    g = np.asarray(gathered, dtype=np.uint8).reshape(ws, R, width)
+    g = _u8(gathered).reshape(ws, R, width)
     return np.concatenate([g[r, :dealer_range(r, ws, n)[1] - dealer_range(r, ws, n)[0]] for r in range(ws)])
 
 
 def pad(dense, ws, n, width, fill=0xEE):
     """dense [n][width] -> the [ws][R][width] layout an all-gather produces (padding rows = fill)."""
     R = rows_per_rank(ws, n)
-    d = np.asarray(dense, dtype=np.uint8).reshape(n, width)
+    d = _u8(dense).reshape(n, width)
     out = np.full((ws, R, width), fill, dtype=np.uint8)
     for r in range(ws):
         a, b = dealer_range(r, ws, n)
@@ -57,8 +64,8 @@ def combine(dec2, dec4, n, t) -> Outcome:
     disqualified dealers are skipped in round 4 (:522); a round-4 REJECT puts a qualified dealer in the
     reconstruction set (:660-670); receiver j counts itself plus the qualified dealers it accepted in
     round 4 (:515-516, 567-569); qualified minus reconstructable <= t fails Phase4 (:673-677)."""
-    dec2 = np.asarray(dec2, dtype=np.uint8).reshape(n, n)
-    dec4 = np.array(dec4, dtype=np.uint8).reshape(n, n)
+    dec2 = _u8(dec2).reshape(n, n)
+    dec4 = _u8(dec4).reshape(n, n).copy()
     rej2 = dec2 == REJECT
     qualified = (~(rej2 | (dec2 == MISSING)).any(axis=1)).astype(np.uint8)
     complaints = rej2.sum(axis=0).astype(np.int32)
