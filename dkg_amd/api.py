@@ -149,6 +149,10 @@ class Backend:
         2 column sums; results are identical."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_field_mode(self._ctx, mode))
 
+    def set_binomial(self, mode: int):
+        """0 (default) / 2: the binomial as one persistent dataflow launch; 1: one launch per step."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
+
     def set_stepping(self, mode: int):
         """Stepping slots of a split table: 0 cost model, 1 one per column (all pieces), 2 one per
         piece; results are identical."""

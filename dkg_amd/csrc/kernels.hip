@@ -470,6 +470,148 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
   return in;
 }
 
+// ---- The same Horner steps as ONE persistent dataflow launch (k_binom_flow) ----
+// Item (r, m, cw) = step r, position m >= 1, column wave cw (64 columns of one piece): e'_m =
+// m (e_{m-1} + e_m) needs positions m-1 and m of step r-1 of the SAME columns, and it overwrites
+// position m of step r-2 (ping-pong), which items (r-1, m) and (r-1, m+1) read.  So it waits for
+// done[cw][m'] >= r-1, m' in {m-1, m, m+1} (those that exist at step r-1); position 0 of step r-1 is
+// the coefficient C_{L-r}, read from C.  Items are handed out in the order (r ascending, m
+// descending -- the longest NAF chains of a step first --, cw ascending) by a ticket counter, four
+// consecutive items per workgroup (one per wave), so every item waits only on items dequeued before
+// it by running waves: no deadlock at any residency, and the t launch tails of the per-step grid --
+// each drained to zero before the next step could start -- overlap the next step's work.
+// Hand-off (cdna_hip_programming.md Guideline 16, recipe R1): the producer stores its point
+// write-through (sc1), waits for the stores, then one lane stores the flag (agent-scope atomic);
+// the consumer polls relaxed, then ONE agent acquire, then plain loads.  Spins are bounded: a wait
+// that gives up sets *err (the host raises) and the wave carries on, so the grid always drains.
+typedef __attribute__((address_space(1))) uint32_t flow_gu32;
+constexpr int FLOW_WAVES = 4;
+constexpr uint32_t FLOW_SPIN_LIMIT = 1u << 20;  // polls (~1 us each) before a wait gives up
+
+__device__ __forceinline__ uint32_t flow_ld(const uint32_t* p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load((flow_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// wait until *flag >= want; false (and *err set) if the wait gave up.  Once *err is set anywhere,
+// every wait returns at its first check, so the grid drains in a few loads per item.
+__device__ __forceinline__ bool flow_wait(const uint32_t* flag, uint32_t want, uint32_t* err) {
+  for (uint32_t spins = 0;; spins++) {
+    if (flow_ld(flag) >= want) return true;
+    if (spins >= FLOW_SPIN_LIMIT || ((spins & 255u) == 0u && flow_ld(err))) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store((flow_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+DKG_DEV void pt_store_wt(uint32_t* __restrict__ base, size_t stride, size_t e, const ge_p3& p) {
+#pragma unroll
+  for (int w = 0; w < PT_WORDS; w++)
+    __hip_atomic_store((flow_gu32*)(base + (size_t)w * stride + e), pt_word(p, w), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64 * FLOW_WAVES, 4) void k_binom_flow(int L, size_t npad, const uint32_t* __restrict__ C,
+                                                                  uint32_t* e0, uint32_t* e1, size_t pstride,
+                                                                  unsigned gx, unsigned CW, unsigned last_piece,
+                                                                  int last_off, uint32_t* done, uint32_t* ticket,
+                                                                  uint32_t* err, unsigned long long total) {
+  // each wave's cached addend (lane-interleaved); the dequeued ticket is broadcast through word 0 of
+  // wave 0's slot, which wave 0 rewrites only after the second barrier (40 KB exactly: 4 workgroups
+  // = 16 waves per CU)
+  __shared__ uint32_t qs[FLOW_WAVES][PT_WORDS * 64];
+  uint32_t& tk = qs[0][0];
+  // wave-uniform values go through readfirstlane so that they live in SGPRs (the chain needs the
+  // VGPRs: <= 128 for 4 waves per SIMD)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint32_t* q = qs[wave] + lane;
+  const size_t S = (size_t)L * npad;
+  for (;;) {
+    if (threadIdx.x == 0) tk = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const unsigned long long first = (unsigned long long)__builtin_amdgcn_readfirstlane(tk) * FLOW_WAVES;
+    __syncthreads();  // tk is rewritten by the next iteration's dequeue
+    if (first >= total) break;  // workgroup-uniform exit
+    const unsigned long long item = first + wave;
+    if (item < total) {
+      // decode (r, m, cw): CW * r (r - 1) / 2 items precede step r
+      const unsigned long long x = item / CW;
+      int r = __builtin_amdgcn_readfirstlane((int)((sqrtf(8.0f * (float)x + 1.0f) + 1.0f) * 0.5f));
+      while ((unsigned long long)r * (r - 1) / 2 > x) r--;
+      while ((unsigned long long)(r + 1) * r / 2 <= x) r++;
+      const unsigned long long off = item - (unsigned long long)CW * ((unsigned long long)r * (r - 1) / 2);
+      const int m = __builtin_amdgcn_readfirstlane(r - (int)(off / CW));
+      const unsigned cw = __builtin_amdgcn_readfirstlane((unsigned)(off % CW));
+      const unsigned piece = cw / gx, grp = cw - piece * gx;
+      const size_t d = piece * pstride + (size_t)grp * 64 + lane;
+      uint32_t* fl = done + (size_t)cw * L;
+      const uint32_t prev = (uint32_t)(r - 1);
+      if (m >= 2) flow_wait(fl + m - 1, prev, err);
+      if (m <= r - 1) flow_wait(fl + m, prev, err);
+      if (m + 1 <= r - 1) flow_wait(fl + m + 1, prev, err);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const uint32_t* ein = (r & 1) ? e0 : e1;  // step r reads step r-1's table
+      uint32_t* eout = (r & 1) ? e1 : e0;
+      // a short last piece (last_off = L - its length) has degree re = r - last_off after step r;
+      // positions above re are never read
+      const int re = r - (piece == last_piece ? last_off : 0);
+      if (m <= re) {
+        {
+          ge_p3 cur;
+          pt_load(cur, ein, S, (size_t)m * npad + d);
+          // position re of step r-1 does not exist (identity); branch-free, opaque select as in
+          // k_binom_step (the load of that slot is harmless: it is masked)
+          uint32_t keep = (m == re) ? 0u : 0xffffffffu;
+          asm volatile("" : "+v"(keep));
+          uint32_t* cw32 = reinterpret_cast<uint32_t*>(&cur);
+#pragma unroll
+          for (int w = 0; w < PT_WORDS; w++) cw32[w] = (cw32[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
+          ge_cached cc;
+          ge_to_cached(cc, cur);
+          lds_put_cached(q, cc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        ge_p3 xv;
+        // position 0 of step r-1 is C_{L-r}
+        pt_load(xv, m == 1 ? C : ein, S, (size_t)(m == 1 ? L - r : m - 1) * npad + d);
+        ge_add_lds(xv, xv, q, false);        // e_{m-1} + e_m
+        mul_small_lds(xv, (uint32_t)m, q);   // * m
+        pt_store_wt(eout, S, (size_t)m * npad + d, xv);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the point has completed
+      if (lane == 0) __hip_atomic_store((flow_gu32*)(fl + m), (uint32_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Flow items of a chunk: L(L-1)/2 per column wave
+unsigned long long binom_flow_items(size_t width, size_t pieces, size_t L) {
+  return (unsigned long long)(width / 64 * pieces) * (unsigned long long)L * (L - 1) / 2;
+}
+
+// done: [width/64 * pieces][L] words and ticket, err: one word each, all zeroed by the caller before
+// the launch.  Returns the table holding the result (position 0 included).
+uint32_t* binomial_flow(size_t width, size_t npad, size_t L, const uint32_t* C, uint32_t* e0, uint32_t* e1,
+                        hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* done,
+                        uint32_t* ticket, uint32_t* err, unsigned grid_cap) {
+  binom_init(width, npad, L, C, e0, stream, pieces, pstride);
+  if (L < 2) return e0;
+  const unsigned CW = (unsigned)(width / 64 * pieces);
+  const unsigned long long total = binom_flow_items(width, pieces, L);
+  const int last_off = (last_len && last_len < L) ? (int)(L - last_len) : 0;
+  const unsigned long long wgs = (total + FLOW_WAVES - 1) / FLOW_WAVES;
+  const unsigned grid = (unsigned)(wgs < grid_cap ? wgs : grid_cap);
+  hipLaunchKernelGGL(k_binom_flow, dim3(grid), dim3(64 * FLOW_WAVES), 0, stream, (int)L, npad, C, e0, e1, pstride,
+                     (unsigned)(width / 64), CW, (unsigned)(pieces - 1), last_off, done, ticket, err, total);
+  uint32_t* fin = ((L - 1) & 1) ? e1 : e0;
+  // position 0 after the last step is C_0 (the flow never writes position 0)
+  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,
+                     npad, L, C, (size_t)0, fin, pstride);
+  return fin;
+}
+
 // ------------------------------------------------------------------ K3b stepping
 // D_m <- D_m + D_{m+1} (m = 0..t-1) once per receiver; D_0 after step j is P_i(j+1).
 // Positions are cut into blocks of BS lanes (one position per lane, registers only).  D_m depends

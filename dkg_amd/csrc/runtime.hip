@@ -41,6 +41,11 @@ struct dkg_ctx {
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
+  int binom_mode = 0;                   // binomial: 0/2 one dataflow launch (k_binom_flow), 1 one
+                                        // launch per Horner step (k_binom_step)
+  uint32_t* flow_state = nullptr;       // dataflow binomial: per chunk [flags | ticket | err] words,
+  size_t flow_chunk_words = 0;          // flow_chunk_words per chunk; err at word flow_chunk_words-1
+  size_t flow_chunks = 0;               // chunks whose err word the next sync checks
   int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece
   int fe_mode = 0;                      // field multiplication per launch: 0 by occupancy, 1 product
                                         // scanning (dkgk), 2 column sums (dkgk_ilp)
@@ -73,6 +78,10 @@ struct dkg_ctx {
   std::string timed_tag;                // set while pev[] hold a serialised verify_device's phases
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
+
+namespace ContextLimits {
+constexpr size_t MAX_FLOW_CHUNKS = 8;  // = dkg_ctx::MAX_SUB
+}
 
 namespace {
 
@@ -124,7 +133,21 @@ void h2d(dkg_ctx* ctx, void* d, const void* h, size_t n) {
 void d2h(dkg_ctx* ctx, void* h, const void* d, size_t n) {
   if (n) HCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->stream));
 }
-void sync(dkg_ctx* ctx) { HCK(hipStreamSynchronize(ctx->stream)); }
+void sync(dkg_ctx* ctx) {
+  HCK(hipStreamSynchronize(ctx->stream));
+  if (ctx->flow_chunks) {  // the dataflow binomial's bounded waits (kernels.hip k_binom_flow)
+    const size_t k = ctx->flow_chunks;
+    ctx->flow_chunks = 0;
+    std::vector<uint32_t> err(k);
+    for (size_t c = 0; c < k; c++)
+      HCK(hipMemcpy(&err[c], ctx->flow_state + (c + 1) * ctx->flow_chunk_words - 1, 4, hipMemcpyDeviceToHost));
+    for (uint32_t e : err)
+      if (e) {
+        ctx->err = "binomial dataflow: a dependency wait gave up (results invalid)";
+        throw Fail{DKG_E_DEVICE};
+      }
+  }
+}
 void check_launch(dkg_ctx* ctx) { HCK(hipGetLastError()); }
 
 size_t pad64(size_t x) { return (x + 63) / 64 * 64; }
@@ -524,18 +547,40 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     }
   };
   // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
-  auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
+  // dataflow binomial state: per chunk the flags of its column waves ([cw][L]), the ticket and the
+  // err word, zeroed on the chunk's stream before its launch
+  const bool flow = ctx->binom_mode != 1 && L > 1;
+  if (flow) {
+    ctx->flow_chunk_words = (npad / 64 * U * L + 2 + 63) / 64 * 64;
+    ctx->flow_state = buf<uint32_t>(ctx, "v.flow", 4 * ctx->flow_chunk_words * ContextLimits::MAX_FLOW_CHUNKS);
+  }
+  // persistent grid: 4 workgroups (16 waves) per CU fill the chip; chunks launched side by side share it
+  const unsigned flow_grid = 1024;
+  auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm, size_t chunk_idx) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
-    uint32_t *bin = e0 + c0, *bout = e1 + c0;
-    for (size_t r = 1; r < L; r++) {
-      // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
-      const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (r + 1) / 1024 < 1.5);
-      (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
-      std::swap(bin, bout);
+    const uint32_t* e;
+    if (flow) {
+      // one persistent dataflow launch for all L-1 steps: the column-sum copy when the whole table
+      // averages fewer than 1.5 waves per SIMD per step (small shards: latency-bound chains)
+      const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (L / 2.0) / 1024 < 1.5);
+      uint32_t* fs = ctx->flow_state + chunk_idx * ctx->flow_chunk_words;
+      HCK(hipMemsetAsync(fs, 0, 4 * ctx->flow_chunk_words, st));
+      const size_t fl_words = (w / 64) * U * L;
+      e = (ilp ? dkgk_ilp::binomial_flow : dkgk::binomial_flow)(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad,
+                                                               Lr, fs, fs + fl_words, fs + ctx->flow_chunk_words - 1,
+                                                               flow_grid);
+    } else {
+      dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
+      uint32_t *bin = e0 + c0, *bout = e1 + c0;
+      for (size_t r = 1; r < L; r++) {
+        // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
+        const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (r + 1) / 1024 < 1.5);
+        (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+        std::swap(bin, bout);
+      }
+      e = bin;
     }
-    const uint32_t* e = bin;
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
@@ -567,7 +612,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
   ctx->timed_tag.clear();
   if (nsub <= 1) {
-    chunk(0, groups, home, timed);
+    chunk(0, groups, home, timed, 0);
     if (timed) ctx->timed_tag = tag;
   } else {
     HCK(hipEventRecord(ctx->fork, home));
@@ -575,12 +620,13 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     for (size_t c = 0; c < nsub; c++) {
       const size_t g1 = groups * (c + 1) / nsub;
       HCK(hipStreamWaitEvent(ctx->sub[c], ctx->fork, 0));
-      chunk(g0, g1, ctx->sub[c], false);
+      chunk(g0, g1, ctx->sub[c], false, c);
       HCK(hipEventRecord(ctx->join[c], ctx->sub[c]));
       HCK(hipStreamWaitEvent(home, ctx->join[c], 0));
       g0 = g1;
     }
   }
+  if (flow) ctx->flow_chunks = std::max<size_t>(ctx->flow_chunks, std::max<size_t>(nsub, 1));
   check_launch(ctx);
 }
 
@@ -1397,6 +1443,12 @@ size_t dkg_ctx_fallback_rows(const dkg_ctx* ctx) { return ctx ? ctx->fallback_ro
 int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
   if (!ctx || pieces < 0 || pieces > 16) return DKG_E_ARG;
   ctx->split = pieces;
+  return DKG_OK;
+}
+
+int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return DKG_E_ARG;
+  ctx->binom_mode = mode;
   return DKG_OK;
 }
 

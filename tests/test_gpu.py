@@ -779,6 +779,32 @@ def test_field_modes_goldens(be, golden, name, mode):
         be.set_split(0)
 
 
+@pytest.mark.parametrize("field", [1, 2])
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json", "ceremony_n16_t7.json", "ceremony_n3_t1.json"])
+def test_binomial_schedules_goldens(be, golden, name, field):
+    """Both schedules of the binomial-basis Horner (dkg_ctx_set_binomial): one launch per step, and
+    the persistent dataflow launch (k_binom_flow) in both field-multiplication copies, with and
+    without a degree split (short last pieces included), one and two chunk streams: every output
+    bit-exact against the fixture."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    try:
+        be.set_field_mode(field)
+        for mode in (1, 2):
+            be.set_binomial(mode)
+            for pieces, streams in ((1, 2), (min(3, t + 1), 1), (min(2, t + 1), 2)):
+                be.set_split(pieces)
+                be.set_streams(streams)
+                r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+                _check_ceremony(c, r, n)
+    finally:
+        be.set_field_mode(0)
+        be.set_binomial(0)
+        be.set_split(0)
+        be.set_streams(2)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json"])
 def test_stepping_modes_goldens(be, golden, name, mode):

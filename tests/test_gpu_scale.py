@@ -497,3 +497,30 @@ def test_shard_ranks_n1024_all_match_single(be):
     bad = {dkg_amd.shard_range(n, ws, r)[0] + i for r in range(ws) for i in (0, 1, 3, 4)}
     assert o.qualified == [int(i not in bad) for i in range(n)]
     assert o.reconstruct == [int(i in {dkg_amd.shard_range(n, ws, r)[0] + 2 for r in range(ws)}) for i in range(n)]
+
+
+@pytest.mark.parametrize("n,t,split", [(1024, 511, 4), (1024, 511, 3), (1100, 549, 2), (300, 149, 1)])
+def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
+    """The dataflow binomial (k_binom_flow: all Horner steps in one persistent launch with
+    per-position dependency flags) against one launch per step at the BASELINE size and on ragged
+    ones (n=1100 at U=2: a short last piece joining 90 steps late; n=300 unsplit: a padded column
+    group), with tampered dealers: identical decision matrices, qualification, reconstruction and mpk
+    -- and the same as the oracle on the tampered rows (test_faults_baseline_sizes checks the flow
+    schedule, the default, against the oracle)."""
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([split + 7]) * 32, 9, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
+    _inject(random.Random(n + split), n, t, E, A, s, sp)
+    out = []
+    try:
+        be.set_split(split)
+        for mode in (2, 1):
+            be.set_binomial(mode)
+            r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            assert be.last_split() == split
+            out.append((r.dec2, r.dec4, r.qualified, r.reconstruct, r.mpk, r.final_share))
+    finally:
+        be.set_binomial(0)
+        be.set_split(0)
+    assert out[0] == out[1]
+    assert out[0][2][:5] == [0, 0, 1, 0, 0] and out[0][3][:5] == [0, 0, 1, 0, 0]
