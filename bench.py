@@ -51,7 +51,7 @@ SLOTS = {k: v[1] for k, v in VALU.items()}
 def kernel_rooflines(ph, work, work_i):
     """Per-kernel VALU roofline of a serialised pass: ph = device ms per kernel (HIP events)."""
     rl = {}
-    for k in ("binomial", "stepping", "combine", "check"):
+    for k in work:
         ms = ph.get(k, 0.0)
         if ms > 0:
             rl[k] = {"ms_per_pass": round(ms, 3), "valu_slots": work[k], "valu_instr": work_i[k],
@@ -65,6 +65,41 @@ def roofline_line(rl, dom, work_text):
     return {"bound": "valu-issue", "kernel": dom, "achieved": ach, "peak": INT32_PEAK / 1e12,
             "unit": "T VALU issue slots/s", "frac": ach / (INT32_PEAK / 1e12), "instr_frac": rl[dom]["instr_frac"],
             "traffic": None, "work": work_text, "all_kernels": rl}
+
+
+# Full mode (hybrid encryption, hybrid.hip): per item (dealer, recipient, w) closed forms.  Encode /
+# decode: one fe_pow22523 (252 squarings + 11 products) plus the Ristretto map's products
+# (ge25519.h ristretto_encode / ristretto_decode: 11 and 13 more); Blake2b-512 of one block (12
+# rounds x 8 G: six 64-bit adds at 3 slots, four 64-bit xors at 2, three non-trivial 64-bit
+# rotates at 4) + one ChaCha20 block (20 rounds x 4 quarter-rounds: 4 adds, 4 xors, 4 rotates at 2)
+# + the 32-byte XOR: an op-count model (its loops defeat a static count).
+HY_ENCODE = (252, 22)   # (fe_sq, fe_mul)
+HY_DECODE = (252, 24)
+HY_SYM_SLOTS = 12 * 8 * (6 * 3 + 4 * 2 + 3 * 4) + 20 * 4 * (4 + 4 + 4 * 2) + 64
+
+
+def hybrid_valu(n, sk, VALU=SLOTS):
+    """Closed-form VALU work of full mode's encryption and decryption of all 2 n^2 items (n dealers x n
+    recipients x {randomness, share}): k_enc_mul (26 radix-2^10 windows of g + 64 radix-16 windows of
+    pk_q per item), k_dec_mul (sk_q's NAF: one doubling per digit below the top, an addition per
+    nonzero digit, wave-uniform), the encode / decode kernels and k_sym_xor (model above)."""
+    items = 2 * n * n
+    enc = items * (COMBW_WINDOWS * VALU["combw_window"] + 64 * VALU["comb_window"])
+    dec = 0
+    for q in range(n):
+        ds = _naf(int.from_bytes(sk[32 * q:32 * q + 32], "little"))
+        c = VALU["ge_to_cached"]
+        for i in range(len(ds) - 2, -1, -1):
+            nz = ds[i] != 0
+            c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
+            if nz:
+                c += VALU["ge_add_signed"]
+        dec += 2 * n * c
+    encode = HY_ENCODE[0] * VALU["fe_sq"] + HY_ENCODE[1] * VALU["fe_mul"]
+    decode = HY_DECODE[0] * VALU["fe_sq"] + HY_DECODE[1] * VALU["fe_mul"]
+    sym = HY_SYM_SLOTS if VALU is SLOTS else HY_SYM_SLOTS * 0.7
+    return {"enc_mul": enc, "enc_encode": 2 * items * encode, "enc_sym": items * sym,
+            "dec_decode": items * decode, "dec_mul": dec, "dec_encode": items * encode, "dec_sym": items * sym}
 
 
 PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
@@ -307,14 +342,17 @@ def host_cpu():
                    "os_cpu_count": os.cpu_count()}
 
 
-def cpu_baseline(n, t, seconds_target=20.0):
+def cpu_baseline(n, t, seconds_target=20.0, ceremonies=1):
     """Reference-algorithm CPU baseline of the WHOLE ceremony, extrapolated from a bounded sample.
     The oracle follows dalek-3's u64 algorithms (5x51 field, radix-16 variable-base mul, Straus /
-    Pippenger MSM at dalek's thresholds) loop for loop with committee.rs.  On batches of 8 dealers it
-    times round-1 share generation (commitments + all n shares, committee.rs:148-186), round-2 checks
+    Pippenger MSM at dalek's thresholds) loop for loop with committee.rs.  On blocks of dealers
+    (8 up to n = 1024, 2 above: a block of n = 4096 dealers is 2 x 8190 MSMs of 2048 points) it times
+    round-1 share generation (commitments + all n shares, committee.rs:148-186), round-2 checks
     (:287-305) and round-4 checks (:532-548) against all receivers on every host core, until about
-    `seconds_target` seconds; the ceremony time is n x (share gen per dealer) + n(n-1) x (round-2 +
-    round-4 per pair) -- rounds 3 and 5 are negligible -- and value = n(n-1) / that time."""
+    `seconds_target` seconds, moving on to the next ceremony (other seeds) when one is complete
+    (small n, config 5); the ceremony time is n x (share gen per dealer) + n(n-1) x (round-2 +
+    round-4 per pair) -- rounds 3 and 5 are negligible -- and value = n(n-1) / that time (the same
+    rate in verified shares/s for `ceremonies` independent ceremonies)."""
     import ctypes
 
     from tests import oracle_lib as O
@@ -329,41 +367,48 @@ def cpu_baseline(n, t, seconds_target=20.0):
     fe_ns = lib.or_bench_fe_mul(5_000_000)
     msm_ms = lib.or_bench_msm(t + 1, 3)
     master = b"\x05" * 32
-    nd = 8
+    nd = min(n, 8 if n <= 1024 else 2)
     h = O.call32("or_pt_hash_to_group", b"Example of a shared string.", 27)[0]
     t_gen = t_r2 = t_r4 = 0.0
     dealers = pairs = 0
-    while t_gen + t_r2 + t_r4 < seconds_target and dealers + nd <= n:
-        d0 = dealers
-        a, b = dkg_amd.dealer_coefficients(master, 0, d0, nd, t)
+    cer = d0 = 0
+    warm = False
+    while t_gen + t_r2 + t_r4 < seconds_target:
+        if d0 + nd > n:  # this ceremony is complete: the next one
+            if n > 1024:
+                break
+            cer, d0 = cer + 1, 0
+        a, b = dkg_amd.dealer_coefficients(master, cer, d0, nd, t)
         t0 = time.perf_counter()
         E, A, s, sp = O.share_gen(nd, n, t, a, b, h, cores)
         t_gen += time.perf_counter() - t0
-        # rows of the sampled dealers at their own indices; other rows are never read
-        pad = lambda x, w: bytes(w * d0) + x + bytes(w * (n - d0 - nd))  # noqa: E731
-        C2, C4, S, SP = pad(E, 32 * (t + 1)), pad(A, 32 * (t + 1)), pad(s, 32 * n), pad(sp, 32 * n)
-        if dealers == 0:
-            O.verify_pairs(n, t, 2, C2, h, S, SP, d0, d0 + nd, 0, 1, cores)  # warm the thread pool
+        # rows of the sampled dealers at their own indices (the diagonal stays global)
+        if not warm:
+            O.verify_rows(n, t, 2, E, h, s, sp, d0, d0 + nd, 0, 1, cores)  # warm the thread pool
+            warm = True
         t0 = time.perf_counter()
-        acc2, _ = O.verify_pairs(n, t, 2, C2, h, S, SP, d0, d0 + nd, 0, n, cores)
+        acc2, _ = O.verify_rows(n, t, 2, E, h, s, sp, d0, d0 + nd, 0, n, cores)
         t_r2 += time.perf_counter() - t0
         t0 = time.perf_counter()
-        acc4, _ = O.verify_pairs(n, t, 4, C4, h, S, None, d0, d0 + nd, 0, n, cores)
+        acc4, _ = O.verify_rows(n, t, 4, A, h, s, None, d0, d0 + nd, 0, n, cores)
         t_r4 += time.perf_counter() - t0
         assert set(acc2) <= {1, 2} and set(acc4) <= {1, 2}
         dealers += nd
+        d0 += nd
         pairs += sum(1 for x in acc2 if x == 1)
     gen_per_dealer, r2_per_pair, r4_per_pair = t_gen / dealers, t_r2 / pairs, t_r4 / pairs
     ceremony_s = n * gen_per_dealer + n * (n - 1) * (r2_per_pair + r4_per_pair)
+    what = (f"{dealers // n} whole ceremonies + {dealers % n} dealers" if dealers >= n
+            else f"{dealers} dealers x all {n} receivers")
     return {"value": n * (n - 1) / ceremony_s, "unit": "verified shares/s", "cores": cores, "kind": "port",
-            "ceremony_s_extrapolated": ceremony_s,
+            "ceremony_s_extrapolated": ceremony_s, "batch_s_extrapolated": ceremony_s * ceremonies,
             "round1_ms_per_dealer": gen_per_dealer * 1e3, "round2_ms_per_pair": r2_per_pair * 1e3,
             "round4_ms_per_pair": r4_per_pair * 1e3,
             "fe_mul_ns_1thread": fe_ns, f"msm_N{t + 1}_ms_1thread": msm_ms, **cpu,
-            "sample": f"{dealers} dealers x all {n} receivers at n={n}, t={t} ({pairs} pairs): share generation, "
-                      f"round-2 and round-4 checks (vartime MSM over t+1={t + 1} points per pair, dalek-3's "
-                      f"algorithms) timed on {cores} threads in {t_gen + t_r2 + t_r4:.1f} s; whole-ceremony "
-                      f"time extrapolated linearly in dealers and pairs"}
+            "sample": f"{what} at n={n}, t={t} ({pairs} pairs): share generation, round-2 and round-4 checks "
+                      f"(vartime MSM over t+1={t + 1} points per pair, dalek-3's algorithms) timed on {cores} "
+                      f"threads in {t_gen + t_r2 + t_r4:.1f} s; time of {ceremonies} ceremon"
+                      f"{'ies' if ceremonies > 1 else 'y'} extrapolated linearly in dealers and pairs"}
 
 
 def bench_batch(args, ws, rank, local):
@@ -412,6 +457,17 @@ def bench_batch(args, ws, rank, local):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     assert all(q == n for q in res.n_qualified), "an honest ceremony disqualified a dealer"
+    # per-kernel device times: one extra serialised batch (one chunk stream)
+    be.set_streams(1)
+    step()
+    torch.cuda.synchronize()
+    be.set_streams(args.streams)
+    ph = be.phase_times("r24")
+    U, Ls = be.last_split(), be.last_split_len()
+    mults = dkg_amd.split_multipliers(n, Ls, U) if be.last_combine() == 2 else None
+    work = {k: v * B for k, v in fused_valu(n, t, U, plen=Ls, mults=mults).items()}
+    work_i = {k: v * B for k, v in fused_valu(n, t, U, INSTR, Ls, mults).items()}
+    rl = kernel_rooflines(ph, work, work_i)
     pairs = B * n * (n - 1) * ws  # whole node: every rank runs its own B ceremonies
     out = {"metric": f"verified shares/sec (whole node) of {B} independent n={n},t={t} ceremonies per GPU "
                      f"x {ws} GPU(s) (BASELINE config 5)",
@@ -424,6 +480,15 @@ def bench_batch(args, ws, rank, local):
                       "pairs_per_step": pairs, "parallelism": f"replicas x{ws}" if ws > 1 else "single GPU"},
            "ceremonies_per_s": B * ws * args.steps / elapsed,
            "phases_ms": {k: round(v, 3) for k, v in res.ms.items()}}
+    out["config"]["degree_split"] = U
+    if rl:
+        dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
+        out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} instructions) "
+                                                 f"per batch: {B} x the closed form of one ceremony's fused "
+                                                 f"round-2/4 pipeline; device time in a serialised batch")
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(n, t, 20.0, ceremonies=B)
+        out["gpu_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     be.close()
@@ -455,6 +520,8 @@ def main():
                     help="short-multiplier recombination addends: 0 affine Niels, 1 cached projective")
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
+    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2],
+                    help="binomial schedule: 0/2 one persistent dataflow launch, 1 one launch per Horner step")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")
@@ -483,6 +550,7 @@ def main():
     be.set_combine(args.combine)
     be.set_addends(args.addends)
     be.set_stepping_formula(args.step_formula)
+    be.set_binomial(args.binomial)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1
@@ -557,6 +625,40 @@ def main():
         out["config"]["mode"] = "full: shares hybrid-encrypted (elgamal.rs) and decrypted by each receiver"
     if rank == 0 and ws == 1 and res is not None and args.mode == "full":
         out["phases_ms"] = {k: round(v, 3) for k, v in res.ms.items()}
+        # per-kernel roofline of the whole full-mode ceremony: one serialised extra ceremony
+        be.set_streams(1)
+        step()
+        torch.cuda.synchronize()
+        be.set_streams(args.streams)
+        ph = dict(be.phase_times("r24"))
+        ph.update(be.phase_times("full"))
+        U, Ls = be.last_split(), be.last_split_len()
+        mults = dkg_amd.split_multipliers(n, Ls, U) if be.last_combine() == 2 else None
+        work = fused_valu(n, t, U, plen=Ls, mults=mults)
+        work_i = fused_valu(n, t, U, INSTR, Ls, mults)
+        work.update(hybrid_valu(n, msk))
+        work_i.update(hybrid_valu(n, msk, INSTR))
+        rl = kernel_rooflines(ph, work, work_i)
+        dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
+        out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} instructions) "
+                                                 f"per full-mode ceremony (closed form; hybrid kernels: "
+                                                 f"bench.py hybrid_valu); device time in a serialised ceremony")
+        if not args.no_cpu:
+            cb = cpu_baseline(n, t)
+            lib = __import__("tests.oracle_lib", fromlist=["lib"]).lib()
+            lib.or_bench_hybrid.restype = ctypes.c_double
+            lib.or_bench_hybrid.argtypes = [ctypes.c_size_t, ctypes.c_int]
+            items = 2 * n * n
+            sample = 40000
+            per_item = lib.or_bench_hybrid(sample, cb["cores"])
+            assert per_item > 0, "oracle hybrid round trip failed"
+            full_s = cb["ceremony_s_extrapolated"] + items * per_item
+            cb.update({"value": n * (n - 1) / full_s, "ceremony_s_extrapolated": full_s,
+                       "hybrid_us_per_item": per_item * 1e6,
+                       "sample": cb["sample"] + f"; plus hybrid encryption + decryption of {sample} sampled "
+                                                f"items (elgamal.rs:134-193), extrapolated to all {items}"})
+            out["cpu_baseline"] = cb
+            out["gpu_vs_cpu"] = value / cb["value"]
     if args.verify == "interp":
         out["metric"] += " -- committee verification by interpolation (identical decisions)"
         out["config"]["verify"] = ("interp: shares at receivers 1..t+1 fix F, F'; commitments tested once; "

@@ -197,13 +197,15 @@ class Backend:
 
     def phase_times(self, tag="r24") -> dict:
         """Device ms of binomial / stepping / combine / check in the last ceremony's checks: tag "r24" (rounds
-        2 and 4 fused, the default schedule), "r2" or "r4" (protocol order).  Only recorded with
+        2 and 4 fused, the default schedule), "r2" or "r4" (protocol order), "full" (the hybrid
+        encryption / decryption kernels of the last full-mode ceremony).  Only recorded with
         set_streams(1); -1 otherwise."""
         L = _lib.lib()
         if isinstance(tag, int):
             tag = f"r{tag}"
         names = (("interpolate", "coef_check", "decide", "fallback") if tag == "interp"
-                 else ("binomial", "stepping", "combine", "check"))
+                 else ("enc_mul", "enc_encode", "enc_sym", "dec_decode", "dec_mul", "dec_encode", "dec_sym")
+                 if tag == "full" else ("binomial", "stepping", "combine", "check"))
         return {k: L.dkg_ctx_phase_ms(self._ctx, f"{tag}.{k}".encode()) for k in names}
 
     def env_init(self, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT) -> bytes:

@@ -30,6 +30,8 @@ struct dkg_ctx {
   size_t threshold = 0, nr_members = 0;
   hipEvent_t ev[8] = {};
   hipEvent_t pev[5] = {};               // phase profiling inside verify_device (nsub == 1)
+  hipEvent_t hev[9] = {};               // full mode: encrypt / decrypt kernels (nsub == 1)
+  bool hy_timed = false;                // hev[] hold the last full-mode ceremony's phases
   static constexpr int MAX_SUB = 8;
   int nsub = 2;                         // dealer-chunk streams of verify_device
   hipStream_t sub[MAX_SUB] = {};
@@ -1243,10 +1245,16 @@ void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
   uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
   uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
+  // phase events (serialised runs, nsub == 1): the bench's per-kernel roofline of full mode
+  const bool tm = ctx->nsub == 1;
+  if (tm) HCK(hipEventRecord(ctx->hev[0], st));
   dkgk::enc_mul(D, n, r, ctx->tab_gw, tabs, R, K, st);
+  if (tm) HCK(hipEventRecord(ctx->hev[1], st));
   dkgk::encode_points(R, items, items, e1, st);
   dkgk::encode_points(K, items, items, Kc, st);
+  if (tm) HCK(hipEventRecord(ctx->hev[2], st));
   dkgk::sym_xor(D, n, Kc, false, ct, const_cast<uint32_t*>(s), const_cast<uint32_t*>(sp), st);
+  if (tm) HCK(hipEventRecord(ctx->hev[3], st));
   check_launch(ctx);
 }
 
@@ -1259,12 +1267,32 @@ void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const 
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
   uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
   uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
+  const bool tm = ctx->nsub == 1;
+  if (tm) HCK(hipEventRecord(ctx->hev[4], st));
   dkgk::decode_points(e1, items, R, items, item_ok, st);
+  if (tm) HCK(hipEventRecord(ctx->hev[5], st));
   dkgk::dec_mul(D, n, sk, R, K, st);
+  if (tm) HCK(hipEventRecord(ctx->hev[6], st));
   dkgk::encode_points(K, items, items, Kc, st);
+  if (tm) HCK(hipEventRecord(ctx->hev[7], st));
   dkgk::sym_xor(D, n, Kc, true, const_cast<uint32_t*>(ct), s, sp, st);
+  if (tm) HCK(hipEventRecord(ctx->hev[8], st));
   if (dealer_ok_out) dkgk::dealer_ok(D, 2 * n, item_ok, dealer_ok_out, st);
   check_launch(ctx);
+}
+
+// After a sync: the full-mode kernels' device times of the last serialised encrypt + decrypt
+// (dkg_ctx_phase_ms "full.enc_mul", "full.enc_encode", "full.enc_sym", "full.dec_decode",
+// "full.dec_mul", "full.dec_encode", "full.dec_sym").
+void collect_hybrid_phases(dkg_ctx* ctx) {
+  if (ctx->nsub != 1) return;
+  const char* names[8] = {"enc_mul", "enc_encode", "enc_sym", "", "dec_decode", "dec_mul", "dec_encode", "dec_sym"};
+  for (int i = 0; i < 8; i++) {
+    if (!names[i][0]) continue;
+    float ms = 0;
+    HCK(hipEventElapsedTime(&ms, ctx->hev[i], ctx->hev[i + 1]));
+    ctx->phase_ms[std::string("full.") + names[i]] = ms;
+  }
 }
 
 // ---- complaint proofs (dl_equality/zkp.rs, broadcast.rs:50-135, 181-283)
@@ -1364,6 +1392,7 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     HCK(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, greatest));
     for (auto& e : ctx->ev) HCK(hipEventCreate(&e));
     for (auto& e : ctx->pev) HCK(hipEventCreate(&e));
+    for (auto& e : ctx->hev) HCK(hipEventCreate(&e));
     for (auto& st : ctx->sub) HCK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
     HCK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
     HCK(hipEventCreateWithFlags(&ctx->side_fork, hipEventDisableTiming));
@@ -1404,6 +1433,8 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->pev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->hev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->join)
     if (e) (void)hipEventDestroy(e);
@@ -2500,6 +2531,7 @@ int dkg_ceremony_run_full_device(dkg_ctx* ctx, size_t n, size_t t, const void* d
     decrypt_device(ctx, n, n, dsk, e1, ct, rs, rsp, iok, eok);  // committee.rs:282-286
     ExtScope ext(ctx, n, N);
     receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, false, eok);
+    collect_hybrid_phases(ctx);
     out->ms_round1 = ev_ms(ctx, 0, 1);
     out->ms_round2 = ev_ms(ctx, 1, 2);
     out->ms_round3 = ev_ms(ctx, 2, 3);

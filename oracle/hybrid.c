@@ -9,6 +9,10 @@
  */
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "oracle.h"
 
@@ -231,4 +235,38 @@ int or_complaint3_verify(const uint8_t h[32], size_t t, uint32_t accuser, const 
   if (memcmp(pass, rE, 32) != 0) return 3;
   if (memcmp(fail, rA, 32) == 0) return 2;
   return 0;
+}
+
+/* ---- CPU baseline of full mode (bench.py --mode full): seconds per (encrypt + decrypt) of one
+ * 32-byte share, as committee.rs:169-172 and :282-286 do them for every (dealer, recipient, w),
+ * over `items` items on `nthreads` threads (recipients' keys cycle over 16 seeded members). */
+double or_bench_hybrid(size_t items, int nthreads) {
+  enum { K = 16 };
+  uint8_t sk[K][32], pk[K][32], master[32] = {9};
+  for (int j = 0; j < K; j++) {
+    or_member_sk(sk[j], master, 0, (uint32_t)j);
+    or_pt_base_mul(pk[j], sk[j]);
+  }
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+  struct timespec a, b;
+  int bad = 0;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+#pragma omp parallel for schedule(static) reduction(| : bad)
+  for (long long i = 0; i < (long long)items; i++) {
+    uint8_t r[32], msg[32], e1[32], e2[32], back[32], seed[32] = {0};
+    memcpy(seed, &i, sizeof i);
+    or_chacha20_stream(seed, 0, r, 32);
+    r[31] &= 0x0f;
+    memcpy(msg, r, 32);
+    msg[0] ^= 0x5a;
+    const int q = (int)(i % K);
+    bad |= or_hybrid_encrypt(e1, e2, pk[q], r, msg, 32);
+    bad |= or_hybrid_decrypt(back, sk[q], e1, e2, 32);
+    bad |= memcmp(back, msg, 32) != 0;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  if (bad) return -1.0;
+  return ((b.tv_sec - a.tv_sec) + 1e-9 * (b.tv_nsec - a.tv_nsec)) / (double)items;
 }

@@ -82,6 +82,8 @@ int or_verify_pairs_rows(size_t n, size_t t, int round, const uint8_t *C, const 
                          const uint8_t *s, const uint8_t *sp, size_t d0, size_t d1, size_t r0, size_t r1,
                          uint8_t *accept, int nthreads);
 /* ---- full (encrypted-share) mode: hybrid.c (elgamal.rs, procedure_keys.rs) ---- */
+/* bench.py's full-mode CPU baseline: seconds per encrypt + decrypt of one 32-byte share */
+double or_bench_hybrid(size_t items, int nthreads);
 void or_chacha20_ietf_xor(uint8_t *out, const uint8_t *in, size_t len, const uint8_t key[32],
                           const uint8_t nonce[12]);
 /* e1 = G r, e2 = msg XOR ChaCha20(Blake2b-512(pk r)) (elgamal.rs:134-145, 172-193); -1 if pk is invalid */

@@ -4,7 +4,7 @@ Rank 0 of an N-way split owns dealers [0, n/N); dkg_ceremony_shard_device runs e
 rank runs (share gen + round-2/4 checks of its rows against all n receivers + partial sums).  The
 RCCL all-gathers that follow are not included (they move n^2 * 2 bytes of decisions plus ~n*64 B).
 usage: python3 tools/shard_time.py [n t] [--no-overlap] [--streams K] [--split U] [--stepping M] [--field F]
-                                  [--combine C] [--ws 1,2,4,8]
+                                  [--combine C] [--binomial B] [--ws 1,2,4,8]
 """
 import argparse
 import json
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--stepping", type=int, default=0, help="stepping slots: 0 model, 1 per column, 2 per piece")
     ap.add_argument("--field", type=int, default=0, help="field multiply: 0 by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--combine", type=int, default=0, help="recombination: 0 short multipliers (U <= 4), 1 powers of j^L")
+    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule: 0/2 dataflow launch, 1 one launch per step")
     args = ap.parse_args()
     import torch
 
@@ -41,6 +42,7 @@ def main():
     be.set_stepping(args.stepping)
     be.set_field_mode(args.field)
     be.set_combine(args.combine)
+    be.set_binomial(args.binomial)
     be.env_init(t, n)
     dev = torch.device("cuda", 0)
     res = {}
@@ -69,6 +71,7 @@ def main():
         print(json.dumps({"n": n, "t": t, "ws": ws, "dealers": D, "ms_wall": res[ws],
                           "overlap": not args.no_overlap, "streams": args.streams, "split": be.last_split(),
                           "split_len": be.last_split_len(), "stepping": args.stepping, "field": args.field, "combine": be.last_combine(),
+                          "binomial": args.binomial,
                           "phases_ms_if_serialised": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     base = res.get(1)
     if base:
