@@ -521,7 +521,7 @@ def main():
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2],
-                    help="binomial schedule: 0/2 one persistent dataflow launch, 1 one launch per Horner step")
+                    help="binomial schedule: 0/1 one launch per Horner step, 2 one persistent dataflow launch")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")

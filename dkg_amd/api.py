@@ -150,7 +150,7 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_ctx_set_field_mode(self._ctx, mode))
 
     def set_binomial(self, mode: int):
-        """0 (default) / 2: the binomial as one persistent dataflow launch; 1: one launch per step."""
+        """0 (default) / 1: the binomial as one launch per Horner step; 2: one persistent dataflow launch."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
     def set_stepping(self, mode: int):

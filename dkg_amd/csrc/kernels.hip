@@ -675,7 +675,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
     uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast,
-    uint32_t* __restrict__ flags) {
+    uint32_t* __restrict__ flags, size_t col0, size_t dreal, unsigned gw) {
   const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
   if (!DED && flags && !flags[wg]) return;  // a redo launch: this workgroup's tables were exact
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
@@ -692,6 +692,11 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const int Pseg = sg == nseg - 1 ? Plast : P;
   const size_t dl = (size_t)blockIdx.x * (bs / Ncol) + slot;
   const bool live = slot < bs / Ncol && dl < ndealers;
+  // a column of a real dealer (dealer groups of 64 in `gw`-column groups; the padding columns of a
+  // group past the last dealer hold the identity, whose dedicated additions always have Z = 0):
+  // only real columns mark their workgroup for the complete redo
+  const size_t gcol = col0 + dl;
+  const bool real = live && (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
   const size_t d = (blockIdx.y + piece0 + sg) * pstride + dl;  // piece of a degree-split table
   const size_t S = N * npad;
   const size_t pos = pos0 + q;
@@ -735,7 +740,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     if (live && pos + 1 < Nlive && (q + 1 < Pseg || up) && pos + j < nrecv) {
       if (DED) {
         ge_add_ded_lds(D, D, nbr, MAXBS);
-        bad |= fe_tight_zero(D.Z);
+        bad |= real && fe_tight_zero(D.Z);
       } else {
         ge_add_lds(D, D, nbr, false, MAXBS);
       }
@@ -824,25 +829,32 @@ double stepping_waves_per_simd(size_t cols, size_t N, size_t pieces, size_t last
 
 size_t stepping_flag_words(size_t ndealers, size_t pieces) { return ndealers * (pieces + 1); }
 
+struct ColReal {  // which table columns belong to real dealers (k_stepping's `real`)
+  size_t col0, dreal;
+  unsigned gw;
+};
+
 template <bool DED>
 void step_launch(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t ndealers, size_t npad, size_t N,
                  const uint32_t* e, size_t nrecv, size_t pos0, int P, const uint32_t* up, uint32_t* down,
-                 uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags) {
+                 uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags,
+                 const ColReal& cr) {
   if (maxbs == 192)
     hipLaunchKernelGGL((k_stepping<192, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags);
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw);
   else if (maxbs == 256)
     hipLaunchKernelGGL((k_stepping<256, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags);
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw);
   else
     hipLaunchKernelGGL((k_stepping<512, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags);
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw);
 }
 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
-              size_t last_len, bool whole, uint32_t* flags) {
+              size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw) {
   if (!ndealers || !nrecv) return;
+  const ColReal cr{col0, dreal, gw ? gw : 64u};
   if (!last_len || last_len > N) last_len = N;
   // with flags (stepping_flag_words zeroed words): every launch below runs dedicated, then again
   // complete in its marked workgroups (its own flag words: a grid has at most ndealers x pieces)
@@ -851,10 +863,10 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
                  uint32_t* Rout, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* f) {
     if (f) {
       step_launch<true>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
-                        Nlive, piece0, nseg, Plast, f);
+                        Nlive, piece0, nseg, Plast, f, cr);
     }
     step_launch<false>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
-                       Nlive, piece0, nseg, Plast, f);
+                       Nlive, piece0, nseg, Plast, f, cr);
   };
   auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
     const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), (unsigned)np), block((unsigned)s.bs);
@@ -884,10 +896,10 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
           uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
           if (pass == 0)
             step_launch<true>(512, grid, block, stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down,
-                              b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f);
+                              b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f, cr);
           else
             step_launch<false>(512, grid, block, stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down,
-                               b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f);
+                               b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f, cr);
           up = down;
         }
       }

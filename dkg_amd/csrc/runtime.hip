@@ -43,8 +43,8 @@ struct dkg_ctx {
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
-  int binom_mode = 0;                   // binomial: 0/2 one dataflow launch (k_binom_flow), 1 one
-                                        // launch per Horner step (k_binom_step)
+  int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step),
+                                        // 2 one persistent dataflow launch (k_binom_flow)
   uint32_t* flow_state = nullptr;       // dataflow binomial: per chunk [flags | ticket | err] words,
   size_t flow_chunk_words = 0;          // flow_chunk_words per chunk; err at word flow_chunk_words-1
   size_t flow_chunks = 0;               // chunks whose err word the next sync checks
@@ -551,7 +551,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
   // dataflow binomial state: per chunk the flags of its column waves ([cw][L]), the ticket and the
   // err word, zeroed on the chunk's stream before its launch
-  const bool flow = ctx->binom_mode != 1 && L > 1;
+  const bool flow = ctx->binom_mode == 2 && L > 1;
   if (flow) {
     ctx->flow_chunk_words = (npad / 64 * U * L + 2 + 63) / 64 * 64;
     ctx->flow_state = buf<uint32_t>(ctx, "v.flow", 4 * ctx->flow_chunk_words * ContextLimits::MAX_FLOW_CHUNKS);
@@ -588,7 +588,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl);
+                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     if (short_mult && Aff) {
       dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st);
@@ -850,6 +850,9 @@ template <typename F>
 void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
                    const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
                    hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
+  // dkg_ctx_stepping_redos reports THIS verification's stepping (none if it builds no tables)
+  ctx->last_step_flags = nullptr;
+  ctx->last_step_flag_words = 0;
   if (ctx->verify_mode == 1)
     verify_rounds_interp(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok);
   else
@@ -1752,6 +1755,8 @@ int dkg_verify_receiver(dkg_ctx* ctx, size_t n, size_t t, int round, size_t j, c
                         const uint8_t* s_prime, uint8_t* decision) {
   return guarded(ctx, [&] {
     if ((round != 2 && round != 4) || j >= n) return DKG_E_ARG;
+    ctx->last_step_flags = nullptr;  // Horner per receiver: no stepping tables
+    ctx->last_step_flag_words = 0;
     if (round == 2) {
       int rc = need_env(ctx);
       if (rc) return rc;

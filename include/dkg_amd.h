@@ -71,9 +71,9 @@ int dkg_ctx_set_stepping(dkg_ctx *ctx, int mode);
  * product scanning (fewest issue slots), 2 always column sums (most independent chains; for
  * latency-bound launches).  Outputs do not depend on it. */
 int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
-/* Schedule of the binomial-basis Horner: 0 (default) and 2 -- all t steps in
- * ONE persistent dataflow launch (each item waits only for the three table positions of the previous
- * step it reads or overwrites); 1 -- one grid launch per step.  Outputs do not depend on it. */
+/* Schedule of the binomial-basis Horner: 0 (default) and 1 -- one grid launch
+ * per step; 2 -- all t steps in ONE persistent dataflow launch (each item waits only for the table
+ * positions of the previous step it reads or overwrites).  Outputs do not depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and

@@ -524,3 +524,20 @@ def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
         be.set_split(0)
     assert out[0] == out[1]
     assert out[0][2][:5] == [0, 0, 1, 0, 0] and out[0][3][:5] == [0, 0, 1, 0, 0]
+
+
+@pytest.mark.parametrize("n,t,split", [(100, 49, 0), (300, 149, 2), (1100, 549, 0), (65, 32, 3)])
+def test_honest_ragged_no_stepping_redo(be, n, t, split):
+    """Identity padding columns (a dealer count that is not a multiple of 64) are the identity, whose
+    dedicated additions always have Z = 0: they must not mark their workgroups for the complete redo
+    (runtime passes the real dealer count to k_stepping).  An honest ragged ceremony redoes nothing,
+    and dkg_ctx_stepping_redos reports the last verification only (0 after a receiver-view call)."""
+    be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([n % 251]) * 32, 4, 0, n, t)
+    try:
+        be.set_split(split)
+        r = be.ceremony(a, b, n, t)
+    finally:
+        be.set_split(0)
+    assert r.qualified == [1] * n and r.n_qualified == n
+    assert be.stepping_redos() == 0, (n, t, be.last_split())

@@ -1,5 +1,7 @@
 """Per-launch efficiency of the binomial step kernel from a rocprofv3 kernel-trace CSV
-(tools/profile.sh output).  usage: python3 tools/prof_binom.py gpurun_out/prof_<tag> [t n]"""
+(tools/profile.sh output): the launches of ONE serialised pass, step r covering positions 1..r of
+`cols` table columns (fused pass at n=1024, U=4: 2 n x 4 = 8192 columns of L = 128 positions).
+usage: python3 tools/prof_binom.py gpurun_out/prof_<tag> [L cols]"""
 import csv
 import os
 import sys
@@ -8,13 +10,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
-def main(d, t=511, n=1024):
+def main(d, t=128, n=8192):
+    """t = L (positions per piece), n = columns (pieces x 2 x dealers)."""
     rows = [r for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv")))
             if "binom" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    V = bench.VALU
+    V = bench.SLOTS
     cost = {}
-    for m in range(1, t + 1):
+    for m in range(1, t):
         ds = bench._naf(m)
         cc = V["ge_to_cached"] + V["ge_add"]
         if len(ds) > 1:
@@ -25,7 +28,7 @@ def main(d, t=511, n=1024):
                 if nz:
                     cc += V["ge_add_signed"]
         cost[m] = cc
-    seg = rows[:t]
+    seg = rows[:t - 1]
     tot = totw = 0
     for i, r in enumerate(seg):
         rr = i + 1
@@ -33,7 +36,7 @@ def main(d, t=511, n=1024):
         w = sum(cost[m] for m in range(1, rr + 1)) * n
         tot += dur
         totw += w
-        if rr in (1, 2, 4, 8, 16, 32, 64, 128, 192, 255, 256, 257, 300, 384, 448, 500, 511):
+        if rr in (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 120, 127, 128, 192, 255, 256, 257, 300, 384, 448, 500, 511):
             print(f"r={rr:4d} grid={r['Grid_Size_X']}x{r['Grid_Size_Y']} dur={dur / 1e3:8.1f}us "
                   f"eff={w / (dur * 1e-9) / bench.INT32_PEAK * 100:5.1f}%")
     print("total %.1f ms eff %.1f%%" % (tot / 1e6, totw / (tot * 1e-9) / bench.INT32_PEAK * 100))
