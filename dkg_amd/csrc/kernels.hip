@@ -513,6 +513,19 @@ DKG_DEV void pt_store_wt(uint32_t* __restrict__ base, size_t stride, size_t e, c
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Items of K consecutive positions: step r has nb(r) = ceil(r / K) blocks, block b holding positions
+// b K + 1 .. min((b + 1) K, r); CW * P(r) items precede step r, P(r) = sum_{r' < r} ceil(r' / K).
+__host__ __device__ inline unsigned long long flow_prefix(unsigned long long r, unsigned K) {
+  const unsigned long long R = r - 1, q = R / K, sr = R % K;
+  return (unsigned long long)K * q * (q + 1) / 2 + sr * (q + 1);
+}
+
+// One item = (step r, block b of K positions, column wave cw): the K chains run one after the other
+// in the wave (each position's inputs come from step r-1), so the hand-off -- ticket, dependency
+// polls, acquire, flag -- is paid once per K chains.  Dependencies: blocks b-1 (position b K, read by
+// the lowest position), b and b+1 (read, and overwritten in the ping-pong table) at step r-1;
+// done[cw][block] = the last step the block completed.
+template <int K>
 __global__ __launch_bounds__(64 * FLOW_WAVES, 4) void k_binom_flow(int L, size_t npad, const uint32_t* __restrict__ C,
                                                                   uint32_t* e0, uint32_t* e1, size_t pstride,
                                                                   unsigned gx, unsigned CW, unsigned last_piece,
@@ -528,6 +541,7 @@ __global__ __launch_bounds__(64 * FLOW_WAVES, 4) void k_binom_flow(int L, size_t
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint32_t* q = qs[wave] + lane;
   const size_t S = (size_t)L * npad;
+  const int nblocks = (L - 1 + K - 1) / K;  // flag words per column wave
   for (;;) {
     if (threadIdx.x == 0) tk = atomicAdd(ticket, 1u);
     __syncthreads();
@@ -536,28 +550,36 @@ __global__ __launch_bounds__(64 * FLOW_WAVES, 4) void k_binom_flow(int L, size_t
     if (first >= total) break;  // workgroup-uniform exit
     const unsigned long long item = first + wave;
     if (item < total) {
-      // decode (r, m, cw): CW * r (r - 1) / 2 items precede step r
+      // decode (r, b, cw): the largest r with CW * P(r) <= item (binary search, wave-uniform)
       const unsigned long long x = item / CW;
-      int r = __builtin_amdgcn_readfirstlane((int)((sqrtf(8.0f * (float)x + 1.0f) + 1.0f) * 0.5f));
-      while ((unsigned long long)r * (r - 1) / 2 > x) r--;
-      while ((unsigned long long)(r + 1) * r / 2 <= x) r++;
-      const unsigned long long off = item - (unsigned long long)CW * ((unsigned long long)r * (r - 1) / 2);
-      const int m = __builtin_amdgcn_readfirstlane(r - (int)(off / CW));
+      int lo = 1, hi = L - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (flow_prefix(mid, K) <= x) lo = mid;
+        else hi = mid - 1;
+      }
+      const int r = __builtin_amdgcn_readfirstlane(lo);
+      const unsigned long long off = item - (unsigned long long)CW * flow_prefix(r, K);
+      const int nb = (r + K - 1) / K;
+      const int b = __builtin_amdgcn_readfirstlane(nb - 1 - (int)(off / CW));
       const unsigned cw = __builtin_amdgcn_readfirstlane((unsigned)(off % CW));
       const unsigned piece = cw / gx, grp = cw - piece * gx;
       const size_t d = piece * pstride + (size_t)grp * 64 + lane;
-      uint32_t* fl = done + (size_t)cw * L;
+      uint32_t* fl = done + (size_t)cw * nblocks;
       const uint32_t prev = (uint32_t)(r - 1);
-      if (m >= 2) flow_wait(fl + m - 1, prev, err);
-      if (m <= r - 1) flow_wait(fl + m, prev, err);
-      if (m + 1 <= r - 1) flow_wait(fl + m + 1, prev, err);
+      const int nbp = (r - 1 + K - 1) / K;  // blocks that exist at step r-1
+      if (b >= 1 && b - 1 < nbp) flow_wait(fl + b - 1, prev, err);
+      if (b < nbp) flow_wait(fl + b, prev, err);
+      if (b + 1 < nbp) flow_wait(fl + b + 1, prev, err);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const uint32_t* ein = (r & 1) ? e0 : e1;  // step r reads step r-1's table
       uint32_t* eout = (r & 1) ? e1 : e0;
       // a short last piece (last_off = L - its length) has degree re = r - last_off after step r;
       // positions above re are never read
       const int re = r - (piece == last_piece ? last_off : 0);
-      if (m <= re) {
+      const int mhi = min((b + 1) * K, re), mlo = b * K + 1;
+#pragma unroll 1
+      for (int m = mhi; m >= mlo; m--) {
         {
           ge_p3 cur;
           pt_load(cur, ein, S, (size_t)m * npad + d);
@@ -580,31 +602,41 @@ __global__ __launch_bounds__(64 * FLOW_WAVES, 4) void k_binom_flow(int L, size_t
         mul_small_lds(xv, (uint32_t)m, q);   // * m
         pt_store_wt(eout, S, (size_t)m * npad + d, xv);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the point has completed
-      if (lane == 0) __hip_atomic_store((flow_gu32*)(fl + m), (uint32_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the block has completed
+      if (lane == 0) __hip_atomic_store((flow_gu32*)(fl + b), (uint32_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-// Flow items of a chunk: L(L-1)/2 per column wave
-unsigned long long binom_flow_items(size_t width, size_t pieces, size_t L) {
-  return (unsigned long long)(width / 64 * pieces) * (unsigned long long)L * (L - 1) / 2;
+// Flow items of a chunk with K positions per item; flag words per column wave
+unsigned long long binom_flow_items(size_t width, size_t pieces, size_t L, unsigned K) {
+  return (unsigned long long)(width / 64 * pieces) * flow_prefix(L, K);
+}
+size_t binom_flow_flag_words(size_t width, size_t pieces, size_t L, unsigned K) {
+  return (width / 64 * pieces) * ((L - 1 + K - 1) / K);
 }
 
-// done: [width/64 * pieces][L] words and ticket, err: one word each, all zeroed by the caller before
+// done: binom_flow_flag_words words and ticket, err: one word each, all zeroed by the caller before
 // the launch.  Returns the table holding the result (position 0 included).
 uint32_t* binomial_flow(size_t width, size_t npad, size_t L, const uint32_t* C, uint32_t* e0, uint32_t* e1,
                         hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* done,
-                        uint32_t* ticket, uint32_t* err, unsigned grid_cap) {
+                        uint32_t* ticket, uint32_t* err, unsigned grid_cap, unsigned K) {
   binom_init(width, npad, L, C, e0, stream, pieces, pstride);
   if (L < 2) return e0;
   const unsigned CW = (unsigned)(width / 64 * pieces);
-  const unsigned long long total = binom_flow_items(width, pieces, L);
+  const unsigned long long total = binom_flow_items(width, pieces, L, K);
   const int last_off = (last_len && last_len < L) ? (int)(L - last_len) : 0;
   const unsigned long long wgs = (total + FLOW_WAVES - 1) / FLOW_WAVES;
   const unsigned grid = (unsigned)(wgs < grid_cap ? wgs : grid_cap);
-  hipLaunchKernelGGL(k_binom_flow, dim3(grid), dim3(64 * FLOW_WAVES), 0, stream, (int)L, npad, C, e0, e1, pstride,
-                     (unsigned)(width / 64), CW, (unsigned)(pieces - 1), last_off, done, ticket, err, total);
+  const unsigned gx = (unsigned)(width / 64), lp = (unsigned)(pieces - 1);
+#define DKG_FLOW_LAUNCH(KK)                                                                                       \
+  hipLaunchKernelGGL(k_binom_flow<KK>, dim3(grid), dim3(64 * FLOW_WAVES), 0, stream, (int)L, npad, C, e0, e1, pstride, \
+                     gx, CW, lp, last_off, done, ticket, err, total)
+  if (K >= 8) DKG_FLOW_LAUNCH(8);
+  else if (K >= 4) DKG_FLOW_LAUNCH(4);
+  else if (K >= 2) DKG_FLOW_LAUNCH(2);
+  else DKG_FLOW_LAUNCH(1);
+#undef DKG_FLOW_LAUNCH
   uint32_t* fin = ((L - 1) & 1) ? e1 : e0;
   // position 0 after the last step is C_0 (the flow never writes position 0)
   hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,

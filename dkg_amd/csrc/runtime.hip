@@ -551,9 +551,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
   // dataflow binomial state: per chunk the flags of its column waves ([cw][L]), the ticket and the
   // err word, zeroed on the chunk's stream before its launch
-  const bool flow = ctx->binom_mode == 2 && L > 1;
+  const bool flow = ctx->binom_mode >= 2 && L > 1;
+  const unsigned flow_k = 1u << std::min(ctx->binom_mode >= 2 ? ctx->binom_mode - 2 : 0, 3);  // 2..5 -> K = 1..8
   if (flow) {
-    ctx->flow_chunk_words = (npad / 64 * U * L + 2 + 63) / 64 * 64;
+    ctx->flow_chunk_words = (dkgk::binom_flow_flag_words(npad, U, L, flow_k) + 2 + 63) / 64 * 64;
     ctx->flow_state = buf<uint32_t>(ctx, "v.flow", 4 * ctx->flow_chunk_words * ContextLimits::MAX_FLOW_CHUNKS);
   }
   // persistent grid: 4 workgroups (16 waves) per CU fill the chip; chunks launched side by side share it
@@ -568,10 +569,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (L / 2.0) / 1024 < 1.5);
       uint32_t* fs = ctx->flow_state + chunk_idx * ctx->flow_chunk_words;
       HCK(hipMemsetAsync(fs, 0, 4 * ctx->flow_chunk_words, st));
-      const size_t fl_words = (w / 64) * U * L;
+      const size_t fl_words = dkgk::binom_flow_flag_words(w, U, L, flow_k);
       e = (ilp ? dkgk_ilp::binomial_flow : dkgk::binomial_flow)(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad,
                                                                Lr, fs, fs + fl_words, fs + ctx->flow_chunk_words - 1,
-                                                               flow_grid);
+                                                               flow_grid, flow_k);
     } else {
       dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
       uint32_t *bin = e0 + c0, *bout = e1 + c0;
@@ -1481,7 +1482,7 @@ int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
 }
 
 int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 2) return DKG_E_ARG;
+  if (!ctx || mode < 0 || mode > 5) return DKG_E_ARG;
   ctx->binom_mode = mode;
   return DKG_OK;
 }

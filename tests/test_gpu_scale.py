@@ -514,7 +514,7 @@ def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
     out = []
     try:
         be.set_split(split)
-        for mode in (2, 1):
+        for mode in (1, 2, 4, 5):  # per step; dataflow with K = 1, 4, 8 positions per item
             be.set_binomial(mode)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             assert be.last_split() == split
@@ -522,7 +522,7 @@ def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
     finally:
         be.set_binomial(0)
         be.set_split(0)
-    assert out[0] == out[1]
+    assert all(o == out[0] for o in out[1:])
     assert out[0][2][:5] == [0, 0, 1, 0, 0] and out[0][3][:5] == [0, 0, 1, 0, 0]
 
 
