@@ -118,14 +118,15 @@ def algorithmic_bytes(kernel, n, t, U, plen=None):
         per_pass = sum(cols * (2 * PT_BYTES + max(r - (Lp0 - Lp), 0) * 3 * PT_BYTES)
                        for r in range(1, Lp0) for Lp in pieces)
         return per_pass / max(Lp0 - 1, 1), max(Lp0 - 1, 1)
-    if kernel == "stepping":  # the table once, then D_0 out per (piece, receiver)
+    if kernel == "stepping":  # the table once, then D_0 out per (piece, receiver) + its dense Z (40 B)
         nblk = -(-Lp0 // 512)
-        return cols * (t + 1 + U * n) * PT_BYTES / nblk, nblk
+        zb = 40 if U > 1 else 0  # the Z copy exists for the affine recombination addends (U > 1)
+        return cols * ((t + 1) * PT_BYTES + U * n * (PT_BYTES + zb)) / nblk, nblk
     if kernel == "combine":  # U affine piece values (128-B slots) in, P(j) out per (column, receiver)
         return 2 * n * n * (U * AFF_BYTES + PT_BYTES), 1
-    if kernel == "affine":  # per stepped value: Z twice (3 x 16 B each), the point, a block prefix
-        # (48 B written and read per 4 points), the 128-B affine slot out
-        return 2 * n * U * n * (2 * 48 + PT_BYTES + 2 * 12 + AFF_BYTES), 1
+    if kernel == "affine":  # per stepped value: Z twice (the stepping's dense 40-B copy), the point, a
+        # block prefix (48 B written and read per 4 points), the 128-B affine slot out
+        return 2 * n * U * n * (2 * 40 + PT_BYTES + 2 * 12 + AFF_BYTES), 1
     return None, None
 
 

@@ -707,7 +707,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
     uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast,
-    uint32_t* __restrict__ flags, size_t col0, size_t dreal, unsigned gw) {
+    uint32_t* __restrict__ flags, size_t col0, size_t dreal, unsigned gw, uint32_t* __restrict__ Rz) {
   const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
   if (!DED && flags && !flags[wg]) return;  // a redo launch: this workgroup's tables were exact
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
@@ -778,7 +778,15 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       }
     }
     __syncthreads();  // every column read before the next step overwrites it
-    if (live && q == 0 && R) pt_store_aos(R, d * nrecv + j, D);
+    if (live && q == 0 && R) {
+      pt_store_aos(R, d * nrecv + j, D);
+      // Z once more in a dense 40-B record: the affine normalisation reads only Z in its first pass
+      if (Rz) {
+        uint2* z2 = reinterpret_cast<uint2*>(Rz + (d * nrecv + j) * 10);
+#pragma unroll
+        for (int k = 0; k < 5; k++) z2[k] = make_uint2(D.Z.v[2 * k], D.Z.v[2 * k + 1]);
+      }
+    }
   }
   if (DED && bad) flags[wg] = 1u;  // any lane: the same value
 }
@@ -861,9 +869,10 @@ double stepping_waves_per_simd(size_t cols, size_t N, size_t pieces, size_t last
 
 size_t stepping_flag_words(size_t ndealers, size_t pieces) { return ndealers * (pieces + 1); }
 
-struct ColReal {  // which table columns belong to real dealers (k_stepping's `real`)
+struct ColReal {  // which table columns belong to real dealers (k_stepping's `real`); Rz: dense Z copy
   size_t col0, dreal;
   unsigned gw;
+  uint32_t* Rz;
 };
 
 template <bool DED>
@@ -873,20 +882,23 @@ void step_launch(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t nd
                  const ColReal& cr) {
   if (maxbs == 192)
     hipLaunchKernelGGL((k_stepping<192, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw);
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
+                       R ? cr.Rz : nullptr);
   else if (maxbs == 256)
     hipLaunchKernelGGL((k_stepping<256, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw);
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
+                       R ? cr.Rz : nullptr);
   else
     hipLaunchKernelGGL((k_stepping<512, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw);
+                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
+                       R ? cr.Rz : nullptr);
 }
 
 void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
-              size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw) {
+              size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw, uint32_t* Rz) {
   if (!ndealers || !nrecv) return;
-  const ColReal cr{col0, dreal, gw ? gw : 64u};
+  const ColReal cr{col0, dreal, gw ? gw : 64u, Rz};
   if (!last_len || last_len > N) last_len = N;
   // with flags (stepping_flag_words zeroed words): every launch below runs dedicated, then again
   // complete in its marked workgroups (its own flag words: a grid has at most ndealers x pieces)
@@ -1130,14 +1142,21 @@ DKG_DEV void for_desc(F&& f) {
   }
 }
 
-DKG_DEV void ld_z(fe& z, const uint32_t* R, size_t e) {  // Z of point e (words 20..29)
-  const uint4* p4 = reinterpret_cast<const uint4*>(R + e * PT_WORDS);
+DKG_DEV void ld_z(fe& z, const uint32_t* R, const uint32_t* Rz, size_t e) {  // Z of point e
+  if (Rz) {  // the stepping's dense copy: 40 B per point, a half-wave reads 1280 contiguous bytes
+    const uint2* z2 = reinterpret_cast<const uint2*>(Rz + e * 10);
+    const uint2 a = z2[0], b = z2[1], c = z2[2], d = z2[3], f = z2[4];
+    z = fe{{a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, f.x, f.y}};
+    return;
+  }
+  const uint4* p4 = reinterpret_cast<const uint4*>(R + e * PT_WORDS);  // words 20..29 of the point
   const uint4 z0 = p4[5], z1 = p4[6], z2 = p4[7];
   z = fe{{z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w, z2.x, z2.y}};
 }
 
 __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstride, size_t pieces, size_t nrecv,
-                                                       const uint32_t* __restrict__ R, uint32_t* __restrict__ A) {
+                                                       const uint32_t* __restrict__ R, uint32_t* __restrict__ A,
+                                                       const uint32_t* __restrict__ Rz) {
   const size_t span = 32 * AFF_RUN, runs = (nrecv + span - 1) / span;
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t item = gid / 32;
@@ -1162,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstr
       const int i = AFF_BLK * b + k;
       if (i < cnt) {
         fe z;
-        ld_z(z, R, pt(i));
+        ld_z(z, R, Rz, pt(i));
         fe_mul(acc, acc, z);
       }
     }
@@ -1177,7 +1196,7 @@ __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstr
     static_assert(AFF_BLK >= 2, "q[1] = z[0] below");
 #pragma unroll
     for (int k = 0; k < AFF_BLK; k++) {
-      if (AFF_BLK * b + k < cnt) ld_z(z[k], R, pt(AFF_BLK * b + k));
+      if (AFF_BLK * b + k < cnt) ld_z(z[k], R, Rz, pt(AFF_BLK * b + k));
       else fe_one(z[k]);
     }
     fe_copy(q[1], z[0]);
@@ -1221,11 +1240,11 @@ __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstr
 }
 
 void affine_pieces(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* R, uint32_t* A,
-                   hipStream_t stream) {
+                   hipStream_t stream, const uint32_t* Rz) {
   if (!width || !nrecv || !pieces) return;
   const size_t runs = (nrecv + 32 * AFF_RUN - 1) / (32 * AFF_RUN), lanes = pieces * width * runs * 32;
   hipLaunchKernelGGL(k_affine_pieces, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, width, pstride,
-                     pieces, nrecv, R, A);
+                     pieces, nrecv, R, A, Rz);
 }
 
 template <int U, int K, int KL>

@@ -518,6 +518,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   ctx->last_step_flag_words = sflags ? dkgk::stepping_flag_words(npad, U) : 0;
   // affine addends: one 128-B slot per (piece column, receiver), like R
   uint32_t* Aff = short_mult && ctx->addend_mode == 0 ? buf<uint32_t>(ctx, "v.Aff", 4 * AFFP_WORDS_H * W * n) : nullptr;
+  // the stepping's dense copy of each stored point's Z (40 B), read by the affine normalisation
+  uint32_t* Rz = Aff ? buf<uint32_t>(ctx, "v.Rz", 40 * W * n) : nullptr;
   if (short_mult) split_short(ctx, n, L, U, &sdig, &stop, &sscale);
   else if (U > 1) split_digits(ctx, n, L, &ydig, &ytop);
   ctx->last_combine = U > 1 ? (short_mult ? 2 : 1) : 0;
@@ -589,10 +591,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw);
+                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw,
+                   Rz ? Rz + c0 * n * 10 : nullptr);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     if (short_mult && Aff) {
-      dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st);
+      dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st, Rz + c0 * n * 10);
       dkgk::combine_short_aff(w, npad, U, n, sdig, stop, Aff + c0 * n * AFFP_WORDS_H, R + c0 * n * PT_WORDS_H, st);
     } else if (short_mult) dkgk::combine_short(w, npad, U, n, sdig, stop, R + c0 * n * PT_WORDS_H, st);
     else dkgk::combine(w, npad, U, n, ydig, ytop, R + c0 * n * PT_WORDS_H, st);
