@@ -140,6 +140,8 @@ def pmc_traffic(kernel, n, t, U, plen=None):
         return None
     if (doc.get("n"), doc.get("t"), doc.get("split")) != (n, t, U) or kernel not in doc.get("kernels", {}):
         return None
+    if kernel in ("stepping", "affine") and not doc.get("stepping_z_copy"):
+        return None  # measured before the stepping wrote the dense Z copy the affine pass reads
     if plen is not None and doc.get("split_len", split_pieces(t, U)[1]) != plen:
         return None
     return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
