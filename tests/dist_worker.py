@@ -1,6 +1,7 @@
 """One rank of tests/test_gpu_dist.py (not a test module): a dealer-sharded ceremony end to end
 through dkg_amd.distributed.ShardedCeremony on GPU 0, ranks sharing the GPU over gloo (the
-rehearsal mode of bench.py --dist-backend gloo).  Started as a child process with RANK /
+rehearsal mode of bench.py --dist-backend gloo), or one rank over RCCL (DKG_DIST_BACKEND=nccl: the
+real collectives and the device-side fences, world size 1 on a one-GPU box).  Started as a child process with RANK /
 WORLD_SIZE / MASTER_ADDR / MASTER_PORT set; rank 0 writes every ceremony's combined outputs as
 JSON to argv[1]."""
 import json
@@ -34,14 +35,20 @@ def summary(res):
             "qualified": [int(x) for x in d.qualified], "reconstruct": [int(x) for x in d.reconstruct],
             "complaints2": [int(x) for x in d.complaints2], "r4_error": [int(x) for x in d.r4_error],
             "phase4_error": bool(d.phase4_error), "final_share": res.final_share.hex(),
+            "public_share": res.public_share.hex() if res.public_share is not None else None,
             "mpk": res.mpk.hex() if res.mpk is not None else None}
 
 
 def main(out_path):
     rank = int(os.environ["RANK"])
-    dist.init_process_group("gloo")
-    ws = dist.get_world_size()
+    backend = os.environ.get("DKG_DIST_BACKEND", "gloo")
     dev = torch.device("cuda", 0)
+    if backend == "nccl":  # RCCL: one GPU per rank, so world size 1 on a one-GPU box
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    ws = dist.get_world_size()
     be = dkg_amd.Backend(0)
     put = lambda x: torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)  # noqa: E731
     out = {}

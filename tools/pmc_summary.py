@@ -87,7 +87,8 @@ def write_traffic(d, out, n, t, U, split_len=None):
                                  + e["write_bytes"] / max(e["write_launches"], 1))
     doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
                      f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
-           "n": n, "t": t, "split": U, "kernels": kern}
+           "n": n, "t": t, "split": U, "kernels": kern,
+           "stepping_z_copy": True}  # round 3+: the stepping also writes the dense Z copy
     if split_len:
         doc["split_len"] = split_len
     with open(out, "w") as f:
