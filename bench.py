@@ -124,6 +124,8 @@ def algorithmic_bytes(kernel, n, t, U, plen=None):
         return cols * ((t + 1) * PT_BYTES + U * n * (PT_BYTES + zb)) / nblk, nblk
     if kernel == "combine":  # U affine piece values (128-B slots) in, P(j) out per (column, receiver)
         return 2 * n * n * (U * AFF_BYTES + PT_BYTES), 1
+    if kernel == "check":  # s and s' (32 B each), b_j P(j) of the E and A columns (160 B each), 2 decisions
+        return n * n * (2 * 32 + 2 * PT_BYTES + 2), 1
     if kernel == "affine":  # per stepped value: Z twice (the stepping's dense 40-B copy), the point, a
         # block prefix (48 B written and read per 4 points), the 128-B affine slot out
         return 2 * n * U * n * (2 * 40 + PT_BYTES + 2 * 12 + AFF_BYTES), 1

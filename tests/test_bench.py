@@ -28,7 +28,7 @@ def test_algorithmic_bytes_stepping_and_combine():
     assert nl == 1 and step == 2 * n * U * (256 * 160 + n * (160 + 40))
     comb, nl = bench.algorithmic_bytes("combine", n, t, U)
     assert nl == 1 and comb == 2 * n * n * (2 * 128 + 160)  # two affine piece values in, P(j) out
-    assert bench.algorithmic_bytes("check", n, t, U) == (None, None)
+    assert bench.algorithmic_bytes("check", n, t, U) == (n * n * (2 * 32 + 2 * 160 + 2), 1)
 
 
 def test_pmc_traffic_matches_workload():

@@ -52,6 +52,23 @@ def main(d):
               f"{100 * c.get('SQ_WAIT_INST_ANY', 0) / wc:9.1f} "
               f"{c.get('SQ_ACTIVE_INST_VALU', 0) / (c.get('SQ_ACTIVE_INST_ANY', 0) or 1):11.2f} "
               f"{2 * fe[k].get('FETCH_SIZE', 0) / 1e3:12.1f} {wr[k].get('WRITE_SIZE', 0) / 1e3:10.1f}")
+    va, vcalls = load_counters(os.path.join(d, "pmc_valu", "run_counter_collection.csv"))
+    if va:
+        print()
+        print("VALU unit (pmc_valu): cyc/instr = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU), the SIMD cycles a")
+        print("wave64 VALU instruction occupies (2 for a full-rate one on a 32-lane SIMD); slots/instr = cyc/instr / 2,")
+        print("the roofline's issue-slot unit (bench.py: half-rate instructions count 2)")
+        print(f"{'kernel':24s} {'disp':>5s} {'INSTS_VALU x64':>15s} {'THREAD_CYC':>12s} {'cyc/instr':>9s} {'slots/instr':>11s} "
+              f"{'INT64/VALU':>10s} {'INT32/VALU':>10s} {'ACTIVE_VALU/INSTS':>17s} {'VALU2/ACTIVE':>12s}")
+        for k in sorted(va, key=lambda k: -va[k].get("SQ_THREAD_CYCLES_VALU", 0)):
+            c = va[k]
+            ins = c.get("SQ_INSTS_VALU", 0) or 1
+            print(f"{k:24s} {len(vcalls[k]):5d} {ins * 64:15.4g} {c.get('SQ_THREAD_CYCLES_VALU', 0):12.4g} "
+                  f"{c.get('SQ_THREAD_CYCLES_VALU', 0) / (64 * ins):9.3f} "
+                  f"{c.get('SQ_THREAD_CYCLES_VALU', 0) / (128 * ins):11.3f} "
+                  f"{c.get('SQ_INSTS_VALU_INT64', 0) / ins:10.3f} {c.get('SQ_INSTS_VALU_INT32', 0) / ins:10.3f} "
+                  f"{c.get('SQ_ACTIVE_INST_VALU', 0) / ins:17.3f} "
+                  f"{c.get('SQ_ACTIVE_INST_VALU2', 0) / (c.get('SQ_ACTIVE_INST_VALU', 0) or 1):12.4f}")
 
 
 PHASE = {"k_binom_step": "binomial", "void k_stepping<192>": "stepping", "void k_stepping<256>": "stepping",
