@@ -104,7 +104,7 @@ def hybrid_valu(n, sk, VALU=SLOTS):
 
 PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
 AFF_BYTES = 128  # kernels.hip AFFP_WORDS: one affine addend slot
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
 
 
 def algorithmic_bytes(kernel, n, t, U, plen=None):

@@ -123,10 +123,158 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uin
   if (live) pt_store(K_ext, count, idx, x);
 }
 
-void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream) {
+#ifdef DKG_DEC_W4
+// K = sk_q * R with a width-4 signed window (wNAF: digits 0, +-1, +-3, +-5, +-7, at least three zeros
+// after each nonzero one: ~51 additions instead of NAF's ~85 for a 253-bit scalar).  Each lane's odd
+// multiples R, 3R, 5R, 7R (cached form) live in a global table T laid out [wave][4][40 words][64
+// lanes]; the addend of the next nonzero digit is copied into the wave's LDS slot by LDS-DMA
+// (global_load_lds, no VGPRs) right after the previous addition, and lands during the >= 3 doublings
+// in between.  LDS stays one point per wave (4 waves per SIMD, as k_dec_mul).
+typedef __attribute__((address_space(3))) uint32_t dec_lds_u32;
+typedef __attribute__((address_space(1))) uint32_t dec_g_u32;
+
+// words 0..N-1 (64 lanes each) from sg (+ k * 256 B immediates) into the LDS rows at q
+template <int N, int K = 0>
+DKG_DEV void glds_words(const dec_g_u32* sg, uint32_t* q) {
+  if constexpr (K < N) {
+    __builtin_amdgcn_global_load_lds(sg, (dec_lds_u32*)(q + K * 64), 4, K * 256, 0);
+    glds_words<N, K + 1>(sg, q);
+  }
+}
+
+__global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const uint32_t* __restrict__ sk,
+                                                      const uint32_t* __restrict__ R_ext, uint32_t* __restrict__ K_ext,
+                                                      uint32_t* __restrict__ T) {
+  __shared__ uint32_t qs[PT_WORDS * 64];
+  __shared__ int16_t nzb[96];  // bits of the nonzero digits, top first
+  __shared__ int8_t nzd[96];   // their digits
+  __shared__ int8_t dig[288];  // the recoding (LDS: a private array would live in scratch)
+  __shared__ int nnz_s;
+  uint32_t* qcol = qs + threadIdx.x;
+  const size_t q = blockIdx.y, w = blockIdx.z;
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const bool live = i < D;
+  const size_t count = 2 * D * n;
+  const size_t idx = ((live ? i : 0) * n + q) * 2 + w;
+  const size_t wb = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  uint32_t* tb = T + wb * (4 * PT_WORDS * 64);
+  if (threadIdx.x == 0) {
+    uint32_t k[9];
+    for (int j = 0; j < 8; j++) k[j] = sk[8 * q + j];
+    k[8] = 0;
+    for (int b = 0; b < 288; b++) {
+      int8_t d = 0;
+      if (k[0] & 1u) {
+        int v = (int)(k[0] & 15u);
+        if (v >= 8) v -= 16;
+        d = (int8_t)v;
+        if (v > 0) {  // k -= v
+          uint32_t sub = (uint32_t)v;
+          for (int wi = 0; wi < 9; wi++) {
+            const uint32_t old = k[wi];
+            k[wi] = old - sub;
+            if (old >= sub) break;
+            sub = 1u;
+          }
+        } else {      // k += -v
+          uint32_t add = (uint32_t)(-v);
+          for (int wi = 0; wi < 9; wi++) {
+            const uint32_t old = k[wi];
+            k[wi] = old + add;
+            if (k[wi] >= old) break;
+            add = 1u;
+          }
+        }
+      }
+      dig[b] = d;
+      for (int wi = 0; wi < 8; wi++) k[wi] = (k[wi] >> 1) | (k[wi + 1] << 31);
+      k[8] >>= 1;
+    }
+    int c = 0;
+    for (int b = 287; b >= 0; b--)
+      if (dig[b]) {
+        nzb[c] = (int16_t)b;
+        nzd[c] = dig[b];
+        c++;
+      }
+    nnz_s = c;
+  }
+  // the lane's table of odd multiples
+  ge_p3 x;
+  if (live) pt_load(x, R_ext, count, idx);
+  else ge_identity(x);
+  {
+    ge_cached c;
+    ge_to_cached(c, x);
+    lds_put_cached(tb + threadIdx.x, c);  // T[0] = R (global, lane-interleaved like the LDS slot)
+    ge_p3 x2;
+    ge_dbl<true>(x2, x);
+    ge_to_cached(c, x2);
+    lds_put_cached(qcol, c);              // 2R in the LDS slot
+#pragma unroll 1
+    for (int m = 1; m < 4; m++) {
+      ge_add_lds(x, x, qcol, false);      // (2m+1) R
+      ge_to_cached(c, x);
+      lds_put_cached(tb + m * PT_WORDS * 64 + threadIdx.x, c);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // table stored, slot reads done
+  __syncthreads();
+  const int nnz = __builtin_amdgcn_readfirstlane(nnz_s);
+  auto fetch = [&](int e) {  // addend of nonzero digit e into the LDS slot (LDS-DMA, one word per instr)
+    const int a = (nzd[e] < 0 ? -nzd[e] : nzd[e]) >> 1;
+    // one lane address per 16 words, the rest as the instruction's immediate offset (k * 256 B)
+    const uint32_t* src = tb + a * PT_WORDS * 64 + threadIdx.x;
+    glds_words<16>((const dec_g_u32*)src, qs);
+    glds_words<16>((const dec_g_u32*)(src + 16 * 64), qs + 16 * 64);
+    glds_words<8>((const dec_g_u32*)(src + 32 * 64), qs + 32 * 64);
+  };
+  ge_identity(x);
+  if (nnz > 0) {
+    fetch(0);
+    int b = __builtin_amdgcn_readfirstlane((int)nzb[0]);
+#pragma unroll 1
+    for (int e = 0; e < nnz; e++) {
+      const int be = __builtin_amdgcn_readfirstlane((int)nzb[e]);
+      const int de = __builtin_amdgcn_readfirstlane((int)nzd[e]);
+#pragma unroll 1
+      for (; b > be; b--) ge_dbl_lean(x, x, b - 1 == be);  // T only before the addition
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the DMA'd addend has landed
+      __builtin_amdgcn_s_barrier();
+      ge_add_lds(x, x, qcol, de < 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done
+      if (e + 1 < nnz) fetch(e + 1);
+    }
+#pragma unroll 1
+    for (; b > 0; b--) ge_dbl_lean(x, x, b == 1);          // trailing zero digits
+  }
+  if (live) pt_store(K_ext, count, idx, x);
+}
+#endif
+
+void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream,
+             uint32_t* table) {
   if (!D || !n) return;
+#ifdef DKG_DEC_W4
+  if (table) {
+    hipLaunchKernelGGL(k_dec_mul_w4, dim3((unsigned)((D + 63) / 64), (unsigned)n, 2u), dim3(64), 0, stream, D, n, sk,
+                       R_ext, K_ext, table);
+    return;
+  }
+#endif
+  (void)table;
   hipLaunchKernelGGL(k_dec_mul, dim3((unsigned)((D + 63) / 64), (unsigned)n, 2u), dim3(64), 0, stream, D, n, sk,
                      R_ext, K_ext);
+}
+
+size_t dec_mul_table_words(size_t D, size_t n) {
+#ifdef DKG_DEC_W4
+  return ((D + 63) / 64) * n * 2 * 4 * PT_WORDS * 64;
+#else
+  (void)D;
+  (void)n;
+  return 0;
+#endif
 }
 
 // SymmetricKey::process (elgamal.rs:172-193) on 32-byte messages: one Blake2b-512 of the key's

@@ -1278,7 +1278,8 @@ void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const 
   if (tm) HCK(hipEventRecord(ctx->hev[4], st));
   dkgk::decode_points(e1, items, R, items, item_ok, st);
   if (tm) HCK(hipEventRecord(ctx->hev[5], st));
-  dkgk::dec_mul(D, n, sk, R, K, st);
+  const size_t tw = dkgk::dec_mul_table_words(D, n);
+  dkgk::dec_mul(D, n, sk, R, K, st, tw ? buf<uint32_t>(ctx, "hy.dec_tab", 4 * tw) : nullptr);
   if (tm) HCK(hipEventRecord(ctx->hev[6], st));
   dkgk::encode_points(K, items, items, Kc, st);
   if (tm) HCK(hipEventRecord(ctx->hev[7], st));
