@@ -114,3 +114,28 @@ def test_split_pieces_and_bytes():
     w_even = bench.algorithmic_valu(1100, 549, 2, 2)
     assert w["stepping"] == pytest.approx(w_even["stepping"], rel=0.01)  # the same 550 positions
     assert w_even["binomial"] < w["binomial"] < 1.1 * w_even["binomial"]
+
+
+def test_hybrid_valu_closed_form():
+    """Full mode's closed forms (bench.hybrid_valu): k_enc_mul prices 26 radix-2^10 windows of g plus 64
+    radix-16 windows of pk_q per item; k_dec_mul one doubling per NAF digit below the top of sk_q
+    and one addition per other nonzero digit, for the 2n items of recipient q."""
+    n = 3
+    sk = (5).to_bytes(32, "little") + (1).to_bytes(32, "little") + (2**252 + 3).to_bytes(32, "little")
+    w = bench.hybrid_valu(n, sk)
+    S = bench.SLOTS
+    assert w["enc_mul"] == 2 * n * n * (26 * S["combw_window"] + 64 * S["comb_window"])
+    # NAF(5) = 1 0 1: two doublings (the last with T), one addition; NAF(1): nothing but the cached form;
+    # NAF(2^252 + 3) = 2^252 + 4 - 1: 252 doublings (T before the two additions), two additions
+    c5 = S["ge_to_cached"] + S["ge_dbl_not"] + S["ge_dbl_t"] + S["ge_add_signed"]
+    c1 = S["ge_to_cached"]
+    cb = S["ge_to_cached"] + 250 * S["ge_dbl_not"] + 2 * S["ge_dbl_t"] + 2 * S["ge_add_signed"]
+    assert w["dec_mul"] == 2 * n * (c5 + c1 + cb)
+    assert w["enc_sym"] == w["dec_sym"] == 2 * n * n * bench.HY_SYM_SLOTS
+
+
+def test_cpu_baseline_small_batch():
+    """The CPU baseline's sampler at config-5 scale: whole ceremonies in the sample, a positive rate."""
+    r = bench.cpu_baseline(16, 7, 1.0, ceremonies=10)
+    assert r["value"] > 0 and r["kind"] == "port" and "whole ceremonies" in r["sample"]
+    assert r["batch_s_extrapolated"] == pytest.approx(10 * r["ceremony_s_extrapolated"])
