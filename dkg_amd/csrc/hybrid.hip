@@ -133,11 +133,13 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uin
 typedef __attribute__((address_space(3))) uint32_t dec_lds_u32;
 typedef __attribute__((address_space(1))) uint32_t dec_g_u32;
 
-// words 0..N-1 (64 lanes each) from sg (+ k * 256 B immediates) into the LDS rows at q
+// words 0..N-1 (64 lanes each) from sg into the LDS rows at q.  The instruction's immediate offset
+// (K * 256 B) moves BOTH addresses -- the global one and the LDS one (M0 + offset + lane * 4) -- so
+// the LDS base stays q for every word of the group.
 template <int N, int K = 0>
 DKG_DEV void glds_words(const dec_g_u32* sg, uint32_t* q) {
   if constexpr (K < N) {
-    __builtin_amdgcn_global_load_lds(sg, (dec_lds_u32*)(q + K * 64), 4, K * 256, 0);
+    __builtin_amdgcn_global_load_lds(sg, (dec_lds_u32*)q, 4, K * 256, 0);
     glds_words<N, K + 1>(sg, q);
   }
 }

@@ -225,6 +225,11 @@ struct VerifySeg {
 // Which copy of a kernel runs a launch: product scanning (dkgk, fewer issue slots) or column sums
 // (dkgk_ilp, ten independent chains per multiplication) when the launch leaves too few waves per
 // SIMD to hide the serial chain (`latency_bound`), unless dkg_ctx_set_field_mode forces one.
+// Binomial steps with fewer waves per SIMD than this run the column-sum copy (kernels_ilp.h).
+#ifndef DKG_BINOM_ILP_WAVES
+#define DKG_BINOM_ILP_WAVES 1.5
+#endif
+
 bool use_ilp(const dkg_ctx* ctx, bool latency_bound) {
   return ctx->fe_mode == 2 || (ctx->fe_mode == 0 && latency_bound);
 }
@@ -580,7 +585,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       uint32_t *bin = e0 + c0, *bout = e1 + c0;
       for (size_t r = 1; r < L; r++) {
         // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
-        const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (r + 1) / 1024 < 1.5);
+        const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (r + 1) / 1024 < DKG_BINOM_ILP_WAVES);
         (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
         std::swap(bin, bout);
       }
