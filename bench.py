@@ -81,18 +81,23 @@ HY_SYM_SLOTS = 12 * 8 * (6 * 3 + 4 * 2 + 3 * 4) + 20 * 4 * (4 + 4 + 4 * 2) + 64
 def hybrid_valu(n, sk, VALU=SLOTS):
     """Closed-form VALU work of full mode's encryption and decryption of all 2 n^2 items (n dealers x n
     recipients x {randomness, share}): k_enc_mul (26 radix-2^10 windows of g + 64 radix-16 windows of
-    pk_q per item), k_dec_mul (sk_q's NAF: one doubling per digit below the top, an addition per
-    nonzero digit, wave-uniform), the encode / decode kernels and k_sym_xor (model above)."""
+    pk_q per item), k_dec_mul_w4 (sk_q's width-4 window, wave-uniform: a doubling per digit below the
+    top, an addition per nonzero digit, the odd multiples), the encode / decode kernels and k_sym_xor
+    (model above)."""
     items = 2 * n * n
     enc = items * (COMBW_WINDOWS * VALU["combw_window"] + 64 * VALU["comb_window"])
     dec = 0
     for q in range(n):
-        ds = _naf(int.from_bytes(sk[32 * q:32 * q + 32], "little"))
-        c = VALU["ge_to_cached"]
-        for i in range(len(ds) - 2, -1, -1):
-            nz = ds[i] != 0
-            c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
-            if nz:
+        ds = _wnaf(int.from_bytes(sk[32 * q:32 * q + 32], "little"), 4)
+        # k_dec_mul_w4: the odd multiples R, 3R, 5R, 7R (one doubling, three additions, four cached
+        # forms); then from the top nonzero digit down: an addition per nonzero digit (the first onto
+        # the identity), a doubling per digit below the top (T when an addition or the end follows)
+        c = VALU["ge_dbl_t"] + 3 * VALU["ge_add"] + 5 * VALU["ge_to_cached"]
+        top = max((i for i, d in enumerate(ds) if d), default=-1)
+        for i in range(top, -1, -1):
+            if i != top:
+                c += VALU["ge_dbl_t"] if (ds[i] or i == 0) else VALU["ge_dbl_not"]
+            if ds[i]:
                 c += VALU["ge_add_signed"]
         dec += 2 * n * c
     encode = HY_ENCODE[0] * VALU["fe_sq"] + HY_ENCODE[1] * VALU["fe_mul"]
@@ -202,6 +207,23 @@ def _naf(m):
     while v:
         if v & 1:
             d = 2 - (v & 3)
+            v -= d
+        else:
+            d = 0
+        digits.append(d)
+        v >>= 1
+    return digits
+
+
+def _wnaf(m, w):
+    """Width-w non-adjacent form, least significant digit first (odd digits |d| < 2^(w-1))."""
+    digits = []
+    v = m
+    while v:
+        if v & 1:
+            d = v & ((1 << w) - 1)
+            if d >= 1 << (w - 1):
+                d -= 1 << w
             v -= d
         else:
             d = 0

@@ -10,7 +10,8 @@
 //              for all n dealers, so it gets its own LDS-resident comb table (64 mixed additions,
 //              no doublings) instead of a 253-doubling variable-base multiplication;
 //   dec_mul  : sk_q * e1 with sk_q uniform across the wave (lanes = dealers of one recipient), a
-//              branch-uniform NAF double-and-add with the addend parked in LDS;
+//              branch-uniform width-4 window chain (k_dec_mul_w4; the plain NAF chain k_dec_mul
+//              with -DDKG_DEC_NAF) with the addend staged in LDS;
 //   encode / decode : the K5 kernels;  sym_xor : Blake2b + one ChaCha20 block + XOR (+ reduce).
 #include "kernels.h"
 #include "points.h"
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uin
   if (live) pt_store(K_ext, count, idx, x);
 }
 
-#ifdef DKG_DEC_W4
+#ifndef DKG_DEC_NAF
 // K = sk_q * R with a width-4 signed window (wNAF: digits 0, +-1, +-3, +-5, +-7, at least three zeros
 // after each nonzero one: ~51 additions instead of NAF's ~85 for a 253-bit scalar).  Each lane's odd
 // multiples R, 3R, 5R, 7R (cached form) live in a global table T laid out [wave][4][40 words][64
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const 
 void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream,
              uint32_t* table) {
   if (!D || !n) return;
-#ifdef DKG_DEC_W4
+#ifndef DKG_DEC_NAF
   if (table) {
     hipLaunchKernelGGL(k_dec_mul_w4, dim3((unsigned)((D + 63) / 64), (unsigned)n, 2u), dim3(64), 0, stream, D, n, sk,
                        R_ext, K_ext, table);
@@ -270,7 +271,7 @@ void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint
 }
 
 size_t dec_mul_table_words(size_t D, size_t n) {
-#ifdef DKG_DEC_W4
+#ifndef DKG_DEC_NAF
   return ((D + 63) / 64) * n * 2 * 4 * PT_WORDS * 64;
 #else
   (void)D;

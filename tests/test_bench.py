@@ -118,18 +118,19 @@ def test_split_pieces_and_bytes():
 
 def test_hybrid_valu_closed_form():
     """Full mode's closed forms (bench.hybrid_valu): k_enc_mul prices 26 radix-2^10 windows of g plus 64
-    radix-16 windows of pk_q per item; k_dec_mul one doubling per NAF digit below the top of sk_q
-    and one addition per other nonzero digit, for the 2n items of recipient q."""
+    radix-16 windows of pk_q per item; k_dec_mul_w4 the odd multiples, then an addition per nonzero
+    width-4 window digit of sk_q and a doubling per digit below the top, for the 2n items of q."""
     n = 3
     sk = (5).to_bytes(32, "little") + (1).to_bytes(32, "little") + (2**252 + 3).to_bytes(32, "little")
+    assert bench._wnaf(5, 4) == [5] and bench._wnaf(2**252 + 3, 4) == [3] + [0] * 251 + [1]
+    assert bench._wnaf(23, 4) == [7, 0, 0, 0, 1]  # 23 = 16 + 7
     w = bench.hybrid_valu(n, sk)
     S = bench.SLOTS
     assert w["enc_mul"] == 2 * n * n * (26 * S["combw_window"] + 64 * S["comb_window"])
-    # NAF(5) = 1 0 1: two doublings (the last with T), one addition; NAF(1): nothing but the cached form;
-    # NAF(2^252 + 3) = 2^252 + 4 - 1: 252 doublings (T before the two additions), two additions
-    c5 = S["ge_to_cached"] + S["ge_dbl_not"] + S["ge_dbl_t"] + S["ge_add_signed"]
-    c1 = S["ge_to_cached"]
-    cb = S["ge_to_cached"] + 250 * S["ge_dbl_not"] + 2 * S["ge_dbl_t"] + 2 * S["ge_add_signed"]
+    pre = S["ge_dbl_t"] + 3 * S["ge_add"] + 5 * S["ge_to_cached"]
+    c5 = pre + S["ge_add_signed"]  # one digit: one addition onto the identity
+    c1 = pre + S["ge_add_signed"]
+    cb = pre + 2 * S["ge_add_signed"] + 251 * S["ge_dbl_not"] + S["ge_dbl_t"]
     assert w["dec_mul"] == 2 * n * (c5 + c1 + cb)
     assert w["enc_sym"] == w["dec_sym"] == 2 * n * n * bench.HY_SYM_SLOTS
 
