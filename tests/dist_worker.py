@@ -3,10 +3,15 @@ through dkg_amd.distributed.ShardedCeremony on GPU 0, ranks sharing the GPU over
 rehearsal mode of bench.py --dist-backend gloo), or one rank over RCCL (DKG_DIST_BACKEND=nccl: the
 real collectives and the device-side fences, world size 1 on a one-GPU box).  Started as a child process with RANK /
 WORLD_SIZE / MASTER_ADDR / MASTER_PORT set; rank 0 writes every ceremony's combined outputs as
-JSON to argv[1]."""
+JSON to argv[1].  With argv[2] = a directory holding cfg.json and a tampered committee's E.bin,
+A.bin, s.bin, sp.bin (tests/test_gpu_dist.py, BASELINE size), each rank reads its dealers' slices
+of those and runs them, plus an honest ceremony of cfg's seed; digests of the large outputs."""
+import hashlib
 import json
 import os
 import sys
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -39,7 +44,36 @@ def summary(res):
             "mpk": res.mpk.hex() if res.mpk is not None else None}
 
 
-def main(out_path):
+def digest(res):
+    """summary() with the n x n decision matrices and the share vectors as SHA-256 digests."""
+    d = summary(res)
+    for k in ("dec2", "dec4", "final_share", "public_share"):
+        d[k] = hashlib.sha256(d[k].encode()).hexdigest() if d[k] is not None else None
+    return d
+
+
+def big(be, dev, rank, ws, d):
+    with open(os.path.join(d, "cfg.json")) as f:
+        cfg = json.load(f)
+    n, t = cfg["n"], cfg["t"]
+    N = t + 1
+    be.env_init(t, n)
+    d0, d1 = dealer_range(rank, ws, n)
+
+    def load(name, w):  # this rank's dealers' rows only
+        a = np.fromfile(os.path.join(d, name), dtype=np.uint8, count=w * (d1 - d0), offset=w * d0)
+        return torch.from_numpy(a).to(dev)
+
+    tE, tA, ts, tsp = load("E.bin", 32 * N), load("A.bin", 32 * N), load("s.bin", 32 * n), load("sp.bin", 32 * n)
+    out = {"tampered": digest(ShardedCeremony(be, dist, n, t, dev).run_verify(
+        tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr()))}
+    a, b = dkg_amd.dealer_coefficients(H(cfg["master_seed"]), cfg["ceremony"], d0, d1 - d0, t)
+    ta, tb = (torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev) for x in (a, b))
+    out["honest"] = digest(ShardedCeremony(be, dist, n, t, dev).run(ta.data_ptr(), tb.data_ptr()))
+    return out
+
+
+def main(out_path, big_dir=None):
     rank = int(os.environ["RANK"])
     backend = os.environ.get("DKG_DIST_BACKEND", "gloo")
     dev = torch.device("cuda", 0)
@@ -52,6 +86,15 @@ def main(out_path):
     be = dkg_amd.Backend(0)
     put = lambda x: torch.frombuffer(bytearray(x or b"\0"), dtype=torch.uint8).to(dev)  # noqa: E731
     out = {}
+    if big_dir:
+        out = big(be, dev, rank, ws, big_dir)
+        dist.barrier()
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump(out, f)
+        be.close()
+        dist.destroy_process_group()
+        return
     for name in HONEST:  # share generation + checks of this rank's dealers, exchange, combine, finalise
         c = golden(name)
         n, t = c["n"], c["t"]
@@ -80,4 +123,4 @@ def main(out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:3])

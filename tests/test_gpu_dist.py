@@ -2,7 +2,8 @@
 run_verify + dkg_ceremony_shard_device / _shard_verify_device + the all-gathers + the library's
 combine, reconstruction exchange and finalise (dkg_amd/distributed.py), in 2 and 3 spawned ranks that
 share GPU 0 over gloo and in one rank over RCCL (tests/dist_worker.py).  Every combined output equals
-the single-GPU golden ceremony."""
+the single-GPU golden ceremony; at BASELINE config 2's size (n=1024) the combined outputs of two
+processes equal the single-GPU ceremony on the same inputs."""
 import json
 import os
 import socket
@@ -13,6 +14,23 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _spawn(ws, backend, args, timeout=100):
+    port = _free_port()
+    procs = []
+    for r in range(ws):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(ws), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), DKG_DIST_BACKEND=backend)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py")] + args,
+                                      env=env))
+    try:
+        rcs = [p.wait(timeout=timeout) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * ws, rcs
 
 
 def _free_port():
@@ -27,20 +45,7 @@ def test_sharded_ceremony_processes(tmp_path, golden, ws, backend):
     RCCL -- the real all_gather_into_tensor on device buffers and the stream fences around the
     library's calls (one GPU per rank, so world size 1 here; the driver's 8-GPU node runs more)."""
     out = tmp_path / "dist.json"
-    port = _free_port()
-    procs = []
-    for r in range(ws):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(ws), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), DKG_DIST_BACKEND=backend)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"), str(out)],
-                                      env=env))
-    try:
-        rcs = [p.wait(timeout=100) for p in procs]
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-    assert rcs == [0] * ws, rcs
+    _spawn(ws, backend, [str(out)])
     res = json.loads(out.read_text())
     assert len(res) == 7
     for name, got in res.items():
@@ -53,3 +58,56 @@ def test_sharded_ceremony_processes(tmp_path, golden, ws, backend):
             assert got["mpk"] is None, name  # Phases<Phase4>::proceed fails for everyone (committee.rs:673-677)
         else:
             assert got["mpk"] == c["mpk"], name
+
+
+def test_sharded_processes_n1024(tmp_path):
+    """Two processes (gloo, sharing GPU 0), n=1024, t=511: a committee with faults inside both ranks'
+    dealer ranges (tests/test_gpu_scale.py _inject: tampered shares and randomness, replaced E and A
+    coefficients, undecodable E rows, tampered self-shares at the global diagonal) through
+    ShardedCeremony.run_verify, and an honest ceremony through ShardedCeremony.run.  The combined
+    decision matrices, qualified / complaints / r2 and r4 errors / reconstruction set, final and
+    public shares and mpk equal the single-GPU ceremony on the same inputs (committee.rs:287-305,
+    311-398, 454-467, 532-569, 660-805)."""
+    import hashlib
+
+    import torch
+
+    import dkg_amd
+    from tests.test_gpu_scale import _device_committee, _tamper_rank
+
+    n, t, ws = 1024, 511, 2
+    N = t + 1
+    be = dkg_amd.Backend(0)
+    try:
+        be.env_init(t, n)
+        ta, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([47]) * 32, 3)
+        del ta
+        for r in range(ws):
+            _tamper_rank(be, n, t, dkg_amd.shard_range(n, ws, r)[0], tE, tA, ts, tsp, seed=200 + r)
+        host = {k: bytes(v.cpu().numpy()) for k, v in (("E", tE), ("A", tA), ("s", ts), ("sp", tsp))}
+        for k, v in host.items():
+            (tmp_path / f"{k}.bin").write_bytes(v)
+        cfg = {"n": n, "t": t, "master_seed": "31" * 32, "ceremony": 5}
+        (tmp_path / "cfg.json").write_text(json.dumps(cfg))
+        single = be.ceremony_verify(host["E"], host["A"], host["s"], host["sp"], n, t)
+        a, b = dkg_amd.dealer_coefficients(bytes.fromhex(cfg["master_seed"]), cfg["ceremony"], 0, n, t)
+        honest = be.ceremony(a, b, n, t)
+        assert len(host["E"]) == 32 * N * n
+    finally:
+        be.close()
+    torch.cuda.synchronize()
+    out = tmp_path / "dist.json"
+    _spawn(ws, "gloo", [str(out), str(tmp_path)], timeout=300)
+    res = json.loads(out.read_text())
+    sha = lambda b: hashlib.sha256("".join(str(v) for v in b).encode()).hexdigest()  # noqa: E731
+    for name, ref in (("tampered", single), ("honest", honest)):
+        got = res[name]
+        assert got["dec2"] == sha(ref.dec2) and got["dec4"] == sha(ref.dec4), name
+        for k in ("qualified", "reconstruct", "complaints2", "r4_error"):
+            assert got[k] == [int(x) for x in getattr(ref, k)], (name, k)
+        assert got["phase4_error"] == bool(ref.phase4_error), name
+        assert got["final_share"] == hashlib.sha256(ref.final_share.hex().encode()).hexdigest(), name
+        assert got["public_share"] == hashlib.sha256(ref.public_share.hex().encode()).hexdigest(), name
+        assert got["mpk"] == ref.mpk.hex(), name
+    assert sum(res["tampered"]["qualified"]) == n - 8 and sum(res["tampered"]["reconstruct"]) == 2
+    assert sum(res["honest"]["qualified"]) == n
