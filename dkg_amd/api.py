@@ -153,6 +153,14 @@ class Backend:
         """0 (default) / 1: the binomial as one launch per Horner step; 2: one persistent dataflow launch."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
+    def set_receiver_parts(self, parts: int):
+        """Stepping in receiver parts with the recombination and checks of each part on a second
+        stream: 0 auto (a lone chunk with < 3 waves per SIMD), 1 off, 2..8 forced; results are identical."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_receiver_parts(self._ctx, parts))
+
+    def last_receiver_parts(self) -> int:
+        return _lib.lib().dkg_ctx_last_receiver_parts(self._ctx)
+
     def set_stepping(self, mode: int):
         """Stepping slots of a split table: 0 cost model, 1 one per column (all pieces), 2 one per
         piece; results are identical."""

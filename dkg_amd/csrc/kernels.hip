@@ -701,13 +701,19 @@ void to_column_major(size_t width, size_t npad, size_t N, const uint32_t* e, uin
 // reachable by crafted commitments or identity padding) marks its workgroup in flags[wg].  !DED with
 // flags: the complete formula, only in the workgroups marked (the same grid is relaunched), which
 // recompute their tables from the start -- so every value is the complete formula's.
-template <int MAXBS, bool DED>
+//
+// Receiver parts: steps j0 .. j1-1 only.  j0 > 0 starts from `sin` (the table after step j0 - 1,
+// laid out like e) instead of e; j1 < nrecv leaves the table after step j1 - 1 in `sout` (another
+// buffer: a part's redo launch restarts from the unchanged `sin`, and rewrites `sout` for the
+// workgroups it redoes before the next part reads it).
+template <int MAXBS, bool DED, bool PARTS>
 __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_stepping(
     size_t ndealers, size_t npad, size_t N, const uint32_t* __restrict__ e, size_t nrecv, size_t pos0, int P,
     const uint32_t* __restrict__ up,  // NULL: top block
     uint32_t* __restrict__ down,      // NULL: block 0
     uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast,
-    uint32_t* __restrict__ flags, size_t col0, size_t dreal, unsigned gw, uint32_t* __restrict__ Rz) {
+    uint32_t* __restrict__ flags, size_t col0, size_t dreal, unsigned gw, uint32_t* __restrict__ Rz, size_t j0,
+    size_t j1, const uint32_t* __restrict__ sin, uint32_t* __restrict__ sout) {
   const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
   if (!DED && flags && !flags[wg]) return;  // a redo launch: this workgroup's tables were exact
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
@@ -734,7 +740,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const size_t pos = pos0 + q;
   ge_p3 D;
   // positions >= Nlive (a short last piece) are the identity whatever the table holds there
-  if (live && pos < Nlive) pt_load(D, e, S, d * N + pos);  // column-major: a segment reads contiguously
+  if (live && pos < Nlive) pt_load(D, (PARTS && j0) ? sin : e, S, d * N + pos);  // column-major: a segment reads contiguously
   else ge_identity(D);
   const bool top_lane = live && (q == Pseg - 1);
   const uint4* upd = (up && live) ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
@@ -743,7 +749,10 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   uint32_t* base = cols + (l - q);
   const uint32_t* nbr = base + ((q + 1) % Pseg);
   bool bad = false;
-  for (size_t j = 0; j < nrecv; j++) {
+  // PARTS = false: the whole receiver range, and nothing of the part machinery in the kernel (the
+  // loop body sits at the 128-VGPR budget)
+  const size_t jbeg = PARTS ? j0 : 0, jend = PARTS ? j1 : nrecv;
+  for (size_t j = jbeg; j < jend; j++) {
     {
       ge_cached c0;
       if (DED) ge_to_cached_ded(c0, D);
@@ -786,6 +795,14 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 #pragma unroll
         for (int k = 0; k < 5; k++) z2[k] = make_uint2(D.Z.v[2 * k], D.Z.v[2 * k + 1]);
       }
+    }
+  }
+  if constexpr (PARTS) {
+    if (j1 < nrecv) {  // uniform; an opaque copy keeps the index out of the loop's live set
+      size_t dd = d;
+      int qq = q;
+      asm volatile("" : "+v"(dd), "+v"(qq));
+      if (live && pos0 + qq < Nlive) pt_store(sout, S, dd * N + pos0 + qq, D);
     }
   }
   if (DED && bad) flags[wg] = 1u;  // any lane: the same value
@@ -875,29 +892,53 @@ struct ColReal {  // which table columns belong to real dealers (k_stepping's `r
   uint32_t* Rz;
 };
 
+template <bool DED, bool PARTS>
+void step_launch_p(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t ndealers, size_t npad, size_t N,
+                   const uint32_t* e, size_t nrecv, size_t pos0, int P, const uint32_t* up, uint32_t* down,
+                   uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags,
+                   const ColReal& cr, size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
+  if (maxbs == 192)
+    hipLaunchKernelGGL((k_stepping<192, DED, PARTS>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P,
+                       up, down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
+                       R ? cr.Rz : nullptr, j0, j1, sin, sout);
+  else if (maxbs == 256)
+    hipLaunchKernelGGL((k_stepping<256, DED, PARTS>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P,
+                       up, down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
+                       R ? cr.Rz : nullptr, j0, j1, sin, sout);
+  else
+    hipLaunchKernelGGL((k_stepping<512, DED, PARTS>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P,
+                       up, down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
+                       R ? cr.Rz : nullptr, j0, j1, sin, sout);
+}
+
 template <bool DED>
 void step_launch(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t ndealers, size_t npad, size_t N,
                  const uint32_t* e, size_t nrecv, size_t pos0, int P, const uint32_t* up, uint32_t* down,
                  uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags,
-                 const ColReal& cr) {
-  if (maxbs == 192)
-    hipLaunchKernelGGL((k_stepping<192, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
-                       R ? cr.Rz : nullptr);
-  else if (maxbs == 256)
-    hipLaunchKernelGGL((k_stepping<256, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
-                       R ? cr.Rz : nullptr);
+                 const ColReal& cr, size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
+  if (j0 != 0 || j1 != nrecv)
+    step_launch_p<DED, true>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, R, pstride,
+                             Nlive, piece0, nseg, Plast, flags, cr, j0, j1, sin, sout);
   else
-    hipLaunchKernelGGL((k_stepping<512, DED>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P, up,
-                       down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
-                       R ? cr.Rz : nullptr);
+    step_launch_p<DED, false>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, R, pstride,
+                              Nlive, piece0, nseg, Plast, flags, cr, 0, nrecv, nullptr, nullptr);
 }
 
-void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
+bool stepping_parts_ok(size_t N, size_t pieces, size_t last_len, bool whole) {
+  return whole && stepping_whole_columns(N, pieces, (!last_len || last_len > N) ? N : last_len);
+}
+
+bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
-              size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw, uint32_t* Rz) {
-  if (!ndealers || !nrecv) return;
+              size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw, uint32_t* Rz,
+              size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
+  if (!j1) j1 = nrecv;
+  // receiver parts: whole-column slots only (tables carried between parts, no block chaining)
+  if ((j0 != 0 || j1 != nrecv) &&
+      !(j0 < j1 && j1 <= nrecv && (!j0 || sin) && (j1 == nrecv || sout) && sin != sout &&
+        stepping_parts_ok(N, pieces, last_len, whole)))
+    return false;
+  if (!ndealers || !nrecv) return true;
   const ColReal cr{col0, dreal, gw ? gw : 64u, Rz};
   if (!last_len || last_len > N) last_len = N;
   // with flags (stepping_flag_words zeroed words): every launch below runs dedicated, then again
@@ -907,10 +948,10 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
                  uint32_t* Rout, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* f) {
     if (f) {
       step_launch<true>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
-                        Nlive, piece0, nseg, Plast, f, cr);
+                        Nlive, piece0, nseg, Plast, f, cr, j0, j1, sin, sout);
     }
     step_launch<false>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
-                       Nlive, piece0, nseg, Plast, f, cr);
+                       Nlive, piece0, nseg, Plast, f, cr, j0, j1, sin, sout);
   };
   auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
     const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), (unsigned)np), block((unsigned)s.bs);
@@ -924,7 +965,7 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
     StepShape s = stepping_shape((pieces - 1) * N + last_len);
     s.P = N;
     launch(s, N, 0u, 1, (int)pieces, (int)last_len);
-    return;
+    return true;
   }
   const StepShape sh = stepping_shape(N);
   if (sh.nblk > 1) {  // one dealer per workgroup, top block first, block values streamed down
@@ -940,10 +981,12 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
           uint32_t* down = b ? ((sh.nblk - 1 - b) % 2 ? stream_b : stream_a) : nullptr;
           if (pass == 0)
             step_launch<true>(512, grid, block, stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down,
-                              b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f, cr);
+                              b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f, cr, 0, nrecv,
+                              nullptr, nullptr);
           else
             step_launch<false>(512, grid, block, stream, ndealers, npad, N, e, nrecv, b * sh.P, (int)sh.P, up, down,
-                               b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f, cr);
+                               b ? nullptr : R, pstride, Nlive, piece0, 1, (int)sh.P, f, cr, 0, nrecv,
+                              nullptr, nullptr);
           up = down;
         }
       }
@@ -955,17 +998,18 @@ void stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
       blocks(N, 0u, pieces - 1);
       blocks(last_len, (unsigned)(pieces - 1), 1);
     }
-    return;
+    return true;
   }
   // whole table in one segment of N lanes, sh.per tables per workgroup; a short last piece in its
   // own launch with segments of last_len lanes (the same column-major stride N)
   if (last_len == N) {
     launch(sh, N, 0u, pieces, 1, (int)sh.P);
-    return;
+    return true;
   }
   if (pieces > 1) launch(sh, N, 0u, pieces - 1, 1, (int)sh.P);
   const StepShape sl = stepping_shape(last_len);
   launch(sl, last_len, (unsigned)(pieces - 1), 1, 1, (int)sl.P);
+  return true;
 }
 
 // Degree split: P(x) = sum_u x^(uL) Q_u(x).  With the stepped values Q_u(j) of
@@ -1154,19 +1198,22 @@ DKG_DEV void ld_z(fe& z, const uint32_t* R, const uint32_t* Rz, size_t e) {  // 
   z = fe{{z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w, z2.x, z2.y}};
 }
 
+// Receivers [j0, j0 + jn) of rows nrecv long; ls (a power of two <= 32) lanes share a run of
+// ls * AFF_RUN receivers, lane k taking receivers k, k + ls, .. of it.
 __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstride, size_t pieces, size_t nrecv,
                                                        const uint32_t* __restrict__ R, uint32_t* __restrict__ A,
-                                                       const uint32_t* __restrict__ Rz) {
-  const size_t span = 32 * AFF_RUN, runs = (nrecv + span - 1) / span;
+                                                       const uint32_t* __restrict__ Rz, size_t j0, size_t jn,
+                                                       unsigned ls) {
+  const size_t span = (size_t)ls * AFF_RUN, runs = (jn + span - 1) / span;
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t item = gid / 32;
+  const size_t item = gid / ls;
   if (item >= pieces * width * runs) return;
   const size_t c = item % width, rest = item / width, run = rest % runs, u = rest / runs;
-  const size_t e0 = (u * pstride + c) * nrecv;
-  const size_t jb = run * span + (gid % 32);  // receivers jb + 32 i, i < cnt
-  const int cnt = jb < nrecv ? (int)min((size_t)AFF_RUN, (nrecv - jb + 31) / 32) : 0;
+  const size_t e0 = (u * pstride + c) * nrecv + j0;
+  const size_t jb = run * span + (gid % ls);  // receivers j0 + jb + ls i, i < cnt
+  const int cnt = jb < jn ? (int)min((size_t)AFF_RUN, (jn - jb + ls - 1) / ls) : 0;
   const int nblk = (cnt + AFF_BLK - 1) / AFF_BLK;
-  auto pt = [&](int i) { return e0 + jb + 32 * (size_t)i; };
+  auto pt = [&](int i) { return e0 + jb + ls * (size_t)i; };
   // points past cnt in the last block count as Z = 1
   fe acc;
   fe_one(acc);
@@ -1240,11 +1287,16 @@ __global__ __launch_bounds__(256) void k_affine_pieces(size_t width, size_t pstr
 }
 
 void affine_pieces(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* R, uint32_t* A,
-                   hipStream_t stream, const uint32_t* Rz) {
-  if (!width || !nrecv || !pieces) return;
-  const size_t runs = (nrecv + 32 * AFF_RUN - 1) / (32 * AFF_RUN), lanes = pieces * width * runs * 32;
+                   hipStream_t stream, const uint32_t* Rz, size_t j0, size_t jn) {
+  if (!jn) jn = nrecv - j0;
+  if (!width || !jn || !pieces) return;
+  // lanes per run: 32, or fewer for a short receiver part so that each lane still normalises up to
+  // AFF_RUN points with its one inversion
+  unsigned ls = 32;
+  while (ls > 1 && (size_t)(ls / 2) * AFF_RUN >= jn) ls /= 2;
+  const size_t runs = (jn + (size_t)ls * AFF_RUN - 1) / ((size_t)ls * AFF_RUN), lanes = pieces * width * runs * ls;
   hipLaunchKernelGGL(k_affine_pieces, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, width, pstride,
-                     pieces, nrecv, R, A, Rz);
+                     pieces, nrecv, R, A, Rz, j0, jn, ls);
 }
 
 template <int U, int K, int KL>
@@ -1292,10 +1344,11 @@ template <int K, int KL>
 __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width, size_t pstride, size_t nrecv,
                                                       const uint32_t* __restrict__ digits,
                                                       const int16_t* __restrict__ top,
-                                                      const uint32_t* __restrict__ A, uint32_t* __restrict__ R) {
+                                                      const uint32_t* __restrict__ A, uint32_t* __restrict__ R,
+                                                      size_t j0) {
   __shared__ uint32_t qs[KL * AFF_WORDS * 64];
   const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
-  const size_t j = blockIdx.y;
+  const size_t j = j0 + blockIdx.y;
   const bool live = c < width;
   const size_t cc = live ? c : 0;
   ge_aff qr[K - KL > 0 ? K - KL : 1];
@@ -1314,15 +1367,16 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
 }
 
 void combine_short_aff(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* digits,
-                       const int16_t* top, const uint32_t* A, uint32_t* R, hipStream_t stream) {
-  if (!width || !nrecv || pieces < 2 || pieces > 4) return;
-  const dim3 grid((unsigned)((width + 63) / 64), (unsigned)nrecv);
+                       const int16_t* top, const uint32_t* A, uint32_t* R, hipStream_t stream, size_t j0, size_t jn) {
+  if (!jn) jn = nrecv - j0;
+  if (!width || !jn || pieces < 2 || pieces > 4) return;
+  const dim3 grid((unsigned)((width + 63) / 64), (unsigned)jn);
   if (pieces == 2)
-    hipLaunchKernelGGL((k_combine_aff<2, 1>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R);
+    hipLaunchKernelGGL((k_combine_aff<2, 1>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
   else if (pieces == 3)
-    hipLaunchKernelGGL((k_combine_aff<3, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R);
+    hipLaunchKernelGGL((k_combine_aff<3, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
   else
-    hipLaunchKernelGGL((k_combine_aff<4, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R);
+    hipLaunchKernelGGL((k_combine_aff<4, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
 }
 
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,
@@ -1388,10 +1442,11 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
                                                     const uint32_t* __restrict__ tab_g,
                                                     const uint32_t* __restrict__ tab_h,
                                                     const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
-                                                    uint8_t* __restrict__ dec4, const uint32_t* __restrict__ scale) {
+                                                    uint8_t* __restrict__ dec4, const uint32_t* __restrict__ scale,
+                                                    size_t j0, size_t jn) {
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ndealers * nrecv) return;
-  const size_t i = dealer0 + p / nrecv, j = p % nrecv;
+  if (p >= ndealers * jn) return;
+  const size_t i = dealer0 + p / jn, j = j0 + p % jn;
   const size_t cE = (i / 64) * 128 + i % 64, cA = cE + 64;
   const size_t q = i * nrecv + j;  // share / decision index
   const bool self = (uint32_t)((i + dealer_base) % nmod) == (uint32_t)j;
@@ -1415,11 +1470,13 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
 
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
                 const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
-                const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream, const uint32_t* scale) {
-  const size_t total = ndealers * nrecv;
+                const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream, const uint32_t* scale, size_t j0,
+                size_t jn) {
+  if (!jn) jn = nrecv - j0;
+  const size_t total = ndealers * jn;
   if (!total) return;
   hipLaunchKernelGGL(k_check_both, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
-                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale);
+                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale, j0, jn);
 }
 
 // Identity in every column of a position-major table [40][S] (S = N * npad words apart).

@@ -43,6 +43,9 @@ struct dkg_ctx {
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
+  int recv_parts = 0;                   // receiver parts of a lone chunk's stepping (0: auto, 1: off)
+  int last_recv_parts = 1;              // parts used by the last verify_device
+  hipEvent_t rpart[8] = {}, rjoin = nullptr;  // part h's stepping done / the aux stream's work done
   int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step),
                                         // 2 one persistent dataflow launch (k_binom_flow)
   uint32_t* flow_state = nullptr;       // dataflow binomial: per chunk [flags | ticket | err] words,
@@ -542,13 +545,13 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   for (int k = 0; k < nseg; k++)
     if (segs[k].extra_ok) dkgk::and_dealer_mask(D, nseg, k, segs[k].extra_ok, dok, home);
   // checks of dealers [d0, d1) on stream st
-  auto checks = [&](size_t d0, size_t d1, hipStream_t st) {
+  auto checks = [&](size_t d0, size_t d1, hipStream_t st, size_t j0 = 0, size_t jn = 0) {
     if (d1 <= d0) return;
     wait_shares(ctx, st);
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
       dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
-                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st, sscale);
+                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st, sscale, j0, jn);
     } else {
       dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, g.self_mod ? g.self_mod : n, g.round, g.s + d0 * n * 8,
                   g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n * PT_WORDS_H, ctx->tab_gw, ctx->tab_hw,
@@ -566,6 +569,35 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   }
   // persistent grid: 4 workgroups (16 waves) per CU fill the chip; chunks launched side by side share it
   const unsigned flow_grid = 1024;
+  // Chunk streams pay when the binomial saturates the GPU (chunk c+1's triangle fills the CUs that
+  // chunk c's launch tails leave idle), or when the stepping is long enough (W * L * n lane-steps)
+  // that the chunks' phases drift apart and one chunk's recombination and checks run beside the
+  // other's stepping.  A small ceremony or shard is latency-bound -- every binomial step is one
+  // dependent NAF chain long whatever its width -- and two half-width pipelines only double its
+  // launches.  Measured (tools/shard_time.py): chunks gain 1.2-2.4 ms on n=512 1- and 2-way (>= 6.7e7
+  // lane-steps) and 0.3-0.8 ms on n=1024 1- to 4-way, and lose 0.9-2.5 ms on n=512 4-way and n=256
+  // (<= 3.4e7) -- and 2 ms on the 8-way n=1024 shard (256 columns: two half-width stepping launches
+  // of 128 workgroups each, 18.1 vs 20.2 ms, profiles/r02_shard_stepping_ab.txt), so a long stepping
+  // needs at least 512 columns too.
+  const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
+  const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
+  const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
+  // Receiver parts: a lone chunk whose stepping holds few waves per SIMD (the 8-way n=1024 shard:
+  // 2) leaves issue slots idle for n dependent steps.  Its stepping then runs in H launches over
+  // receiver ranges (the table carried between them in v.rstate), and part h's normalisation,
+  // recombination and checks run on a second stream beside part h+1's stepping.  Off with one
+  // stream (ctx->nsub == 1: the serialised, per-kernel-timed schedule).
+  size_t H = 1;
+  const bool parts_ok = nsub == 1 && ctx->nsub > 1 && short_mult && Aff && nseg == 2 &&
+                        dkgk::stepping_parts_ok(L, U, Lr, whole) && n >= 128;
+  if (parts_ok) {
+    if (ctx->recv_parts > 1) H = (size_t)ctx->recv_parts;
+    else if (ctx->recv_parts == 0 && dkgk::stepping_waves_per_simd(npad, L, U, Lr, whole) < 3.0) H = 4;
+    H = std::min(H, n / 32);
+  }
+  ctx->last_recv_parts = (int)H;
+  // the table between parts, double-buffered (part h reads one and writes the other)
+  uint32_t* rstate = H > 1 ? buf<uint32_t>(ctx, "v.rstate", 2 * PTB * L * W) : nullptr;
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm, size_t chunk_idx) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
@@ -595,9 +627,36 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
-    (step_ilp ? dkgk_ilp::stepping : dkgk::stepping)(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-                   sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw,
-                   Rz ? Rz + c0 * n * 10 : nullptr);
+    auto step = step_ilp ? dkgk_ilp::stepping : dkgk::stepping;
+    if (H > 1) {
+      // part h: receivers [jb(h), jb(h+1)); its flag words follow part h-1's (a whole-column grid
+      // uses at most w of them, stepping_flag_words leaves (U + 1) w per chunk; parts U + 1 apart
+      // share words, which can only cost a redundant -- exact -- redo)
+      hipStream_t aux = ctx->sub[0];
+      auto jb = [&](size_t h) { return h == H ? n : (n * h / H) / 32 * 32; };
+      for (size_t h = 0; h < H; h++) {
+        const size_t j0 = jb(h), j1 = jb(h + 1);
+        if (!step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, nullptr, nullptr, st, U, npad, Lr, whole,
+                  fl ? fl + (h % (U + 1)) * w : nullptr, c0, D, (unsigned)gw, Rz + c0 * n * 10, j0, j1,
+                  rstate + (h % 2) * 40 * L * W + c0 * L, rstate + ((h + 1) % 2) * 40 * L * W + c0 * L)) {
+          ctx->err = "verify_device: receiver parts need whole-column stepping";
+          throw Fail{DKG_E_ARG};
+        }
+        HCK(hipEventRecord(ctx->rpart[h % 8], st));
+        HCK(hipStreamWaitEvent(aux, ctx->rpart[h % 8], 0));
+        dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, aux,
+                            Rz + c0 * n * 10, j0, j1 - j0);
+        dkgk::combine_short_aff(w, npad, U, n, sdig, stop, Aff + c0 * n * AFFP_WORDS_H, R + c0 * n * PT_WORDS_H,
+                                aux, j0, j1 - j0);
+        checks(g0 * 64, std::min(D, g1 * 64), aux, j0, j1 - j0);
+      }
+      HCK(hipEventRecord(ctx->rjoin, aux));
+      HCK(hipStreamWaitEvent(st, ctx->rjoin, 0));
+      return;
+    }
+    step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
+         sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw,
+         Rz ? Rz + c0 * n * 10 : nullptr, 0, 0, nullptr, nullptr);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     if (short_mult && Aff) {
       dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st, Rz + c0 * n * 10);
@@ -608,23 +667,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     checks(g0 * 64, std::min(D, g1 * 64), st);
     if (tm) HCK(hipEventRecord(ctx->pev[4], st));
   };
-  // Chunk streams pay when the binomial saturates the GPU (chunk c+1's triangle fills the CUs that
-  // chunk c's launch tails leave idle), or when the stepping is long enough (W * L * n lane-steps)
-  // that the chunks' phases drift apart and one chunk's recombination and checks run beside the
-  // other's stepping.  A small ceremony or shard is latency-bound -- every binomial step is one
-  // dependent NAF chain long whatever its width -- and two half-width pipelines only double its
-  // launches.  Measured (tools/shard_time.py): chunks gain 1.2-2.4 ms on n=512 1- and 2-way (>= 6.7e7
-  // lane-steps) and 0.3-0.8 ms on n=1024 1- to 4-way, and lose 0.9-2.5 ms on n=512 4-way and n=256
-  // (<= 3.4e7) -- and 2 ms on the 8-way n=1024 shard (256 columns: two half-width stepping launches
-  // of 128 workgroups each, 18.1 vs 20.2 ms, profiles/r02_shard_stepping_ab.txt), so a long stepping
-  // needs at least 512 columns too.
-  const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
-  const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
-  const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
   ctx->timed_tag.clear();
   if (nsub <= 1) {
-    chunk(0, groups, home, timed, 0);
-    if (timed) ctx->timed_tag = tag;
+    // the receiver-part schedule interleaves the phases on two streams: no per-phase times
+    chunk(0, groups, home, timed && H == 1, 0);
+    if (timed && H == 1) ctx->timed_tag = tag;
   } else {
     HCK(hipEventRecord(ctx->fork, home));
     size_t g0 = 0;
@@ -1413,6 +1460,8 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     HCK(hipEventCreateWithFlags(&ctx->pub_done, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : ctx->rpart) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&ctx->rjoin, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_gw, COMBW_BYTES));
@@ -1451,6 +1500,9 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->join)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->rpart)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->rjoin) (void)hipEventDestroy(ctx->rjoin);
   if (ctx->fork) (void)hipEventDestroy(ctx->fork);
   for (auto& st : ctx->sub)
     if (st) (void)hipStreamDestroy(st);
@@ -1489,6 +1541,13 @@ int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
   ctx->split = pieces;
   return DKG_OK;
 }
+
+int dkg_ctx_set_receiver_parts(dkg_ctx* ctx, int parts) {
+  if (!ctx || parts < 0 || parts > 8) return DKG_E_ARG;
+  ctx->recv_parts = parts;
+  return DKG_OK;
+}
+int dkg_ctx_last_receiver_parts(const dkg_ctx* ctx) { return ctx ? ctx->last_recv_parts : 0; }
 
 int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 5) return DKG_E_ARG;

@@ -499,6 +499,46 @@ def test_shard_ranks_n1024_all_match_single(be):
     assert o.reconstruct == [int(i in {dkg_amd.shard_range(n, ws, r)[0] + 2 for r in range(ws)}) for i in range(n)]
 
 
+@pytest.mark.parametrize("n,t,ws,rank", [(1024, 511, 8, 3), (512, 255, 4, 1)])
+def test_receiver_parts_match(be, n, t, ws, rank):
+    """A lone dealer chunk with few waves per SIMD (a rank of the 8-way n=1024 split: 2; of the 4-way
+    n=512 split: 1) steps its receivers in parts, each part's normalisation, recombination and checks
+    on a second stream beside the next part's stepping (the table carried between parts in a
+    double-buffered state).  With tampered dealers inside the rank and an identity E row and A row
+    (exceptional dedicated additions: the marked workgroups are redone per part from that part's
+    starting table), 1 (off), 2, 3, 4, 8 and the automatic choice (4) give identical rows, and the
+    tampered dealers' rows equal the oracle's (committee.rs:287-305, 532-548)."""
+    n_, N = n, t + 1
+    h = be.env_init(t, n, CK)
+    ta, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([53]) * 32, 4)
+    del ta
+    d0, d1 = dkg_amd.shard_range(n, ws, rank)
+    E, A, s, sp = _tamper_rank(be, n, t, d0, tE, tA, ts, tsp, seed=300 + rank)
+    for d, tb in ((d0 + 7, tE), (d0 + 70, tA)):  # identity rows (committee.rs:1127 style)
+        tb[32 * N * d:32 * N * (d + 1)] = 0
+    outs = []
+    try:
+        for parts in (1, 2, 3, 4, 8, 0):
+            be.set_receiver_parts(parts)
+            d2, d4 = _rank_rows(be, n, t, d0, d1, tE, tA, ts, tsp)
+            outs.append((d2.cpu().numpy().tobytes(), d4.cpu().numpy().tobytes(), be.last_receiver_parts(),
+                         be.stepping_redos()))
+    finally:
+        be.set_receiver_parts(0)
+    assert outs[0][2] == 1
+    for o, parts in zip(outs[1:], (2, 3, 4, 8, 0)):
+        assert o[2] == (parts or 4), (parts, o[2])
+        assert o[0] == outs[0][0] and o[1] == outs[0][1], parts
+        assert o[3] > 0, parts
+    exp = _expected_rows(n_, t, h, E, A, s, sp, base=d0)
+    D = d1 - d0
+    r2 = [outs[0][0][i * n:(i + 1) * n] for i in range(D)]
+    r4 = [outs[0][1][i * n:(i + 1) * n] for i in range(D)]
+    for i in range(5):
+        assert r2[i] == exp[(i, 2)] and r4[i] == exp[(i, 4)], i
+    assert r2[7].count(REJECT) == n - 1 and r4[70].count(REJECT) == n - 1
+
+
 @pytest.mark.parametrize("n,t,split", [(1024, 511, 4), (1024, 511, 3), (1100, 549, 2), (300, 149, 1)])
 def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
     """The dataflow binomial (k_binom_flow: all Horner steps in one persistent launch with
