@@ -924,19 +924,16 @@ void step_launch(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t nd
                               Nlive, piece0, nseg, Plast, flags, cr, 0, nrecv, nullptr, nullptr);
 }
 
-bool stepping_parts_ok(size_t N, size_t pieces, size_t last_len, bool whole) {
-  return whole && stepping_whole_columns(N, pieces, (!last_len || last_len > N) ? N : last_len);
-}
+bool stepping_parts_ok(size_t N) { return N <= 512; }  // one block per table: no boundary streams
 
 bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
               size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw, uint32_t* Rz,
               size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
   if (!j1) j1 = nrecv;
-  // receiver parts: whole-column slots only (tables carried between parts, no block chaining)
+  // receiver parts: tables carried between parts; not with block chaining (N > 512)
   if ((j0 != 0 || j1 != nrecv) &&
-      !(j0 < j1 && j1 <= nrecv && (!j0 || sin) && (j1 == nrecv || sout) && sin != sout &&
-        stepping_parts_ok(N, pieces, last_len, whole)))
+      !(j0 < j1 && j1 <= nrecv && (!j0 || sin) && (j1 == nrecv || sout) && sin != sout && stepping_parts_ok(N)))
     return false;
   if (!ndealers || !nrecv) return true;
   const ColReal cr{col0, dreal, gw ? gw : 64u, Rz};

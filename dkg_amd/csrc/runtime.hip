@@ -589,15 +589,23 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // stream (ctx->nsub == 1: the serialised, per-kernel-timed schedule).
   size_t H = 1;
   const bool parts_ok = nsub == 1 && ctx->nsub > 1 && short_mult && Aff && nseg == 2 &&
-                        dkgk::stepping_parts_ok(L, U, Lr, whole) && n >= 128;
+                        dkgk::stepping_parts_ok(L) && n >= 128;
   if (parts_ok) {
     if (ctx->recv_parts > 1) H = (size_t)ctx->recv_parts;
     else if (ctx->recv_parts == 0 && dkgk::stepping_waves_per_simd(npad, L, U, Lr, whole) < 3.0) H = 4;
     H = std::min(H, n / 32);
   }
   ctx->last_recv_parts = (int)H;
-  // the table between parts, double-buffered (part h reads one and writes the other)
+  // the table between parts, double-buffered (part h reads one and writes the other); flag words
+  // of the dedicated additions per part (every stepping() call numbers its launches from 0)
   uint32_t* rstate = H > 1 ? buf<uint32_t>(ctx, "v.rstate", 2 * PTB * L * W) : nullptr;
+  const size_t pfw = dkgk::stepping_flag_words(npad, U);
+  uint32_t* pflags = H > 1 && sflags ? buf<uint32_t>(ctx, "v.sflags_parts", 4 * H * pfw) : nullptr;
+  if (pflags) {
+    HCK(hipMemsetAsync(pflags, 0, 4 * H * pfw, home));
+    ctx->last_step_flags = pflags;
+    ctx->last_step_flag_words = H * pfw;
+  }
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm, size_t chunk_idx) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
@@ -629,15 +637,13 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     auto step = step_ilp ? dkgk_ilp::stepping : dkgk::stepping;
     if (H > 1) {
-      // part h: receivers [jb(h), jb(h+1)); its flag words follow part h-1's (a whole-column grid
-      // uses at most w of them, stepping_flag_words leaves (U + 1) w per chunk; parts U + 1 apart
-      // share words, which can only cost a redundant -- exact -- redo)
+      // part h: receivers [jb(h), jb(h+1)), flag words pflags[h * pfw ..] (a lone chunk: c0 = 0)
       hipStream_t aux = ctx->sub[0];
       auto jb = [&](size_t h) { return h == H ? n : (n * h / H) / 32 * 32; };
       for (size_t h = 0; h < H; h++) {
         const size_t j0 = jb(h), j1 = jb(h + 1);
         if (!step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, nullptr, nullptr, st, U, npad, Lr, whole,
-                  fl ? fl + (h % (U + 1)) * w : nullptr, c0, D, (unsigned)gw, Rz + c0 * n * 10, j0, j1,
+                  pflags ? pflags + h * pfw : nullptr, c0, D, (unsigned)gw, Rz + c0 * n * 10, j0, j1,
                   rstate + (h % 2) * 40 * L * W + c0 * L, rstate + ((h + 1) % 2) * 40 * L * W + c0 * L)) {
           ctx->err = "verify_device: receiver parts need whole-column stepping";
           throw Fail{DKG_E_ARG};
