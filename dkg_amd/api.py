@@ -155,7 +155,7 @@ class Backend:
 
     def set_receiver_parts(self, parts: int):
         """Stepping in receiver parts with the recombination and checks of each part on a second
-        stream: 0 auto (a lone chunk with < 3 waves per SIMD), 1 off, 2..8 forced; results are identical."""
+        stream (opt-in, measured slower): 0/1 off, 2..8 parts; results are identical."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_receiver_parts(self._ctx, parts))
 
     def last_receiver_parts(self) -> int:

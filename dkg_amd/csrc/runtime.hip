@@ -43,7 +43,7 @@ struct dkg_ctx {
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
-  int recv_parts = 0;                   // receiver parts of a lone chunk's stepping (0: auto, 1: off)
+  int recv_parts = 0;                   // receiver parts of the stepping (0/1: off, 2..8: opt-in)
   int last_recv_parts = 1;              // parts used by the last verify_device
   hipEvent_t rpart[8] = {}, rjoin = nullptr;  // part h's stepping done / the aux stream's work done
   int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step),
@@ -581,19 +581,21 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // needs at least 512 columns too.
   const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
   const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
-  const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
-  // Receiver parts: a lone chunk whose stepping holds few waves per SIMD (the 8-way n=1024 shard:
-  // 2) leaves issue slots idle for n dependent steps.  Its stepping then runs in H launches over
-  // receiver ranges (the table carried between them in v.rstate), and part h's normalisation,
-  // recombination and checks run on a second stream beside part h+1's stepping.  Off with one
-  // stream (ctx->nsub == 1: the serialised, per-kernel-timed schedule).
+  // Receiver parts (opt-in, dkg_ctx_set_receiver_parts 2..8): the stepping runs in H launches
+  // over receiver ranges (the table carried between them in v.rstate), and part h's normalisation,
+  // recombination and checks run on a second stream beside part h+1's stepping, in place of the
+  // dealer chunks.  Meant for a lone chunk with few waves per SIMD (the 8-way n=1024 shard: 2), it
+  // measured no gain there: every part's recombination and checks are latency-bound themselves
+  // and slow the stepping they share the CUs with (14.8 ms unsplit, 14.8 / 15.6 / 22.0 ms at 2 / 4
+  // / 8 parts; 19.6 with the part work on the low-priority stream; the 4-way shard 23.1 vs 25.1,
+  // profiles/r03_receiver_parts_ab.txt).  Needs >= 2 streams (ctx->nsub > 1).
+  const bool parts_able = ctx->nsub > 1 && short_mult && Aff && nseg == 2 && dkgk::stepping_parts_ok(L) && n >= 128;
+  const size_t nsub = (parts_able && ctx->recv_parts > 1) ? 1
+                      : (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
   size_t H = 1;
-  const bool parts_ok = nsub == 1 && ctx->nsub > 1 && short_mult && Aff && nseg == 2 &&
-                        dkgk::stepping_parts_ok(L) && n >= 128;
+  const bool parts_ok = nsub == 1 && parts_able;
   if (parts_ok) {
-    if (ctx->recv_parts > 1) H = (size_t)ctx->recv_parts;
-    else if (ctx->recv_parts == 0 && dkgk::stepping_waves_per_simd(npad, L, U, Lr, whole) < 3.0) H = 4;
-    H = std::min(H, n / 32);
+    if (ctx->recv_parts > 1) H = std::min((size_t)ctx->recv_parts, n / 32);
   }
   ctx->last_recv_parts = (int)H;
   // the table between parts, double-buffered (part h reads one and writes the other); flag words

@@ -75,12 +75,11 @@ int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
  * per step; 2 -- all t steps in ONE persistent dataflow launch (each item waits only for the table
  * positions of the previous step it reads or overwrites).  Outputs do not depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
-/* Receiver parts of the stepping when the verification runs as ONE dealer chunk with few waves per
- * SIMD (a small shard, e.g. 128 dealers of n = 1024): the stepping runs in `parts` launches over
+/* Receiver parts of the stepping (opt-in schedule): the stepping runs in `parts` launches over
  * receiver ranges, and each part's recombination and checks run on a second stream beside the next
- * part's stepping.  0 (default) -- 4 parts when the stepping holds < 3 waves per SIMD and the
- * context has >= 2 streams (dkg_ctx_set_streams), 1 -- off, 2..8 -- that many wherever usable
- * (whole-column stepping, short multipliers, fused rounds 2/4).  Outputs do not depend on it;
+ * part's stepping, in place of the dealer-chunk streams.  0 / 1 (default) -- off, 2..8 -- that many
+ * wherever usable (>= 2 streams, tables of <= 512 positions, short multipliers, fused rounds 2/4).
+ * Measured slower than the default schedule.  Outputs do not depend on it;
  * dkg_ctx_last_receiver_parts reports what the last verification used. */
 int dkg_ctx_set_receiver_parts(dkg_ctx *ctx, int parts);
 int dkg_ctx_last_receiver_parts(const dkg_ctx *ctx);

@@ -501,13 +501,14 @@ def test_shard_ranks_n1024_all_match_single(be):
 
 @pytest.mark.parametrize("n,t,ws,rank", [(1024, 511, 8, 3), (512, 255, 4, 1)])
 def test_receiver_parts_match(be, n, t, ws, rank):
-    """A lone dealer chunk with few waves per SIMD (a rank of the 8-way n=1024 split: 2; of the 4-way
-    n=512 split: 1) steps its receivers in parts, each part's normalisation, recombination and checks
-    on a second stream beside the next part's stepping (the table carried between parts in a
-    double-buffered state).  With tampered dealers inside the rank and an identity E row and A row
-    (exceptional dedicated additions: the marked workgroups are redone per part from that part's
-    starting table), 1 (off), 2, 3, 4, 8 and the automatic choice (4) give identical rows, and the
-    tampered dealers' rows equal the oracle's (committee.rs:287-305, 532-548)."""
+    """The opt-in receiver-part schedule (dkg_ctx_set_receiver_parts) on a rank of the 8-way n=1024
+    split and of the 4-way n=512 split: the stepping in receiver ranges, each part's normalisation,
+    recombination and checks on a second stream beside the next part's stepping (the table carried
+    between parts in a double-buffered state).  With tampered dealers inside the rank and an identity
+    E row and A row (exceptional dedicated additions: the marked workgroups are redone per part from
+    that part's starting table), 2, 3, 4 and 8 parts give the same rows as the default schedule (0
+    and 1: unsplit), and the tampered dealers' rows equal the oracle's (committee.rs:287-305,
+    532-548)."""
     n_, N = n, t + 1
     h = be.env_init(t, n, CK)
     ta, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([53]) * 32, 4)
@@ -518,7 +519,7 @@ def test_receiver_parts_match(be, n, t, ws, rank):
         tb[32 * N * d:32 * N * (d + 1)] = 0
     outs = []
     try:
-        for parts in (1, 2, 3, 4, 8, 0):
+        for parts in (1, 2, 3, 4, 8):
             be.set_receiver_parts(parts)
             d2, d4 = _rank_rows(be, n, t, d0, d1, tE, tA, ts, tsp)
             outs.append((d2.cpu().numpy().tobytes(), d4.cpu().numpy().tobytes(), be.last_receiver_parts(),
@@ -526,8 +527,8 @@ def test_receiver_parts_match(be, n, t, ws, rank):
     finally:
         be.set_receiver_parts(0)
     assert outs[0][2] == 1
-    for o, parts in zip(outs[1:], (2, 3, 4, 8, 0)):
-        assert o[2] == (parts or 4), (parts, o[2])
+    for o, parts in zip(outs[1:], (2, 3, 4, 8)):
+        assert o[2] == parts, (parts, o[2])
         assert o[0] == outs[0][0] and o[1] == outs[0][1], parts
         assert o[3] > 0, parts
     exp = _expected_rows(n_, t, h, E, A, s, sp, base=d0)
