@@ -40,10 +40,22 @@ BATCH = {"B5": (10000, 64, 31)}  # BASELINE config 5: 10,000 independent n=64, t
 #   instr -- plain VALU instruction count (the round-1 unit, reported beside it as instr_frac).
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
 VALU = {"fe_mul": (140, 256), "fe_sq": (109, 185), "ge_add": (1184, 2152), "ge_add_signed": (1228, 2200),
-        "ge_madd_signed": (1130, 1992), "ge_add_ded": (1198, 2180), "ge_to_cached_ded": (70, 70),
+        "ge_madd_signed": (1130, 1992), "ge_madd_signed_not": (1001, 1744), "ge_add_signed_not": (1100, 1954),
+        "ge_add_ded": (1198, 2180), "ge_to_cached_ded": (70, 70),
         "fe_tight_zero": (16, 31), "ge_dbl_t": (1058, 1855), "ge_dbl_not": (930, 1611), "comb_window": (1181, 2074),
         "combw_window": (1171, 2037), "ge_to_cached": (193, 309), "eq": (633, 1151), "sc_mont_mul": (580, 834)}
 INSTR = {k: v[0] for k, v in VALU.items()}
+# an addition followed by a doubling skips T (ge_add_signed / ge_madd_signed / ge_add_lds with_t = false):
+# one product less; the "_not" counts are measured for the signed forms, ge_add's is derived
+NO_T = {"ge_add_signed": "ge_add_signed_not", "ge_madd_signed": "ge_madd_signed_not"}
+
+
+def add_cost(VALU, name, with_t=True):
+    if with_t:
+        return VALU[name]
+    if name in NO_T:
+        return VALU[NO_T[name]]
+    return VALU[name] - (VALU["ge_add_signed"] - VALU["ge_add_signed_not"])
 COMBW_WINDOWS = 26  # points.h: radix-2^10 fixed-base comb, one mixed addition per window
 SLOTS = {k: v[1] for k, v in VALU.items()}
 
@@ -97,8 +109,8 @@ def hybrid_valu(n, sk, VALU=SLOTS):
         for i in range(top, -1, -1):
             if i != top:
                 c += VALU["ge_dbl_t"] if (ds[i] or i == 0) else VALU["ge_dbl_not"]
-            if ds[i]:
-                c += VALU["ge_add_signed"]
+            if ds[i]:  # a doubling follows unless i = 0: no T
+                c += add_cost(VALU, "ge_add_signed", i == 0)
         dec += 2 * n * c
     encode = HY_ENCODE[0] * VALU["fe_sq"] + HY_ENCODE[1] * VALU["fe_mul"]
     decode = HY_DECODE[0] * VALU["fe_sq"] + HY_DECODE[1] * VALU["fe_mul"]
@@ -263,10 +275,13 @@ def short_combine_valu(mults, VALU=SLOTS, affine=True):
             nz = [u for u in range(U) if i < len(ds[u]) and ds[u][i] != 0]
             if i != top:
                 c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
-            if affine:
-                c += len(nz) * VALU["ge_madd_signed"]
-            else:
-                c += sum(VALU["ge_add"] if u < KL else VALU["ge_add_signed"] for u in nz)
+            # the last addition of a position above 0 is followed by a doubling: no T
+            for u in nz:
+                wt = i == 0 or u != nz[-1]
+                if affine:
+                    c += add_cost(VALU, "ge_madd_signed", wt)
+                else:
+                    c += add_cost(VALU, "ge_add" if u < KL else "ge_add_signed", wt)
         total += c
     return total
 
@@ -287,8 +302,8 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
             for i in range(len(ds) - 2, -1, -1):
                 nz = ds[i] != 0
                 c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
-                if nz:
-                    c += VALU["ge_add_signed"]
+                if nz:  # a doubling follows unless i = 0: no T
+                    c += add_cost(VALU, "ge_add_signed", i == 0)
         cost_m[m] = c
     # position m of a piece of length Lp is live for Lp-m steps (a short last piece starts late)
     binom = sum(sum(cost_m[m] * (Lp - m) for m in range(1, Lp)) for Lp in pieces)
@@ -316,13 +331,16 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
                     nz = d1[i] != 0
                     c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
                     if nz:
-                        c += VALU["ge_add_signed"]
+                        c += add_cost(VALU, "ge_add_signed", i == 0)
             joint = 3 * VALU["ge_to_cached"] + VALU["ge_add"]  # two addends, Q_2v, + Q_2v
             for i in range(max(len(d1), len(d2)) - 1, -1, -1):
                 e1 = d1[i] if i < len(d1) else 0
                 e2 = d2[i] if i < len(d2) else 0
                 joint += VALU["ge_dbl_t"] if (e1 or e2 or i == 0) else VALU["ge_dbl_not"]
-                joint += VALU["ge_add_signed"] * ((e1 != 0) + (e2 != 0))
+                if e2:
+                    joint += add_cost(VALU, "ge_add_signed", e1 != 0 or i == 0)
+                if e1:
+                    joint += add_cost(VALU, "ge_add_signed", i == 0)
             c += ((U + 1) // 2 - 1) * joint
             combine += c
     nsc = 2 if rnd == 2 else 1

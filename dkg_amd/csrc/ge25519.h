@@ -212,7 +212,9 @@ DKG_DEV void ge_dbl_lean(ge_p3& r, const ge_p3& p, bool with_t) {
 
 // r = p + q (neg = false) or p - q (neg = true) with one code path: the sign only selects
 // which of (Y+X, Y-X) multiplies which, and the sign of the 2dT product.
-DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg) {
+// with_t = false skips T (one product): valid when the next operation is a doubling, which does not
+// read it.
+DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg, bool with_t = true) {
   fe a, b, e, h, t, qa, qb;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -235,7 +237,7 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
   fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
-  fe_mul(r.T, e, h);
+  if (with_t) fe_mul(r.T, e, h);
 }
 
 // r = p + q (neg = false) or p - q (neg = true), q affine Niels (Z = 1): 7M, one code path.  The
@@ -243,7 +245,7 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
 // f and g keep ge_add_signed's bounds whatever the sign.  q's fields are second operands only, so
 // they may carry the cached form's uncarried bounds (y+x <= 2^27, y-x <= 2^27.585;
 // tools/fe_bounds.py).
-DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg) {
+DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg, bool with_t = true) {
   fe a, b, e, h, t, qa, qb;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -267,7 +269,7 @@ DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg)
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
   fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
-  fe_mul(r.T, e, h);
+  if (with_t) fe_mul(r.T, e, h);
 }
 
 // ---- Ristretto255 (RFC 9496 section 4.3) ----

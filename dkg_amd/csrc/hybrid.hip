@@ -118,7 +118,7 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uin
     for (int b = top - 1; b >= 0; b--) {
       const int d = __builtin_amdgcn_readfirstlane((int)digits[b]);
       ge_dbl_lean(x, x, d != 0 || b == 0);
-      if (d != 0) ge_add_lds(x, x, qcol, d < 0);
+      if (d != 0) ge_add_lds(x, x, qcol, d < 0, 64, b == 0);
     }
   }
   if (live) pt_store(K_ext, count, idx, x);
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const 
       for (; b > be; b--) ge_dbl_lean(x, x, b - 1 == be);  // T only before the addition
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the DMA'd addend has landed
       __builtin_amdgcn_s_barrier();
-      ge_add_lds(x, x, qcol, de < 0);
+      ge_add_lds(x, x, qcol, de < 0, 64, be == 0);          // a doubling follows unless be = 0
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done
       if (e + 1 < nnz) fetch(e + 1);
     }

@@ -311,7 +311,7 @@ __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q)
     const uint32_t bit = 1u << i;
     const bool nz = ((pos | neg) & bit) != 0;
     ge_dbl_lean(y, y, nz || i == 0);
-    if (nz) ge_add_lds(y, y, q, (neg & bit) != 0);
+    if (nz) ge_add_lds(y, y, q, (neg & bit) != 0, 64, i == 0);  // T only for the result
   }
 }
 
@@ -341,7 +341,7 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
     const uint32_t bit = 1u << i;
     const bool nz = ((pos | neg) & bit) != 0;
     ge_dbl_rt(y, y, nz || i == 0);           // T only when an addition (or the result) needs it
-    if (nz) ge_add_signed(y, y, xc, (neg & bit) != 0);
+    if (nz) ge_add_signed(y, y, xc, (neg & bit) != 0, i == 0);
   }
 }
 
@@ -1046,7 +1046,7 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
     for (int b = t1 - 1; b >= 0; b--) {  // leading NAF digit +1: acc already holds 1 * Q
       const int dg = __builtin_amdgcn_readfirstlane((int)d1[b]);
       ge_dbl_lean(acc, acc, dg != 0 || b == 0);
-      if (dg != 0) ge_add_lds(acc, acc, slot_y, dg < 0);
+      if (dg != 0) ge_add_lds(acc, acc, slot_y, dg < 0, 64, b == 0);
     }
     load_q(q, 2 * v);
     put(slot_y, q);  // the chain is done with slot_y: the last addend goes through LDS too
@@ -1066,8 +1066,8 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
         const int e1 = __builtin_amdgcn_readfirstlane((int)d1[b]);
         const int e2 = __builtin_amdgcn_readfirstlane((int)d2[b]);
         ge_dbl_lean(acc, acc, e1 != 0 || e2 != 0 || b == 0);
-        if (e2 != 0) ge_add_lds(acc, acc, slot_y2, e2 < 0);
-        if (e1 != 0) ge_add_lds(acc, acc, slot_y, e1 < 0);
+        if (e2 != 0) ge_add_lds(acc, acc, slot_y2, e2 < 0, 64, e1 != 0 || b == 0);
+        if (e1 != 0) ge_add_lds(acc, acc, slot_y, e1 < 0, 64, b == 0);
       }
       load_q(q, 2 * v);
       put(slot_y, q);
@@ -1084,6 +1084,13 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
 // LDS (10 KB each per wave), the others stay in VGPRs, so that K = 3 and 4 keep 2 waves per SIMD.
 // digits[j][b] packs the K signed digits of position b, one byte each; top[j] the highest position.
 // (Compile-time recursion over the pieces keeps the register-resident addends out of scratch.)
+// digits of pieces above U at this chain position (wave-uniform): another addition follows
+template <int U, int K>
+DKG_DEV bool higher_digits(uint32_t w) {
+  if constexpr (U + 1 < K) return (w >> (8 * (U + 1))) != 0;
+  else return false;
+}
+
 template <int U, int K, int KL>
 DKG_DEV void short_addends(uint32_t* qs, ge_cached* qr, const uint32_t* R, size_t pstride, size_t cc, size_t nrecv,
                            size_t j) {
@@ -1101,14 +1108,15 @@ DKG_DEV void short_addends(uint32_t* qs, ge_cached* qr, const uint32_t* R, size_
   }
 }
 template <int U, int K, int KL>
-DKG_DEV void short_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_cached* qr) {
+DKG_DEV void short_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_cached* qr, bool last) {
   if constexpr (U < K) {
     const int e = (int8_t)(w >> (8 * U));
     if (e != 0) {
-      if constexpr (U < KL) ge_add_lds(acc, acc, qs + U * PT_WORDS * 64 + threadIdx.x, e < 0);
-      else ge_add_signed(acc, acc, qr[U - KL], e < 0);
+      const bool t = last || higher_digits<U, K>(w);  // else a doubling follows: no T
+      if constexpr (U < KL) ge_add_lds(acc, acc, qs + U * PT_WORDS * 64 + threadIdx.x, e < 0, 64, t);
+      else ge_add_signed(acc, acc, qr[U - KL], e < 0, t);
     }
-    short_position<U + 1, K, KL>(acc, w, qs, qr);
+    short_position<U + 1, K, KL>(acc, w, qs, qr, last);
   }
 }
 
@@ -1131,7 +1139,7 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_short(size_t wid
   for (int b = tp; b >= 0; b--) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(dw[b]);
     if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
-    short_position<0, K, KL>(acc, w, qs, qr);
+    short_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
   if (live) pt_store_aos(R, c * nrecv + j, acc);
 }
@@ -1326,14 +1334,15 @@ DKG_DEV void aff_addends(uint32_t* qs, ge_aff* qr, const uint32_t* A, size_t pst
   }
 }
 template <int U, int K, int KL>
-DKG_DEV void aff_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_aff* qr) {
+DKG_DEV void aff_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_aff* qr, bool last) {
   if constexpr (U < K) {
     const int e = (int8_t)(w >> (8 * U));
     if (e != 0) {
-      if constexpr (U < KL) ge_madd_lds(acc, acc, qs + U * AFF_WORDS * 64 + threadIdx.x, e < 0);
-      else ge_madd_signed(acc, acc, qr[U - KL], e < 0);
+      const bool t = last || higher_digits<U, K>(w);  // else a doubling follows: no T
+      if constexpr (U < KL) ge_madd_lds(acc, acc, qs + U * AFF_WORDS * 64 + threadIdx.x, e < 0, 64, t);
+      else ge_madd_signed(acc, acc, qr[U - KL], e < 0, t);
     }
-    aff_position<U + 1, K, KL>(acc, w, qs, qr);
+    aff_position<U + 1, K, KL>(acc, w, qs, qr, last);
   }
 }
 
@@ -1358,7 +1367,7 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
   for (int b = tp; b >= 0; b--) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(dw[b]);
     if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
-    aff_position<0, K, KL>(acc, w, qs, qr);
+    aff_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
   if (live) pt_store_aos(R, c * nrecv + j, acc);
 }

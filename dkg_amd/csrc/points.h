@@ -216,8 +216,8 @@ DKG_DEV void lds_get_fe(fe& r, const uint32_t* q, int which, int stride = 64) {
 }
 
 // r = p +/- Q with Q the cached point in LDS; `neg` must be wave-uniform.
-DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
-                                           int stride = 64) {
+DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,
+                        bool with_t = true) {
   fe a, b, e, h, t, qv;
   fe_sub(t, p.Y, p.X);
   lds_get_fe(qv, q, neg ? 0 : 1, stride);
@@ -237,7 +237,7 @@ DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg,
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
   fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
-  fe_mul(r.T, e, h);
+  if (with_t) fe_mul(r.T, e, h);
 }
 
 // Dedicated addition (Hisil-Wong-Carter-Dawson 2008, "add-2008-hwcd-4", a = -1): r = p + Q with Q
@@ -277,7 +277,8 @@ DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int str
 
 // r = p +/- Q with Q affine Niels (y+x, y-x, 2dxy) in LDS, read like the cached form above (fields
 // 0, 1, 2): 7M, d = 2Z carried as in ge_madd_signed.  `neg` must be wave-uniform.
-DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64) {
+DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,
+                         bool with_t = true) {
   fe a, b, e, h, t, qv;
   fe_sub(t, p.Y, p.X);
   lds_get_fe(qv, q, neg ? 0 : 1, stride);
@@ -297,6 +298,6 @@ DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, 
   fe_mul(r.X, e, t);
   fe_mul(r.Y, b, h);
   fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
-  fe_mul(r.T, e, h);
+  if (with_t) fe_mul(r.T, e, h);
 }
 

@@ -130,7 +130,8 @@ def test_hybrid_valu_closed_form():
     pre = S["ge_dbl_t"] + 3 * S["ge_add"] + 5 * S["ge_to_cached"]
     c5 = pre + S["ge_add_signed"]  # one digit: one addition onto the identity
     c1 = pre + S["ge_add_signed"]
-    cb = pre + 2 * S["ge_add_signed"] + 251 * S["ge_dbl_not"] + S["ge_dbl_t"]
+    # the top digit's addition is followed by doublings: no T (ge_add_signed_not)
+    cb = pre + S["ge_add_signed_not"] + S["ge_add_signed"] + 251 * S["ge_dbl_not"] + S["ge_dbl_t"]
     assert w["dec_mul"] == 2 * n * (c5 + c1 + cb)
     assert w["enc_sym"] == w["dec_sym"] == 2 * n * n * bench.HY_SYM_SLOTS
 

@@ -29,6 +29,11 @@ PRIMS = {
                       "ST10(a.v);"),
     "ge_madd_signed": ("ge_p3 p; ge_aff q; LDP(p, 0); LD10(q.ypx.v, 3000); LD10(q.ymx.v, 3640); LD10(q.xy2d.v, 4280); "
                        "bool ng = o[9999] & 1;", "ge_madd_signed(p, p, q, ng); ng = !ng;", "STP(p);"),
+    "ge_madd_signed_not": ("ge_p3 p; ge_aff q; LDP(p, 0); LD10(q.ypx.v, 3000); LD10(q.ymx.v, 3640); "
+                           "LD10(q.xy2d.v, 4280); bool ng = o[9999] & 1;",
+                           "ge_madd_signed(p, p, q, ng, false); ng = !ng; p.T.v[0] ^= ng;", "STP(p);"),
+    "ge_add_signed_not": ("ge_p3 p; ge_cached q; LDP(p, 0); LDP(q, 2560); bool ng = o[9999] & 1;",
+                          "ge_add_signed(p, p, q, ng, false); ng = !ng; p.T.v[0] ^= ng;", "STP(p);"),
     "ge_madd": ("ge_p3 p; ge_aff q; LDP(p, 0); LD10(q.ypx.v, 3000); LD10(q.ymx.v, 3640); LD10(q.xy2d.v, 4280);",
                 "ge_madd(p, p, q);", "STP(p);"),
     "comb_window": ("ge_p3 p; LDP(p, 0); sc x; for (int i_ = 0; i_ < 8; i_++) x.v[i_] = o[9000 + i_];",

@@ -26,7 +26,7 @@ def main(d, t=128, n=8192):
                 nz = ds[i] != 0
                 cc += V["ge_dbl_t"] if (nz or i == 0) else V["ge_dbl_not"]
                 if nz:
-                    cc += V["ge_add_signed"]
+                    cc += bench.add_cost(V, "ge_add_signed", i == 0)
         cost[m] = cc
     seg = rows[:t - 1]
     tot = totw = 0
