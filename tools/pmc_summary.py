@@ -10,6 +10,7 @@ per-launch HBM bytes of the check-pipeline kernels, which bench.py reports as ro
 import csv
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -71,18 +72,19 @@ def main(d):
                   f"{c.get('SQ_ACTIVE_INST_VALU2', 0) / (c.get('SQ_ACTIVE_INST_VALU', 0) or 1):12.4f}")
 
 
-PHASE = {"k_binom_step": "binomial", "void k_stepping<192>": "stepping", "void k_stepping<256>": "stepping",
-         "void k_stepping<512>": "stepping",
-         # dedicated stepping, and its complete-formula redo launches (separate: near-empty when no
-         # workgroup was marked, they would halve the per-launch average)
-         "void k_stepping<192, true>": "stepping", "void k_stepping<256, true>": "stepping",
-         "void k_stepping<512, true>": "stepping", "void k_stepping<192, false>": "stepping_redo",
-         "void k_stepping<256, false>": "stepping_redo", "void k_stepping<512, false>": "stepping_redo",
-         "void k_combine_aff<2, 1>": "combine", "void k_combine_aff<3, 2>": "combine",
-         "void k_combine_aff<4, 2>": "combine", "k_affine_pieces": "affine",
-         "void k_combine<1>": "combine", "void k_combine<2>": "combine", "void k_combine_short<2, 1>": "combine",
-         "void k_combine_short<3, 2>": "combine", "void k_combine_short<4, 2>": "combine",
-         "k_check_both": "check", "k_check": "check"}
+def phase(name):
+    """Pipeline phase of a kernel-trace name (template arguments as rocprofv3 prints them): the
+    dedicated stepping (k_stepping<MAXBS, true, PARTS>) and its complete-formula redo launches
+    (<MAXBS, false, ..>: near-empty when no workgroup was marked, kept apart so that they do not
+    halve the per-launch average), the recombination, the normalisation, the binomial and the check."""
+    if name == "k_binom_step":
+        return "binomial"
+    m = re.match(r"void k_stepping<\d+(?:, (true|false))?", name)
+    if m:
+        return "stepping_redo" if m.group(1) == "false" else "stepping"
+    if re.match(r"void k_combine(_aff|_short)?<", name):
+        return "combine"
+    return {"k_affine_pieces": "affine", "k_check_both": "check", "k_check": "check"}.get(name)
 
 
 def write_traffic(d, out, n, t, U, split_len=None):
@@ -91,8 +93,9 @@ def write_traffic(d, out, n, t, U, split_len=None):
     fe, fcalls = load_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
     wr, wcalls = load_counters(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
     kern = {}
-    for k, ph in PHASE.items():
-        if k not in fe or k not in wr:
+    for k in fe:
+        ph = phase(k)
+        if ph is None or k not in wr:
             continue
         e = kern.setdefault(ph, {"fetch_bytes_x2": 0.0, "write_bytes": 0.0, "fetch_launches": 0, "write_launches": 0})
         e["fetch_bytes_x2"] += 2 * fe[k].get("FETCH_SIZE", 0) * 1024  # FETCH_SIZE and WRITE_SIZE are in KiB
