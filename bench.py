@@ -565,8 +565,8 @@ def main():
                     help="short-multiplier recombination addends: 0 affine Niels, 1 cached projective")
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
-    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
-                    help="binomial schedule: 0/1 one launch per Horner step, 2..5 one persistent dataflow launch with 1, 2, 4, 8 positions per item")
+    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4, 5, 6],
+                    help="binomial schedule: 0 one launch per Horner step (lane pairs for the latency-bound steps), 1 the same without lane pairs, 2..5 one persistent dataflow launch with 1, 2, 4, 8 positions per item, 6 lane pairs for every step")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")

@@ -12,6 +12,7 @@
 #define dkgk dkgk_ilp
 #endif
 #include "kernels.h"
+#include "split.h"
 
 #include <algorithm>
 #include <cmath>
@@ -441,6 +442,57 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
   ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
   mul_small_lds(x, (uint32_t)m, q);        // * m
   pt_store(eout, S, (size_t)m * npad + d, x);
+}
+
+// k_binom_step with lane pairs (split.h): one wave per (position, 32 columns), each column's point
+// held by two lanes that compute half of every field product each -- half the dependent
+// instructions per lane for a latency-bound step (few waves per SIMD), at twice the lanes.
+__global__ __launch_bounds__(64, 4) void k_binom_pair(int r, int k, size_t npad, size_t N,
+                                                    const uint32_t* __restrict__ C,
+                                                    const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
+                                                    size_t pstride, unsigned gx, unsigned last_piece,
+                                                    int last_off) {
+  __shared__ uint32_t xb[20 * 64];
+  __shared__ uint32_t qs[PT_WORDS * 32];
+  const int lane = threadIdx.x;
+  const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
+  const size_t d = piece * pstride + (size_t)grp * 32 + (lane >> 1);
+  const size_t S = N * npad;
+  const int m = r - (int)blockIdx.y;
+  if (m == 0) {
+    if (lane & 1) return;
+#pragma unroll 8
+    for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
+    return;
+  }
+  const int re = r - (piece == last_piece ? last_off : 0);
+  if (m > re) return;
+  const pair_ctx c{xb, qs + (lane >> 1), lane & 1, lane};
+  {
+    ge_p3 cur;
+    pt_load(cur, ein, S, (size_t)m * npad + d);
+    uint32_t keep = (m == re) ? 0u : 0xffffffffu;
+    asm volatile("" : "+v"(keep));
+    uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
+#pragma unroll
+    for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
+    pair_put_cached(c, cur);
+  }
+  ge_p3 x;
+  pt_load(x, ein, S, (size_t)(m - 1) * npad + d);
+  ge_add_pair(x, x, c, false);             // e_{m-1} + e_m
+  mul_small_pair(x, (uint32_t)m, c);       // * m
+  if (lane & 1) return;
+  pt_store(eout, S, (size_t)m * npad + d, x);
+}
+
+void binom_step_pair(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in,
+                     uint32_t* out, hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
+  const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
+  // width is a multiple of 64: one wave per (position 0..r, 32 columns, piece)
+  hipLaunchKernelGGL(k_binom_pair, dim3((unsigned)(width / 32 * pieces), (unsigned)(r + 1)), dim3(64), 0, stream,
+                     (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 32),
+                     (unsigned)(pieces - 1), last_off);
 }
 
 void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, hipStream_t stream,

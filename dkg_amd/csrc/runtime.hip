@@ -46,8 +46,10 @@ struct dkg_ctx {
   int recv_parts = 0;                   // receiver parts of the stepping (0/1: off, 2..8: opt-in)
   int last_recv_parts = 1;              // parts used by the last verify_device
   hipEvent_t rpart[8] = {}, rjoin = nullptr;  // part h's stepping done / the aux stream's work done
-  int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step),
-                                        // 2 one persistent dataflow launch (k_binom_flow)
+  int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step;
+                                        // 0 with lane pairs, k_binom_pair, for the steps under one
+                                        // wave per SIMD), 2..5 one persistent dataflow launch
+                                        // (k_binom_flow), 6 lane pairs for every step
   uint32_t* flow_state = nullptr;       // dataflow binomial: per chunk [flags | ticket | err] words,
   size_t flow_chunk_words = 0;          // flow_chunk_words per chunk; err at word flow_chunk_words-1
   size_t flow_chunks = 0;               // chunks whose err word the next sync checks
@@ -229,6 +231,9 @@ struct VerifySeg {
 // (dkgk_ilp, ten independent chains per multiplication) when the launch leaves too few waves per
 // SIMD to hide the serial chain (`latency_bound`), unless dkg_ctx_set_field_mode forces one.
 // Binomial steps with fewer waves per SIMD than this run the column-sum copy (kernels_ilp.h).
+#ifndef DKG_BINOM_PAIR_WAVES
+#define DKG_BINOM_PAIR_WAVES 1.0
+#endif
 #ifndef DKG_BINOM_ILP_WAVES
 #define DKG_BINOM_ILP_WAVES 1.5
 #endif
@@ -561,7 +566,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
   // dataflow binomial state: per chunk the flags of its column waves ([cw][L]), the ticket and the
   // err word, zeroed on the chunk's stream before its launch
-  const bool flow = ctx->binom_mode >= 2 && L > 1;
+  const bool flow = ctx->binom_mode >= 2 && ctx->binom_mode <= 5 && L > 1;
   const unsigned flow_k = 1u << std::min(ctx->binom_mode >= 2 ? ctx->binom_mode - 2 : 0, 3);  // 2..5 -> K = 1..8
   if (flow) {
     ctx->flow_chunk_words = (dkgk::binom_flow_flag_words(npad, U, L, flow_k) + 2 + 63) / 64 * 64;
@@ -627,8 +632,15 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       uint32_t *bin = e0 + c0, *bout = e1 + c0;
       for (size_t r = 1; r < L; r++) {
         // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
-        const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (r + 1) / 1024 < DKG_BINOM_ILP_WAVES);
-        (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+        const double wps = (double)npad / 64 * U * (r + 1) / 1024;  // waves per SIMD, all chunks
+        const bool ilp = use_ilp(ctx, wps < DKG_BINOM_ILP_WAVES);
+        // lane pairs (k_binom_pair): by default the steps with under one wave per SIMD, mode 6 every
+        // step (1-, 2-, 4-, 8-way n=1024 shards 0.2-0.4 ms faster; profiles/r03_binomial_pairs_ab.txt)
+        const bool pair = ctx->binom_mode == 6 || (ctx->binom_mode == 0 && wps < DKG_BINOM_PAIR_WAVES);
+        if (pair)
+          (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+        else
+          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
         std::swap(bin, bout);
       }
       e = bin;
@@ -1558,7 +1570,7 @@ int dkg_ctx_set_receiver_parts(dkg_ctx* ctx, int parts) {
 int dkg_ctx_last_receiver_parts(const dkg_ctx* ctx) { return ctx ? ctx->last_recv_parts : 0; }
 
 int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 5) return DKG_E_ARG;
+  if (!ctx || mode < 0 || mode > 6) return DKG_E_ARG;
   ctx->binom_mode = mode;
   return DKG_OK;
 }

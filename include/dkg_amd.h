@@ -71,9 +71,12 @@ int dkg_ctx_set_stepping(dkg_ctx *ctx, int mode);
  * product scanning (fewest issue slots), 2 always column sums (most independent chains; for
  * latency-bound launches).  Outputs do not depend on it. */
 int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
-/* Schedule of the binomial-basis Horner: 0 (default) and 1 -- one grid launch
- * per step; 2 -- all t steps in ONE persistent dataflow launch (each item waits only for the table
- * positions of the previous step it reads or overwrites).  Outputs do not depend on it. */
+/* Schedule of the binomial-basis Horner: 0 (default) -- one grid launch per
+ * step, the steps with under one wave per SIMD with lane pairs (each point on two lanes sharing its
+ * field products); 1 -- one launch per step, no lane pairs; 2..5 -- all t steps in ONE persistent
+ * dataflow launch (each item waits only for the table positions of the previous step it reads or
+ * overwrites; 1, 2, 4, 8 positions per item); 6 -- lane pairs for every step.  Outputs do not
+ * depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
 /* Receiver parts of the stepping (opt-in schedule): the stepping runs in `parts` launches over
  * receiver ranges, and each part's recombination and checks run on a second stream beside the next

@@ -543,7 +543,8 @@ def test_receiver_parts_match(be, n, t, ws, rank):
 @pytest.mark.parametrize("n,t,split", [(1024, 511, 4), (1024, 511, 3), (1100, 549, 2), (300, 149, 1)])
 def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
     """The dataflow binomial (k_binom_flow: all Horner steps in one persistent launch with
-    per-position dependency flags) against one launch per step at the BASELINE size and on ragged
+    per-position dependency flags) and the lane-pair steps (k_binom_pair, every step or the
+    latency-bound ones) against one launch per step at the BASELINE size and on ragged
     ones (n=1100 at U=2: a short last piece joining 90 steps late; n=300 unsplit: a padded column
     group), with tampered dealers: identical decision matrices, qualification, reconstruction and mpk
     -- and the same as the oracle on the tampered rows (test_faults_baseline_sizes checks the flow
@@ -555,7 +556,7 @@ def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
     out = []
     try:
         be.set_split(split)
-        for mode in (1, 2, 4, 5):  # per step; dataflow with K = 1, 4, 8 positions per item
+        for mode in (1, 2, 4, 5, 6, 0):  # per step; dataflow with K = 1, 4, 8; lane pairs all / auto (default)
             be.set_binomial(mode)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             assert be.last_split() == split

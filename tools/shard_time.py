@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--field", type=int, default=0, help="field multiply: 0 by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--combine", type=int, default=0, help="recombination: 0 short multipliers (U <= 4), 1 powers of j^L")
     ap.add_argument("--parts", type=int, default=0, help="receiver parts of the stepping (opt-in schedule): 0/1 off, 2..8")
-    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule: 0/1 one launch per step, 2..5 dataflow launch with 1, 2, 4, 8 positions per item")
+    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule: 0/1 one launch per step, 2..5 dataflow launch with 1, 2, 4, 8 positions per item, 0 with / 1 without lane pairs for latency-bound steps, 6 lane pairs for all")
     args = ap.parse_args()
     import torch
 
