@@ -473,6 +473,7 @@ def bench_batch(args, ws, rank, local):
     be.set_streams(args.streams)
     be.set_overlap(not args.no_overlap)
     be.set_verify_mode(args.verify)
+    be.set_binomial(args.binomial)
     be.env_init(t, n)
     dev = torch.device("cuda", local)
     ta = torch.empty(B * n * N * 32, dtype=torch.uint8, device=dev)
