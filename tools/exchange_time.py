@@ -48,8 +48,31 @@ def main():
         torch.cuda.synchronize()
         full.append((time.perf_counter() - t0) * 1e3)
         shard.append(r.ms_shard)
+    # the parts of ShardedCeremony._finish, one by one (device work synchronised after each)
+    parts = {}
+
+    def timed(name, f):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = f()
+        torch.cuda.synchronize()
+        parts[name] = min(parts.get(name, 1e9), (time.perf_counter() - t0) * 1e3)
+        return out
+
+    for _ in range(args.reps):
+        timed("shard_device", lambda: be.ceremony_shard_device(n, t, sc.d0, sc.d1, ta.data_ptr(), tb.data_ptr(),
+                                                               sc.dec2.data_ptr(), sc.dec4.data_ptr(),
+                                                               sc.A0.data_ptr(), sc.part.data_ptr()))
+        timed("all_gathers", sc.exchange)
+        o = timed("combine", lambda: be.shard_combine_device(n, t, 1, sc.g_dec2.data_ptr(), sc.g_dec4.data_ptr(),
+                                                             sc.c_dec2.data_ptr(), sc.c_dec4.data_ptr()))
+        q = [int(x) for x in o.qualified]
+        timed("finalise", lambda: be.shard_finalise_device(n, t, 1, sc.g_A0.data_ptr(), sc.g_part.data_ptr(), q,
+                                                           bool(o.phase4_error), sc.fs.data_ptr(), sc.pub.data_ptr()))
+        timed("copy_out", lambda: (bytes(sc.fs.cpu().numpy()), bytes(sc.pub.cpu().numpy())))
     print(json.dumps({"n": n, "t": t, "run_ms": round(min(full), 3), "shard_device_ms": round(min(shard), 3),
-                      "exchange_and_combine_ms": round(min(full) - min(shard), 3)}))
+                      "exchange_and_combine_ms": round(min(full) - min(shard), 3),
+                      "parts_ms": {k: round(v, 3) for k, v in parts.items()}}))
     be.close()
     dist.destroy_process_group()
 
