@@ -536,10 +536,29 @@ def bench_batch(args, ws, rank, local):
         out["cpu_baseline"] = cpu_baseline(n, t, 20.0, ceremonies=B)
         out["gpu_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     be.close()
     if dist:
         dist.destroy_process_group()
+
+
+_RESULT_OUT = None
+
+
+def keep_stdout_for_result():
+    """The result line must be the only line on stdout: RCCL's banner, the gloo backend and native
+    libraries write to fd 1.  Keep a private copy of stdout for emit() and point fd 1 (and Python's
+    sys.stdout) at stderr for everything else."""
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit(out):
+    f = _RESULT_OUT or sys.stdout
+    f.write(json.dumps(out) + "\n")
+    f.flush()
 
 
 def main():
@@ -574,6 +593,7 @@ def main():
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
+    keep_stdout_for_result()
     ws, rank, local = dist_env()
     if ws != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
@@ -804,7 +824,7 @@ def main():
             out["roofline"] = roofline_line(rl, dom, f"rank 0's shard ({D} dealers): {work[dom]:.4g} VALU issue "
                                                      f"slots per pass (closed form); device time in a serialised pass")
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     be.close()
     if dist:
         dist.destroy_process_group()
