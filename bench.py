@@ -670,6 +670,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    if ws == 1:  # an honest ceremony: every dealer qualifies
+        assert res.n_qualified == n, "an honest ceremony disqualified a dealer"
     if ws > 1:  # the sharded honest ceremony: everyone qualified, an mpk, no round errors
         assert res.decisions.qualified.all() and not res.decisions.r2_error.any() and res.mpk is not None
     pairs = n * (n - 1)

@@ -547,12 +547,18 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       dkgk::decode_position_major(segs[k].Ccomp, D, N, W, Cpm, pok, home, nseg, k, L, npad);
   }
   dkgk::dealer_ok(npad, N, pok, dok, home);
+  // an extra mask produced by the overlapped decryption (full mode) is applied by each chunk's
+  // checks once the shares are there; otherwise here
+  const bool defer_masks = ctx->shares_pending;
   for (int k = 0; k < nseg; k++)
-    if (segs[k].extra_ok) dkgk::and_dealer_mask(D, nseg, k, segs[k].extra_ok, dok, home);
+    if (segs[k].extra_ok && !defer_masks) dkgk::and_dealer_mask(D, nseg, k, segs[k].extra_ok, dok, home);
   // checks of dealers [d0, d1) on stream st
   auto checks = [&](size_t d0, size_t d1, hipStream_t st, size_t j0 = 0, size_t jn = 0) {
     if (d1 <= d0) return;
     wait_shares(ctx, st);
+    if (defer_masks)  // dealers [d0, d1) start a column group (d0 = 64 g0): relative indexing
+      for (int k = 0; k < nseg; k++)
+        if (segs[k].extra_ok) dkgk::and_dealer_mask(d1 - d0, nseg, k, segs[k].extra_ok + d0, dok + d0 * nseg, st);
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
       dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
@@ -1313,9 +1319,9 @@ void batch_times(dkg_ctx* ctx, dkg_batch_out* out, bool round1) {
 // ---- full (encrypted-share) mode: hybrid.hip (elgamal.rs:134-193, committee.rs:164-172, 282-286)
 // Items (dealer i, recipient q, w) at (i * n + q) * 2 + w: w = 0 the randomness s', w = 1 the share s.
 void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const uint32_t* s, const uint32_t* sp,
-                    const uint32_t* r, uint32_t* e1, uint32_t* ct) {
+                    const uint32_t* r, uint32_t* e1, uint32_t* ct, hipStream_t st = nullptr) {
   const size_t items = 2 * D * n;
-  hipStream_t st = ctx->stream;
+  if (!st) st = ctx->stream;
   uint32_t* pk_ext = buf<uint32_t>(ctx, "hy.pk_ext", PTB * n);
   uint8_t* pk_ok = buf<uint8_t>(ctx, "hy.pk_ok", n);
   dkgk::decode_points(pkc, n, pk_ext, n, pk_ok, st);
@@ -1340,9 +1346,9 @@ void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const
 // Receivers' side: item_ok[item] = e1 decodes; dealer_ok_out[i] = all of dealer i's items decode (a
 // broadcast that does not deserialize is missing data, committee.rs:331-335).
 void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const uint32_t* e1, const uint32_t* ct,
-                    uint32_t* s, uint32_t* sp, uint8_t* item_ok, uint8_t* dealer_ok_out) {
+                    uint32_t* s, uint32_t* sp, uint8_t* item_ok, uint8_t* dealer_ok_out, hipStream_t st = nullptr) {
   const size_t items = 2 * D * n;
-  hipStream_t st = ctx->stream;
+  if (!st) st = ctx->stream;
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
   uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
   uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
@@ -2613,16 +2619,27 @@ int dkg_ceremony_run_full_device(dkg_ctx* ctx, size_t n, size_t t, const void* d
     uint32_t* Ac = buf<uint32_t>(ctx, "cer_A", 32 * n * N);
     uint32_t* ds = buf<uint32_t>(ctx, "cer_s", 32 * n * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "cer_sp", 32 * n * n);
-    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
+    // With chunk streams (not the serialised roofline pass) the share evaluation, the encryption and
+    // the receivers' decryption run on the low-priority side stream beside the check pipeline:
+    // nothing before the checks reads a share, so the pipeline's binomial, stepping and
+    // recombination start on the commitments alone, and the checks (and round 3) wait for the
+    // decrypted shares (wait_shares); the decode mask of the ciphertexts joins the dealer mask there.
+    const bool side = ctx->nsub > 1 && ctx->verify_mode == 0;
+    hipStream_t hy = side ? ctx->side : ctx->stream;
+    round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false, side);
     uint32_t* e1 = buf<uint32_t>(ctx, "fm_e1", 32 * items);
     uint32_t* ct = buf<uint32_t>(ctx, "fm_ct", 32 * items);
-    encrypt_device(ctx, n, n, dpk, ds, dsp, (const uint32_t*)d_r, e1, ct);  // committee.rs:169-172
+    encrypt_device(ctx, n, n, dpk, ds, dsp, (const uint32_t*)d_r, e1, ct, hy);  // committee.rs:169-172
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     uint32_t* rs = buf<uint32_t>(ctx, "fm_s", 32 * n * n);
     uint32_t* rsp = buf<uint32_t>(ctx, "fm_sp", 32 * n * n);
     uint8_t* iok = buf<uint8_t>(ctx, "fm_iok", items);
     uint8_t* eok = buf<uint8_t>(ctx, "fm_eok", n);
-    decrypt_device(ctx, n, n, dsk, e1, ct, rs, rsp, iok, eok);  // committee.rs:282-286
+    decrypt_device(ctx, n, n, dsk, e1, ct, rs, rsp, iok, eok, hy);  // committee.rs:282-286
+    if (side) {
+      HCK(hipEventRecord(ctx->shares_done, ctx->side));
+      ctx->shares_pending = true;
+    }
     ExtScope ext(ctx, n, N);
     receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, false, eok);
     collect_hybrid_phases(ctx);
@@ -2658,10 +2675,21 @@ int dkg_ceremony_verify_full(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E,
     uint32_t* rsp = buf<uint32_t>(ctx, "fm_sp", 32 * n * n);
     uint8_t* iok = buf<uint8_t>(ctx, "fm_iok", items);
     uint8_t* eok = buf<uint8_t>(ctx, "fm_eok", n);
-    decrypt_device(ctx, n, n, dsk, de1, dct, rs, rsp, iok, eok);
+    // the decryption on the side stream beside the check pipeline, as in dkg_ceremony_run_full_device
+    const bool side = ctx->nsub > 1 && ctx->verify_mode == 0;
+    if (side) {
+      HCK(hipEventRecord(ctx->side_fork, ctx->stream));
+      HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
+    }
+    decrypt_device(ctx, n, n, dsk, de1, dct, rs, rsp, iok, eok, side ? ctx->side : ctx->stream);
+    if (side) {
+      HCK(hipEventRecord(ctx->shares_done, ctx->side));
+      ctx->shares_pending = true;
+    }
+    receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, true, eok);  // waits for the shares before it returns
     if (out->s) d2h(ctx, out->s, rs, 32 * n * n);
     if (out->s_prime) d2h(ctx, out->s_prime, rsp, 32 * n * n);
-    receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, true, eok);
+    sync(ctx);
     out->ms_round1 = 0;
     out->ms_round2 = ev_ms(ctx, 1, 2);
     out->ms_round3 = ev_ms(ctx, 2, 3);
