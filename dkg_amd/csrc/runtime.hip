@@ -46,6 +46,7 @@ struct dkg_ctx {
   int recv_parts = 0;                   // receiver parts of the stepping (0/1: off, 2..8: opt-in)
   int last_recv_parts = 1;              // parts used by the last verify_device
   hipEvent_t rpart[8] = {}, rjoin = nullptr;  // part h's stepping done / the aux stream's work done
+  std::vector<uint8_t> key_tabs_pk;     // member keys whose decoded points and combs sit in hy.* (encrypt)
   int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step;
                                         // 0 with lane pairs, k_binom_pair, for the steps under one
                                         // wave per SIMD), 2..5 one persistent dataflow launch
@@ -1318,15 +1319,25 @@ void batch_times(dkg_ctx* ctx, dkg_batch_out* out, bool round1) {
 
 // ---- full (encrypted-share) mode: hybrid.hip (elgamal.rs:134-193, committee.rs:164-172, 282-286)
 // Items (dealer i, recipient q, w) at (i * n + q) * 2 + w: w = 0 the randomness s', w = 1 the share s.
+// pk_host (optional): the same keys on the host.  Member keys outlive a ceremony (procedure_keys.rs),
+// so their decoded points and comb tables are kept in the arena and rebuilt only when the keys
+// differ from the last build's (compared byte for byte).
 void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const uint32_t* s, const uint32_t* sp,
-                    const uint32_t* r, uint32_t* e1, uint32_t* ct, hipStream_t st = nullptr) {
+                    const uint32_t* r, uint32_t* e1, uint32_t* ct, hipStream_t st = nullptr,
+                    const uint8_t* pk_host = nullptr) {
   const size_t items = 2 * D * n;
   if (!st) st = ctx->stream;
   uint32_t* pk_ext = buf<uint32_t>(ctx, "hy.pk_ext", PTB * n);
   uint8_t* pk_ok = buf<uint8_t>(ctx, "hy.pk_ok", n);
-  dkgk::decode_points(pkc, n, pk_ext, n, pk_ok, st);
   uint32_t* tabs = buf<uint32_t>(ctx, "hy.tabs", COMB_BYTES * n);
-  dkgk::build_comb(pk_ext, n, 0, tabs, st, n);  // one comb per recipient key: r * pk_q is fixed-base
+  const bool cached = pk_host && ctx->key_tabs_pk.size() == 32 * n &&
+                      memcmp(ctx->key_tabs_pk.data(), pk_host, 32 * n) == 0;
+  if (!cached) {
+    ctx->key_tabs_pk.clear();  // invalid until this build is queued
+    dkgk::decode_points(pkc, n, pk_ext, n, pk_ok, st);
+    dkgk::build_comb(pk_ext, n, 0, tabs, st, n);  // one comb per recipient key: r * pk_q is fixed-base
+    if (pk_host) ctx->key_tabs_pk.assign(pk_host, pk_host + 32 * n);
+  }
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
   uint32_t* K = buf<uint32_t>(ctx, "hy.K", PTB * items);
   uint32_t* Kc = buf<uint32_t>(ctx, "hy.Kc", 32 * items);
@@ -2629,7 +2640,7 @@ int dkg_ceremony_run_full_device(dkg_ctx* ctx, size_t n, size_t t, const void* d
     round1_device(ctx, n, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false, side);
     uint32_t* e1 = buf<uint32_t>(ctx, "fm_e1", 32 * items);
     uint32_t* ct = buf<uint32_t>(ctx, "fm_ct", 32 * items);
-    encrypt_device(ctx, n, n, dpk, ds, dsp, (const uint32_t*)d_r, e1, ct, hy);  // committee.rs:169-172
+    encrypt_device(ctx, n, n, dpk, ds, dsp, (const uint32_t*)d_r, e1, ct, hy, pk);  // committee.rs:169-172
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     uint32_t* rs = buf<uint32_t>(ctx, "fm_s", 32 * n * n);
     uint32_t* rsp = buf<uint32_t>(ctx, "fm_sp", 32 * n * n);

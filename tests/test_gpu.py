@@ -637,6 +637,31 @@ def test_full_mode_device_ceremony(be, golden, name):
     assert e1.hex() == c["e1"] and ct.hex() == c["ct"]
 
 
+def test_full_mode_key_tables_follow_the_keys(be):
+    """The member keys' comb tables are kept across full-mode ceremonies and rebuilt when the keys
+    change (compared byte for byte): three ceremonies of the same size with keys A, B, A must each
+    decrypt their own ciphertexts -- stale tables would encrypt to the previous keys and every
+    receiver would reject."""
+    import torch
+
+    n, t = 16, 7
+    N = t + 1
+    be.env_init(t, n, CK)
+    dev = torch.device("cuda", 0)
+    ta = torch.empty(32 * n * N, dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    tr = torch.empty(64 * n * n, dtype=torch.uint8, device=dev)
+    be.dealer_coefficients_device(b"\x11" * 32, 0, 1, 0, n, t, ta.data_ptr(), tb.data_ptr())
+    be.enc_randomness_device(b"\x11" * 32, 0, 1, 0, n, n, t, tr.data_ptr())
+    keys = [be.member_keys(m, 0, n) for m in (b"\x21" * 32, b"\x22" * 32)]
+    mpks = []
+    for sk, pk in (keys[0], keys[1], keys[0]):
+        r = be.ceremony_full_device(ta.data_ptr(), tb.data_ptr(), tr.data_ptr(), sk, pk, n, t)
+        assert r.n_qualified == n and r.qualified == [1] * n
+        mpks.append(r.mpk)
+    assert mpks[0] == mpks[1] == mpks[2]  # the same coefficients: the same master key
+
+
 def test_full_mode_oracle_random(be):
     """Random keys / messages / randomness: device encryption equals the CPU oracle's, and device
     decryption inverts it (a wrong key does not)."""
