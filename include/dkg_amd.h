@@ -404,7 +404,11 @@ int dkg_encrypt_shares(dkg_ctx *ctx, size_t D, size_t n, const uint8_t *pk, cons
 int dkg_decrypt_shares(dkg_ctx *ctx, size_t D, size_t n, const uint8_t *sk, const uint8_t *e1, const uint8_t *ct,
                        uint8_t *s, uint8_t *s_prime, uint8_t *ok);
 /* Whole ceremony in full mode from device coefficients d_a, d_b [n][t+1][32] and encryption
- * randomness d_r [n][n][2][32]; sk, pk = dkg_member_keys output (host).  Encryption is timed in
+ * randomness d_r [n][n][2][32]; sk, pk = dkg_member_keys output (host).  With chunk streams
+ * (dkg_ctx_set_streams > 1) the share evaluation, encryption and decryption run on a low-priority
+ * stream beside the checks' difference tables (the checks wait for the decrypted shares), and the
+ * members' key combs are kept on the ctx until the keys change; ms_round1 then times the
+ * commitments and ms_round2 the rest up to the round-2/4 decisions.  With one stream: encryption in
  * ms_round1, decryption in ms_round2. */
 int dkg_ceremony_run_full_device(dkg_ctx *ctx, size_t n, size_t t, const void *d_a, const void *d_b, const void *d_r,
                                  const uint8_t *sk, const uint8_t *pk, dkg_ceremony_out *out);
