@@ -64,7 +64,8 @@ def split_multipliers(n: int, L: int, pieces: int):
     if rc != _lib.DKG_OK:
         raise DkgError(rc, "split_multipliers")
     sg = [1 if b < 128 else -1 for b in sign.raw]
-    return [[sg[j * pieces + u] * int.from_bytes(mag.raw[(j * pieces + u) * 32:(j * pieces + u + 1) * 32], "little")
+    m = mag.raw  # one copy (each .raw access copies the whole buffer)
+    return [[sg[j * pieces + u] * int.from_bytes(m[(j * pieces + u) * 32:(j * pieces + u + 1) * 32], "little")
              for u in range(pieces)] for j in range(n)]
 
 
@@ -150,7 +151,9 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_ctx_set_field_mode(self._ctx, mode))
 
     def set_binomial(self, mode: int):
-        """0 (default) / 1: the binomial as one launch per Horner step; 2: one persistent dataflow launch."""
+        """Binomial schedule (dkg_ctx_set_binomial): 0 (default) one launch per Horner step with lane
+        pairs for the steps under one wave per SIMD, 1 without lane pairs, 2..5 one persistent
+        dataflow launch (1, 2, 4, 8 positions per item), 6 lane pairs for every step."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
     def set_receiver_parts(self, parts: int):
@@ -444,7 +447,8 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_finalise_parties(
             self._ctx, n, t, mask(qualified), mask(reconstruct), mask(r2_error), mask(r4_error), mask(disclosed),
             A0, s, mpk, st, ri))
-        return PartyFinalise([mpk.raw[32 * p:32 * p + 32] for p in range(n)], list(st)[:n], list(ri)[:n])
+        m = mpk.raw
+        return PartyFinalise([m[32 * p:32 * p + 32] for p in range(n)], list(st)[:n], list(ri)[:n])
 
     def shard_combine_device(self, n: int, t: int, world_size: int, d_dec2_g: int, d_dec4_g: int,
                              d_dec2: Optional[int] = None, d_dec4: Optional[int] = None) -> "ShardOutcome":
@@ -520,7 +524,7 @@ class BatchResult:
     qualified: bytes
     r2_error: bytes
     r4_error: bytes
-    complaints2: List[int]
+    complaints2: "Int32s"  # list-like: indexing, slices (lists), iteration, == with a list
     reconstruct: bytes
     final_share: Optional[bytes]
     public_share: Optional[bytes]
@@ -562,16 +566,41 @@ def _batch_out(B, n, big):
     return o, bufs
 
 
+class Int32s:
+    """Little-endian int32 rows of a batch output, converted to Python ints only where read: a
+    10,000-ceremony batch holds 640,000 of them, and building the whole list up front costs more
+    host time than the ceremonies' round 3."""
+
+    def __init__(self, raw: bytes):
+        self._mv = memoryview(raw).cast("i")
+
+    def __len__(self):
+        return len(self._mv)
+
+    def __getitem__(self, i):
+        return self._mv[i].tolist() if isinstance(i, slice) else self._mv[i]
+
+    def __iter__(self):
+        return iter(self._mv.tolist())
+
+    def __eq__(self, other):
+        return self._mv.tolist() == list(other)
+
+    def tolist(self):
+        return self._mv.tolist()
+
+
 def _batch_result(B, n, t, o, bufs):
     import struct
     V = B * n
     g = lambda k, size: bufs[k].raw[:size] if k in bufs else None  # noqa: E731
+    mpk = bufs["mpk"].raw  # one copy (each .raw access copies the whole buffer)
     return BatchResult(
-        B=B, n=n, t=t, mpk=[bufs["mpk"].raw[32 * c:32 * c + 32] for c in range(B)],
+        B=B, n=n, t=t, mpk=[mpk[32 * c:32 * c + 32] for c in range(B)],
         n_qualified=list(struct.unpack(f"<{B}i", bufs["n_qualified"].raw[:4 * B])),
         phase4_error=g("phase4_error", B),
         qualified=g("qualified", V), r2_error=g("r2_error", V), r4_error=g("r4_error", V),
-        complaints2=list(struct.unpack(f"<{V}i", bufs["complaints2"].raw[:4 * V])),
+        complaints2=Int32s(bufs["complaints2"].raw[:4 * V]),
         reconstruct=g("reconstruct", V), final_share=g("final_share", 32 * V), public_share=g("public_share", 32 * V),
         dec2=g("dec2", V * n), dec4=g("dec4", V * n),
         ms={"round1": o.ms_round1, "checks": o.ms_checks, "round3": o.ms_round3, "finalise": o.ms_finalise,
