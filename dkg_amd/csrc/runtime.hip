@@ -2384,10 +2384,18 @@ int dkg_shard_finalise_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_siz
     HCK(hipMemsetAsync(ones, 1, world_size, ctx->stream));
     dkgk::sum_shares(world_size, n, (const uint32_t*)d_partials_g, ones, (uint32_t*)d_final_share, ctx->stream);
     if (d_public_share) {
+      // the public shares run on the side stream beside the mpk's decode/sum/encode (both chains
+      // are a few latency-bound launches of n threads); joined below before anything is read
       uint32_t* pub = buf<uint32_t>(ctx, "sf.pub", PTB * n);
-      dkgk::fixed_base(n, (const uint32_t*)d_final_share, ctx->tab_gw, pub, ctx->stream);
-      dkgk::encode_points(pub, n, n, (uint32_t*)d_public_share, ctx->stream);
+      HCK(hipEventRecord(ctx->side_fork, ctx->stream));
+      HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
+      dkgk::fixed_base(n, (const uint32_t*)d_final_share, ctx->tab_gw, pub, ctx->side);
+      dkgk::encode_points(pub, n, n, (uint32_t*)d_public_share, ctx->side);
+      HCK(hipEventRecord(ctx->pub_done, ctx->side));
     }
+    auto join_public = [&] {
+      if (d_public_share) HCK(hipStreamWaitEvent(ctx->stream, ctx->pub_done, 0));
+    };
     memset(mpk, 0, 32);
     if (!phase4_error) {
       // finalise (committee.rs:790-795): the qualified dealers' terms -- A_i0 for the final parties,
@@ -2403,6 +2411,7 @@ int dkg_shard_finalise_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_siz
       dkgk::decode_points(terms, n, ext, n, ok, ctx->stream);
       dkgk::sum_points(n, ext, n, qm, sum, 1, 0, ctx->stream);
       dkgk::encode_points(sum, 1, 1, mc, ctx->stream);
+      join_public();
       check_launch(ctx);
       std::vector<uint8_t> okh(n);
       d2h(ctx, okh.data(), ok, n);
@@ -2414,6 +2423,8 @@ int dkg_shard_finalise_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_siz
           ctx->err = "shard_finalise: a qualified dealer's master-key term does not decode";
           return DKG_E_DECODE;
         }
+    } else {
+      join_public();
     }
     check_launch(ctx);
     sync(ctx);
