@@ -60,6 +60,32 @@ COMBW_WINDOWS = 26  # points.h: radix-2^10 fixed-base comb, one mixed addition p
 SLOTS = {k: v[1] for k, v in VALU.items()}
 
 
+def dalek_msm_fp_mults(N):
+    """SURVEY.md 8(d) cost model of curve25519-dalek 3.x's vartime_multiscalar_mul over N points in
+    Fp multiplications: Straus below 190 points, else Pippenger with w = 6 / 7 / 8 (N < 500 / 800 /
+    above) over ceil(256 / w) digits (w = 8: 33, the carry digit)."""
+    if N < 190:
+        return 1792 + 408 * N
+    w = 6 if N < 500 else 7 if N < 800 else 8
+    digits = -(-256 // w) if w < 8 else 33
+    return digits * (8 * N + 18 * (2 ** (w - 1) - 1)) + (digits - 1) * (7 * w + 10) + N
+
+
+VARBASE_MUL = 2403  # dalek-3 constant-time variable-base scalar multiplication, Fp-mults
+
+
+def ref_equiv(n, t, value):
+    """The reference-equivalent work rate: W2 = MSM(t+1) + 2 variable-base muls + 9
+    Fp-mults per verified share (the receiver's round-2 check, committee.rs:287-305), W4 = MSM + 1
+    mul (round 4, :532-548); value x W2 is what the reference's per-pair MSM schedule would have to
+    sustain to match this throughput."""
+    msm = dalek_msm_fp_mults(t + 1)
+    w2, w4 = msm + 2 * VARBASE_MUL + 9, msm + VARBASE_MUL
+    return {"W2_fp_mults_per_share": w2, "W4_fp_mults_per_share": w4,
+            "ref_equiv_W2_fp_mults_per_s": value * w2, "ref_equiv_W2_W4_fp_mults_per_s": value * (w2 + w4),
+            "note": "dalek-3 cost model of the reference's per-pair checks (SURVEY.md 8(d)) x verified shares/s"}
+
+
 def kernel_rooflines(ph, work, work_i):
     """Per-kernel VALU roofline of a serialised pass: ph = device ms per kernel (HIP events)."""
     rl = {}
@@ -166,10 +192,12 @@ def pmc_traffic(kernel, n, t, U, plen=None):
     return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
 
 
-def spawn_ranks(args):
+def spawn_ranks(args, poll_s=0.2):
     """`--gpus N` (N > 1) without a launcher: start N fresh worker processes of this script, one per
     GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torchrun sets),
-    before this process touches the GPU; rank 0 prints the JSON line.  Returns the worst exit code."""
+    before this process touches the GPU; rank 0 prints the JSON line.  Every child is polled: the
+    first one to exit non-zero ends the run -- its peers, blocked in a collective it will never
+    join, are terminated (then killed) at once -- and its exit code is returned; 0 when all succeed."""
     import socket
     import subprocess
 
@@ -181,9 +209,27 @@ def spawn_ranks(args):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    failed = 0
+    while not failed and any(p.returncode is None for p in procs):
+        time.sleep(poll_s)
+        for r, p in enumerate(procs):
+            if p.poll() not in (None, 0):
+                failed = p.returncode
+                print(f"bench.py: rank {r} exited with {failed}; stopping the other ranks", file=sys.stderr)
+                break
+    if failed:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(deadline - time.time(), 0.1))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        return failed if failed > 0 else 1
+    return 0
 
 
 def dist_env():
@@ -196,15 +242,36 @@ def dist_env():
 def init_dist(args, local):
     """One process per GPU over RCCL ("nccl").  --dist-backend gloo is a rehearsal mode for boxes
     with fewer GPUs than ranks: ranks share GPUs (local % device_count) and the exchange is staged
-    through host memory; its timings say nothing about xGMI."""
+    through host memory; its timings say nothing about xGMI.  A collective that waits longer than
+    --dist-timeout seconds fails the rank instead of hanging it."""
+    import datetime
+
     import torch
     import torch.distributed as dist
 
+    timeout = datetime.timedelta(seconds=args.dist_timeout)
     if args.dist_backend == "nccl":
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     else:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
     return dist
+
+
+def fault_rehearsal(args, rank):
+    """DKG_BENCH_FAIL_RANK=r (tests/test_bench_dist.py): rank r exits 1 right after the process group
+    is up, the others enter a barrier it never joins -- the failure a crashed rank leaves behind.
+    No GPU is touched, so the launcher's fail-fast path is testable on CPU."""
+    bad = int(os.environ["DKG_BENCH_FAIL_RANK"])
+    import datetime
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
+    if rank == bad:
+        print(f"rank {rank}: injected failure", file=sys.stderr)
+        sys.exit(1)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def gpu_index(args, local):
@@ -474,6 +541,7 @@ def bench_batch(args, ws, rank, local):
     be.set_overlap(not args.no_overlap)
     be.set_verify_mode(args.verify)
     be.set_binomial(args.binomial)
+    be.set_stepping(args.stepping)
     be.env_init(t, n)
     dev = torch.device("cuda", local)
     ta = torch.empty(B * n * N * 32, dtype=torch.uint8, device=dev)
@@ -527,6 +595,7 @@ def bench_batch(args, ws, rank, local):
            "ceremonies_per_s": B * ws * args.steps / elapsed,
            "phases_ms": {k: round(v, 3) for k, v in res.ms.items()}}
     out["config"]["degree_split"] = U
+    out["ref_equiv"] = ref_equiv(n, t, out["value"])
     if rl:
         dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
         out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} instructions) "
@@ -540,6 +609,42 @@ def bench_batch(args, ws, rank, local):
     be.close()
     if dist:
         dist.destroy_process_group()
+
+
+def sharded_self_check(args, dist, be, res, ta, D, N, dev):
+    """N > 1: the honest sharded ceremony must qualify everyone with no round errors, and the mpk
+    every rank derived (sum of the gathered A_i0, dkg_shard_finalise_device) must equal g * sum_i a_i0
+    -- each rank sums its dealers' constant terms mod l, the partial sums are all-gathered, and the
+    total goes through the fixed-base path (a different computation from the commitments').  Returns
+    the per-rank spread of the last timed step: shard device ms and the exchange / combine /
+    reconstruction / finalise host ms (min and max over ranks)."""
+    import torch
+
+    d = res.decisions
+    assert d.qualified.all(), "an honest sharded ceremony disqualified a dealer"
+    assert not d.r2_error.any() and not d.r4_error.any() and not d.phase4_error, "round error in an honest ceremony"
+    xdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    own = ta[:D * N * 32].view(D, N, 32)[:, 0, :].cpu().numpy() if D else []
+    part = sum(int.from_bytes(bytes(r), "little") for r in own) % L
+    mine = torch.frombuffer(bytearray(part.to_bytes(32, "little")), dtype=torch.uint8).to(xdev)
+    allp = torch.empty(32 * dist.get_world_size(), dtype=torch.uint8, device=xdev)
+    dist.all_gather_into_tensor(allp, mine)
+    raw = bytes(allp.cpu().numpy())
+    secret = sum(int.from_bytes(raw[32 * r:32 * r + 32], "little") for r in range(dist.get_world_size())) % L
+    expect = be.fixed_base_batch(secret.to_bytes(32, "little"))
+    assert res.mpk == expect, "sharded mpk != g * sum of the dealers' a_i0"
+    keys = ["shard_device", "exchange", "combine", "recon", "finalise"]
+    vals = [res.ms_shard] + [res.ms_steps.get(k, 0.0) for k in keys[1:]]
+    mine = torch.tensor(vals, dtype=torch.float64, device=xdev)
+    allv = torch.empty(len(vals) * dist.get_world_size(), dtype=torch.float64, device=xdev)
+    dist.all_gather_into_tensor(allv, mine)
+    per = allv.cpu().view(-1, len(vals)).tolist()
+    return {"mpk_check": "mpk == g * sum_i a_i0 (partial sums all-gathered)",
+            "rank_ms": {k: {"min": round(min(r[i] for r in per), 3), "max": round(max(r[i] for r in per), 3)}
+                        for i, k in enumerate(keys)},
+            "rank_ms_note": "last timed step; shard_device = HIP-event time of the rank's share gen + checks, the "
+                            "rest host wall time of the steps after it (all-gathers fenced, combine, round-4 "
+                            "reconstruction, finalise)"}
 
 
 _RESULT_OUT = None
@@ -573,6 +678,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="dealer-chunk streams of the round-2/4 checks")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal with ranks sharing GPUs")
+    ap.add_argument("--dist-timeout", type=float, default=180.0,
+                    help="seconds a collective may wait for its peers before the rank fails")
     ap.add_argument("--verify", default="group", choices=["group", "interp"],
                     help="group: every P_i(j) computed in the group (default); interp: committee verification "
                          "by interpolation (identical decisions, DESIGN.md section 2)")
@@ -585,8 +692,10 @@ def main():
                     help="short-multiplier recombination addends: 0 affine Niels, 1 cached projective")
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
-    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4, 5, 6],
-                    help="binomial schedule: 0 one launch per Horner step (lane pairs for the latency-bound steps), 1 the same without lane pairs, 2..5 one persistent dataflow launch with 1, 2, 4, 8 positions per item, 6 lane pairs for every step")
+    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4],
+                    help="binomial schedule (dkg_ctx_set_binomial): 0 default (lane pairs for the latency-bound steps, mixed item order for the many-round ones), 1 no lane pairs, 2 lane pairs for every step, 3 no mixed order, 4 mixed order for every step")
+    ap.add_argument("--stepping", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="stepping slots (dkg_ctx_set_stepping): 0 cost model, 1 per column, 2 per piece, 3 no dead-position repack")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
     ap.add_argument("--mode", default="plain", choices=["plain", "full"],
                     help="plain: shares in the clear (headline); full: hybrid-encrypted shares (SURVEY 8 f1)")
@@ -597,6 +706,8 @@ def main():
     ws, rank, local = dist_env()
     if ws != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
+    if "DKG_BENCH_FAIL_RANK" in os.environ:
+        return fault_rehearsal(args, rank)
     if args.config in BATCH:
         return bench_batch(args, ws, rank, local)
     n, t = CONFIGS[args.config]
@@ -617,6 +728,7 @@ def main():
     be.set_addends(args.addends)
     be.set_stepping_formula(args.step_formula)
     be.set_binomial(args.binomial)
+    be.set_stepping(args.stepping)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)
     N = t + 1
@@ -672,8 +784,9 @@ def main():
 
     if ws == 1:  # an honest ceremony: every dealer qualifies
         assert res.n_qualified == n, "an honest ceremony disqualified a dealer"
-    if ws > 1:  # the sharded honest ceremony: everyone qualified, an mpk, no round errors
-        assert res.decisions.qualified.all() and not res.decisions.r2_error.any() and res.mpk is not None
+    shard_stats = None
+    if ws > 1:
+        shard_stats = sharded_self_check(args, dist, be, res, ta, D, N, dev)
     pairs = n * (n - 1)
     value = pairs * args.steps / elapsed
     metric = f"verified shares/sec (whole node) at n={n},t={t}; full-ceremony wall time"
@@ -689,6 +802,7 @@ def main():
                    "n": n, "t": t, "pairs_per_step": pairs,
                    "parallelism": f"dealer-sharded x{ws}" if ws > 1 else "single GPU"},
     }
+    out["ref_equiv"] = ref_equiv(n, t, value)
     if args.mode == "full":
         out["config"]["mode"] = "full: shares hybrid-encrypted (elgamal.rs) and decrypted by each receiver"
     if rank == 0 and ws == 1 and res is not None and args.mode == "full":
@@ -805,6 +919,8 @@ def main():
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(n, t)
             out["gpu_vs_cpu"] = value / out["cpu_baseline"]["value"]
+    if shard_stats is not None:
+        out.update(shard_stats)
     if ws > 1 and args.mode != "full" and args.verify == "group":
         # per-GPU roofline of this rank's shard: one extra serialised pass (every rank joins its
         # collectives); the rank's work is its D dealers' share of the closed form

@@ -74,11 +74,13 @@ def lib():
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C dkg_amd` or __graft_entry__.build()")
     # When torch shares the process, its HIP runtime must be the one the dynamic loader binds
     # first: loading libdkg_amd.so (linked against /opt/rocm's libamdhip64) before torch leaves
-    # torch.cuda without a device.  Import torch first whenever it is importable.
-    if "torch" not in sys.modules:
+    # torch.cuda without a device.  Import torch first whenever it is importable; a torch install
+    # that fails to import for any reason (its ROCm libraries included) must not stop the library
+    # from loading for callers that never use torch (DKG_NO_TORCH_PREIMPORT=1 skips the attempt).
+    if "torch" not in sys.modules and not os.environ.get("DKG_NO_TORCH_PREIMPORT"):
         try:
             import torch  # noqa: F401
-        except ImportError:
+        except Exception:  # noqa: BLE001 -- ImportError, OSError, RuntimeError from a broken install
             pass
     L = ctypes.CDLL(LIB_PATH)
     sz, p, u8p = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
@@ -97,8 +99,6 @@ def lib():
     L.dkg_ctx_set_stepping.argtypes = [p, ctypes.c_int]
     L.dkg_ctx_set_field_mode.argtypes = [p, ctypes.c_int]
     L.dkg_ctx_set_binomial.argtypes = [p, ctypes.c_int]
-    L.dkg_ctx_set_receiver_parts.argtypes = [p, ctypes.c_int]
-    L.dkg_ctx_last_receiver_parts.argtypes = [p]
     L.dkg_ctx_last_split.argtypes = [p]
     L.dkg_ctx_last_split_len.argtypes = [p]
     L.dkg_ctx_last_split_len.restype = sz
@@ -165,7 +165,7 @@ EXPORTED = [
     "dkg_device_count", "dkg_env_init",
     "dkg_env_check", "dkg_msm_batch", "dkg_fixed_base_batch", "dkg_poly_eval_batch",
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
-    "dkg_ctx_set_split", "dkg_ctx_set_stepping", "dkg_ctx_set_field_mode", "dkg_ctx_set_binomial", "dkg_ctx_set_receiver_parts", "dkg_ctx_last_receiver_parts", "dkg_ctx_last_split", "dkg_ctx_last_split_len", "dkg_ctx_set_verify_mode", "dkg_ctx_fallback_rows", "dkg_split_model_ms", "dkg_split_len",
+    "dkg_ctx_set_split", "dkg_ctx_set_stepping", "dkg_ctx_set_field_mode", "dkg_ctx_set_binomial", "dkg_ctx_last_split", "dkg_ctx_last_split_len", "dkg_ctx_set_verify_mode", "dkg_ctx_fallback_rows", "dkg_split_model_ms", "dkg_split_len",
     "dkg_ctx_set_combine", "dkg_ctx_last_combine", "dkg_ctx_set_addends", "dkg_ctx_set_stepping_formula", "dkg_ctx_stepping_redos", "dkg_split_multipliers",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_verify_fetched", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
     "dkg_ceremony_shard_verify_device",

@@ -13,6 +13,7 @@ Reference interface -> here:
 Scalars and points are 32-byte encodings (bytes), exactly the reference's wire values.
 """
 import ctypes
+from collections.abc import Sequence
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -151,22 +152,15 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_ctx_set_field_mode(self._ctx, mode))
 
     def set_binomial(self, mode: int):
-        """Binomial schedule (dkg_ctx_set_binomial): 0 (default) one launch per Horner step with lane
-        pairs for the steps under one wave per SIMD, 1 without lane pairs, 2..5 one persistent
-        dataflow launch (1, 2, 4, 8 positions per item), 6 lane pairs for every step."""
+        """Binomial schedule (dkg_ctx_set_binomial), one launch per Horner step: 0 (default) lane pairs
+        for the steps under one wave per SIMD and the mixed item order for many-round launches, 1
+        without lane pairs, 2 lane pairs for every step, 3 as 0 without the mixed order, 4 the mixed
+        order for every step."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
-    def set_receiver_parts(self, parts: int):
-        """Stepping in receiver parts with the recombination and checks of each part on a second
-        stream (opt-in, measured slower): 0/1 off, 2..8 parts; results are identical."""
-        _check(self._ctx, _lib.lib().dkg_ctx_set_receiver_parts(self._ctx, parts))
-
-    def last_receiver_parts(self) -> int:
-        return _lib.lib().dkg_ctx_last_receiver_parts(self._ctx)
-
     def set_stepping(self, mode: int):
-        """Stepping slots of a split table: 0 cost model, 1 one per column (all pieces), 2 one per
-        piece; results are identical."""
+        """Stepping slots: 0 cost model, 1 one per column (all pieces of a split table), 2 one per
+        piece, 3 as 0 without the dead-position repack of short unsplit tables; results are identical."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_stepping(self._ctx, mode))
 
     def set_combine(self, mode: int):
@@ -566,10 +560,12 @@ def _batch_out(B, n, big):
     return o, bufs
 
 
-class Int32s:
+class Int32s(Sequence):
     """Little-endian int32 rows of a batch output, converted to Python ints only where read: a
     10,000-ceremony batch holds 640,000 of them, and building the whole list up front costs more
-    host time than the ceremonies' round 3."""
+    host time than the ceremonies' round 3.  A read-only Sequence (len, indexing, slices -> list,
+    iteration, `in`, index, count, == against any sequence); tolist() / list(x) for a list (JSON,
+    concatenation).  Unhashable, like the list it stands for."""
 
     def __init__(self, raw: bytes):
         self._mv = memoryview(raw).cast("i")
@@ -584,7 +580,18 @@ class Int32s:
         return iter(self._mv.tolist())
 
     def __eq__(self, other):
-        return self._mv.tolist() == list(other)
+        try:
+            return self._mv.tolist() == list(other)
+        except TypeError:
+            return NotImplemented
+
+    __hash__ = None
+
+    def __add__(self, other):
+        return self._mv.tolist() + list(other)
+
+    def __repr__(self):
+        return f"Int32s({self._mv.tolist()!r})" if len(self) <= 16 else f"Int32s(<{len(self)} values>)"
 
     def tolist(self):
         return self._mv.tolist()

@@ -401,17 +401,41 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 // (position, 64 dealers); position 0 just copies the next coefficient C_k.  Grid (dealer groups x
 // pieces, r+1) with m = r - blockIdx.y: workgroups are dispatched x-fastest, so the longest NAF
 // chains (largest m) of EVERY piece start first and the launch tail is made of the short ones.
+//
+// Mixed order (items > 0: a 1-D grid of `items` = (column groups x pieces) x (r+1) waves): a launch
+// of many rounds of waves (config 5: up to 620k waves) is HBM-co-bound -- the short chains of small m
+// move the same 480 B per item as the long ones -- so the positions of one column group are
+// dispatched back to back (m fastest, longest first) and the groups are dealt to the XCDs in
+// contiguous ranges (workgroup b runs on XCD b mod 8): items (g, m) and (g, m-1), which both read
+// e_{m-1}, run on the same XCD at nearly the same time, so the second read hits its L2, and every
+// CU holds a mix of memory-heavy and chain-heavy waves.
+__device__ __forceinline__ void binom_item(unsigned items, unsigned& bx, unsigned& by, int r) {
+  if (!items) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    return;
+  }
+  const unsigned per = (items + 7) / 8;  // items per XCD
+  const unsigned i = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  bx = i / (unsigned)(r + 1);
+  by = i - bx * (unsigned)(r + 1);
+  if (i >= items) bx = 0xffffffffu;  // padding of the last XCD's range
+}
+
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
                                                     size_t pstride, unsigned gx, unsigned last_piece,
-                                                    int last_off) {
+                                                    int last_off, unsigned items) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
-  const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
+  unsigned bx, by;
+  binom_item(items, bx, by, r);
+  if (bx == 0xffffffffu) return;
+  const unsigned piece = bx / gx, grp = bx - piece * gx;
   const size_t d = piece * pstride + (size_t)grp * blockDim.x + threadIdx.x;
   const size_t S = N * npad;
-  const int m = r - (int)blockIdx.y;
+  const int m = r - (int)by;
   if (m == 0) {
 #pragma unroll 8
     for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
@@ -502,12 +526,19 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 }
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
-                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
+                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, bool mixed) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
+  const size_t items = width / 64 * pieces * (r + 1);
+  if (mixed && items < (1ull << 31)) {
+    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)((items + 7) / 8 * 8)), dim3(64), 0, stream, (int)r,
+                       (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1),
+                       last_off, (unsigned)items);
+    return;
+  }
   hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64 * pieces), (unsigned)(r + 1)), dim3(64), 0, stream,
                      (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 64),
-                     (unsigned)(pieces - 1), last_off);
+                     (unsigned)(pieces - 1), last_off, 0u);
 }
 
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
@@ -516,184 +547,10 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
   uint32_t* in = e0;
   uint32_t* out = e1;
   for (size_t r = 1; r < N; r++) {
-    binom_step(r, width, npad, N, C, in, out, stream, pieces, pstride, last_len);
+    binom_step(r, width, npad, N, C, in, out, stream, pieces, pstride, last_len, false);
     std::swap(in, out);
   }
   return in;
-}
-
-// ---- The same Horner steps as ONE persistent dataflow launch (k_binom_flow) ----
-// Item (r, m, cw) = step r, position m >= 1, column wave cw (64 columns of one piece): e'_m =
-// m (e_{m-1} + e_m) needs positions m-1 and m of step r-1 of the SAME columns, and it overwrites
-// position m of step r-2 (ping-pong), which items (r-1, m) and (r-1, m+1) read.  So it waits for
-// done[cw][m'] >= r-1, m' in {m-1, m, m+1} (those that exist at step r-1); position 0 of step r-1 is
-// the coefficient C_{L-r}, read from C.  Items are handed out in the order (r ascending, m
-// descending -- the longest NAF chains of a step first --, cw ascending) by a ticket counter, four
-// consecutive items per workgroup (one per wave), so every item waits only on items dequeued before
-// it by running waves: no deadlock at any residency, and the t launch tails of the per-step grid --
-// each drained to zero before the next step could start -- overlap the next step's work.
-// Hand-off (cdna_hip_programming.md Guideline 16, recipe R1): the producer stores its point
-// write-through (sc1), waits for the stores, then one lane stores the flag (agent-scope atomic);
-// the consumer polls relaxed, then ONE agent acquire, then plain loads.  Spins are bounded: a wait
-// that gives up sets *err (the host raises) and the wave carries on, so the grid always drains.
-typedef __attribute__((address_space(1))) uint32_t flow_gu32;
-constexpr int FLOW_WAVES = 4;
-constexpr uint32_t FLOW_SPIN_LIMIT = 1u << 20;  // polls (~1 us each) before a wait gives up
-
-__device__ __forceinline__ uint32_t flow_ld(const uint32_t* p) {
-  return __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load((flow_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// wait until *flag >= want; false (and *err set) if the wait gave up.  Once *err is set anywhere,
-// every wait returns at its first check, so the grid drains in a few loads per item.
-__device__ __forceinline__ bool flow_wait(const uint32_t* flag, uint32_t want, uint32_t* err) {
-  for (uint32_t spins = 0;; spins++) {
-    if (flow_ld(flag) >= want) return true;
-    if (spins >= FLOW_SPIN_LIMIT || ((spins & 255u) == 0u && flow_ld(err))) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store((flow_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
-DKG_DEV void pt_store_wt(uint32_t* __restrict__ base, size_t stride, size_t e, const ge_p3& p) {
-#pragma unroll
-  for (int w = 0; w < PT_WORDS; w++)
-    __hip_atomic_store((flow_gu32*)(base + (size_t)w * stride + e), pt_word(p, w), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Items of K consecutive positions: step r has nb(r) = ceil(r / K) blocks, block b holding positions
-// b K + 1 .. min((b + 1) K, r); CW * P(r) items precede step r, P(r) = sum_{r' < r} ceil(r' / K).
-__host__ __device__ inline unsigned long long flow_prefix(unsigned long long r, unsigned K) {
-  const unsigned long long R = r - 1, q = R / K, sr = R % K;
-  return (unsigned long long)K * q * (q + 1) / 2 + sr * (q + 1);
-}
-
-// One item = (step r, block b of K positions, column wave cw): the K chains run one after the other
-// in the wave (each position's inputs come from step r-1), so the hand-off -- ticket, dependency
-// polls, acquire, flag -- is paid once per K chains.  Dependencies: blocks b-1 (position b K, read by
-// the lowest position), b and b+1 (read, and overwritten in the ping-pong table) at step r-1;
-// done[cw][block] = the last step the block completed.
-template <int K>
-__global__ __launch_bounds__(64 * FLOW_WAVES, 4) void k_binom_flow(int L, size_t npad, const uint32_t* __restrict__ C,
-                                                                  uint32_t* e0, uint32_t* e1, size_t pstride,
-                                                                  unsigned gx, unsigned CW, unsigned last_piece,
-                                                                  int last_off, uint32_t* done, uint32_t* ticket,
-                                                                  uint32_t* err, unsigned long long total) {
-  // each wave's cached addend (lane-interleaved); the dequeued ticket is broadcast through word 0 of
-  // wave 0's slot, which wave 0 rewrites only after the second barrier (40 KB exactly: 4 workgroups
-  // = 16 waves per CU)
-  __shared__ uint32_t qs[FLOW_WAVES][PT_WORDS * 64];
-  uint32_t& tk = qs[0][0];
-  // wave-uniform values go through readfirstlane so that they live in SGPRs (the chain needs the
-  // VGPRs: <= 128 for 4 waves per SIMD)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  uint32_t* q = qs[wave] + lane;
-  const size_t S = (size_t)L * npad;
-  const int nblocks = (L - 1 + K - 1) / K;  // flag words per column wave
-  for (;;) {
-    if (threadIdx.x == 0) tk = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const unsigned long long first = (unsigned long long)__builtin_amdgcn_readfirstlane(tk) * FLOW_WAVES;
-    __syncthreads();  // tk is rewritten by the next iteration's dequeue
-    if (first >= total) break;  // workgroup-uniform exit
-    const unsigned long long item = first + wave;
-    if (item < total) {
-      // decode (r, b, cw): the largest r with CW * P(r) <= item (binary search, wave-uniform)
-      const unsigned long long x = item / CW;
-      int lo = 1, hi = L - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (flow_prefix(mid, K) <= x) lo = mid;
-        else hi = mid - 1;
-      }
-      const int r = __builtin_amdgcn_readfirstlane(lo);
-      const unsigned long long off = item - (unsigned long long)CW * flow_prefix(r, K);
-      const int nb = (r + K - 1) / K;
-      const int b = __builtin_amdgcn_readfirstlane(nb - 1 - (int)(off / CW));
-      const unsigned cw = __builtin_amdgcn_readfirstlane((unsigned)(off % CW));
-      const unsigned piece = cw / gx, grp = cw - piece * gx;
-      const size_t d = piece * pstride + (size_t)grp * 64 + lane;
-      uint32_t* fl = done + (size_t)cw * nblocks;
-      const uint32_t prev = (uint32_t)(r - 1);
-      const int nbp = (r - 1 + K - 1) / K;  // blocks that exist at step r-1
-      if (b >= 1 && b - 1 < nbp) flow_wait(fl + b - 1, prev, err);
-      if (b < nbp) flow_wait(fl + b, prev, err);
-      if (b + 1 < nbp) flow_wait(fl + b + 1, prev, err);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const uint32_t* ein = (r & 1) ? e0 : e1;  // step r reads step r-1's table
-      uint32_t* eout = (r & 1) ? e1 : e0;
-      // a short last piece (last_off = L - its length) has degree re = r - last_off after step r;
-      // positions above re are never read
-      const int re = r - (piece == last_piece ? last_off : 0);
-      const int mhi = min((b + 1) * K, re), mlo = b * K + 1;
-#pragma unroll 1
-      for (int m = mhi; m >= mlo; m--) {
-        {
-          ge_p3 cur;
-          pt_load(cur, ein, S, (size_t)m * npad + d);
-          // position re of step r-1 does not exist (identity); branch-free, opaque select as in
-          // k_binom_step (the load of that slot is harmless: it is masked)
-          uint32_t keep = (m == re) ? 0u : 0xffffffffu;
-          asm volatile("" : "+v"(keep));
-          uint32_t* cw32 = reinterpret_cast<uint32_t*>(&cur);
-#pragma unroll
-          for (int w = 0; w < PT_WORDS; w++) cw32[w] = (cw32[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
-          ge_cached cc;
-          ge_to_cached(cc, cur);
-          lds_put_cached(q, cc);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        ge_p3 xv;
-        // position 0 of step r-1 is C_{L-r}
-        pt_load(xv, m == 1 ? C : ein, S, (size_t)(m == 1 ? L - r : m - 1) * npad + d);
-        ge_add_lds(xv, xv, q, false);        // e_{m-1} + e_m
-        mul_small_lds(xv, (uint32_t)m, q);   // * m
-        pt_store_wt(eout, S, (size_t)m * npad + d, xv);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the block has completed
-      if (lane == 0) __hip_atomic_store((flow_gu32*)(fl + b), (uint32_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// Flow items of a chunk with K positions per item; flag words per column wave
-unsigned long long binom_flow_items(size_t width, size_t pieces, size_t L, unsigned K) {
-  return (unsigned long long)(width / 64 * pieces) * flow_prefix(L, K);
-}
-size_t binom_flow_flag_words(size_t width, size_t pieces, size_t L, unsigned K) {
-  return (width / 64 * pieces) * ((L - 1 + K - 1) / K);
-}
-
-// done: binom_flow_flag_words words and ticket, err: one word each, all zeroed by the caller before
-// the launch.  Returns the table holding the result (position 0 included).
-uint32_t* binomial_flow(size_t width, size_t npad, size_t L, const uint32_t* C, uint32_t* e0, uint32_t* e1,
-                        hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* done,
-                        uint32_t* ticket, uint32_t* err, unsigned grid_cap, unsigned K) {
-  binom_init(width, npad, L, C, e0, stream, pieces, pstride);
-  if (L < 2) return e0;
-  const unsigned CW = (unsigned)(width / 64 * pieces);
-  const unsigned long long total = binom_flow_items(width, pieces, L, K);
-  const int last_off = (last_len && last_len < L) ? (int)(L - last_len) : 0;
-  const unsigned long long wgs = (total + FLOW_WAVES - 1) / FLOW_WAVES;
-  const unsigned grid = (unsigned)(wgs < grid_cap ? wgs : grid_cap);
-  const unsigned gx = (unsigned)(width / 64), lp = (unsigned)(pieces - 1);
-#define DKG_FLOW_LAUNCH(KK)                                                                                       \
-  hipLaunchKernelGGL(k_binom_flow<KK>, dim3(grid), dim3(64 * FLOW_WAVES), 0, stream, (int)L, npad, C, e0, e1, pstride, \
-                     gx, CW, lp, last_off, done, ticket, err, total)
-  if (K >= 8) DKG_FLOW_LAUNCH(8);
-  else if (K >= 4) DKG_FLOW_LAUNCH(4);
-  else if (K >= 2) DKG_FLOW_LAUNCH(2);
-  else DKG_FLOW_LAUNCH(1);
-#undef DKG_FLOW_LAUNCH
-  uint32_t* fin = ((L - 1) & 1) ? e1 : e0;
-  // position 0 after the last step is C_0 (the flow never writes position 0)
-  hipLaunchKernelGGL(k_copy_pos, dim3((unsigned)((width + 255) / 256), (unsigned)pieces), dim3(256), 0, stream, width,
-                     npad, L, C, (size_t)0, fin, pstride);
-  return fin;
 }
 
 // ------------------------------------------------------------------ K3b stepping
@@ -765,7 +622,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     uint32_t* __restrict__ down,      // NULL: block 0
     uint32_t* __restrict__ R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast,
     uint32_t* __restrict__ flags, size_t col0, size_t dreal, unsigned gw, uint32_t* __restrict__ Rz, size_t j0,
-    size_t j1, const uint32_t* __restrict__ sin, uint32_t* __restrict__ sout) {
+    size_t j1, const uint32_t* __restrict__ sin, uint32_t* __restrict__ sout, size_t nin, size_t nout) {
   const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
   if (!DED && flags && !flags[wg]) return;  // a redo launch: this workgroup's tables were exact
   // Lane l's cached value sits in LDS column l (word k at cols[k * MAXBS + l]); the lane at
@@ -792,8 +649,14 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const size_t pos = pos0 + q;
   ge_p3 D;
   // positions >= Nlive (a short last piece) are the identity whatever the table holds there
-  if (live && pos < Nlive) pt_load(D, (PARTS && j0) ? sin : e, S, d * N + pos);  // column-major: a segment reads contiguously
-  else ge_identity(D);
+  // column-major: a segment reads contiguously (a part's starting state `sin` has its own column
+  // stride nin: only the positions still live there are kept)
+  if (live && pos < Nlive) {
+    if (PARTS && j0) pt_load(D, sin, nin * npad, d * nin + pos);
+    else pt_load(D, e, S, d * N + pos);
+  } else {
+    ge_identity(D);
+  }
   const bool top_lane = live && (q == Pseg - 1);
   const uint4* upd = (up && live) ? reinterpret_cast<const uint4*>(up + d * nrecv * PT_WORDS) : nullptr;
   uint4* downd = (down && live) ? reinterpret_cast<uint4*>(down + d * nrecv * PT_WORDS) : nullptr;
@@ -854,7 +717,7 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       size_t dd = d;
       int qq = q;
       asm volatile("" : "+v"(dd), "+v"(qq));
-      if (live && pos0 + qq < Nlive) pt_store(sout, S, dd * N + pos0 + qq, D);
+      if (live && pos0 + qq < Nlive && pos0 + qq < nout) pt_store(sout, nout * npad, dd * nout + pos0 + qq, D);
     }
   }
   if (DED && bad) flags[wg] = 1u;  // any lane: the same value
@@ -948,45 +811,53 @@ template <bool DED, bool PARTS>
 void step_launch_p(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t ndealers, size_t npad, size_t N,
                    const uint32_t* e, size_t nrecv, size_t pos0, int P, const uint32_t* up, uint32_t* down,
                    uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags,
-                   const ColReal& cr, size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
+                   const ColReal& cr, size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout, size_t nin,
+                   size_t nout) {
   if (maxbs == 192)
     hipLaunchKernelGGL((k_stepping<192, DED, PARTS>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P,
                        up, down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
-                       R ? cr.Rz : nullptr, j0, j1, sin, sout);
+                       R ? cr.Rz : nullptr, j0, j1, sin, sout, nin, nout);
   else if (maxbs == 256)
     hipLaunchKernelGGL((k_stepping<256, DED, PARTS>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P,
                        up, down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
-                       R ? cr.Rz : nullptr, j0, j1, sin, sout);
+                       R ? cr.Rz : nullptr, j0, j1, sin, sout, nin, nout);
   else
     hipLaunchKernelGGL((k_stepping<512, DED, PARTS>), grid, block, 0, stream, ndealers, npad, N, e, nrecv, pos0, P,
                        up, down, R, pstride, Nlive, piece0, nseg, Plast, flags, cr.col0, cr.dreal, cr.gw,
-                       R ? cr.Rz : nullptr, j0, j1, sin, sout);
+                       R ? cr.Rz : nullptr, j0, j1, sin, sout, nin, nout);
 }
 
 template <bool DED>
 void step_launch(int maxbs, dim3 grid, dim3 block, hipStream_t stream, size_t ndealers, size_t npad, size_t N,
                  const uint32_t* e, size_t nrecv, size_t pos0, int P, const uint32_t* up, uint32_t* down,
                  uint32_t* R, size_t pstride, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* flags,
-                 const ColReal& cr, size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
+                 const ColReal& cr, size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout, size_t nin = 0,
+                 size_t nout = 0) {
   if (j0 != 0 || j1 != nrecv)
     step_launch_p<DED, true>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, R, pstride,
-                             Nlive, piece0, nseg, Plast, flags, cr, j0, j1, sin, sout);
+                             Nlive, piece0, nseg, Plast, flags, cr, j0, j1, sin, sout, nin ? nin : N,
+                             nout ? nout : N);
   else
     step_launch_p<DED, false>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, R, pstride,
-                              Nlive, piece0, nseg, Plast, flags, cr, 0, nrecv, nullptr, nullptr);
+                              Nlive, piece0, nseg, Plast, flags, cr, 0, nrecv, nullptr, nullptr, N, N);
 }
 
-bool stepping_parts_ok(size_t N) { return N <= 512; }  // one block per table: no boundary streams
+// Dead-position repack: worth its state copies when the dead lane-steps are a large share of the
+// launch (about N / 2n of them: config 5, n = 64, t = 31, 24 %), not for long tables of big
+// ceremonies whose dead positions fill only the upper wave of the last N steps (n = 1024: 3 %).
+constexpr size_t TAIL_MIN_P = 4;
+int stepping_tail_phases(size_t N, size_t nrecv, size_t pieces) {
+  if (pieces != 1 || N > 512 || N < 2 * TAIL_MIN_P || 10 * N < 2 * nrecv || nrecv + 1 < N) return 1;
+  int k = 1;
+  for (size_t P = N / 2; P >= TAIL_MIN_P; P /= 2) k++;
+  return k;
+}
+size_t stepping_tail_words(size_t ndealers, size_t N) { return PT_WORDS * ndealers * (N / 2); }
 
 bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t nrecv, uint32_t* R,
               uint32_t* stream_a, uint32_t* stream_b, hipStream_t stream, size_t pieces, size_t pstride,
               size_t last_len, bool whole, uint32_t* flags, size_t col0, size_t dreal, unsigned gw, uint32_t* Rz,
-              size_t j0, size_t j1, const uint32_t* sin, uint32_t* sout) {
-  if (!j1) j1 = nrecv;
-  // receiver parts: tables carried between parts; not with block chaining (N > 512)
-  if ((j0 != 0 || j1 != nrecv) &&
-      !(j0 < j1 && j1 <= nrecv && (!j0 || sin) && (j1 == nrecv || sout) && sin != sout && stepping_parts_ok(N)))
-    return false;
+              uint32_t* tail_a, uint32_t* tail_b) {
   if (!ndealers || !nrecv) return true;
   const ColReal cr{col0, dreal, gw ? gw : 64u, Rz};
   if (!last_len || last_len > N) last_len = N;
@@ -997,10 +868,10 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
                  uint32_t* Rout, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* f) {
     if (f) {
       step_launch<true>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
-                        Nlive, piece0, nseg, Plast, f, cr, j0, j1, sin, sout);
+                        Nlive, piece0, nseg, Plast, f, cr, 0, nrecv, nullptr, nullptr);
     }
     step_launch<false>(maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, pos0, P, up, down, Rout, pstride,
-                       Nlive, piece0, nseg, Plast, f, cr, j0, j1, sin, sout);
+                       Nlive, piece0, nseg, Plast, f, cr, 0, nrecv, nullptr, nullptr);
   };
   auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
     const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), (unsigned)np), block((unsigned)s.bs);
@@ -1008,6 +879,36 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
     foff += (size_t)grid.x * grid.y;
     run((int)s.maxbs, grid, block, 0, (int)s.P, nullptr, nullptr, R, Nlive, piece0, nseg, Plast, f);
   };
+  const int phases = (tail_a && tail_b) ? stepping_tail_phases(N, nrecv, pieces) : 1;
+  if (phases > 1) {
+    // phase k: steps [J_k, J_{k+1}) on P_k-lane segments, J_k = nrecv - P_k + 1; it starts from the
+    // state phase k-1 left (P_k positions, stride P_k) and leaves P_{k+1} positions for phase k+1.
+    // Each phase's redo launch restarts from its unchanged starting state (the other buffer).
+    uint32_t* st[2] = {tail_a, tail_b};
+    size_t P = N, j0 = 0;
+    for (int k = 0; k < phases; k++) {
+      const size_t Pn = P / 2, j1 = k + 1 < phases ? nrecv - Pn + 1 : nrecv;
+      const StepShape s = stepping_shape(P);
+      const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), 1u), block((unsigned)s.bs);
+      uint32_t* f = flags ? flags + foff : nullptr;
+      foff += grid.x;
+      // the states are laid out for the whole table ([40][npad][P], word-row stride P npad): this
+      // call's columns start at col0
+      const uint32_t* sin = k ? st[(k - 1) % 2] + col0 * P : nullptr;
+      uint32_t* sout = k + 1 < phases ? st[k % 2] + col0 * Pn : nullptr;
+      for (int pass = f ? 0 : 1; pass < 2; pass++) {
+        if (pass == 0)
+          step_launch_p<true, true>((int)s.maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, 0, (int)P,
+                                    nullptr, nullptr, R, 0, N, 0u, 1, (int)P, f, cr, j0, j1, sin, sout, P, Pn);
+        else
+          step_launch_p<false, true>((int)s.maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, 0, (int)P,
+                                     nullptr, nullptr, R, 0, N, 0u, 1, (int)P, f, cr, j0, j1, sin, sout, P, Pn);
+      }
+      P = Pn;
+      j0 = j1;
+    }
+    return true;
+  }
   if (whole && stepping_whole_columns(N, pieces, last_len)) {
     // one slot of (pieces - 1) N + last_len lanes per column: every workgroup does the same work
     // (a column), so a launch of ndealers columns has no tail of lone pieces

@@ -31,7 +31,8 @@ struct dkg_ctx {
   hipEvent_t ev[8] = {};
   hipEvent_t pev[5] = {};               // phase profiling inside verify_device (nsub == 1)
   hipEvent_t hev[9] = {};               // full mode: encrypt / decrypt kernels (nsub == 1)
-  bool hy_timed = false;                // hev[] hold the last full-mode ceremony's phases
+  int hy_timed = 0;                     // hev[] hold the phases of the last serialised encrypt (1)
+                                        // and / or decrypt (2) since the last collect_hybrid_phases
   static constexpr int MAX_SUB = 8;
   int nsub = 2;                         // dealer-chunk streams of verify_device
   hipStream_t sub[MAX_SUB] = {};
@@ -43,18 +44,14 @@ struct dkg_ctx {
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
-  int recv_parts = 0;                   // receiver parts of the stepping (0/1: off, 2..8: opt-in)
-  int last_recv_parts = 1;              // parts used by the last verify_device
-  hipEvent_t rpart[8] = {}, rjoin = nullptr;  // part h's stepping done / the aux stream's work done
   std::vector<uint8_t> key_tabs_pk;     // member keys whose decoded points and combs sit in hy.* (encrypt)
-  int binom_mode = 0;                   // binomial: 0/1 one launch per Horner step (k_binom_step;
-                                        // 0 with lane pairs, k_binom_pair, for the steps under one
-                                        // wave per SIMD), 2..5 one persistent dataflow launch
-                                        // (k_binom_flow), 6 lane pairs for every step
-  uint32_t* flow_state = nullptr;       // dataflow binomial: per chunk [flags | ticket | err] words,
-  size_t flow_chunk_words = 0;          // flow_chunk_words per chunk; err at word flow_chunk_words-1
-  size_t flow_chunks = 0;               // chunks whose err word the next sync checks
-  int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece
+  int binom_mode = 0;                   // binomial, one launch per Horner step: 0 lane pairs
+                                        // (k_binom_pair) for the steps under one wave per SIMD and
+                                        // the mixed item order for many-round launches, 1 no lane
+                                        // pairs, 2 lane pairs for every step, 3 as 0 without the
+                                        // mixed order, 4 the mixed order for every step
+  int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece,
+                                        // 3 as 0 without the dead-position repack
   int fe_mode = 0;                      // field multiplication per launch: 0 by occupancy, 1 product
                                         // scanning (dkgk), 2 column sums (dkgk_ilp)
   int verify_mode = 0;                  // 0: difference tables (every P_i(j) in the group); 1: interpolation
@@ -86,10 +83,6 @@ struct dkg_ctx {
   std::string timed_tag;                // set while pev[] hold a serialised verify_device's phases
   std::map<std::string, double> phase_ms;  // last value per "r<round>.<phase>"
 };
-
-namespace ContextLimits {
-constexpr size_t MAX_FLOW_CHUNKS = 8;  // = dkg_ctx::MAX_SUB
-}
 
 namespace {
 
@@ -143,18 +136,6 @@ void d2h(dkg_ctx* ctx, void* h, const void* d, size_t n) {
 }
 void sync(dkg_ctx* ctx) {
   HCK(hipStreamSynchronize(ctx->stream));
-  if (ctx->flow_chunks) {  // the dataflow binomial's bounded waits (kernels.hip k_binom_flow)
-    const size_t k = ctx->flow_chunks;
-    ctx->flow_chunks = 0;
-    std::vector<uint32_t> err(k);
-    for (size_t c = 0; c < k; c++)
-      HCK(hipMemcpy(&err[c], ctx->flow_state + (c + 1) * ctx->flow_chunk_words - 1, 4, hipMemcpyDeviceToHost));
-    for (uint32_t e : err)
-      if (e) {
-        ctx->err = "binomial dataflow: a dependency wait gave up (results invalid)";
-        throw Fail{DKG_E_DEVICE};
-      }
-  }
 }
 void check_launch(dkg_ctx* ctx) { HCK(hipGetLastError()); }
 
@@ -237,6 +218,12 @@ struct VerifySeg {
 #endif
 #ifndef DKG_BINOM_ILP_WAVES
 #define DKG_BINOM_ILP_WAVES 1.5
+#endif
+// Binomial steps with at least this many waves per SIMD (rounds of 4 resident waves) dispatch their
+// items in the mixed order (kernels.hip k_binom_step): many rounds make the launch drain negligible,
+// and the order halves the step's HBM reads.
+#ifndef DKG_BINOM_MIX_WAVES
+#define DKG_BINOM_MIX_WAVES 16.0
 #endif
 
 bool use_ilp(const dkg_ctx* ctx, bool latency_bound) {
@@ -500,7 +487,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // degree split: U pieces of L positions; piece u of column c is table column u * npad + c
   const size_t U = choose_split(ctx, npad, n, N), L = split_len(npad, n, N, U, ctx->combine_mode != 1), W = U * npad;
   const size_t Lr = last_piece_len(N, U, L);  // the last piece's length (L or shorter)
-  const bool whole = ctx->step_mode == 1 || (ctx->step_mode == 0 && stepping_whole_pays(npad, U, L, Lr));
+  const bool whole = ctx->step_mode == 1 || ((ctx->step_mode == 0 || ctx->step_mode == 3) && stepping_whole_pays(npad, U, L, Lr));
   // the stepping keeps product scanning even at 2 waves per SIMD (8-way n=1024 shard, one stream:
   // 6.07 vs 6.12 ms with column sums, profiles/r02_shard_stepping_ab.txt); only a forced mode 2
   // switches it
@@ -571,16 +558,6 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     }
   };
   // dealer groups [g0, g1) = columns [g0 * gw, g1 * gw)
-  // dataflow binomial state: per chunk the flags of its column waves ([cw][L]), the ticket and the
-  // err word, zeroed on the chunk's stream before its launch
-  const bool flow = ctx->binom_mode >= 2 && ctx->binom_mode <= 5 && L > 1;
-  const unsigned flow_k = 1u << std::min(ctx->binom_mode >= 2 ? ctx->binom_mode - 2 : 0, 3);  // 2..5 -> K = 1..8
-  if (flow) {
-    ctx->flow_chunk_words = (dkgk::binom_flow_flag_words(npad, U, L, flow_k) + 2 + 63) / 64 * 64;
-    ctx->flow_state = buf<uint32_t>(ctx, "v.flow", 4 * ctx->flow_chunk_words * ContextLimits::MAX_FLOW_CHUNKS);
-  }
-  // persistent grid: 4 workgroups (16 waves) per CU fill the chip; chunks launched side by side share it
-  const unsigned flow_grid = 1024;
   // Chunk streams pay when the binomial saturates the GPU (chunk c+1's triangle fills the CUs that
   // chunk c's launch tails leave idle), or when the stepping is long enough (W * L * n lane-steps)
   // that the chunks' phases drift apart and one chunk's recombination and checks run beside the
@@ -593,97 +570,40 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // needs at least 512 columns too.
   const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
   const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
-  // Receiver parts (opt-in, dkg_ctx_set_receiver_parts 2..8): the stepping runs in H launches
-  // over receiver ranges (the table carried between them in v.rstate), and part h's normalisation,
-  // recombination and checks run on a second stream beside part h+1's stepping, in place of the
-  // dealer chunks.  Meant for a lone chunk with few waves per SIMD (the 8-way n=1024 shard: 2), it
-  // measured no gain there: every part's recombination and checks are latency-bound themselves
-  // and slow the stepping they share the CUs with (14.8 ms unsplit, 14.8 / 15.6 / 22.0 ms at 2 / 4
-  // / 8 parts; 19.6 with the part work on the low-priority stream; the 4-way shard 23.1 vs 25.1,
-  // profiles/r03_receiver_parts_ab.txt).  Needs >= 2 streams (ctx->nsub > 1).
-  const bool parts_able = ctx->nsub > 1 && short_mult && Aff && nseg == 2 && dkgk::stepping_parts_ok(L) && n >= 128;
-  const size_t nsub = (parts_able && ctx->recv_parts > 1) ? 1
-                      : (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
-  size_t H = 1;
-  const bool parts_ok = nsub == 1 && parts_able;
-  if (parts_ok) {
-    if (ctx->recv_parts > 1) H = std::min((size_t)ctx->recv_parts, n / 32);
-  }
-  ctx->last_recv_parts = (int)H;
-  // the table between parts, double-buffered (part h reads one and writes the other); flag words
-  // of the dedicated additions per part (every stepping() call numbers its launches from 0)
-  uint32_t* rstate = H > 1 ? buf<uint32_t>(ctx, "v.rstate", 2 * PTB * L * W) : nullptr;
-  const size_t pfw = dkgk::stepping_flag_words(npad, U);
-  uint32_t* pflags = H > 1 && sflags ? buf<uint32_t>(ctx, "v.sflags_parts", 4 * H * pfw) : nullptr;
-  if (pflags) {
-    HCK(hipMemsetAsync(pflags, 0, 4 * H * pfw, home));
-    ctx->last_step_flags = pflags;
-    ctx->last_step_flag_words = H * pfw;
-  }
-  auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm, size_t chunk_idx) {
+  const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
+  // dead-position repack of an unsplit table (kernels.hip stepping_tail_phases): two scratch states
+  const bool tails = ctx->step_mode != 3 && dkgk::stepping_tail_phases(L, n, U) > 1;
+  uint32_t* tail_a = tails ? buf<uint32_t>(ctx, "v.tail_a", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
+  uint32_t* tail_b = tails ? buf<uint32_t>(ctx, "v.tail_b", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
+  auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    const uint32_t* e;
-    if (flow) {
-      // one persistent dataflow launch for all L-1 steps: the column-sum copy when the whole table
-      // averages fewer than 1.5 waves per SIMD per step (small shards: latency-bound chains)
-      const bool ilp = use_ilp(ctx, (double)npad / 64 * U * (L / 2.0) / 1024 < 1.5);
-      uint32_t* fs = ctx->flow_state + chunk_idx * ctx->flow_chunk_words;
-      HCK(hipMemsetAsync(fs, 0, 4 * ctx->flow_chunk_words, st));
-      const size_t fl_words = dkgk::binom_flow_flag_words(w, U, L, flow_k);
-      e = (ilp ? dkgk_ilp::binomial_flow : dkgk::binomial_flow)(w, W, L, Cpm + c0, e0 + c0, e1 + c0, st, U, npad,
-                                                               Lr, fs, fs + fl_words, fs + ctx->flow_chunk_words - 1,
-                                                               flow_grid, flow_k);
-    } else {
-      dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
-      uint32_t *bin = e0 + c0, *bout = e1 + c0;
-      for (size_t r = 1; r < L; r++) {
-        // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
-        const double wps = (double)npad / 64 * U * (r + 1) / 1024;  // waves per SIMD, all chunks
-        const bool ilp = use_ilp(ctx, wps < DKG_BINOM_ILP_WAVES);
-        // lane pairs (k_binom_pair): by default the steps with under one wave per SIMD, mode 6 every
-        // step (1-, 2-, 4-, 8-way n=1024 shards 0.2-0.4 ms faster; profiles/r03_binomial_pairs_ab.txt)
-        const bool pair = ctx->binom_mode == 6 || (ctx->binom_mode == 0 && wps < DKG_BINOM_PAIR_WAVES);
-        if (pair)
-          (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
-        else
-          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
-        std::swap(bin, bout);
-      }
-      e = bin;
+    dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
+    uint32_t *bin = e0 + c0, *bout = e1 + c0;
+    for (size_t r = 1; r < L; r++) {
+      // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
+      const double wps = (double)npad / 64 * U * (r + 1) / 1024;  // waves per SIMD, all chunks
+      const bool ilp = use_ilp(ctx, wps < DKG_BINOM_ILP_WAVES);
+      // lane pairs (k_binom_pair): by default the steps with under one wave per SIMD, mode 2 every
+      // step (1-, 2-, 4-, 8-way n=1024 shards 0.2-0.4 ms faster; profiles/r03_binomial_pairs_ab.txt)
+      const bool pair = ctx->binom_mode == 2 || ((ctx->binom_mode == 0 || ctx->binom_mode == 3) &&
+                                                 wps < DKG_BINOM_PAIR_WAVES);
+      const bool mixed = ctx->binom_mode == 4 || (ctx->binom_mode != 3 && wps >= DKG_BINOM_MIX_WAVES);
+      if (pair)
+        (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+      else
+        (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr, mixed);
+      std::swap(bin, bout);
     }
+    const uint32_t* e = bin;
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     auto step = step_ilp ? dkgk_ilp::stepping : dkgk::stepping;
-    if (H > 1) {
-      // part h: receivers [jb(h), jb(h+1)), flag words pflags[h * pfw ..] (a lone chunk: c0 = 0)
-      hipStream_t aux = ctx->sub[0];
-      auto jb = [&](size_t h) { return h == H ? n : (n * h / H) / 32 * 32; };
-      for (size_t h = 0; h < H; h++) {
-        const size_t j0 = jb(h), j1 = jb(h + 1);
-        if (!step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, nullptr, nullptr, st, U, npad, Lr, whole,
-                  pflags ? pflags + h * pfw : nullptr, c0, D, (unsigned)gw, Rz + c0 * n * 10, j0, j1,
-                  rstate + (h % 2) * 40 * L * W + c0 * L, rstate + ((h + 1) % 2) * 40 * L * W + c0 * L)) {
-          ctx->err = "verify_device: receiver parts need whole-column stepping";
-          throw Fail{DKG_E_ARG};
-        }
-        HCK(hipEventRecord(ctx->rpart[h % 8], st));
-        HCK(hipStreamWaitEvent(aux, ctx->rpart[h % 8], 0));
-        dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, aux,
-                            Rz + c0 * n * 10, j0, j1 - j0);
-        dkgk::combine_short_aff(w, npad, U, n, sdig, stop, Aff + c0 * n * AFFP_WORDS_H, R + c0 * n * PT_WORDS_H,
-                                aux, j0, j1 - j0);
-        checks(g0 * 64, std::min(D, g1 * 64), aux, j0, j1 - j0);
-      }
-      HCK(hipEventRecord(ctx->rjoin, aux));
-      HCK(hipStreamWaitEvent(st, ctx->rjoin, 0));
-      return;
-    }
     step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
          sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw,
-         Rz ? Rz + c0 * n * 10 : nullptr, 0, 0, nullptr, nullptr);
+         Rz ? Rz + c0 * n * 10 : nullptr, tail_a, tail_b);
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     if (short_mult && Aff) {
       dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st, Rz + c0 * n * 10);
@@ -696,22 +616,20 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   };
   ctx->timed_tag.clear();
   if (nsub <= 1) {
-    // the receiver-part schedule interleaves the phases on two streams: no per-phase times
-    chunk(0, groups, home, timed && H == 1, 0);
-    if (timed && H == 1) ctx->timed_tag = tag;
+    chunk(0, groups, home, timed);
+    if (timed) ctx->timed_tag = tag;
   } else {
     HCK(hipEventRecord(ctx->fork, home));
     size_t g0 = 0;
     for (size_t c = 0; c < nsub; c++) {
       const size_t g1 = groups * (c + 1) / nsub;
       HCK(hipStreamWaitEvent(ctx->sub[c], ctx->fork, 0));
-      chunk(g0, g1, ctx->sub[c], false, c);
+      chunk(g0, g1, ctx->sub[c], false);
       HCK(hipEventRecord(ctx->join[c], ctx->sub[c]));
       HCK(hipStreamWaitEvent(home, ctx->join[c], 0));
       g0 = g1;
     }
   }
-  if (flow) ctx->flow_chunks = std::max<size_t>(ctx->flow_chunks, std::max<size_t>(nsub, 1));
   check_launch(ctx);
 }
 
@@ -1351,6 +1269,7 @@ void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const
   if (tm) HCK(hipEventRecord(ctx->hev[2], st));
   dkgk::sym_xor(D, n, Kc, false, ct, const_cast<uint32_t*>(s), const_cast<uint32_t*>(sp), st);
   if (tm) HCK(hipEventRecord(ctx->hev[3], st));
+  if (tm) ctx->hy_timed |= 1;
   check_launch(ctx);
 }
 
@@ -1374,6 +1293,7 @@ void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const 
   if (tm) HCK(hipEventRecord(ctx->hev[7], st));
   dkgk::sym_xor(D, n, Kc, true, const_cast<uint32_t*>(ct), s, sp, st);
   if (tm) HCK(hipEventRecord(ctx->hev[8], st));
+  if (tm) ctx->hy_timed |= 2;
   if (dealer_ok_out) dkgk::dealer_ok(D, 2 * n, item_ok, dealer_ok_out, st);
   check_launch(ctx);
 }
@@ -1381,11 +1301,16 @@ void decrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* sk, const 
 // After a sync: the full-mode kernels' device times of the last serialised encrypt + decrypt
 // (dkg_ctx_phase_ms "full.enc_mul", "full.enc_encode", "full.enc_sym", "full.dec_decode",
 // "full.dec_mul", "full.dec_encode", "full.dec_sym").
+// Every full.* entry of an earlier ceremony is dropped first: a phase this ceremony did not time
+// (chunk streams, or a verify-only ceremony without encryption) reads -1.
 void collect_hybrid_phases(dkg_ctx* ctx) {
-  if (ctx->nsub != 1) return;
   const char* names[8] = {"enc_mul", "enc_encode", "enc_sym", "", "dec_decode", "dec_mul", "dec_encode", "dec_sym"};
+  for (const char* nm : names)
+    if (nm[0]) ctx->phase_ms.erase(std::string("full.") + nm);
+  const int timed = ctx->hy_timed;
+  ctx->hy_timed = 0;
   for (int i = 0; i < 8; i++) {
-    if (!names[i][0]) continue;
+    if (!names[i][0] || !(timed & (i < 4 ? 1 : 2))) continue;
     float ms = 0;
     HCK(hipEventElapsedTime(&ms, ctx->hev[i], ctx->hev[i + 1]));
     ctx->phase_ms[std::string("full.") + names[i]] = ms;
@@ -1497,8 +1422,6 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     HCK(hipEventCreateWithFlags(&ctx->pub_done, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto& e : ctx->rpart) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HCK(hipEventCreateWithFlags(&ctx->rjoin, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_h, COMB_BYTES));
     HCK(hipMalloc(&ctx->tab_gw, COMBW_BYTES));
@@ -1537,9 +1460,6 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->join)
     if (e) (void)hipEventDestroy(e);
-  for (auto& e : ctx->rpart)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->rjoin) (void)hipEventDestroy(ctx->rjoin);
   if (ctx->fork) (void)hipEventDestroy(ctx->fork);
   for (auto& st : ctx->sub)
     if (st) (void)hipStreamDestroy(st);
@@ -1579,15 +1499,8 @@ int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
   return DKG_OK;
 }
 
-int dkg_ctx_set_receiver_parts(dkg_ctx* ctx, int parts) {
-  if (!ctx || parts < 0 || parts > 8) return DKG_E_ARG;
-  ctx->recv_parts = parts;
-  return DKG_OK;
-}
-int dkg_ctx_last_receiver_parts(const dkg_ctx* ctx) { return ctx ? ctx->last_recv_parts : 0; }
-
 int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 6) return DKG_E_ARG;
+  if (!ctx || mode < 0 || mode > 4) return DKG_E_ARG;
   ctx->binom_mode = mode;
   return DKG_OK;
 }
@@ -1599,7 +1512,7 @@ int dkg_ctx_set_field_mode(dkg_ctx* ctx, int mode) {
 }
 
 int dkg_ctx_set_stepping(dkg_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 2) return DKG_E_ARG;
+  if (!ctx || mode < 0 || mode > 3) return DKG_E_ARG;
   ctx->step_mode = mode;
   return DKG_OK;
 }
@@ -2709,6 +2622,7 @@ int dkg_ceremony_verify_full(dkg_ctx* ctx, size_t n, size_t t, const uint8_t* E,
       ctx->shares_pending = true;
     }
     receivers_rounds(ctx, n, t, Ec, Ac, rs, rsp, out, true, eok);  // waits for the shares before it returns
+    collect_hybrid_phases(ctx);  // decryption phases only (no encryption here: full.enc_* read -1)
     if (out->s) d2h(ctx, out->s, rs, 32 * n * n);
     if (out->s_prime) d2h(ctx, out->s_prime, rsp, 32 * n * n);
     sync(ctx);

@@ -14,8 +14,9 @@ dkg_shard_combine_device derives the common outcome (qualified set, complaints, 
 rows, reconstruction set, r4 errors, Phase4 failure) with the single-GPU drivers' own code, and
 dkg_shard_finalise_device the final shares, public shares and mpk (include/dkg_amd.h).
 """
-from dataclasses import dataclass
-from typing import Any, Optional
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
 
 import numpy as np
 
@@ -51,6 +52,10 @@ class ShardResult:
     public_share: Optional[bytes]  # [n][32] g * s_j (committee.rs:463-467)
     mpk: Optional[bytes]           # 32 bytes (committee.rs:790-795); None when Phase4 fails
     ms_shard: float                # device time of this rank's share gen + checks
+    # host wall ms of the steps after the shard: "exchange" (the all-gathers, fenced), "combine"
+    # (dkg_shard_combine_device + outcome copies), "recon" (round-4 reconstruction + its gather; 0
+    # when nobody was accused), "finalise" (dkg_shard_finalise_device + the share copies)
+    ms_steps: Dict[str, float] = field(default_factory=dict)
 
 
 class ShardedCeremony:
@@ -127,16 +132,22 @@ class ShardedCeremony:
 
     def _finish(self, ms: float, finalise: bool, d_s: Optional[int] = None) -> ShardResult:
         n, t, ws = self.n, self.t, self.ws
+        steps = {}
+        c0 = time.perf_counter()
         self.exchange()
         self._fence()
+        c1 = time.perf_counter()
+        steps["exchange"] = (c1 - c0) * 1e3
         o = self.be.shard_combine_device(n, t, ws, self.g_dec2.data_ptr(), self.g_dec4.data_ptr(),
                                          self.c_dec2.data_ptr(), self.c_dec4.data_ptr())
         dec = Decisions(self.c_dec2.view(n, n), self.c_dec4.view(n, n), np.array(o.qualified, dtype=np.uint8),
                         np.array(o.complaints2, dtype=np.int32), np.array(o.r2_error, dtype=np.uint8),
                         np.array(o.reconstruct, dtype=np.uint8), np.array(o.r4_error, dtype=np.uint8),
                         o.phase4_error)
+        c2 = time.perf_counter()
+        steps["combine"] = (c2 - c1) * 1e3
         if not finalise:
-            return ShardResult(dec, None, None, None, ms)
+            return ShardResult(dec, None, None, None, ms, steps)
         if dec.reconstruct.any() and not dec.phase4_error:
             # a dealer accused in round 4 (committee.rs:660-670) enters mpk as g * a_i0 over the final
             # parties' shares (:747-789): the owning rank replaces its term and the terms are gathered
@@ -145,7 +156,10 @@ class ShardedCeremony:
                                                 self.A0.data_ptr())
             self._all_gather(self.g_A0, self.A0)
             self._fence()
+        c3 = time.perf_counter()
+        steps["recon"] = (c3 - c2) * 1e3
         mpk = self.be.shard_finalise_device(n, t, ws, self.g_A0.data_ptr(), self.g_part.data_ptr(), dec.qualified,
                                             dec.phase4_error, self.fs.data_ptr(), self.pub.data_ptr())
         fs, pub = bytes(self.fs.cpu().numpy()), bytes(self.pub.cpu().numpy())
-        return ShardResult(dec, fs, pub, None if dec.phase4_error else mpk, ms)
+        steps["finalise"] = (time.perf_counter() - c3) * 1e3
+        return ShardResult(dec, fs, pub, None if dec.phase4_error else mpk, ms, steps)

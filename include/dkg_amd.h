@@ -63,29 +63,23 @@ int dkg_ctx_set_overlap(dkg_ctx *ctx, int on);
  * multiplications by j^L; 0 (default) picks U with the cost model dkg_split_model_ms; 1 disables.
  * Decisions and outputs do not depend on it. */
 int dkg_ctx_set_split(dkg_ctx *ctx, int pieces);
-/* How the stepping covers a split table whose pieces fit one 512-lane workgroup together:
- * 0 (default) by the cost model, 1 one workgroup slot per column holding all its pieces, 2 one
- * slot per piece.  Outputs do not depend on it. */
+/* How the stepping covers its tables: 0 (default) by the cost model; 1 one workgroup slot per
+ * column holding all its pieces (split tables whose pieces fit one 512-lane workgroup); 2 one slot
+ * per piece; 3 as 0 without the dead-position repack of short unsplit tables (DESIGN.md section 4:
+ * the last steps on halved segments once the top positions stop adding).  Outputs do not depend
+ * on it. */
 int dkg_ctx_set_stepping(dkg_ctx *ctx, int mode);
 /* Field multiplication of the verification kernels: 0 (default) per launch by occupancy, 1 always
  * product scanning (fewest issue slots), 2 always column sums (most independent chains; for
  * latency-bound launches).  Outputs do not depend on it. */
 int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
-/* Schedule of the binomial-basis Horner: 0 (default) -- one grid launch per
- * step, the steps with under one wave per SIMD with lane pairs (each point on two lanes sharing its
- * field products); 1 -- one launch per step, no lane pairs; 2..5 -- all t steps in ONE persistent
- * dataflow launch (each item waits only for the table positions of the previous step it reads or
- * overwrites; 1, 2, 4, 8 positions per item); 6 -- lane pairs for every step.  Outputs do not
- * depend on it. */
+/* Schedule of the binomial-basis Horner, one grid launch per step: 0
+ * (default) -- the steps with under one wave per SIMD with lane pairs (each point on two lanes
+ * sharing its field products), the steps of many rounds of waves in the mixed item order (the
+ * positions of a column group back to back on one XCD: the two reads of a table position meet in
+ * its L2); 1 -- no lane pairs; 2 -- lane pairs for every step; 3 -- as 0 without the mixed order;
+ * 4 -- the mixed order for every step without lane pairs.  Outputs do not depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
-/* Receiver parts of the stepping (opt-in schedule): the stepping runs in `parts` launches over
- * receiver ranges, and each part's recombination and checks run on a second stream beside the next
- * part's stepping, in place of the dealer-chunk streams.  0 / 1 (default) -- off, 2..8 -- that many
- * wherever usable (>= 2 streams, tables of <= 512 positions, short multipliers, fused rounds 2/4).
- * Measured slower than the default schedule.  Outputs do not depend on it;
- * dkg_ctx_last_receiver_parts reports what the last verification used. */
-int dkg_ctx_set_receiver_parts(dkg_ctx *ctx, int parts);
-int dkg_ctx_last_receiver_parts(const dkg_ctx *ctx);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and
  *                 compared with g s_ij + h s'_ij, as each receiver of the reference does;

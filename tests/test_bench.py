@@ -141,3 +141,13 @@ def test_cpu_baseline_small_batch():
     r = bench.cpu_baseline(16, 7, 1.0, ceremonies=10)
     assert r["value"] > 0 and r["kind"] == "port" and "whole ceremonies" in r["sample"]
     assert r["batch_s_extrapolated"] == pytest.approx(10 * r["ceremony_s_extrapolated"])
+
+
+def test_ref_equiv_w2_matches_survey():
+    """SURVEY.md 8(d)'s tabulated reference-equivalent work per verified share (dalek-3 cost model):
+    W2 = A 8,647 (t=4); B 19,663; C 58,831; D 200,961; E 625,085 Fp-mults; W4 = D 198,549, E 622,673."""
+    got = {t: bench.ref_equiv(2 * t + 1, t, 1.0) for t in (4, 31, 127, 511, 2047)}
+    assert [got[t]["W2_fp_mults_per_share"] for t in (4, 31, 127, 511, 2047)] == [8647, 19663, 58831, 200961, 625085]
+    assert got[511]["W4_fp_mults_per_share"] == 198549 and got[2047]["W4_fp_mults_per_share"] == 622673
+    r = bench.ref_equiv(1024, 511, 12.5e6)
+    assert r["ref_equiv_W2_fp_mults_per_s"] == pytest.approx(12.5e6 * 200961)

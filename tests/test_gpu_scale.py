@@ -499,56 +499,53 @@ def test_shard_ranks_n1024_all_match_single(be):
     assert o.reconstruct == [int(i in {dkg_amd.shard_range(n, ws, r)[0] + 2 for r in range(ws)}) for i in range(n)]
 
 
-@pytest.mark.parametrize("n,t,ws,rank", [(1024, 511, 8, 3), (512, 255, 4, 1)])
-def test_receiver_parts_match(be, n, t, ws, rank):
-    """The opt-in receiver-part schedule (dkg_ctx_set_receiver_parts) on a rank of the 8-way n=1024
-    split and of the 4-way n=512 split: the stepping in receiver ranges, each part's normalisation,
-    recombination and checks on a second stream beside the next part's stepping (the table carried
-    between parts in a double-buffered state).  With tampered dealers inside the rank and an identity
-    E row and A row (exceptional dedicated additions: the marked workgroups are redone per part from
-    that part's starting table), 2, 3, 4 and 8 parts give the same rows as the default schedule (0
-    and 1: unsplit), and the tampered dealers' rows equal the oracle's (committee.rs:287-305,
-    532-548)."""
-    n_, N = n, t + 1
+@pytest.mark.parametrize("n,t", [(64, 31), (100, 49), (41, 20)])
+def test_stepping_tail_repack_faults(be, n, t):
+    """The dead-position repack of short unsplit tables (kernels.hip stepping_tail_phases: the last
+    steps on halved segments, the live positions carried in a compact state) on tampered committees
+    with an identity E row and A row (exceptional dedicated additions: each phase's marked workgroups
+    are redone from that phase's starting state), alone and batched: the same decision matrices,
+    qualification and mpk as the plain stepping (dkg_ctx_set_stepping 3), and the tampered dealers'
+    rows equal the oracle's per-pair MSM checks (committee.rs:287-305, 532-548)."""
     h = be.env_init(t, n, CK)
-    ta, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([53]) * 32, 4)
-    del ta
-    d0, d1 = dkg_amd.shard_range(n, ws, rank)
-    E, A, s, sp = _tamper_rank(be, n, t, d0, tE, tA, ts, tsp, seed=300 + rank)
-    for d, tb in ((d0 + 7, tE), (d0 + 70, tA)):  # identity rows (committee.rs:1127 style)
-        tb[32 * N * d:32 * N * (d + 1)] = 0
-    outs = []
+    a, b = dkg_amd.dealer_coefficients(bytes([n]) * 32, 6, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
+    _inject(random.Random(n + 17), n, t, E, A, s, sp)
+    N = t + 1
+    for d, buf in ((7, E), (9, A)):  # identity rows (committee.rs:1127 style)
+        buf[32 * N * d:32 * N * (d + 1)] = bytes(32 * N)
+    out = []
     try:
-        for parts in (1, 2, 3, 4, 8):
-            be.set_receiver_parts(parts)
-            d2, d4 = _rank_rows(be, n, t, d0, d1, tE, tA, ts, tsp)
-            outs.append((d2.cpu().numpy().tobytes(), d4.cpu().numpy().tobytes(), be.last_receiver_parts(),
-                         be.stepping_redos()))
+        for mode in (3, 0):
+            be.set_stepping(mode)
+            r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            assert be.last_split() == 1
+            out.append((r.dec2, r.dec4, r.qualified, r.reconstruct, r.mpk, r.final_share, be.stepping_redos()))
+            B = 3  # the same committee three times in one batch: column offsets of later ceremonies
+            rb = dkg_amd.ceremony_batch_verify(be, B, n, t, bytes(E) * B, bytes(A) * B, bytes(s) * B,
+                                               bytes(sp) * B)
+            for c in range(B):
+                d = rb.ceremony(c)
+                assert bytes(d["dec2"]) == bytes(r.dec2) and bytes(d["dec4"]) == bytes(r.dec4), (mode, c)
     finally:
-        be.set_receiver_parts(0)
-    assert outs[0][2] == 1
-    for o, parts in zip(outs[1:], (2, 3, 4, 8)):
-        assert o[2] == parts, (parts, o[2])
-        assert o[0] == outs[0][0] and o[1] == outs[0][1], parts
-        assert o[3] > 0, parts
-    exp = _expected_rows(n_, t, h, E, A, s, sp, base=d0)
-    D = d1 - d0
-    r2 = [outs[0][0][i * n:(i + 1) * n] for i in range(D)]
-    r4 = [outs[0][1][i * n:(i + 1) * n] for i in range(D)]
+        be.set_stepping(0)
+    assert out[0] == out[1][:6] + (out[0][6],)
+    assert out[1][6] > 0  # the identity rows took the complete-formula redo in the repacked phases
+    exp = _expected_rows(n, t, h, E, A, s, sp)
+    d2, d4 = out[1][0], out[1][1]
     for i in range(5):
-        assert r2[i] == exp[(i, 2)] and r4[i] == exp[(i, 4)], i
-    assert r2[7].count(REJECT) == n - 1 and r4[70].count(REJECT) == n - 1
+        assert bytes(d2[i * n:(i + 1) * n]) == exp[(i, 2)], (i, "round 2")
+        assert bytes(d4[i * n:(i + 1) * n]) == exp[(i, 4)], (i, "round 4")
+    assert bytes(d2[7 * n:8 * n]).count(REJECT) == n - 1 and bytes(d4[9 * n:10 * n]).count(REJECT) == n - 1
 
 
 @pytest.mark.parametrize("n,t,split", [(1024, 511, 4), (1024, 511, 3), (1100, 549, 2), (300, 149, 1)])
-def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
-    """The dataflow binomial (k_binom_flow: all Horner steps in one persistent launch with
-    per-position dependency flags) and the lane-pair steps (k_binom_pair, every step or the
-    latency-bound ones) against one launch per step at the BASELINE size and on ragged
-    ones (n=1100 at U=2: a short last piece joining 90 steps late; n=300 unsplit: a padded column
-    group), with tampered dealers: identical decision matrices, qualification, reconstruction and mpk
-    -- and the same as the oracle on the tampered rows (test_faults_baseline_sizes checks the flow
-    schedule, the default, against the oracle)."""
+def test_binomial_schedules_match_at_scale(be, n, t, split):
+    """The binomial schedules (dkg_ctx_set_binomial: lane pairs for no / every / the latency-bound
+    steps, the mixed m-fastest XCD-grouped item order for every / no / the many-round steps) at the
+    BASELINE size and on ragged ones (n=1100 at U=2: a short last piece joining 90 steps late; n=300
+    unsplit: a padded column group), with tampered dealers: identical decision matrices,
+    qualification, reconstruction and mpk."""
     be.env_init(t, n, CK)
     a, b = dkg_amd.dealer_coefficients(bytes([split + 7]) * 32, 9, 0, n, t)
     E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
@@ -556,7 +553,7 @@ def test_binomial_flow_matches_steps_at_scale(be, n, t, split):
     out = []
     try:
         be.set_split(split)
-        for mode in (1, 2, 4, 5, 6, 0):  # per step; dataflow with K = 1, 4, 8; lane pairs all / auto (default)
+        for mode in (1, 2, 3, 4, 0):
             be.set_binomial(mode)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             assert be.last_split() == split

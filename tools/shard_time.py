@@ -24,11 +24,10 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--split", type=int, default=0, help="degree split (0: cost model)")
-    ap.add_argument("--stepping", type=int, default=0, help="stepping slots: 0 model, 1 per column, 2 per piece")
+    ap.add_argument("--stepping", type=int, default=0, help="stepping slots: 0 model, 1 per column, 2 per piece, 3 no dead-position repack")
     ap.add_argument("--field", type=int, default=0, help="field multiply: 0 by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--combine", type=int, default=0, help="recombination: 0 short multipliers (U <= 4), 1 powers of j^L")
-    ap.add_argument("--parts", type=int, default=0, help="receiver parts of the stepping (opt-in schedule): 0/1 off, 2..8")
-    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule: 0/1 one launch per step, 2..5 dataflow launch with 1, 2, 4, 8 positions per item, 0 with / 1 without lane pairs for latency-bound steps, 6 lane pairs for all")
+    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule (dkg_ctx_set_binomial): 0 default, 1 no lane pairs, 2 lane pairs for all steps, 3 no mixed order, 4 mixed order for all steps")
     args = ap.parse_args()
     import torch
 
@@ -44,7 +43,6 @@ def main():
     be.set_field_mode(args.field)
     be.set_combine(args.combine)
     be.set_binomial(args.binomial)
-    be.set_receiver_parts(args.parts)
     be.env_init(t, n)
     dev = torch.device("cuda", 0)
     res = {}
@@ -73,7 +71,7 @@ def main():
         print(json.dumps({"n": n, "t": t, "ws": ws, "dealers": D, "ms_wall": res[ws],
                           "overlap": not args.no_overlap, "streams": args.streams, "split": be.last_split(),
                           "split_len": be.last_split_len(), "stepping": args.stepping, "field": args.field, "combine": be.last_combine(),
-                          "binomial": args.binomial, "receiver_parts": be.last_receiver_parts(),
+                          "binomial": args.binomial,
                           "phases_ms_if_serialised": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     base = res.get(1)
     if base:
