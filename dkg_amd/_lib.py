@@ -148,7 +148,8 @@ def lib():
     L.dkg_scalar_sum_device.argtypes = [p, sz, sz, p, p, p]
     L.dkg_point_sum_device.argtypes = [p, sz, p, p, p]
     L.dkg_share_gen_device.argtypes = [p, sz, sz, sz, p, p, p, p, p, p]
-    L.dkg_ceremony_shard_recon_device.argtypes = [p, sz, sz, sz, sz, u8p, u8p, p, p]
+    L.dkg_ceremony_shard_recon_device.argtypes = [p, sz, sz, sz, sz, u8p, u8p, u8p, u8p, p, p,
+                                                  ctypes.POINTER(ctypes.c_int32)]
     L.dkg_finalise_parties.argtypes = [p, sz, sz, u8p, u8p, u8p, u8p, u8p, u8p, u8p, p, p, p]
     L.dkg_shard_range.argtypes = [sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.dkg_shard_range.restype = None

@@ -422,13 +422,19 @@ class Backend:
             vp(d_partial), ctypes.byref(ms)))
         return ms.value
 
-    def ceremony_shard_recon_device(self, n, t, d0, d1, qualified, reconstruct, d_s: Optional[int], d_terms: int):
+    def ceremony_shard_recon_device(self, n, t, d0, d1, qualified, reconstruct, d_s: Optional[int], d_terms: int,
+                                    r2_error=None, r4_error=None) -> bool:
         """After the exchange: replace the terms of this rank's reconstructed dealers by g * a_i0
-        interpolated over the final parties' shares (d_s None = the last shard call's rows)."""
+        interpolated over the disclosing final parties' shares (no r2 / r4 error; d_s None = the
+        last shard call's rows).  Returns True when fewer than t final parties disclose
+        (InsufficientSharesForRecovery for everyone: no mpk; the terms are untouched)."""
         vp = ctypes.c_void_p
+        opt = lambda m: None if m is None else bytes(bytearray(m))  # noqa: E731
+        fails = ctypes.c_int32(0)
         _check(self._ctx, _lib.lib().dkg_ceremony_shard_recon_device(
-            self._ctx, n, t, d0, d1, bytes(bytearray(qualified)), bytes(bytearray(reconstruct)), vp(d_s),
-            vp(d_terms)))
+            self._ctx, n, t, d0, d1, bytes(bytearray(qualified)), bytes(bytearray(reconstruct)), opt(r2_error),
+            opt(r4_error), vp(d_s), vp(d_terms), ctypes.byref(fails)))
+        return bool(fails.value)
 
     def finalise_parties(self, n: int, t: int, qualified, reconstruct, A0: bytes, s: bytes, r2_error=None,
                          r4_error=None, disclosed=None) -> "PartyFinalise":

@@ -147,14 +147,14 @@ DKG_DEV void glds_words(const dec_g_u32* sg, uint32_t* q) {
 
 __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const uint32_t* __restrict__ sk,
                                                       const uint32_t* __restrict__ R_ext, uint32_t* __restrict__ K_ext,
-                                                      uint32_t* __restrict__ T) {
+                                                      uint32_t* __restrict__ T, size_t q0) {
   __shared__ uint32_t qs[PT_WORDS * 64];
   __shared__ int16_t nzb[96];  // bits of the nonzero digits, top first
   __shared__ int8_t nzd[96];   // their digits
   __shared__ int8_t dig[288];  // the recoding (LDS: a private array would live in scratch)
   __shared__ int nnz_s;
   uint32_t* qcol = qs + threadIdx.x;
-  const size_t q = blockIdx.y, w = blockIdx.z;
+  const size_t q = q0 + blockIdx.y, w = blockIdx.z;
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   const bool live = i < D;
   const size_t count = 2 * D * n;
@@ -255,13 +255,27 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const 
 }
 #endif
 
+// The width-4 window's odd multiples live in a global table of one 40-KB slot per wave of a launch
+// (T, indexed by the wave's place in its grid).  Launches are capped at DEC_TAB_WAVES waves -- four
+// rounds of a full chip's resident waves -- and cover the recipients in slices, back to back on the
+// stream, so the table never exceeds DEC_TAB_WAVES slots (655 MB) whatever n is (n = 4096: 32
+// launches instead of one grid of 524,288 waves and a 21-GB table).
+constexpr size_t DEC_TAB_WAVES = 16384;
+
+size_t dec_mul_recipients_per_launch(size_t D, size_t n) {
+  const size_t per_q = ((D + 63) / 64) * 2;
+  return std::max<size_t>(1, std::min(n, DEC_TAB_WAVES / per_q));
+}
+
 void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint32_t* K_ext, hipStream_t stream,
              uint32_t* table) {
   if (!D || !n) return;
 #ifndef DKG_DEC_NAF
   if (table) {
-    hipLaunchKernelGGL(k_dec_mul_w4, dim3((unsigned)((D + 63) / 64), (unsigned)n, 2u), dim3(64), 0, stream, D, n, sk,
-                       R_ext, K_ext, table);
+    const size_t qc = dec_mul_recipients_per_launch(D, n);
+    for (size_t q0 = 0; q0 < n; q0 += qc)
+      hipLaunchKernelGGL(k_dec_mul_w4, dim3((unsigned)((D + 63) / 64), (unsigned)std::min(qc, n - q0), 2u), dim3(64),
+                         0, stream, D, n, sk, R_ext, K_ext, table, q0);
     return;
   }
 #endif
@@ -272,7 +286,7 @@ void dec_mul(size_t D, size_t n, const uint32_t* sk, const uint32_t* R_ext, uint
 
 size_t dec_mul_table_words(size_t D, size_t n) {
 #ifndef DKG_DEC_NAF
-  return ((D + 63) / 64) * n * 2 * 4 * PT_WORDS * 64;
+  return ((D + 63) / 64) * dec_mul_recipients_per_launch(D, n) * 2 * 4 * PT_WORDS * 64;
 #else
   (void)D;
   (void)n;

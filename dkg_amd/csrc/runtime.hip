@@ -910,12 +910,33 @@ std::vector<uint8_t> final_parties(size_t n, const uint8_t* qualified, const uin
   return f;
 }
 
+// The final parties whose phase-5 disclosures reach the others: a party whose Phase1 or Phase3
+// proceed failed (r2 / r4 error, committee.rs:340-347, 567-569) never reaches Phases<Phase4>::proceed
+// and never broadcasts a BroadcastPhase5 (:684); it does not finalise either.  r2err / r4err may be
+// null (no errors).
+std::vector<uint8_t> disclosing_parties(size_t n, const uint8_t* qualified, const uint8_t* recon, const uint8_t* r2err,
+                                        const uint8_t* r4err) {
+  std::vector<uint8_t> f = final_parties(n, qualified, recon);
+  for (size_t j = 0; j < n; j++) f[j] = f[j] && !(r2err && r2err[j]) && !(r4err && r4err[j]);
+  return f;
+}
+
+// With reconstructed dealers, every finalising party holds its own share plus the other disclosing
+// final parties' -- exactly the disclosing set S -- and fails with InsufficientSharesForRecovery when
+// that is fewer than `threshold` = t points (:779-781): then no party has an mpk.
+bool recovery_fails(const std::vector<uint8_t>& S, size_t t) {
+  size_t c = 0;
+  for (auto v : S) c += v != 0;
+  return c < t;
+}
+
 // Secrets of the reconstructed dealers (rows `rows` of hs, share row r at hs + 32 * n * r) as the
-// final parties recover them in finalise: a final party p interpolates dealer i's shares at its own
-// index and at every other final party's (committee.rs:754-788), i.e. at exactly the final set, so
-// every final party computes this same value (when all of their phase-5 disclosures arrive; the
-// per-party view with missing disclosures is dkg_finalise_parties).  The dealer's share to itself
-// is never used (it is not a final party), and its other shares all passed round 2.
+// finalising parties recover them: a final party p interpolates dealer i's shares at its own index
+// and at every other disclosing final party's (committee.rs:754-788), i.e. at exactly the disclosing
+// set `fin` (disclosing_parties), so every finalising party computes this same value (with exactly t
+// points a wrong one, as the reference does; the per-party view with missing disclosures is
+// dkg_finalise_parties).  The dealer's share to itself is never used (it is not a final party), and
+// its other shares all passed round 2.
 std::vector<uint8_t> recon_secrets(size_t n, const std::vector<uint8_t>& fin, const uint8_t* hs,
                                    const std::vector<size_t>& rows) {
   const std::vector<dkgh::Zl> lam = lagrange_zero_coeffs(n, fin.data());
@@ -1005,6 +1026,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
   std::vector<uint8_t> honest_mask = final_parties(n, qualified.data(), recon.data());
+  const std::vector<uint8_t> disc = disclosing_parties(n, qualified.data(), recon.data(), r2err.data(), r4e.data());
   size_t nrecon = 0;
   int32_t nq = 0;
   for (size_t i = 0; i < n; i++) {
@@ -1015,7 +1037,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   // (committee.rs:673-677): nobody finalises, so there is no master public key (mpk zeroed)
   const bool phase4_error = nq - (int32_t)nrecon <= (int32_t)t;
   memset(out->mpk, 0, 32);
-  if (!phase4_error) {
+  if (!phase4_error && !(nrecon && recovery_fails(disc, t))) {
     uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
     if (ctx->ext_A) {
       dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, n, A0, n, ctx->stream);
@@ -1038,7 +1060,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
           rows.push_back(rows.size());
         }
       sync(ctx);
-      std::vector<uint8_t> secrets = recon_secrets(n, honest_mask, hs.data(), rows);
+      std::vector<uint8_t> secrets = recon_secrets(n, disc, hs.data(), rows);
       uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
       h2d(ctx, sec, secrets.data(), secrets.size());
       uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
@@ -1149,10 +1171,10 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   verify_rounds(ctx, n, t, V, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3);
   // round-4 outcome: a qualified dealer rejected by someone is reconstructed (committee.rs:660-670),
   // disqualified dealers' rows SKIPPED (:522)
-  std::vector<uint8_t> r4e(out->r4_error ? V : 0);
-  round4_outcome(ctx, B, n, t, dec4, qmask, qualified.data(), recon.data(), out->r4_error ? r4e.data() : nullptr);
+  std::vector<uint8_t> r4e(V);
+  round4_outcome(ctx, B, n, t, dec4, qmask, qualified.data(), recon.data(), r4e.data());
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
-  std::vector<size_t> recon_cer;
+  std::vector<size_t> recon_cer, nompk;
   std::vector<uint8_t> p4err(B, 0);
   for (size_t c = 0; c < B; c++) {
     bool any = false;
@@ -1163,7 +1185,13 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
       h += honest[i];
     }
     p4err[c] = h <= (int32_t)t;  // committee.rs:673-677: nobody finalises, no mpk
-    if (any && !p4err[c]) recon_cer.push_back(c);
+    if (any && !p4err[c]) {
+      // InsufficientSharesForRecovery for every finalising party: no mpk either (recovery_fails)
+      if (recovery_fails(disclosing_parties(n, &qualified[c * n], &recon[c * n], &r2err[c * n], &r4e[c * n]), t))
+        nompk.push_back(c);
+      else
+        recon_cer.push_back(c);
+    }
   }
   // finalise (committee.rs:726-805): mpk_c = sum of honest A_i0 (+ g * reconstructed secrets)
   uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
@@ -1188,8 +1216,8 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
       std::vector<size_t> rows;
       for (size_t i = 0; i < n; i++)
         if (recon[c * n + i]) rows.push_back(i);
-      std::vector<uint8_t> secrets = recon_secrets(n, std::vector<uint8_t>(&honest[c * n], &honest[(c + 1) * n]),
-                                                   hs.data(), rows);
+      std::vector<uint8_t> secrets = recon_secrets(
+          n, disclosing_parties(n, &qualified[c * n], &recon[c * n], &r2err[c * n], &r4e[c * n]), hs.data(), rows);
       const size_t nr = secrets.size() / 32;
       uint32_t* sec = buf<uint32_t>(ctx, "b.recon_sec", 32 * nr);
       h2d(ctx, sec, secrets.data(), secrets.size());
@@ -1216,9 +1244,11 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   if (out->complaints2) memcpy(out->complaints2, complaints.data(), 4 * V);
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), V);
   if (out->phase4_error) memcpy(out->phase4_error, p4err.data(), B);  // committee.rs:673-677
-  if (out->mpk)
+  if (out->mpk) {
     for (size_t c = 0; c < B; c++)
       if (p4err[c]) memset(out->mpk + 32 * c, 0, 32);  // no party finalises: no master key
+    for (size_t c : nompk) memset(out->mpk + 32 * c, 0, 32);  // no party recovers the secrets
+  }
   if (out->n_qualified)
     for (size_t c = 0; c < B; c++) {
       int32_t q = 0;
@@ -2017,10 +2047,18 @@ int dkg_ceremony_shard_verify_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0
 }
 
 int dkg_ceremony_shard_recon_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t d1, const uint8_t* qualified,
-                                    const uint8_t* reconstruct, const void* d_s, void* d_terms) {
+                                    const uint8_t* reconstruct, const uint8_t* r2_error, const uint8_t* r4_error,
+                                    const void* d_s, void* d_terms, int32_t* recovery_error) {
   return guarded(ctx, [&] {
     if (!qualified || !reconstruct || !d_terms || d1 < d0 || d1 > n || dkg_env_check(t, n) != DKG_OK) return DKG_E_ARG;
     const size_t D = d1 - d0;
+    // decided from the common outcome alone: the same on every rank, whichever dealers it holds
+    const std::vector<uint8_t> disc = disclosing_parties(n, qualified, reconstruct, r2_error, r4_error);
+    bool any = false;
+    for (size_t i = 0; i < n; i++) any |= reconstruct[i] != 0;
+    const bool fails = any && recovery_fails(disc, t);
+    if (recovery_error) *recovery_error = fails ? 1 : 0;
+    if (fails) return DKG_OK;  // nobody recovers: the caller zeroes the mpk
     std::vector<size_t> rows;
     for (size_t i = 0; i < D; i++) {
       if (reconstruct[d0 + i] && !qualified[d0 + i]) {
@@ -2048,7 +2086,7 @@ int dkg_ceremony_shard_recon_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0,
     sync(ctx);
     std::vector<size_t> idx(R);
     for (size_t r = 0; r < R; r++) idx[r] = r;
-    std::vector<uint8_t> secrets = recon_secrets(n, final_parties(n, qualified, reconstruct), hs.data(), idx);
+    std::vector<uint8_t> secrets = recon_secrets(n, disc, hs.data(), idx);
     uint32_t* sec = buf<uint32_t>(ctx, "sh_rsec", 32 * R);
     uint32_t* gsec = buf<uint32_t>(ctx, "sh_rext", PTB * R);
     uint32_t* gc = buf<uint32_t>(ctx, "sh_rcomp", 32 * R);

@@ -148,18 +148,21 @@ class ShardedCeremony:
         steps["combine"] = (c2 - c1) * 1e3
         if not finalise:
             return ShardResult(dec, None, None, None, ms, steps)
+        no_mpk = dec.phase4_error
         if dec.reconstruct.any() and not dec.phase4_error:
-            # a dealer accused in round 4 (committee.rs:660-670) enters mpk as g * a_i0 over the final
-            # parties' shares (:747-789): the owning rank replaces its term and the terms are gathered
-            # again (the interpolation points depend on every rank's rows)
-            self.be.ceremony_shard_recon_device(n, t, self.d0, self.d1, dec.qualified, dec.reconstruct, d_s,
-                                                self.A0.data_ptr())
-            self._all_gather(self.g_A0, self.A0)
-            self._fence()
+            # a dealer accused in round 4 (committee.rs:660-670) enters mpk as g * a_i0 over the
+            # disclosing final parties' shares (:747-789): the owning rank replaces its term and the
+            # terms are gathered again (the interpolation points depend on every rank's rows).  Fewer
+            # than t disclosing parties: nobody recovers (:779-781), the same verdict on every rank.
+            no_mpk = self.be.ceremony_shard_recon_device(n, t, self.d0, self.d1, dec.qualified, dec.reconstruct, d_s,
+                                                         self.A0.data_ptr(), dec.r2_error, dec.r4_error)
+            if not no_mpk:
+                self._all_gather(self.g_A0, self.A0)
+                self._fence()
         c3 = time.perf_counter()
         steps["recon"] = (c3 - c2) * 1e3
         mpk = self.be.shard_finalise_device(n, t, ws, self.g_A0.data_ptr(), self.g_part.data_ptr(), dec.qualified,
-                                            dec.phase4_error, self.fs.data_ptr(), self.pub.data_ptr())
+                                            no_mpk, self.fs.data_ptr(), self.pub.data_ptr())
         fs, pub = bytes(self.fs.cpu().numpy()), bytes(self.pub.cpu().numpy())
         steps["finalise"] = (time.perf_counter() - c3) * 1e3
-        return ShardResult(dec, fs, pub, None if dec.phase4_error else mpk, ms, steps)
+        return ShardResult(dec, fs, pub, None if no_mpk else mpk, ms, steps)

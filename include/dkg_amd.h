@@ -196,11 +196,16 @@ typedef struct {
   uint8_t *reconstruct;         /* [n] dealers whose secret is reconstructed in finalise */
   uint8_t *final_share;         /* [n][32] s_j = sum_{i in Q} s_ij (committee.rs:454-462) */
   uint8_t *public_share;        /* [n][32] g * s_j (committee.rs:464-466) */
-  uint8_t mpk[32];              /* MasterPublicKey (committee.rs:726-805) that every final party
-                                   (qualified, not reconstructable) computes when all final parties'
-                                   phase-5 disclosures arrive: a reconstructed dealer's secret is
-                                   interpolated at zero over exactly the final parties' shares
-                                   (:754-788).  ALL ZERO and meaningless when phase4_error == 1.
+  uint8_t mpk[32];              /* MasterPublicKey (committee.rs:726-805) that every finalising
+                                   final party (qualified, not reconstructable, no r2 / r4 error)
+                                   computes when all phase-5 disclosures arrive: a reconstructed
+                                   dealer's secret is interpolated at zero over exactly the shares of
+                                   the final parties that disclose (:754-788) -- a party with an r2 /
+                                   r4 error never broadcasts its phase-5 shares (:340-347, 567-569,
+                                   684); with exactly t of them a wrong secret, as the reference.
+                                   ALL ZERO and meaningless when phase4_error == 1, and when a
+                                   dealer is reconstructed and fewer than t final parties disclose
+                                   (InsufficientSharesForRecovery for everyone, :779-781).
                                    Other parties' views, and missing disclosures:
                                    dkg_finalise_parties. */
   int32_t n_qualified;
@@ -255,12 +260,19 @@ int dkg_ceremony_shard_verify_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0
 /* Finalise step of a sharded run, after the exchange (committee.rs:747-789): for this rank's dealers
  * [d0, d1) with reconstruct[i] (host [n], the combined round-4 outcome), d_terms[i - d0] (device
  * [d1-d0][32], the rank's exchanged master-key terms, in/out) is replaced by g * a_i0 recovered by
- * Lagrange interpolation at zero over the shares of the final parties (qualified[j] && !reconstruct[j],
- * host [n]) -- the value every final party computes.  d_s: the dealers' share rows [d1-d0][n][32]
- * (from_bits semantics), or NULL for the rows of the last dkg_ceremony_shard_device /
- * _shard_verify_device call on this ctx (same n, d0, d1).  Dealers without reconstruct are untouched. */
+ * Lagrange interpolation at zero over the shares of the DISCLOSING final parties: qualified[j] &&
+ * !reconstruct[j] && !r2_error[j] && !r4_error[j] (host [n]; r2_error / r4_error may be NULL) -- a
+ * party whose Phase1 or Phase3 failed never broadcasts its phase-5 disclosures (:340-347, 567-569,
+ * 684) -- the value every finalising party computes.  When some dealer is reconstructed and fewer
+ * than t parties disclose, every finalising party fails with InsufficientSharesForRecovery
+ * (:779-781): *recovery_error (may be NULL) = 1, d_terms is untouched and the caller has no mpk
+ * (pass it as phase4_error to dkg_shard_finalise_device); else 0.  It depends on the common outcome
+ * only, so every rank gets the same.  d_s: the dealers' share rows [d1-d0][n][32] (from_bits
+ * semantics), or NULL for the rows of the last dkg_ceremony_shard_device / _shard_verify_device call
+ * on this ctx (same n, d0, d1).  Dealers without reconstruct are untouched. */
 int dkg_ceremony_shard_recon_device(dkg_ctx *ctx, size_t n, size_t t, size_t d0, size_t d1, const uint8_t *qualified,
-                                    const uint8_t *reconstruct, const void *d_s, void *d_terms);
+                                    const uint8_t *reconstruct, const uint8_t *r2_error, const uint8_t *r4_error,
+                                    const void *d_s, void *d_terms, int32_t *recovery_error);
 /* Combine step of the sharded run (device pointers):
  * round-3 sum (committee.rs:454-462): out[j] = sum over rows r with mask[r] (NULL = all) of in[r][j]
  * mod l; in [rows][n][32] canonical scalars (e.g. the all-gathered per-rank partials), out [n][32]. */
@@ -276,7 +288,7 @@ int dkg_point_sum_device(dkg_ctx *ctx, size_t count, const void *d_points, const
  *   all-gather dec2, dec4 (each rank's [R][n] block), A0 ([R][32]), partials ([n][32])
  *   dkg_shard_combine_device                           the common outcome (identical on every rank)
  *   if reconstruct has any member and !phase4_error:
- *     dkg_ceremony_shard_recon_device, all-gather the terms again
+ *     dkg_ceremony_shard_recon_device, all-gather the terms again (unless recovery_error)
  *   dkg_shard_finalise_device                          final shares, public shares, mpk
  * Rank r of world_size owns dealers [r*n/ws, (r+1)*n/ws); R = dkg_shard_rows(n, ws) is the padded
  * block height every rank gathers. */

@@ -24,7 +24,8 @@ from dkg_amd.distributed import ShardedCeremony, dealer_range  # noqa: E402
 
 HONEST = ["ceremony_n16_t7.json", "ceremony_n64_t31.json"]
 FAULTS = ["fault_a_generator_n10_t4.json", "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json",
-          "fault_a_many_n10_t4.json", "fault_share_flip_n10_t4.json"]
+          "fault_a_many_n10_t4.json", "fault_share_flip_n10_t4.json", "fault_recon_r2err_n16_t3.json",
+          "fault_recon_insufficient_n16_t3.json"]
 H = bytes.fromhex
 
 

@@ -75,10 +75,16 @@ def party_finalise(p, n, t, qualified, recon, A0, share, own_A0=None, disclosed=
     return "OK", -1, gsum(terms + [g_mul(secret)])
 
 
-def final_party_mpk(n, qualified, recon, A0, share):
-    """The master public key every final party computes when all disclosures arrive: the
-    reconstructed secrets are interpolated over exactly the final set."""
+def final_party_mpk(n, qualified, recon, A0, share, r2_error=None, r4_error=None, t=None):
+    """The master public key every finalising final party computes when all disclosures arrive: the
+    reconstructed secrets are interpolated over the final parties that disclose -- a party whose
+    Phase1 or Phase3 proceed failed (r2 / r4 error, committee.rs:340-347, 567-569, 684) never
+    broadcasts its phase-5 shares.  None when those are fewer than t (InsufficientSharesForRecovery
+    for every finalising party, :779-781; t must be given then)."""
     final = [q and not r for q, r in zip(qualified, recon)]
-    xs = [j + 1 for j in range(n) if final[j]]
+    err = [bool((r2_error and r2_error[j]) or (r4_error and r4_error[j])) for j in range(n)]
+    xs = [j + 1 for j in range(n) if final[j] and not err[j]]
+    if any(recon) and t is not None and len(xs) < t:
+        return None
     secret = sum(lagrange_at_zero([share(i, x - 1) for x in xs], xs) for i in range(n) if recon[i]) % L
     return gsum([A0[i] for i in range(n) if final[i]] + [g_mul(secret)])

@@ -48,16 +48,18 @@ def play(be, n, t, ws, shard_call, dev):
     c2 = torch.empty(n * n, **u8)
     c4 = torch.empty(n * n, **u8)
     o = be.shard_combine_device(n, t, ws, g2.data_ptr(), g4.data_ptr(), c2.data_ptr(), c4.data_ptr())
+    no_mpk = o.phase4_error
     if any(o.reconstruct) and not o.phase4_error:
         for r in range(ws):
             d0, d1 = dkg_amd.shard_range(n, ws, r)
             if d1 > d0:
                 s = shares[r]
-                be.ceremony_shard_recon_device(n, t, d0, d1, o.qualified, o.reconstruct,
-                                               None if s is None else s.data_ptr(), gA[r * R * 32:].data_ptr())
+                no_mpk = be.ceremony_shard_recon_device(n, t, d0, d1, o.qualified, o.reconstruct,
+                                                        None if s is None else s.data_ptr(), gA[r * R * 32:].data_ptr(),
+                                                        o.r2_error, o.r4_error)
     fs = torch.empty(n * 32, **u8)
     pub = torch.empty(n * 32, **u8)
-    mpk = be.shard_finalise_device(n, t, ws, gA.data_ptr(), gp.data_ptr(), o.qualified, o.phase4_error, fs.data_ptr(),
+    mpk = be.shard_finalise_device(n, t, ws, gA.data_ptr(), gp.data_ptr(), o.qualified, no_mpk, fs.data_ptr(),
                                    pub.data_ptr())
     return Played(bytes(c2.cpu().numpy()), bytes(c4.cpu().numpy()), b"".join(rd4), o, bytes(fs.cpu().numpy()),
                   bytes(pub.cpu().numpy()), mpk, rd2, rd4)

@@ -183,16 +183,23 @@ class OracleBackend:
         self._shares = (d0, d1, self._rd(ds, 32 * n * D) if D else b"")
         return 0.0
 
-    def ceremony_shard_recon_device(self, n, t, d0, d1, qualified, reconstruct, d_s, d_terms):
+    def ceremony_shard_recon_device(self, n, t, d0, d1, qualified, reconstruct, d_s, d_terms, r2_error=None,
+                                    r4_error=None):
         from tests import finalise_ref as FR
         s = self._rd(d_s, 32 * n * (d1 - d0))
-        final = [int(q and not r) for q, r in zip(qualified, reconstruct)]
+        # the disclosing final parties (no r2 / r4 error: committee.rs:340-347, 567-569, 684)
+        final = [int(q and not r and not (r2_error is not None and r2_error[j]) and
+                     not (r4_error is not None and r4_error[j]))
+                 for j, (q, r) in enumerate(zip(qualified, reconstruct))]
         xs = [j + 1 for j in range(n) if final[j]]
+        if any(reconstruct) and len(xs) < t:
+            return True  # InsufficientSharesForRecovery for everyone (:779-781)
         for i in range(d0, d1):
             if reconstruct[i]:
                 row = s[32 * n * (i - d0):32 * n * (i - d0 + 1)]
                 ys = [int.from_bytes(row[32 * (x - 1):32 * x], "little") for x in xs]
                 self._wr(d_terms + 32 * (i - d0), FR.g_mul(FR.lagrange_at_zero(ys, xs)))
+        return False
 
     def shard_combine_device(self, n, t, ws, d_dec2_g, d_dec4_g, d_dec2=None, d_dec4=None):
         from dkg_amd.api import ShardOutcome
@@ -249,7 +256,7 @@ def _run_verify_main(rank, ws, port, names, errq):
             assert d.qualified.tolist() == c["qualified"] and d.reconstruct.tolist() == c["reconstruct"], name
             assert res.final_share.hex() == c["final_share"], name
             assert res.public_share.hex() == c["public_share"], name
-            if c["phase4_error"]:
+            if c["phase4_error"] or c["mpk"] == "00" * 32:
                 assert res.mpk is None, name
             else:
                 assert res.mpk.hex() == c["mpk"], name
@@ -264,12 +271,14 @@ def _run_verify_main(rank, ws, port, names, errq):
 def test_sharded_run_verify_gloo(ws):
     """ShardedCeremony.run_verify end to end over gloo with the oracle standing in for the GPU:
     the reconstruction exchange of dealers accused in round 4 (fault_a_generator, fault_self_share
-    with a tampered self-share, fault_recon_only) and the Phase4 failure (fault_a_many: no mpk)."""
+    with a tampered self-share, fault_recon_only; final parties with round-2 errors that never
+    disclose, leaving t points and then fewer -- no mpk) and the Phase4 failure (fault_a_many: no mpk)."""
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
     names = ["fault_a_generator_n10_t4.json", "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json",
-             "fault_a_many_n10_t4.json", "ceremony_n11_t5.json"]
+             "fault_a_many_n10_t4.json", "ceremony_n11_t5.json", "fault_recon_r2err_n16_t3.json",
+             "fault_recon_insufficient_n16_t3.json"]
     procs = [ctx.Process(target=_run_verify_main, args=(r, ws, port, names, errq)) for r in range(ws)]
     for p in procs:
         p.start()

@@ -105,7 +105,8 @@ CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.jso
               "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
 FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
           "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json",
-          "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json"]
+          "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json", "fault_recon_r2err_n16_t3.json",
+          "fault_recon_insufficient_n16_t3.json"]
 
 
 @pytest.mark.parametrize("name", CEREMONIES)
@@ -477,7 +478,7 @@ def _check_batch_member(c, d, n):
 def test_batch_verify_goldens(be, golden, overlap):
     """BASELINE config 5 path: five n=10, t=4 ceremonies (one honest, four with the fault injections
     of committee.rs:1105-1313) verified as ONE batch give each golden ceremony's outputs bit for bit."""
-    names = ["ceremony_n10_t4.json"] + FAULTS
+    names = ["ceremony_n10_t4.json"] + [x for x in FAULTS if "_n10_t4" in x]
     cs = [golden(x) for x in names]
     n, t = 10, 4
     assert all((c["n"], c["t"]) == (n, t) for c in cs)
@@ -493,6 +494,21 @@ def test_batch_verify_goldens(be, golden, overlap):
         be.set_overlap(True)
     for k, c in enumerate(cs):
         _check_batch_member(c, r.ceremony(k), n)
+
+
+def test_batch_verify_disclosure_goldens(be, golden):
+    """Final parties with round-2 errors never disclose in phase 5 (committee.rs:340-347, 684): a batch
+    of the n=16, t=3 fixtures in which they leave exactly t disclosures (a wrong recovered secret, as
+    the reference) and fewer (no mpk) -- each member equals its golden ceremony bit for bit."""
+    names = ["fault_recon_r2err_n16_t3.json", "fault_recon_insufficient_n16_t3.json", "fault_recon_r2err_n16_t3.json"]
+    cs = [golden(x) for x in names]
+    n, t = 16, 3
+    be.env_init(t, n, CK)
+    r = dkg_amd.ceremony_batch_verify(be, len(cs), n, t, *(b"".join(H(c[k]) for c in cs)
+                                                          for k in ("E", "A", "s", "s_prime")))
+    for k, c in enumerate(cs):
+        _check_batch_member(c, r.ceremony(k), n)
+    assert r.mpk[1] == bytes(32) and r.mpk[0] == r.mpk[2] != bytes(32)
 
 
 def test_batch_device_matches_single(be, golden):
@@ -684,6 +700,29 @@ def test_full_mode_oracle_random(be):
     wrong = b"".join(sks[1:] + sks[:1])
     ds2, _, _ = be.decrypt_shares(wrong, e1, ct, D, n)
     assert ds2 != s
+
+
+def test_full_mode_decryption_slices(be):
+    """The width-4 decryption runs in recipient slices of at most 16,384 waves (one 40-KB odd-multiple
+    table slot per wave of a launch, reused by the next slice): at D=1100, n=512 that is two launches
+    (455 + 57 recipients).  Every one of the 1.1 M items decrypts to its plaintext, and a sample of
+    ciphertexts equals the CPU oracle's (elgamal.rs:134-193)."""
+    rng = random.Random(12)
+    D, n = 1100, 512
+    sks = [rng.randrange(1, L).to_bytes(32, "little") for _ in range(n)]
+    pks = be.fixed_base_batch(b"".join(sks))
+    s = b"".join(rng.randrange(L).to_bytes(32, "little") for _ in range(D * n))
+    sp = b"".join(rng.randrange(L).to_bytes(32, "little") for _ in range(D * n))
+    r = b"".join(rng.randrange(L).to_bytes(32, "little") for _ in range(2 * D * n))
+    e1, ct = be.encrypt_shares(pks, s, sp, r, D, n)
+    for i, q, w in [(0, 0, 0), (D - 1, n - 1, 1), (700, 455, 1), (3, 454, 0)] + \
+            [(rng.randrange(D), rng.randrange(n), rng.randrange(2)) for _ in range(4)]:
+        k = 2 * (i * n + q) + w
+        msg = (sp, s)[w][32 * (i * n + q):32 * (i * n + q) + 32]
+        assert O.hybrid_encrypt(pks[32 * q:32 * q + 32], r[32 * k:32 * k + 32], msg) == \
+            (e1[32 * k:32 * k + 32], ct[32 * k:32 * k + 32]), (i, q, w)
+    ds, dsp, ok = be.decrypt_shares(b"".join(sks), e1, ct, D, n)
+    assert ds == s and dsp == sp and set(ok) == {1}
 
 
 def test_complaint_proofs_device(be, golden):

@@ -109,7 +109,8 @@ CEREMONIES = ["ceremony_n2_t0.json", "ceremony_n3_t1.json", "ceremony_n10_t4.jso
               "ceremony_n11_t5.json", "ceremony_n16_t7.json"]
 FAULTS = ["fault_e_identity_n10_t4.json", "fault_share_flip_n10_t4.json",
           "fault_a_generator_n10_t4.json", "fault_over_threshold_n10_t4.json", "fault_a_many_n10_t4.json",
-          "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json"]
+          "fault_self_share_n10_t4.json", "fault_recon_only_n10_t4.json", "fault_recon_r2err_n16_t3.json",
+          "fault_recon_insufficient_n16_t3.json"]
 
 
 @pytest.mark.parametrize("name", CEREMONIES)
@@ -280,7 +281,9 @@ def test_ceremony_mpk_rule(golden, name):
     if c["phase4_error"]:
         assert c["mpk"] == "00" * 32
     else:
-        assert final_party_mpk(n, c["qualified"], c["reconstruct"], A0, share).hex() == c["mpk"]
+        mpk = final_party_mpk(n, c["qualified"], c["reconstruct"], A0, share,
+                              [int(x) for x in c["r2_error"]], [int(x) for x in c["r4_error"]], t)
+        assert (mpk or bytes(32)).hex() == c["mpk"]
 
 
 @pytest.mark.parametrize("name", ["finalise_parties_n10_t4.json", "finalise_parties_recon_n10_t4.json"])

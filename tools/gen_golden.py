@@ -226,21 +226,31 @@ def ceremony(n, t, master, ceremony_id=0, faults=None, with_coeffs=True, transpo
     phase4_error = sum(qualified) - sum(recon) <= t
     final = [int(qualified[i] and not recon[i]) for i in range(n)]              # :733-739
     mpk = None
-    if not phase4_error:  # else nobody finalises: there is no master public key
+    # the disclosures a finalising final party holds: its own share plus the phase-5 broadcasts of
+    # the other final parties -- which only parties that reached Phases<Phase4>::proceed send: a party
+    # whose Phase1 or Phase3 proceed failed (r2 / r4 error, :340-347, 567-569, 684) never does, and
+    # does not finalise itself.  So every finalising party interpolates over exactly `disc`.
+    disc = [j for j in range(n) if final[j] and not r2_error[j] and not r4_error[j]]
+    if not phase4_error and any(recon) and len(disc) < t:
+        phase4_error_mpk = True  # InsufficientSharesForRecovery(i) for every finalising party (:779-781)
+    else:
+        phase4_error_mpk = phase4_error
+    if not phase4_error_mpk:  # else nobody finalises: there is no master public key
         mpk = ID
+        exact = True
         for i in range(n):
             if recon[i]:
-                # what every final party computes: its own share plus the other final parties'
-                # disclosures, i.e. exactly the final set (:754-775); the dealer's own s_ii is unused
-                xs = [j + 1 for j in range(n) if final[j]]
+                xs = [j + 1 for j in disc]
                 ys = [Sw[i][x - 1] for x in xs]
                 secret = lagrange_at_zero(ys, xs)                                 # :784-788
-                assert secret == A[i][0]
+                # t points (fewer than t+1) interpolate a wrong secret, as the reference computes it
+                exact &= len(xs) >= t + 1
+                assert secret == A[i][0] or len(xs) < t + 1
                 mpk = gadd(mpk, gmul_base(secret))                                # :789
             elif qualified[i]:
                 mpk = gadd(mpk, Aw[i][0])                                         # :790-795
         # property of the honest run (committee.rs:1633-1647): mpk == g * sum of qualified secrets
-        assert mpk == gmul_base(sum(A[i][0] for i in range(n) if qualified[i]))
+        assert mpk == gmul_base(sum(A[i][0] for i in range(n) if qualified[i])) or not exact
     out = {
         "n": n, "t": t, "ceremony": ceremony_id, "master_seed": hx(master), "ck_bytes": hx(CK_BYTES),
         "h": hx(h), "faults": faults,
@@ -771,7 +781,18 @@ def main():
         {"name": "r2 and r4 errors leave t-1 points",
          "r2_error": [1 if j in (0, 1) else 0 for j in range(n10)],
          "r4_error": [1 if j in (3, 4, 5) else 0 for j in range(n10)]}])}
+    # final parties with round-2 errors never disclose in phase 5 (committee.rs:340-347, 684): dealers
+    # 1-4 send bad shares to 8 (then 9) receivers, who raise more than t complaints; dealer 16's
+    # round-3 commitments are wrong, so it is reconstructed from the remaining final parties'
+    # disclosures -- exactly t of them (a wrong secret, as the reference computes it), then t-1
+    # (InsufficientSharesForRecovery for every finalising party: no mpk)
+    for name, last in (("fault_recon_r2err_n16_t3.json", 12), ("fault_recon_insufficient_n16_t3.json", 13)):
+        files[name] = ceremony(16, 3, m, ceremony_id=8, faults=[
+            {"kind": "share_flip", "dealer": d, "receiver": j} for d in range(1, 5) for j in range(5, last + 1)] + [
+            {"kind": "A_generator", "dealer": 16}])
     files["spot_n4096_t2047.json"] = spot(4096, 2047, m, [5, 3000], [0, 1500, 4095])
+    only = set(sys.argv[1].split(",")) if len(sys.argv) > 1 else None
+    files = {k: v for k, v in files.items() if only is None or k in only}
     for obj in files.values():
         obj.pop("_state", None)
     for name, obj in files.items():
