@@ -260,7 +260,10 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const 
 // rounds of a full chip's resident waves -- and cover the recipients in slices, back to back on the
 // stream, so the table never exceeds DEC_TAB_WAVES slots (655 MB) whatever n is (n = 4096: 32
 // launches instead of one grid of 524,288 waves and a 21-GB table).
-constexpr size_t DEC_TAB_WAVES = 16384;
+#ifndef DKG_DEC_TAB_WAVES
+#define DKG_DEC_TAB_WAVES 16384
+#endif
+constexpr size_t DEC_TAB_WAVES = DKG_DEC_TAB_WAVES;
 
 size_t dec_mul_recipients_per_launch(size_t D, size_t n) {
   const size_t per_q = ((D + 63) / 64) * 2;

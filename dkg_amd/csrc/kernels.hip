@@ -378,7 +378,8 @@ __global__ __launch_bounds__(COMBW_ENTRIES) void k_build_combw(const uint32_t* _
   out[31] = 0;
 }
 
-static_assert(COMBW_WORDS * 4 == (size_t)26 * 512 * 32 * 4, "runtime.hip COMBW_BYTES must match points.h");
+static_assert(COMBW_WORDS * 4 == (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW_BITS) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4,
+              "runtime.hip COMBW_BYTES must match points.h");
 
 void build_combw(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
   if (!count) return;

@@ -129,7 +129,10 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
 // entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-512, 511]: one
 // mixed addition per 10 scalar bits (26 per 253-bit scalar; radix 2^8 took 32, the LDS radix-16
 // comb 64), for the bases every kernel shares (g, h).
-constexpr int COMBW_BITS = 10;
+#ifndef DKG_COMBW_BITS
+#define DKG_COMBW_BITS 10  // -DDKG_COMBW_BITS=9: the radix-2^9 A/B build (profiles/r04_comb_radix_ab.txt)
+#endif
+constexpr int COMBW_BITS = DKG_COMBW_BITS;
 constexpr int COMBW_WINDOWS = (256 + COMBW_BITS - 1) / COMBW_BITS;  // 26: bits 250..259 absorb the top carry
 constexpr int COMBW_ENTRIES = 1 << (COMBW_BITS - 1);
 constexpr int COMBW_STRIDE = 32;

@@ -90,7 +90,12 @@ constexpr size_t PTB = 160;  // bytes of one extended point (40 words)
 constexpr size_t PT_WORDS_H = 40;
 constexpr size_t AFFP_WORDS_H = 32;  // affine addend slot of kernels.hip affine_pieces
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
-constexpr size_t COMBW_BYTES = 26 * 512 * 32 * 4;  // points.h COMBW_WORDS (radix 2^10)
+#ifndef DKG_COMBW_BITS
+#define DKG_COMBW_BITS 10
+#endif
+// points.h COMBW_WORDS x 4 (radix 2^10: 26 windows x 512 entries x 128 B)
+constexpr size_t COMBW_BYTES =
+    (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW_BITS) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4;
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
                                0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
                                0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};

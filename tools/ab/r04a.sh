@@ -13,3 +13,9 @@ for v in "" "--binomial 3"; do
 done
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu --mode full > $O/full.json 2>$O/full_err.log || { echo FULL BENCH FAILED; exit 1; }
 python -c "import json,sys; d=json.load(open(sys.argv[1])); print('full', round(d['ms_per_step'],2), {k:v['ms_per_pass'] for k,v in d['roofline']['all_kernels'].items()})" $O/full.json
+for lib in "" "ab_build/c9/libdkg_amd.so"; do
+  for cfg in "D" "B5"; do
+    DKG_AMD_LIB=${lib:-dkg_amd/libdkg_amd.so} timeout -k 10 300 python bench.py --config $cfg --steps 4 --warmup 1 --no-cpu --no-interp > $O/comb_${cfg}_$(basename $(dirname ${lib:-x/base})).json 2>$O/comb_err.log || { echo COMB BENCH FAILED; tail -5 $O/comb_err.log; exit 1; }
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print('comb', sys.argv[1], round(d['ms_per_step'],2), {k:v['ms_per_pass'] for k,v in d['roofline']['all_kernels'].items()})" $O/comb_${cfg}_$(basename $(dirname ${lib:-x/base})).json
+  done
+done
