@@ -693,7 +693,7 @@ def main():
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4],
-                    help="binomial schedule (dkg_ctx_set_binomial): 0 default (lane pairs for the latency-bound steps, mixed item order for the many-round ones), 1 no lane pairs, 2 lane pairs for every step, 3 no mixed order, 4 mixed order for every step")
+                    help="binomial schedule (dkg_ctx_set_binomial): 0 default (per-wave Horner loops for tables of many column groups, else per step with lane pairs for the latency-bound steps), 1 per step without lane pairs, 2 per step with lane pairs for every step, 3 per step as 0, 4 per wave always")
     ap.add_argument("--stepping", type=int, default=0, choices=[0, 1, 2, 3],
                     help="stepping slots (dkg_ctx_set_stepping): 0 cost model, 1 per column, 2 per piece, 3 no dead-position repack")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")

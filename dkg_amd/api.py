@@ -152,10 +152,10 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_ctx_set_field_mode(self._ctx, mode))
 
     def set_binomial(self, mode: int):
-        """Binomial schedule (dkg_ctx_set_binomial), one launch per Horner step: 0 (default) lane pairs
-        for the steps under one wave per SIMD and the mixed item order for many-round launches, 1
-        without lane pairs, 2 lane pairs for every step, 3 as 0 without the mixed order, 4 the mixed
-        order for every step."""
+        """Binomial schedule (dkg_ctx_set_binomial): 0 (default) per-wave Horner loops for tables of
+        many column groups, else one launch per step with lane pairs for the latency-bound steps; 1
+        per step without lane pairs; 2 per step with lane pairs everywhere; 3 per step as 0; 4 per
+        wave always."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
     def set_stepping(self, mode: int):

@@ -402,41 +402,18 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 // (position, 64 dealers); position 0 just copies the next coefficient C_k.  Grid (dealer groups x
 // pieces, r+1) with m = r - blockIdx.y: workgroups are dispatched x-fastest, so the longest NAF
 // chains (largest m) of EVERY piece start first and the launch tail is made of the short ones.
-//
-// Mixed order (items > 0: a 1-D grid of `items` = (column groups x pieces) x (r+1) waves): a launch
-// of many rounds of waves (config 5: up to 620k waves) is HBM-co-bound -- the short chains of small m
-// move the same 480 B per item as the long ones -- so the positions of one column group are
-// dispatched back to back (m fastest, longest first) and the groups are dealt to the XCDs in
-// contiguous ranges (workgroup b runs on XCD b mod 8): items (g, m) and (g, m-1), which both read
-// e_{m-1}, run on the same XCD at nearly the same time, so the second read hits its L2, and every
-// CU holds a mix of memory-heavy and chain-heavy waves.
-__device__ __forceinline__ void binom_item(unsigned items, unsigned& bx, unsigned& by, int r) {
-  if (!items) {
-    bx = blockIdx.x;
-    by = blockIdx.y;
-    return;
-  }
-  const unsigned per = (items + 7) / 8;  // items per XCD
-  const unsigned i = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  bx = i / (unsigned)(r + 1);
-  by = i - bx * (unsigned)(r + 1);
-  if (i >= items) bx = 0xffffffffu;  // padding of the last XCD's range
-}
 
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
                                                     size_t pstride, unsigned gx, unsigned last_piece,
-                                                    int last_off, unsigned items) {
+                                                    int last_off) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
-  unsigned bx, by;
-  binom_item(items, bx, by, r);
-  if (bx == 0xffffffffu) return;
-  const unsigned piece = bx / gx, grp = bx - piece * gx;
+  const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
   const size_t d = piece * pstride + (size_t)grp * blockDim.x + threadIdx.x;
   const size_t S = N * npad;
-  const int m = r - (int)by;
+  const int m = r - (int)blockIdx.y;
   if (m == 0) {
 #pragma unroll 8
     for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
@@ -527,19 +504,82 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 }
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
-                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, bool mixed) {
+                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
-  const size_t items = width / 64 * pieces * (r + 1);
-  if (mixed && items < (1ull << 31)) {
-    hipLaunchKernelGGL(k_binom_step, dim3((unsigned)((items + 7) / 8 * 8)), dim3(64), 0, stream, (int)r,
-                       (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1),
-                       last_off, (unsigned)items);
-    return;
-  }
   hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64 * pieces), (unsigned)(r + 1)), dim3(64), 0, stream,
                      (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 64),
-                     (unsigned)(pieces - 1), last_off, 0u);
+                     (unsigned)(pieces - 1), last_off);
+}
+
+// Every Horner step of one column group in ONE wave (short tables of many columns: config 5's
+// 10,000 ceremonies x 128 columns of t + 1 = 32 positions).  One launch per step there runs 31
+// launches of up to 640,000 waves that each load two points (480 B per item with the store) for a
+// NAF chain of a few additions: the small-m items are HBM-bound and the large-m ones VALU-bound,
+// and the launch boundaries keep the two phases apart (2.4-6.3 TB/s per launch, 0.68 of the issue
+// peak over the binomial, profiles/r04_b5_schedule_ab.txt).  Here a wave walks the steps r = 1..L-1
+// and, inside a step, the positions m = r..1 downwards, updating its columns' table IN PLACE
+// (e_m <- m (e_{m-1} + e_m) reads the old e_{m-1}, which the next item overwrites only after
+// reading it), then writes e_0 = C_{L-1-r}.  The same wave rereads e_{m-1} as the next item's e_m
+// (an L1 / L2 hit), so HBM sees about one load and one store per item, and the grid's waves drift
+// through the steps independently: chain-heavy and load-heavy items overlap on every CU.  Before
+// each step the wave drains its stores (the next step rereads them; the CU's L1 is write-through,
+// so its own stores keep it current -- a workgroup-scope acquire compiles to nothing here).
+__global__ __launch_bounds__(64, 4) void k_binom_wave(int L, size_t npad, const uint32_t* __restrict__ C,
+                                                    uint32_t* e, size_t pstride, unsigned gx, unsigned last_piece,
+                                                    int last_off) {
+  __shared__ uint32_t qs[PT_WORDS * 64];
+  uint32_t* q = qs + threadIdx.x;
+  const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
+  // wave-uniform bases (SGPRs) and a 32-bit lane index: no 64-bit per-lane address stays live
+  const size_t col0 = piece * pstride + (size_t)grp * 64;
+  uint32_t* eb = e + col0;
+  const uint32_t* cb = C + col0;
+  const uint32_t lane = threadIdx.x;
+  const size_t S = (size_t)L * npad;
+  const int off = piece == last_piece ? last_off : 0;
+#pragma unroll 8
+  for (int w = 0; w < PT_WORDS; w++) eb[w * S + lane] = cb[w * S + (size_t)(L - 1) * npad + lane];
+#pragma unroll 1
+  for (int r = 1; r < L; r++) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores land before it rereads them
+    const int re = r - off;  // a short last piece joins late (as k_binom_step)
+#pragma unroll 1
+    for (int m = re; m >= 1; m--) {
+      {
+        ge_p3 cur;
+        pt_load(cur, eb, S, (size_t)m * npad + lane);
+        uint32_t keep = (m == re) ? 0u : 0xffffffffu;  // position re is still the identity
+        asm volatile("" : "+v"(keep));
+        uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
+#pragma unroll
+        for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
+        ge_cached cc;
+        ge_to_cached(cc, cur);
+        lds_put_cached(q, cc);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ge_p3 x;
+      pt_load(x, eb, S, (size_t)(m - 1) * npad + lane);
+      ge_add_lds(x, x, q, false);        // e_{m-1} + e_m
+      mul_small_lds(x, (uint32_t)m, q);  // * m
+      // an opaque copy of the base: otherwise the compiler keeps the 40 addresses of the `cur` load
+      // (the same words) live across the chain for this store, and spills them
+      uint32_t* eo = eb;
+      asm volatile("" : "+s"(eo));
+      pt_store(eo, S, (size_t)m * npad + lane, x);
+    }
+#pragma unroll 8
+    for (int w = 0; w < PT_WORDS; w++) eb[w * S + lane] = cb[w * S + (size_t)(L - 1 - r) * npad + lane];
+  }
+}
+
+uint32_t* binomial_wave(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e, hipStream_t stream,
+                        size_t pieces, size_t pstride, size_t last_len) {
+  const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
+  hipLaunchKernelGGL(k_binom_wave, dim3((unsigned)(width / 64 * pieces)), dim3(64), 0, stream, (int)N, npad, C, e,
+                     pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off);
+  return e;
 }
 
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,
@@ -548,7 +588,7 @@ uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint3
   uint32_t* in = e0;
   uint32_t* out = e1;
   for (size_t r = 1; r < N; r++) {
-    binom_step(r, width, npad, N, C, in, out, stream, pieces, pstride, last_len, false);
+    binom_step(r, width, npad, N, C, in, out, stream, pieces, pstride, last_len);
     std::swap(in, out);
   }
   return in;

@@ -45,11 +45,11 @@ struct dkg_ctx {
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
   std::vector<uint8_t> key_tabs_pk;     // member keys whose decoded points and combs sit in hy.* (encrypt)
-  int binom_mode = 0;                   // binomial, one launch per Horner step: 0 lane pairs
-                                        // (k_binom_pair) for the steps under one wave per SIMD and
-                                        // the mixed item order for many-round launches, 1 no lane
-                                        // pairs, 2 lane pairs for every step, 3 as 0 without the
-                                        // mixed order, 4 the mixed order for every step
+  int binom_mode = 0;                   // binomial: 0 per-wave Horner loops (k_binom_wave) for
+                                        // tables of many column groups, else one launch per step
+                                        // with lane pairs (k_binom_pair) for the steps under one
+                                        // wave per SIMD; 1 per step, no lane pairs; 2 per step, lane
+                                        // pairs for every step; 3 per step as 0; 4 per wave always
   int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece,
                                         // 3 as 0 without the dead-position repack
   int fe_mode = 0;                      // field multiplication per launch: 0 by occupancy, 1 product
@@ -224,11 +224,12 @@ struct VerifySeg {
 #ifndef DKG_BINOM_ILP_WAVES
 #define DKG_BINOM_ILP_WAVES 1.5
 #endif
-// Binomial steps with at least this many waves per SIMD (rounds of 4 resident waves) dispatch their
-// items in the mixed order (kernels.hip k_binom_step): many rounds make the launch drain negligible,
-// and the order halves the step's HBM reads.
-#ifndef DKG_BINOM_MIX_WAVES
-#define DKG_BINOM_MIX_WAVES 16.0
+// Tables of at least this many 64-column groups (all pieces, all chunks) run the binomial as one
+// launch of per-wave Horner loops (kernels.hip k_binom_wave): each wave then has a long private
+// chain, and 4 rounds of a chip's resident waves keep the last round's tail small.  Fewer groups
+// (n=1024: 128; n=4096: 512) keep one launch per step.
+#ifndef DKG_BINOM_WAVE_GROUPS
+#define DKG_BINOM_WAVE_GROUPS 16384
 #endif
 
 bool use_ilp(const dkg_ctx* ctx, bool latency_bound) {
@@ -576,6 +577,9 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const bool saturating = (W / 64) * (L / 2) >= 4 * 1024;
   const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
   const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
+  // the binomial as per-wave Horner loops (k_binom_wave) for tables of many column groups
+  const bool per_wave = ctx->binom_mode == 4 ||
+                        (ctx->binom_mode == 0 && L > 1 && (double)npad / 64 * U >= DKG_BINOM_WAVE_GROUPS);
   // dead-position repack of an unsplit table (kernels.hip stepping_tail_phases): two scratch states
   const bool tails = ctx->step_mode != 3 && dkgk::stepping_tail_phases(L, n, U) > 1;
   uint32_t* tail_a = tails ? buf<uint32_t>(ctx, "v.tail_a", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
@@ -583,24 +587,30 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
-    dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
-    uint32_t *bin = e0 + c0, *bout = e1 + c0;
-    for (size_t r = 1; r < L; r++) {
-      // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
-      const double wps = (double)npad / 64 * U * (r + 1) / 1024;  // waves per SIMD, all chunks
-      const bool ilp = use_ilp(ctx, wps < DKG_BINOM_ILP_WAVES);
-      // lane pairs (k_binom_pair): by default the steps with under one wave per SIMD, mode 2 every
-      // step (1-, 2-, 4-, 8-way n=1024 shards 0.2-0.4 ms faster; profiles/r03_binomial_pairs_ab.txt)
-      const bool pair = ctx->binom_mode == 2 || ((ctx->binom_mode == 0 || ctx->binom_mode == 3) &&
-                                                 wps < DKG_BINOM_PAIR_WAVES);
-      const bool mixed = ctx->binom_mode == 4 || (ctx->binom_mode != 3 && wps >= DKG_BINOM_MIX_WAVES);
-      if (pair)
-        (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
-      else
-        (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr, mixed);
-      std::swap(bin, bout);
+    const uint32_t* e;
+    if (per_wave) {
+      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr);
+    } else {
+      dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
+      uint32_t *bin = e0 + c0, *bout = e1 + c0;
+      for (size_t r = 1; r < L; r++) {
+        // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
+        const double wps = (double)npad / 64 * U * (r + 1) / 1024;  // waves per SIMD, all chunks
+        const bool ilp = use_ilp(ctx, wps < DKG_BINOM_ILP_WAVES);
+        // lane pairs (k_binom_pair): by default the steps with under one wave per SIMD, mode 2
+        // every step (1-, 2-, 4-, 8-way n=1024 shards 0.2-0.4 ms faster;
+        // profiles/r03_binomial_pairs_ab.txt)
+        const bool pair = ctx->binom_mode == 2 || ((ctx->binom_mode == 0 || ctx->binom_mode == 3) &&
+                                                   wps < DKG_BINOM_PAIR_WAVES);
+        if (pair)
+          (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad,
+                                                                    Lr);
+        else
+          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+        std::swap(bin, bout);
+      }
+      e = bin;
     }
-    const uint32_t* e = bin;
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;

@@ -73,12 +73,11 @@ int dkg_ctx_set_stepping(dkg_ctx *ctx, int mode);
  * product scanning (fewest issue slots), 2 always column sums (most independent chains; for
  * latency-bound launches).  Outputs do not depend on it. */
 int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
-/* Schedule of the binomial-basis Horner, one grid launch per step: 0
- * (default) -- the steps with under one wave per SIMD with lane pairs (each point on two lanes
- * sharing its field products), the steps of many rounds of waves in the mixed item order (the
- * positions of a column group back to back on one XCD: the two reads of a table position meet in
- * its L2); 1 -- no lane pairs; 2 -- lane pairs for every step; 3 -- as 0 without the mixed order;
- * 4 -- the mixed order for every step without lane pairs.  Outputs do not depend on it. */
+/* Schedule of the binomial-basis Horner: 0 (default) -- tables of many column
+ * groups (config 5) as ONE launch in which every wave runs all steps of its 64 columns in place,
+ * others one grid launch per step with the steps under one wave per SIMD on lane pairs (each point
+ * on two lanes sharing its field products); 1 -- per step, no lane pairs; 2 -- per step, lane pairs
+ * for every step; 3 -- per step as 0's; 4 -- per wave always.  Outputs do not depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and

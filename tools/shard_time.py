@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--stepping", type=int, default=0, help="stepping slots: 0 model, 1 per column, 2 per piece, 3 no dead-position repack")
     ap.add_argument("--field", type=int, default=0, help="field multiply: 0 by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--combine", type=int, default=0, help="recombination: 0 short multipliers (U <= 4), 1 powers of j^L")
-    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule (dkg_ctx_set_binomial): 0 default, 1 no lane pairs, 2 lane pairs for all steps, 3 no mixed order, 4 mixed order for all steps")
+    ap.add_argument("--binomial", type=int, default=0, help="binomial schedule (dkg_ctx_set_binomial): 0 default, 1 no lane pairs, 2 lane pairs for all steps, 3 per step as 0, 4 per-wave loops")
     args = ap.parse_args()
     import torch
 
