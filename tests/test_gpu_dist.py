@@ -2,8 +2,8 @@
 run_verify + dkg_ceremony_shard_device / _shard_verify_device + the all-gathers + the library's
 combine, reconstruction exchange and finalise (dkg_amd/distributed.py), in 2 and 3 spawned ranks that
 share GPU 0 over gloo and in one rank over RCCL (tests/dist_worker.py).  Every combined output equals
-the single-GPU golden ceremony; at BASELINE config 2's size (n=1024) the combined outputs of two
-processes equal the single-GPU ceremony on the same inputs."""
+the single-GPU golden ceremony; at config 3's size (n=1024, SURVEY.md 8(d) numbering) the combined
+outputs of two processes equal the single-GPU ceremony on the same inputs."""
 import json
 import os
 import socket

@@ -2,11 +2,13 @@
 
 The oracle (tests/oracle_lib.py: dalek-3's algorithms, a vartime MSM per pair, committee.rs:287-305,
 532-548) recomputes WHOLE decision rows of the tampered dealers; the honest rows are checked by
-properties.  Sizes: n=256 (t=127), n=1024 (t=511, the headline schedule: cost-model split U=3 with
-pieces of 171 + 171 + 170 positions, two dealer-chunk streams, rounds 2 and 4 fused; and forced
-U=2 / U=4), n=1100 (t=549) and n=4096 (t=2047) with splits whose pieces exceed 512 positions, i.e.
-the block-chained stepping (kernels.hip k_stepping<512> with its up/down boundary streams) or end
-in a short last piece, and the 10,000-ceremony batch of config 5.
+properties.  Config numbers are SURVEY.md 8(d)'s (= BASELINE.json configs[0..4]): 2 is n=256 (t=127),
+3 is n=1024 (t=511: the headline schedule -- cost-model split U=4 with pieces of 128 positions,
+short lattice multipliers, two dealer-chunk streams, rounds 2 and 4 fused -- and forced U=2 / 3 /
+5), 4 is n=4096 (t=2047, whose pieces exceed 512 positions: the block-chained stepping,
+kernels.hip k_stepping<512> with its up/down boundary streams), 5 is the 10,000-ceremony batch of
+n=64 (t=31: the per-wave binomial and the stepping's dead-position repack); plus n=1100 (t=549)
+with a short last piece.
 """
 import random
 
@@ -454,7 +456,7 @@ def test_shard_ranks_n4096(be, rank):
 
 
 def test_shard_ranks_n1024_all_match_single(be):
-    """BASELINE config 2 split 8 ways (128 dealers per rank: the latency-bound shard -- column-sum
+    """Config 3 (n=1024) split 8 ways (128 dealers per rank: the latency-bound shard -- column-sum
     binomial copy on every step, one stream, 2-waves-per-SIMD stepping), faults inside EVERY rank's
     range (40 tampered dealers).  Per rank: whole rows of its tampered dealers equal the oracle's.
     Then the eight ranks' blocks, gathered, through the library's combine, reconstruction and
