@@ -21,3 +21,11 @@ cd /tmp
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf -o run -- python3 $R/bench.py --config B5 --steps 1 --warmup 0 --no-cpu --streams 1 > $O/pf.log 2>&1 || { echo PMC FAILED; exit 1; }
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw -o run -- python3 $R/bench.py --config B5 --steps 1 --warmup 0 --no-cpu --streams 1 > $O/pw.log 2>&1 || { echo PMC FAILED; exit 1; }
 echo done
+cd $R
+for lib in dkg_amd/libdkg_amd.so ab_build/c11/libdkg_amd.so; do
+  for cfg in D B5; do
+    tag=$(basename $(dirname $lib))
+    DKG_AMD_LIB=$R/$lib timeout -k 10 300 python bench.py --config $cfg --steps 4 --warmup 1 --no-cpu --no-interp > $O/comb_${cfg}_${tag}.json 2>$O/err.log || { echo COMB FAILED; tail -5 $O/err.log; exit 1; }
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['ms_per_step'],2), {k:v['ms_per_pass'] for k,v in d['roofline']['all_kernels'].items()}, d['phases_ms'])" $O/comb_${cfg}_${tag}.json
+  done
+done
