@@ -56,7 +56,7 @@ def add_cost(VALU, name, with_t=True):
     if name in NO_T:
         return VALU[NO_T[name]]
     return VALU[name] - (VALU["ge_add_signed"] - VALU["ge_add_signed_not"])
-COMBW_WINDOWS = 26  # points.h: radix-2^10 fixed-base comb, one mixed addition per window
+COMBW_WINDOWS = 24  # points.h: radix-2^11 fixed-base comb, one mixed addition per window
 SLOTS = {k: v[1] for k, v in VALU.items()}
 
 
@@ -118,7 +118,7 @@ HY_SYM_SLOTS = 12 * 8 * (6 * 3 + 4 * 2 + 3 * 4) + 20 * 4 * (4 + 4 + 4 * 2) + 64
 
 def hybrid_valu(n, sk, VALU=SLOTS):
     """Closed-form VALU work of full mode's encryption and decryption of all 2 n^2 items (n dealers x n
-    recipients x {randomness, share}): k_enc_mul (26 radix-2^10 windows of g + 64 radix-16 windows of
+    recipients x {randomness, share}): k_enc_mul (24 radix-2^11 windows of g + 64 radix-16 windows of
     pk_q per item), k_dec_mul_w4 (sk_q's width-4 window, wave-uniform: a doubling per digit below the
     top, an addition per nonzero digit, the odd multiples), the encode / decode kernels and k_sym_xor
     (model above)."""
@@ -147,15 +147,24 @@ def hybrid_valu(n, sk, VALU=SLOTS):
 
 PT_BYTES = 160  # one extended point, 40 u32 words (SoA)
 AFF_BYTES = 128  # kernels.hip AFFP_WORDS: one affine addend slot
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "pmc_traffic")
 
 
-def algorithmic_bytes(kernel, n, t, U, plen=None):
+def algorithmic_bytes(kernel, n, t, U, plen=None, per_wave=False, batch=1):
     """(bytes per launch, launches per pass) of a check-pipeline kernel in the serialised fused pass:
     2n columns (E and A rows) x U pieces (split_pieces: L positions, a shorter last one; DESIGN.md
-    sections 3-4)."""
+    sections 3-4), times `batch` ceremonies.  per_wave: the binomial ran as per-wave Horner loops
+    (k_binom_wave, one launch): per column the initial copy of C_t, then per step one load (the old
+    e_{m-1}; e_m is carried in registers) and one store per live position and the copy of C_k."""
+    if batch > 1:
+        b, nl = algorithmic_bytes(kernel, n, t, U, plen, per_wave)
+        return (None, None) if b is None else (b * batch, nl)
     pieces, Lp0 = split_pieces(t, U, plen)
     cols = 2 * n
+    if kernel == "binomial" and per_wave:
+        per_col = sum(2 * PT_BYTES + sum(2 * PT_BYTES * (1 + max(r - (Lp0 - Lp), 0)) for r in range(1, Lp0))
+                      for Lp in pieces)
+        return cols * per_col, 1
     if kernel == "binomial":  # step r: position 0 copies C_k (load+store), positions 1..r' load 2, store 1
         # (r' = r for full pieces, r - (L - Lp) for a short last piece, which starts late)
         per_pass = sum(cols * (2 * PT_BYTES + max(r - (Lp0 - Lp), 0) * 3 * PT_BYTES)
@@ -175,21 +184,44 @@ def algorithmic_bytes(kernel, n, t, U, plen=None):
     return None, None
 
 
-def pmc_traffic(kernel, n, t, U, plen=None):
+def pmc_traffic(kernel, n, t, U, plen=None, batch=1, mode="plain"):
     """HBM-side bytes per launch of `kernel` from the committed PMC passes (tools/profile.sh ->
-    tools/pmc_summary.py), when they were taken on this workload; else None."""
+    tools/pmc_summary.py --traffic, one file per workload in profiles/pmc_traffic/), when one was
+    taken on this workload (n, t, split, piece length, batch, mode); else None."""
+    want = {"n": n, "t": t, "split": U, "split_len": plen if plen is not None else split_pieces(t, U)[1],
+            "batch": batch, "mode": mode}
     try:
-        with open(TRAFFIC_FILE) as f:
-            doc = json.load(f)
-    except (OSError, ValueError):
+        names = sorted(os.listdir(TRAFFIC_DIR))
+    except OSError:
         return None
-    if (doc.get("n"), doc.get("t"), doc.get("split")) != (n, t, U) or kernel not in doc.get("kernels", {}):
-        return None
-    if kernel in ("stepping", "affine") and not doc.get("stepping_z_copy"):
-        return None  # measured before the stepping wrote the dense Z copy the affine pass reads
-    if plen is not None and doc.get("split_len", split_pieces(t, U)[1]) != plen:
-        return None
-    return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
+    for name in names:
+        try:
+            with open(os.path.join(TRAFFIC_DIR, name)) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        key = dict(doc.get("key", {}))
+        if key.get("split_len") is None:
+            key["split_len"] = split_pieces(t, U)[1]
+        if key == want and kernel in doc.get("kernels", {}):
+            return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
+    return None
+
+
+def add_traffic(line, dom, ms_pass, n, t, U, plen, per_wave=False, batch=1, mode="plain"):
+    """roofline.algorithmic_bytes_per_launch / algorithmic_GBps / traffic (PMC) of the dominant kernel."""
+    alg, launches = algorithmic_bytes(dom, n, t, U, plen, per_wave, batch)
+    pmc = pmc_traffic(dom, n, t, U, plen, batch, mode)
+    rl = line["roofline"]
+    if alg is not None:
+        rl["algorithmic_bytes_per_launch"] = alg
+        rl["algorithmic_GBps"] = alg / (ms_pass / launches / 1e3) / 1e9
+    if pmc is not None:
+        rl["traffic"] = pmc[0]
+        rl["traffic_unit"] = "HBM-side bytes per launch (average)"
+        rl["traffic_source"] = pmc[1]
+        if alg:
+            rl["traffic_over_algorithmic"] = pmc[0] / alg
 
 
 def spawn_ranks(args, poll_s=0.2):
@@ -412,13 +444,13 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
             combine += c
     nsc = 2 if rnd == 2 else 1
     scale = nsc * VALU["sc_mont_mul"] if mults is not None else 0
-    check = n * (nsc * COMBW_WINDOWS * VALU["combw_window"] + VALU["eq"] + scale)  # radix-2^10 combs
+    check = n * (nsc * COMBW_WINDOWS * VALU["combw_window"] + VALU["eq"] + scale)  # radix-2^11 combs
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
 def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None, affine=True, ded=True):
     """Work of the fused round-2 + round-4 pipeline: both tables' binomial, stepping and
-    recombination; one check kernel computing g*s once (26 radix-2^10 comb windows), h*s' (26 more)
+    recombination; one check kernel computing g*s once (24 radix-2^11 comb windows), h*s' (24 more)
     and both equalities per pair (with `mults`: s and s' scaled by b_j first)."""
     w2 = algorithmic_valu(n, t, 2, U, VALU, plen, mults, affine, ded)
     w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults, affine, ded)
@@ -596,11 +628,13 @@ def bench_batch(args, ws, rank, local):
            "phases_ms": {k: round(v, 3) for k, v in res.ms.items()}}
     out["config"]["degree_split"] = U
     out["ref_equiv"] = ref_equiv(n, t, out["value"])
+    out["config"]["binomial"] = "per-wave loops" if be.last_binomial() else "one launch per step"
     if rl:
         dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
         out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} instructions) "
                                                  f"per batch: {B} x the closed form of one ceremony's fused "
                                                  f"round-2/4 pipeline; device time in a serialised batch")
+        add_traffic(out, dom, rl[dom]["ms_per_pass"], n, t, U, Ls, bool(be.last_binomial()), B)
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(n, t, 20.0, ceremonies=B)
         out["gpu_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
@@ -825,6 +859,7 @@ def main():
         out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} instructions) "
                                                  f"per full-mode ceremony (closed form; hybrid kernels: "
                                                  f"bench.py hybrid_valu); device time in a serialised ceremony")
+        add_traffic(out, dom, rl[dom]["ms_per_pass"], n, t, U, Ls, bool(be.last_binomial()), 1, "full")
         if not args.no_cpu:
             cb = cpu_baseline(n, t)
             lib = __import__("tests.oracle_lib", fromlist=["lib"]).lib()
@@ -888,18 +923,8 @@ def main():
             out["roofline"] = roofline_line(rl, dom, f"{work[dom]:.4g} VALU issue slots ({work_i[dom]:.4g} "
                                             f"instructions) per pass over {what} (closed form); device time of "
                                             f"the kernel's launches (HIP events) in a serialised pass")
-            alg, launches = algorithmic_bytes(dom, n, t, U, Ls) if ov else (None, None)
-            pmc = pmc_traffic(dom, n, t, U, Ls) if ov else None
-            if alg is not None:
-                ms_launch = rl[dom]["ms_per_pass"] / launches
-                out["roofline"]["algorithmic_bytes_per_launch"] = alg
-                out["roofline"]["algorithmic_GBps"] = alg / (ms_launch / 1e3) / 1e9
-            if pmc is not None:
-                out["roofline"]["traffic"] = pmc[0]
-                out["roofline"]["traffic_unit"] = "HBM-side bytes per launch (average)"
-                out["roofline"]["traffic_source"] = pmc[1]
-                if alg:
-                    out["roofline"]["traffic_over_algorithmic"] = pmc[0] / alg
+            if ov:
+                add_traffic(out, dom, rl[dom]["ms_per_pass"], n, t, U, Ls, bool(be.last_binomial()))
         if not args.no_interp:
             # the opt-in committee verification on the same inputs, reported
             # beside the headline, never as it: every P_i(j) is NOT computed in the group there

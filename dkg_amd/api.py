@@ -189,6 +189,10 @@ class Backend:
         """0 no split, 1 powers of y, 2 short multipliers (the last verification)."""
         return _lib.lib().dkg_ctx_last_combine(self._ctx)
 
+    def last_binomial(self) -> int:
+        """0 one launch per Horner step, 1 per-wave loops (k_binom_wave) in the last verification."""
+        return _lib.lib().dkg_ctx_last_binomial(self._ctx)
+
     def last_split(self) -> int:
         return _lib.lib().dkg_ctx_last_split(self._ctx)
 

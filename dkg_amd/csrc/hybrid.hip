@@ -22,7 +22,7 @@ namespace dkgk {
 constexpr int HY_COMB_WORDS = AFF_WORDS * COMB_ENTRIES;
 
 // grid (ceil(2D / 1024), n): recipient q = blockIdx.y; the recipient's comb table in LDS (60 KB),
-// the generator's radix-2^10 comb (26 mixed additions instead of 64) from global memory / L2.
+// the generator's radix-2^11 comb (24 mixed additions instead of 64) from global memory / L2.
 __global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
                                                   const uint32_t* __restrict__ tab_gw,
                                                   const uint32_t* __restrict__ tabs_pk, uint32_t* __restrict__ R_ext,
@@ -256,12 +256,13 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const 
 #endif
 
 // The width-4 window's odd multiples live in a global table of one 40-KB slot per wave of a launch
-// (T, indexed by the wave's place in its grid).  Launches are capped at DEC_TAB_WAVES waves -- four
+// (T, indexed by the wave's place in its grid).  Launches are capped at DEC_TAB_WAVES waves -- eight
 // rounds of a full chip's resident waves -- and cover the recipients in slices, back to back on the
-// stream, so the table never exceeds DEC_TAB_WAVES slots (655 MB) whatever n is (n = 4096: 32
-// launches instead of one grid of 524,288 waves and a 21-GB table).
+// stream, so the table never exceeds DEC_TAB_WAVES slots (1.3 GB) whatever n is (n = 1024: one
+// launch; n = 4096: 16 launches instead of one grid of 524,288 waves and a 21-GB table).  A cap of
+// 16,384 (two launches at n = 1024) cost 0.8-1.0 ms there (profiles/r04_dec_slices_ab.txt).
 #ifndef DKG_DEC_TAB_WAVES
-#define DKG_DEC_TAB_WAVES 16384
+#define DKG_DEC_TAB_WAVES 32768
 #endif
 constexpr size_t DEC_TAB_WAVES = DKG_DEC_TAB_WAVES;
 

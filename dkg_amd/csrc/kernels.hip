@@ -520,14 +520,21 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
 // peak over the binomial, profiles/r04_b5_schedule_ab.txt).  Here a wave walks the steps r = 1..L-1
 // and, inside a step, the positions m = r..1 downwards, updating its columns' table IN PLACE
 // (e_m <- m (e_{m-1} + e_m) reads the old e_{m-1}, which the next item overwrites only after
-// reading it), then writes e_0 = C_{L-1-r}.  The same wave rereads e_{m-1} as the next item's e_m
-// (an L1 / L2 hit), so HBM sees about one load and one store per item, and the grid's waves drift
-// through the steps independently: chain-heavy and load-heavy items overlap on every CU.  Before
+// reading it), then writes e_0 = C_{L-1-r}.  The old e_{m-1} is the next item's e_m (CARRY below),
+// and the grid's waves drift through the steps independently: chain-heavy and load-heavy items
+// overlap on every CU.  Before
 // each step the wave drains its stores (the next step rereads them; the CU's L1 is write-through,
 // so its own stores keep it current -- a workgroup-scope acquire compiles to nothing here).
-__global__ __launch_bounds__(64, 4) void k_binom_wave(int L, size_t npad, const uint32_t* __restrict__ C,
-                                                    uint32_t* e, size_t pstride, unsigned gx, unsigned last_piece,
-                                                    int last_off) {
+// CARRY: the old e_{m-1} an item loads stays in registers as the next item's e_m (40 more VGPRs:
+// 3 waves per SIMD instead of 4): one load per item instead of two -- the reread otherwise misses
+// L2, evicted during the item's chain by the CU's other waves (profiles/r04_b5_schedule_ab.txt).
+#ifndef DKG_BINOM_WAVE_CARRY
+#define DKG_BINOM_WAVE_CARRY 1
+#endif
+template <bool CARRY>
+__global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t npad, const uint32_t* __restrict__ C,
+                                                                uint32_t* e, size_t pstride, unsigned gx,
+                                                                unsigned last_piece, int last_off) {
   __shared__ uint32_t qs[PT_WORDS * 64];
   uint32_t* q = qs + threadIdx.x;
   const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
@@ -544,23 +551,30 @@ __global__ __launch_bounds__(64, 4) void k_binom_wave(int L, size_t npad, const 
   for (int r = 1; r < L; r++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores land before it rereads them
     const int re = r - off;  // a short last piece joins late (as k_binom_step)
+    ge_p3 carry;
+    if constexpr (CARRY) ge_identity(carry);  // position re is still the identity
 #pragma unroll 1
     for (int m = re; m >= 1; m--) {
       {
-        ge_p3 cur;
-        pt_load(cur, eb, S, (size_t)m * npad + lane);
-        uint32_t keep = (m == re) ? 0u : 0xffffffffu;  // position re is still the identity
-        asm volatile("" : "+v"(keep));
-        uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
-#pragma unroll
-        for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
         ge_cached cc;
-        ge_to_cached(cc, cur);
+        if constexpr (CARRY) {
+          ge_to_cached(cc, carry);
+        } else {
+          ge_p3 cur;
+          pt_load(cur, eb, S, (size_t)m * npad + lane);
+          uint32_t keep = (m == re) ? 0u : 0xffffffffu;  // position re is still the identity
+          asm volatile("" : "+v"(keep));
+          uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
+#pragma unroll
+          for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
+          ge_to_cached(cc, cur);
+        }
         lds_put_cached(q, cc);
       }
       __builtin_amdgcn_sched_barrier(0);
       ge_p3 x;
       pt_load(x, eb, S, (size_t)(m - 1) * npad + lane);
+      if constexpr (CARRY) carry = x;    // the old e_{m-1}: the next item's e_m
       ge_add_lds(x, x, q, false);        // e_{m-1} + e_m
       mul_small_lds(x, (uint32_t)m, q);  // * m
       // an opaque copy of the base: otherwise the compiler keeps the 40 addresses of the `cur` load
@@ -577,8 +591,8 @@ __global__ __launch_bounds__(64, 4) void k_binom_wave(int L, size_t npad, const 
 uint32_t* binomial_wave(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e, hipStream_t stream,
                         size_t pieces, size_t pstride, size_t last_len) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
-  hipLaunchKernelGGL(k_binom_wave, dim3((unsigned)(width / 64 * pieces)), dim3(64), 0, stream, (int)N, npad, C, e,
-                     pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off);
+  hipLaunchKernelGGL(k_binom_wave<DKG_BINOM_WAVE_CARRY != 0>, dim3((unsigned)(width / 64 * pieces)), dim3(64), 0,
+                     stream, (int)N, npad, C, e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off);
   return e;
 }
 
@@ -1748,7 +1762,7 @@ __global__ __launch_bounds__(256, 4) void k_fixed_base(size_t count, const uint3
   pt_store(out, count, e, acc);
 }
 
-// tab: a radix-2^10 comb (build_combw)
+// tab: a radix-2^11 comb (build_combw)
 void fixed_base(size_t count, const uint32_t* scalars, const uint32_t* tab, uint32_t* out_ext, hipStream_t stream) {
   if (!count) return;
   hipLaunchKernelGGL(k_fixed_base, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, scalars, tab,

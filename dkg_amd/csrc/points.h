@@ -124,13 +124,14 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
   }
 }
 
-// Radix-2^10 comb in global memory (L2-resident: 1.7 MB per base, both of g and h fit one XCD's
-// 4 MB L2): 26 windows B_w = 2^(10 w) B of 512 affine Niels entries d B_w (d = 1..512),
-// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-512, 511]: one
-// mixed addition per 10 scalar bits (26 per 253-bit scalar; radix 2^8 took 32, the LDS radix-16
-// comb 64), for the bases every kernel shares (g, h).
+// Radix-2^11 comb in global memory (L2 / Infinity-Cache resident: 3.1 MB per base): 24 windows
+// B_w = 2^(11 w) B of 1024 affine Niels entries d B_w (d = 1..1024), entry-major, 32 words per entry
+// (ypx | ymx | xy2d | 2 pad).  Signed digits in [-1024, 1023]: one mixed addition per 11 scalar bits
+// (24 per 253-bit scalar; radix 2^10 took 26, 2^8 32, the LDS radix-16 comb 64), for the bases every
+// kernel shares (g, h).  The checks and commitments are VALU-bound: the two windows fewer pay more
+// than the table's extra L2 misses cost (radix 2^9 / 2^10 / 2^11: profiles/r04_comb_radix_ab.txt).
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 10  // -DDKG_COMBW_BITS=9: the radix-2^9 A/B build (profiles/r04_comb_radix_ab.txt)
+#define DKG_COMBW_BITS 11  // -DDKG_COMBW_BITS=9 / 10: the A/B builds
 #endif
 constexpr int COMBW_BITS = DKG_COMBW_BITS;
 constexpr int COMBW_WINDOWS = (256 + COMBW_BITS - 1) / COMBW_BITS;  // 26: bits 250..259 absorb the top carry

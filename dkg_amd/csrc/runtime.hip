@@ -23,7 +23,7 @@ struct dkg_ctx {
   std::map<std::string, std::pair<void*, size_t>> bufs;
   uint32_t* tab_g = nullptr;  // comb table of the generator (15360 words)
   uint32_t* tab_h = nullptr;  // comb table of the commitment key h
-  uint32_t* tab_gw = nullptr;  // radix-2^10 combs (global, L2-resident) of g and h: commit, check,
+  uint32_t* tab_gw = nullptr;  // radix-2^11 combs (global, L2 / MALL-resident) of g and h: commit, check,
   uint32_t* tab_hw = nullptr;  // fixed-base products
   uint8_t h[32] = {0};
   bool have_h = false;
@@ -63,6 +63,7 @@ struct dkg_ctx {
   int combine_mode = 0;                 // recombination: 0 short vectors for U <= 4, 1 powers of y,
                                         // 2 short vectors (U <= 4)
   int last_combine = 0;                 // 1: the last verify_device recombined with powers, 2: short vectors
+  int last_binomial = 0;                // 1: the last verify_device ran the per-wave binomial
   int step_formula = 0;                 // stepping additions: 0 dedicated + complete redo of marked
                                         // workgroups, 1 complete formula only
   uint32_t* last_step_flags = nullptr;  // the last verify_device's stepping flags (dedicated mode)
@@ -91,9 +92,9 @@ constexpr size_t PT_WORDS_H = 40;
 constexpr size_t AFFP_WORDS_H = 32;  // affine addend slot of kernels.hip affine_pieces
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 10
+#define DKG_COMBW_BITS 11
 #endif
-// points.h COMBW_WORDS x 4 (radix 2^10: 26 windows x 512 entries x 128 B)
+// points.h COMBW_WORDS x 4 (radix 2^11: 24 windows x 1024 entries x 128 B)
 constexpr size_t COMBW_BYTES =
     (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW_BITS) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4;
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
@@ -162,7 +163,7 @@ int guarded(dkg_ctx* ctx, F&& f) {
 }
 
 // Decode one 32-byte point and build its comb table into `tab`.
-// Comb tables of one point: radix-16 (LDS kernels; may be null) and radix-2^10 (may be null).
+// Comb tables of one point: radix-16 (LDS kernels; may be null) and radix-2^11 (may be null).
 void comb_for_point(dkg_ctx* ctx, const uint8_t p[32], uint32_t* tab, bool* ok, uint32_t* tab8 = nullptr) {
   uint32_t* comp = buf<uint32_t>(ctx, "comb_in", 32);
   uint32_t* ext = buf<uint32_t>(ctx, "comb_ext", PTB);
@@ -580,6 +581,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // the binomial as per-wave Horner loops (k_binom_wave) for tables of many column groups
   const bool per_wave = ctx->binom_mode == 4 ||
                         (ctx->binom_mode == 0 && L > 1 && (double)npad / 64 * U >= DKG_BINOM_WAVE_GROUPS);
+  ctx->last_binomial = per_wave ? 1 : 0;
   // dead-position repack of an unsplit table (kernels.hip stepping_tail_phases): two scratch states
   const bool tails = ctx->step_mode != 3 && dkgk::stepping_tail_phases(L, n, U) > 1;
   uint32_t* tail_a = tails ? buf<uint32_t>(ctx, "v.tail_a", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
@@ -1570,6 +1572,7 @@ int dkg_ctx_set_combine(dkg_ctx* ctx, int mode) {
   return DKG_OK;
 }
 int dkg_ctx_last_combine(const dkg_ctx* ctx) { return ctx ? ctx->last_combine : 0; }
+int dkg_ctx_last_binomial(const dkg_ctx* ctx) { return ctx ? ctx->last_binomial : 0; }
 int dkg_ctx_set_stepping_formula(dkg_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
   ctx->step_formula = mode;

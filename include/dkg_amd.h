@@ -109,6 +109,9 @@ size_t dkg_split_len(size_t columns, size_t n, size_t t, int pieces);
 int dkg_ctx_set_combine(dkg_ctx *ctx, int mode);
 /* What the last verification recombined with: 0 no split, 1 powers of y, 2 short multipliers. */
 int dkg_ctx_last_combine(const dkg_ctx *ctx);
+/* How the last verification ran its binomial: 0 one launch per Horner step, 1 per-wave loops
+ * (k_binom_wave, one launch per chunk stream). */
+int dkg_ctx_last_binomial(const dkg_ctx *ctx);
 /* Addends of the short-multiplier recombination: 0 (default) affine Niels (the stepped values
  * normalised with one inversion per run of receivers; mixed additions, 7M instead of 8M), 1 cached
  * projective.  Outputs do not depend on it. */

@@ -117,7 +117,7 @@ def test_split_pieces_and_bytes():
 
 
 def test_hybrid_valu_closed_form():
-    """Full mode's closed forms (bench.hybrid_valu): k_enc_mul prices 26 radix-2^10 windows of g plus 64
+    """Full mode's closed forms (bench.hybrid_valu): k_enc_mul prices 24 radix-2^11 windows of g plus 64
     radix-16 windows of pk_q per item; k_dec_mul_w4 the odd multiples, then an addition per nonzero
     width-4 window digit of sk_q and a doubling per digit below the top, for the 2n items of q."""
     n = 3
@@ -126,7 +126,7 @@ def test_hybrid_valu_closed_form():
     assert bench._wnaf(23, 4) == [7, 0, 0, 0, 1]  # 23 = 16 + 7
     w = bench.hybrid_valu(n, sk)
     S = bench.SLOTS
-    assert w["enc_mul"] == 2 * n * n * (26 * S["combw_window"] + 64 * S["comb_window"])
+    assert w["enc_mul"] == 2 * n * n * (24 * S["combw_window"] + 64 * S["comb_window"])
     pre = S["ge_dbl_t"] + 3 * S["ge_add"] + 5 * S["ge_to_cached"]
     c5 = pre + S["ge_add_signed"]  # one digit: one addition onto the identity
     c1 = pre + S["ge_add_signed"]

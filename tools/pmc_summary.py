@@ -1,11 +1,12 @@
 """Summarise rocprofv3 CSV output of tools/profile.sh per kernel (sums over dispatches).
 
-usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag> [traffic.json n t U [L]]
+usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag> [--traffic profiles/pmc_traffic/<tag>.json
+       --n N --t T --split U --split-len L [--batch B] [--mode full]]
 Prints kernel-trace stats (calls, total/avg ms) and, per kernel, the SQ issue/wait split,
 VALU instructions (wave-level x 64 lanes) and HBM-side bytes: FETCH_SIZE doubled (gfx950 counts
 half the bytes of wide coalesced reads, MI355X_MICROARCH.md "HBM") and WRITE_SIZE, both in KB.
-With a traffic.json path (and the profiled ceremony's n, t and degree split U) it also writes the
-per-launch HBM bytes of the check-pipeline kernels, which bench.py reports as roofline.traffic.
+With --traffic (and the profiled workload's key) it also writes the per-launch HBM bytes of the
+pipeline kernels, which bench.py reports as roofline.traffic for a line of the same workload.
 """
 import csv
 import json
@@ -76,20 +77,23 @@ def phase(name):
     """Pipeline phase of a kernel-trace name (template arguments as rocprofv3 prints them): the
     dedicated stepping (k_stepping<MAXBS, true, PARTS>) and its complete-formula redo launches
     (<MAXBS, false, ..>: near-empty when no workgroup was marked, kept apart so that they do not
-    halve the per-launch average), the recombination, the normalisation, the binomial and the check."""
-    if name == "k_binom_step":
+    halve the per-launch average), the recombination, the normalisation, the binomial (per step or
+    per wave), the check and full mode's hybrid kernels."""
+    if name == "k_binom_step" or re.match(r"(void )?k_binom_wave<", name):
         return "binomial"
     m = re.match(r"void k_stepping<\d+(?:, (true|false))?", name)
     if m:
         return "stepping_redo" if m.group(1) == "false" else "stepping"
     if re.match(r"void k_combine(_aff|_short)?<", name):
         return "combine"
-    return {"k_affine_pieces": "affine", "k_check_both": "check", "k_check": "check"}.get(name)
+    return {"k_affine_pieces": "affine", "k_check_both": "check", "k_check": "check", "k_commit": "commit",
+            "k_enc_mul": "enc_mul", "k_dec_mul_w4": "dec_mul", "k_sym_xor": "sym"}.get(name)
 
 
-def write_traffic(d, out, n, t, U, split_len=None):
+def write_traffic(d, out, key):
     """Per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, counted in separate --pmc passes) of the
-    check-pipeline kernels, summed over every dispatch the profiled run made."""
+    pipeline kernels, summed over every dispatch the profiled run made, under the workload `key`
+    (n, t, split, split_len, batch, mode) bench.py matches its line against."""
     fe, fcalls = load_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
     wr, wcalls = load_counters(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
     kern = {}
@@ -107,16 +111,25 @@ def write_traffic(d, out, n, t, U, split_len=None):
                                  + e["write_bytes"] / max(e["write_launches"], 1))
     doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
                      f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
-           "n": n, "t": t, "split": U, "kernels": kern,
-           "stepping_z_copy": True}  # round 3+: the stepping also writes the dense Z copy
-    if split_len:
-        doc["split_len"] = split_len
+           "key": key, "kernels": kern}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
-    if len(sys.argv) > 2:
-        write_traffic(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]),
-                      int(sys.argv[6]) if len(sys.argv) > 6 else None)
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--traffic", help="write the per-launch traffic file here (needs --n --t --split)")
+    ap.add_argument("--n", type=int)
+    ap.add_argument("--t", type=int)
+    ap.add_argument("--split", type=int)
+    ap.add_argument("--split-len", type=int)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--mode", default="plain")
+    a = ap.parse_args()
+    main(a.dir)
+    if a.traffic:
+        write_traffic(a.dir, a.traffic, {"n": a.n, "t": a.t, "split": a.split, "split_len": a.split_len,
+                                         "batch": a.batch, "mode": a.mode})
