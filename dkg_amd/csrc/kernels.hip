@@ -194,7 +194,8 @@ __global__ __launch_bounds__(256, 4) void k_commit(size_t count, const uint32_t*
                                                 const uint32_t* __restrict__ b,
                                                 const uint32_t* __restrict__ tab_g,
                                                 const uint32_t* __restrict__ tab_h,
-                                                uint32_t* __restrict__ A_ext, uint32_t* __restrict__ E_ext) {
+                                                uint32_t* __restrict__ A_ext, uint32_t* __restrict__ E_ext,
+                                                size_t stride) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
   sc sa, sb;
@@ -203,16 +204,16 @@ __global__ __launch_bounds__(256, 4) void k_commit(size_t count, const uint32_t*
   ge_p3 acc;
   ge_identity(acc);
   combw_mul_add(acc, sa, tab_g);               // apub = G::generator() * a   (committee.rs:155)
-  pt_store(A_ext, count, e, acc);
+  pt_store(A_ext, stride, e, acc);
   combw_mul_add(acc, sb, tab_h);               // coeff_comm = h * b + apub   (committee.rs:156)
-  pt_store(E_ext, count, e, acc);
+  pt_store(E_ext, stride, e, acc);
 }
 
 void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g, const uint32_t* tab_h,
-            uint32_t* A_ext, uint32_t* E_ext, hipStream_t stream) {
+            uint32_t* A_ext, uint32_t* E_ext, hipStream_t stream, size_t stride) {
   if (!count) return;
   hipLaunchKernelGGL(k_commit, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, count, a, b, tab_g, tab_h,
-                     A_ext, E_ext);
+                     A_ext, E_ext, stride ? stride : count);
 }
 
 // ------------------------------------------------------------------ K1 share evaluation

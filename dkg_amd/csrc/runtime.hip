@@ -76,6 +76,12 @@ struct dkg_ctx {
   // encodings, finalise reads A_i0 from them.  E/A [D][t+1] points, word stride ext_stride.
   const uint32_t* ext_E = nullptr;
   const uint32_t* ext_A = nullptr;
+  // round-1 commitments deferred into the verification's chunks (batches, BatchRound1): coefficients
+  // [r1_D][N][8]; each chunk's stream computes its dealers' E/A into ext_E / ext_A before its
+  // binomial, so one chunk's commitments run beside the other chunk's pipeline
+  const uint32_t* r1_a = nullptr;
+  const uint32_t* r1_b = nullptr;
+  size_t r1_D = 0;
   size_t ext_stride = 0;
   // share rows [shard_D][shard_n][8] of the last sharded call's dealers [shard_d0, +shard_D)
   // (arena-owned; dkg_ceremony_shard_recon_device reads them after the exchange)
@@ -534,7 +540,9 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   // padding columns, and the positions past t of the last piece, are the identity
   if (npad != D * nseg || U * L != N) dkgk::fill_identity(L * W, Cpm, home);
   HCK(hipMemsetAsync(pok, 1, npad * N, home));
-  for (int k = 0; k < nseg; k++) {
+  // deferred round 1 (BatchRound1): the fused pass over the very dealers whose coefficients wait
+  const bool defer_r1 = ctx->r1_a && nseg == 2 && ctx->ext_E && D == ctx->r1_D && ctx->ext_stride == D * N;
+  for (int k = 0; k < nseg && !defer_r1; k++) {
     const uint32_t* ext = segs[k].round == 2 ? ctx->ext_E : ctx->ext_A;
     if (ext)  // generated on this device: group elements, as the reference's broadcasts carry them
       dkgk::place_position_major(ext, ctx->ext_stride, D, N, W, Cpm, home, nseg, k, L, npad);
@@ -588,6 +596,15 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   uint32_t* tail_b = tails ? buf<uint32_t>(ctx, "v.tail_b", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
+    if (defer_r1) {  // this chunk's dealers' commitments (committee.rs:151-159), then their columns
+      const size_t d0 = g0 * 64, d1 = std::min(D, g1 * 64);
+      uint32_t* Ae = const_cast<uint32_t*>(ctx->ext_A) + d0 * N;
+      uint32_t* Ee = const_cast<uint32_t*>(ctx->ext_E) + d0 * N;
+      dkgk::commit((d1 - d0) * N, ctx->r1_a + d0 * N * 8, ctx->r1_b + d0 * N * 8, ctx->tab_gw, ctx->tab_hw, Ae, Ee,
+                   st, D * N);
+      dkgk::place_position_major(Ee, D * N, d1 - d0, N, W, Cpm + c0, st, nseg, 0, L, npad);
+      dkgk::place_position_major(Ae, D * N, d1 - d0, N, W, Cpm + c0, st, nseg, 1, L, npad);
+    }
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
     const uint32_t* e;
     if (per_wave) {
@@ -1159,6 +1176,40 @@ struct ExtScope {
   }
 };
 
+// Round 1 of a batch with the commitments deferred into the verification's chunks (r1_a above):
+// the fused group pass (verify_mode 0, rounds 2 and 4 fused) computes each chunk's dealers'
+// commitments on the chunk's own stream, so the second chunk's commitments (half of config 5's
+// round 1) run beside the first chunk's binomial and stepping; the shares are evaluated on the
+// side stream beside both.  Other schedules get the whole round 1 first (round1_device).
+struct BatchRound1 {
+  dkg_ctx* ctx;
+  BatchRound1(dkg_ctx* c, size_t D, size_t n, size_t t, const uint32_t* a, const uint32_t* b, uint32_t* s,
+              uint32_t* sp)
+      : ctx(c) {
+    const size_t N = t + 1;
+    if (ctx->overlap && ctx->verify_mode == 0) {
+      buf<uint32_t>(ctx, "Aext", PTB * D * N);
+      buf<uint32_t>(ctx, "Eext", PTB * D * N);
+      HCK(hipEventRecord(ctx->side_fork, ctx->stream));
+      HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
+      dkgk::share_eval(D, n, N, a, b, s, sp, ctx->side);  // K1 (committee.rs:164-167)
+      HCK(hipEventRecord(ctx->shares_done, ctx->side));
+      ctx->shares_pending = true;
+      ctx->r1_a = a;
+      ctx->r1_b = b;
+      ctx->r1_D = D;
+    } else {
+      round1_device(ctx, D, n, t, a, b, nullptr, nullptr, s, sp, false);
+    }
+    check_launch(ctx);
+  }
+  ~BatchRound1() {
+    ctx->r1_a = ctx->r1_b = nullptr;
+    ctx->r1_D = 0;
+    ctx->shares_pending = false;
+  }
+};
+
 // ---- batches of independent ceremonies (BASELINE config 5: many small key ceremonies)
 // B ceremonies of n parties are stacked dealer-wise: dealer c*n + i is party i of ceremony c, and
 // its share row addresses that ceremony's n receivers.  The verification pipeline is the same as
@@ -1180,6 +1231,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
     // round-2 outcome per ceremony (committee.rs:311-316, 340-347, 370-398)
     round2_outcome(ctx, B, n, t, dec2, qmask, qualified.data(), complaints.data(), r2err.data());
     // round 3 (committee.rs:433-476) per ceremony
+    wait_shares(ctx, ctx->stream);  // shares evaluated on the side stream (BatchRound1)
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
     dkgk::fixed_base(V, fs, ctx->tab_gw, pub, ctx->stream);
     dkgk::encode_points(pub, V, V, pubc, ctx->stream);
@@ -2414,7 +2466,7 @@ int dkg_ceremony_batch_device(dkg_ctx* ctx, size_t B, size_t n, size_t t, const 
     uint32_t* Ac = buf<uint32_t>(ctx, "bat_A", 32 * V * N);
     uint32_t* ds = buf<uint32_t>(ctx, "bat_s", 32 * V * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "bat_sp", 32 * V * n);
-    round1_device(ctx, V, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
+    BatchRound1 r1(ctx, V, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, ds, dsp);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     ExtScope ext(ctx, V, N);
     batch_receivers(ctx, B, n, t, Ec, Ac, ds, dsp, out);
