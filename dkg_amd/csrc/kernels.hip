@@ -535,7 +535,7 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
 template <bool CARRY>
 __global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t npad, const uint32_t* __restrict__ C,
                                                                 uint32_t* e, size_t pstride, unsigned gx,
-                                                                unsigned last_piece, int last_off) {
+                                                                unsigned last_piece, int last_off, uint32_t* eT) {
   __shared__ uint32_t qs[PT_WORDS * 64];
   uint32_t* q = qs + threadIdx.x;
   const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
@@ -580,20 +580,34 @@ __global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t 
       mul_small_lds(x, (uint32_t)m, q);  // * m
       // an opaque copy of the base: otherwise the compiler keeps the 40 addresses of the `cur` load
       // (the same words) live across the chain for this store, and spills them
-      uint32_t* eo = eb;
-      asm volatile("" : "+s"(eo));
-      pt_store(eo, S, (size_t)m * npad + lane, x);
+      if (r + 1 < L || !eT) {
+        uint32_t* eo = eb;
+        asm volatile("" : "+s"(eo));
+        pt_store(eo, S, (size_t)m * npad + lane, x);
+      } else {  // the last step writes the stepping's column-major table (no to_column_major pass):
+        // the L positions of a column's word w are one line, filled by this lane within the step
+        uint32_t* eo = eT + col0 * L;
+        asm volatile("" : "+s"(eo));
+        pt_store(eo, S, (size_t)lane * L + m, x);
+      }
     }
+    if (r + 1 < L || !eT) {
 #pragma unroll 8
-    for (int w = 0; w < PT_WORDS; w++) eb[w * S + lane] = cb[w * S + (size_t)(L - 1 - r) * npad + lane];
+      for (int w = 0; w < PT_WORDS; w++) eb[w * S + lane] = cb[w * S + (size_t)(L - 1 - r) * npad + lane];
+    } else {
+      uint32_t* eo = eT + col0 * L;
+#pragma unroll 8
+      for (int w = 0; w < PT_WORDS; w++) eo[w * S + (size_t)lane * L] = cb[w * S + lane];
+    }
   }
 }
 
 uint32_t* binomial_wave(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e, hipStream_t stream,
-                        size_t pieces, size_t pstride, size_t last_len) {
+                        size_t pieces, size_t pstride, size_t last_len, uint32_t* eT) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   hipLaunchKernelGGL(k_binom_wave<DKG_BINOM_WAVE_CARRY != 0>, dim3((unsigned)(width / 64 * pieces)), dim3(64), 0,
-                     stream, (int)N, npad, C, e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off);
+                     stream, (int)N, npad, C, e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off,
+                     eT);
   return e;
 }
 

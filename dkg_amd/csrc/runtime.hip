@@ -607,8 +607,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     }
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
     const uint32_t* e;
-    if (per_wave) {
-      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr);
+    if (per_wave) {  // its last step writes the column-major table itself
+      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr, eT + c0 * L);
     } else {
       dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
       uint32_t *bin = e0 + c0, *bout = e1 + c0;
@@ -631,7 +631,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       e = bin;
     }
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
-    dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping it feeds
+    if (!per_wave) dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     auto step = step_ilp ? dkgk_ilp::stepping : dkgk::stepping;

@@ -3,7 +3,7 @@ set -o pipefail
 R=$(pwd)
 O=$R/gpurun_out/r04e
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu.py tests/test_gpu_scale.py -k "batch or config5 or stepping_tail" > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu.py tests/test_gpu_scale.py -k "batch or config5 or stepping_tail or binomial_schedules" > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for i in 1 2; do
   for v in "" "--no-overlap"; do
@@ -14,3 +14,6 @@ for i in 1 2; do
   DKG_AMD_LIB=$R/ab_build/prev/libdkg_amd.so timeout -k 10 300 python bench.py --config B5 --steps 3 --warmup 1 --no-cpu > $O/b5prev_$i.json 2>$O/err.log || { echo BENCH FAILED; exit 1; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print('prev', round(d['ms_per_step'],1), d['phases_ms'])" $O/b5prev_$i.json
 done
+cd $R
+timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --no-cpu > $O/gloo2.json 2>$O/gloo2.err || { echo GLOO FAILED; tail -20 $O/gloo2.err; exit 1; }
+cat $O/gloo2.json | cut -c1-600
