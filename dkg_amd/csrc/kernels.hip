@@ -216,6 +216,40 @@ void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* 
                      A_ext, E_ext, stride ? stride : count);
 }
 
+// The commitments of dealers [0, D) written straight into the fused verification's position-major
+// table (the deferred round 1 of a batch, runtime.hip BatchRound1): one wave per (64-dealer group,
+// coefficient k), lanes = dealers, so the E and A columns of a group (columns 128 g + lane and
+// 128 g + 64 + lane, piece k / L at position k % L) are written coalesced; no extended-form E/A
+// arrays and no placement pass.  The lanes of k = 0 also write A_i0 (A0 [40][A0stride], finalise).
+__global__ __launch_bounds__(64, 4) void k_commit_pm(size_t D, size_t N, const uint32_t* __restrict__ a,
+                                                   const uint32_t* __restrict__ b,
+                                                   const uint32_t* __restrict__ tab_g,
+                                                   const uint32_t* __restrict__ tab_h, uint32_t* __restrict__ out,
+                                                   size_t W, size_t L, size_t pstride,
+                                                   uint32_t* __restrict__ A0, size_t A0stride) {
+  const size_t g = blockIdx.x, k = blockIdx.y, i = g * 64 + threadIdx.x;
+  if (i >= D) return;
+  sc sa, sb;
+  sc_load(sa, a + 8 * (i * N + k));
+  sc_load(sb, b + 8 * (i * N + k));
+  ge_p3 acc;
+  ge_identity(acc);
+  combw_mul_add(acc, sa, tab_g);                    // apub = G::generator() * a   (committee.rs:155)
+  uint32_t* o = out + (k % L) * W + (k / L) * pstride + g * 128 + threadIdx.x;
+  pt_store(o + 64, L * W, 0, acc);                  // the A column (round 4)
+  if (k == 0) pt_store(A0, A0stride, i, acc);
+  combw_mul_add(acc, sb, tab_h);                    // coeff_comm = h * b + apub   (committee.rs:156)
+  pt_store(o, L * W, 0, acc);                       // the E column (round 2)
+}
+
+void commit_position_major(size_t D, size_t N, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g,
+                           const uint32_t* tab_h, uint32_t* out, size_t W, size_t L, size_t pstride, uint32_t* A0,
+                           size_t A0stride, hipStream_t stream) {
+  if (!D || !N) return;
+  hipLaunchKernelGGL(k_commit_pm, dim3((unsigned)((D + 63) / 64), (unsigned)N), dim3(64), 0, stream, D, N, a, b, tab_g,
+                     tab_h, out, W, L, pstride, A0, A0stride);
+}
+
 // ------------------------------------------------------------------ K1 share evaluation
 // Horner at x = j+1: identical field value to the power-sum of polynomial.rs:68-74.  One thread per
 // (dealer i, receiver j), flattened (the dealer count of a batch of ceremonies exceeds grid.y).

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -82,6 +83,7 @@ struct dkg_ctx {
   const uint32_t* r1_a = nullptr;
   const uint32_t* r1_b = nullptr;
   size_t r1_D = 0;
+  uint32_t* r1_A0 = nullptr;            // [40][r1_D]: A_i0 of the deferred commitments (finalise)
   size_t ext_stride = 0;
   // share rows [shard_D][shard_n][8] of the last sharded call's dealers [shard_d0, +shard_D)
   // (arena-owned; dkg_ceremony_shard_recon_device reads them after the exchange)
@@ -541,7 +543,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   if (npad != D * nseg || U * L != N) dkgk::fill_identity(L * W, Cpm, home);
   HCK(hipMemsetAsync(pok, 1, npad * N, home));
   // deferred round 1 (BatchRound1): the fused pass over the very dealers whose coefficients wait
-  const bool defer_r1 = ctx->r1_a && nseg == 2 && ctx->ext_E && D == ctx->r1_D && ctx->ext_stride == D * N;
+  const bool defer_r1 = ctx->r1_a && nseg == 2 && D == ctx->r1_D;
   for (int k = 0; k < nseg && !defer_r1; k++) {
     const uint32_t* ext = segs[k].round == 2 ? ctx->ext_E : ctx->ext_A;
     if (ext)  // generated on this device: group elements, as the reference's broadcasts carry them
@@ -596,14 +598,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   uint32_t* tail_b = tails ? buf<uint32_t>(ctx, "v.tail_b", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
   auto chunk = [&](size_t g0, size_t g1, hipStream_t st, bool tm) {
     const size_t c0 = g0 * gw, w = (g1 - g0) * gw;
-    if (defer_r1) {  // this chunk's dealers' commitments (committee.rs:151-159), then their columns
+    if (defer_r1) {  // this chunk's dealers' commitments (committee.rs:151-159), into their columns
       const size_t d0 = g0 * 64, d1 = std::min(D, g1 * 64);
-      uint32_t* Ae = const_cast<uint32_t*>(ctx->ext_A) + d0 * N;
-      uint32_t* Ee = const_cast<uint32_t*>(ctx->ext_E) + d0 * N;
-      dkgk::commit((d1 - d0) * N, ctx->r1_a + d0 * N * 8, ctx->r1_b + d0 * N * 8, ctx->tab_gw, ctx->tab_hw, Ae, Ee,
-                   st, D * N);
-      dkgk::place_position_major(Ee, D * N, d1 - d0, N, W, Cpm + c0, st, nseg, 0, L, npad);
-      dkgk::place_position_major(Ae, D * N, d1 - d0, N, W, Cpm + c0, st, nseg, 1, L, npad);
+      dkgk::commit_position_major(d1 - d0, N, ctx->r1_a + d0 * N * 8, ctx->r1_b + d0 * N * 8, ctx->tab_gw,
+                                  ctx->tab_hw, Cpm + c0, W, L, npad, ctx->r1_A0 + d0, D, st);
     }
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
     const uint32_t* e;
@@ -1187,9 +1185,7 @@ struct BatchRound1 {
               uint32_t* sp)
       : ctx(c) {
     const size_t N = t + 1;
-    if (ctx->overlap && ctx->verify_mode == 0) {
-      buf<uint32_t>(ctx, "Aext", PTB * D * N);
-      buf<uint32_t>(ctx, "Eext", PTB * D * N);
+    if (deferred()) {
       HCK(hipEventRecord(ctx->side_fork, ctx->stream));
       HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
       dkgk::share_eval(D, n, N, a, b, s, sp, ctx->side);  // K1 (committee.rs:164-167)
@@ -1198,14 +1194,17 @@ struct BatchRound1 {
       ctx->r1_a = a;
       ctx->r1_b = b;
       ctx->r1_D = D;
+      ctx->r1_A0 = buf<uint32_t>(ctx, "r1_A0", PTB * D);
     } else {
       round1_device(ctx, D, n, t, a, b, nullptr, nullptr, s, sp, false);
     }
     check_launch(ctx);
   }
+  bool deferred() const { return ctx->overlap && ctx->verify_mode == 0; }
   ~BatchRound1() {
     ctx->r1_a = ctx->r1_b = nullptr;
     ctx->r1_D = 0;
+    ctx->r1_A0 = nullptr;
     ctx->shares_pending = false;
   }
 };
@@ -1264,7 +1263,9 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   }
   // finalise (committee.rs:726-805): mpk_c = sum of honest A_i0 (+ g * reconstructed secrets)
   uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
-  if (ctx->ext_A) {
+  if (ctx->r1_A0) {  // written by the deferred commitments (k_commit_pm), [40][V]
+    HCK(hipMemcpyAsync(A0, ctx->r1_A0, PTB * V, hipMemcpyDeviceToDevice, ctx->stream));
+  } else if (ctx->ext_A) {
     dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, V, A0, V, ctx->stream);
   } else {
     uint32_t* A0c = buf<uint32_t>(ctx, "b.A0c", 32 * V);
@@ -2468,7 +2469,9 @@ int dkg_ceremony_batch_device(dkg_ctx* ctx, size_t B, size_t n, size_t t, const 
     uint32_t* dsp = buf<uint32_t>(ctx, "bat_sp", 32 * V * n);
     BatchRound1 r1(ctx, V, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, ds, dsp);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
-    ExtScope ext(ctx, V, N);
+    // round 1 in extended form for the verification: from the deferred commitments' position-major
+    // table (BatchRound1), else from round1_device's E/A arrays
+    std::unique_ptr<ExtScope> ext(r1.deferred() ? nullptr : new ExtScope(ctx, V, N));
     batch_receivers(ctx, B, n, t, Ec, Ac, ds, dsp, out);
     batch_times(ctx, out, true);
     return DKG_OK;

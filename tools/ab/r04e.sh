@@ -17,3 +17,7 @@ done
 cd $R
 timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --no-cpu > $O/gloo2.json 2>$O/gloo2.err || { echo GLOO FAILED; tail -20 $O/gloo2.err; exit 1; }
 cat $O/gloo2.json | cut -c1-600
+for f in 0 2 0 2; do
+  timeout -k 10 300 python bench.py --steps 6 --warmup 1 --no-cpu --no-interp --field $f > $O/d_field$f.json 2>$O/err.log || { echo FIELD FAILED; exit 1; }
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print('field', sys.argv[2], round(d['ms_per_step'],2), {k:v['ms_per_pass'] for k,v in d['roofline']['all_kernels'].items()})" $O/d_field$f.json $f
+done
