@@ -26,7 +26,7 @@ Zl zl_mul(const Zl& a, const Zl& b);
 Zl zl_inv(const Zl& a);
 bool zl_is_zero(const Zl& a);
 
-// lattice.cpp: a short (b, a_1, .., a_{K-1}) with a_u = b y^u (mod l), b > 0, 2 <= K <= 4, as
+// lattice.cpp: a short (b, a_1, .., a_{K-1}) with a_u = b y^u (mod l), b > 0, 2 <= K <= 5, as
 // magnitudes (32 bytes LE) and signs; (1, y, .., y^(K-1)) when no shorter row checks out.
 bool short_multipliers(const Zl& y, int K, uint8_t (*mag)[32], int8_t* sign);
 

@@ -1147,6 +1147,12 @@ DKG_DEV bool higher_digits(uint32_t w) {
   if constexpr (U + 1 < K) return (w >> (8 * (U + 1))) != 0;
   else return false;
 }
+// the same over the 64-bit digit word of up to 8 pieces (k_combine_aff: piece u in byte u)
+template <int U, int K>
+DKG_DEV bool higher_digits64(uint64_t w) {
+  if constexpr (U + 1 < K) return (w >> (8 * (U + 1))) != 0;
+  else return false;
+}
 
 template <int U, int K, int KL>
 DKG_DEV void short_addends(uint32_t* qs, ge_cached* qr, const uint32_t* R, size_t pstride, size_t cc, size_t nrecv,
@@ -1391,11 +1397,11 @@ DKG_DEV void aff_addends(uint32_t* qs, ge_aff* qr, const uint32_t* A, size_t pst
   }
 }
 template <int U, int K, int KL>
-DKG_DEV void aff_position(ge_p3& acc, uint32_t w, const uint32_t* qs, const ge_aff* qr, bool last) {
+DKG_DEV void aff_position(ge_p3& acc, uint64_t w, const uint32_t* qs, const ge_aff* qr, bool last) {
   if constexpr (U < K) {
     const int e = (int8_t)(w >> (8 * U));
     if (e != 0) {
-      const bool t = last || higher_digits<U, K>(w);  // else a doubling follows: no T
+      const bool t = last || higher_digits64<U, K>(w);  // else a doubling follows: no T
       if constexpr (U < KL) ge_madd_lds(acc, acc, qs + U * AFF_WORDS * 64 + threadIdx.x, e < 0, 64, t);
       else ge_madd_signed(acc, acc, qr[U - KL], e < 0, t);
     }
@@ -1416,13 +1422,16 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
   const size_t cc = live ? c : 0;
   ge_aff qr[K - KL > 0 ? K - KL : 1];
   aff_addends<0, K, KL>(qs, qr, A, pstride, cc, nrecv, j);
+  // digit words: pieces 0..3 in word 0 (digits[j][b]), pieces 4.. in word 1 (digits + nrecv * 256)
   const uint32_t* dw = digits + j * 256;
+  const uint32_t* dw1 = digits + (nrecv + j) * 256;
   const int tp = top[j];
   ge_p3 acc;
   ge_identity(acc);
 #pragma unroll 1
   for (int b = tp; b >= 0; b--) {
-    const uint32_t w = __builtin_amdgcn_readfirstlane(dw[b]);
+    uint64_t w = __builtin_amdgcn_readfirstlane(dw[b]);
+    if constexpr (K > 4) w |= (uint64_t)__builtin_amdgcn_readfirstlane(dw1[b]) << 32;
     if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
     aff_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
@@ -1432,14 +1441,16 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
 void combine_short_aff(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* digits,
                        const int16_t* top, const uint32_t* A, uint32_t* R, hipStream_t stream, size_t j0, size_t jn) {
   if (!jn) jn = nrecv - j0;
-  if (!width || !jn || pieces < 2 || pieces > 4) return;
+  if (!width || !jn || pieces < 2 || pieces > 5) return;
   const dim3 grid((unsigned)((width + 63) / 64), (unsigned)jn);
   if (pieces == 2)
     hipLaunchKernelGGL((k_combine_aff<2, 1>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
   else if (pieces == 3)
     hipLaunchKernelGGL((k_combine_aff<3, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
-  else
+  else if (pieces == 4)
     hipLaunchKernelGGL((k_combine_aff<4, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
+  else
+    hipLaunchKernelGGL((k_combine_aff<5, 2>), grid, dim3(64), 0, stream, width, pstride, nrecv, digits, top, A, R, j0);
 }
 
 void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const int8_t* digits, const int16_t* top,

@@ -149,7 +149,7 @@ Zl zl_of(const I512& a) {  // a mod l for |a| < 2^512
   return neg ? zl_sub(zl_from_u64(0), z) : z;
 }
 
-const int KMAX = 4;
+const int KMAX = 5;
 
 // v -= q v_j for the long double integer q
 void sub_multiple(I512* v, const I512* vj, int K, long double q) {
@@ -236,9 +236,10 @@ bool short_multipliers(const Zl& y, int K, uint8_t (*mag)[32], int8_t* sign) {
   // whose first nonzero coefficient is positive are priced.  Integer combinations of lattice rows
   // are lattice rows: the Z_l check of the winner below is a safety net.
   // coefficients in {-4..4} (6561 combinations at K = 4, ~0.5 s once per (n, L, U) on 16 threads):
-  // 1.0 % less recombination work than {-2..2} (625), which was 0.9 % below {-1..1}
-  const int CR = 4;
-  I512 mult[KMAX][2 * CR + 1][KMAX];  // mult[i][c + CR] = c B_i, |c| <= CR
+  // 1.0 % less recombination work than {-2..2} (625), which was 0.9 % below {-1..1}; K = 5 keeps
+  // {-2..2} (3125 combinations; {-4..4} would be 59049)
+  const int CRMAX = 4, CR = K <= 4 ? 4 : 2;
+  I512 mult[KMAX][2 * CRMAX + 1][KMAX];  // mult[i][c + CR] = c B_i, |c| <= CR
   for (int i = 0; i < K; i++)
     for (int c = -CR; c <= CR; c++)
       for (int u = 0; u < K; u++) mult[i][c + CR][u] = i_mul_shift(B[i][u], c, 0);

@@ -61,8 +61,8 @@ struct dkg_ctx {
   int last_split = 1;                   // U used by the last verify_device
   size_t last_split_len = 0;            // and its piece length L
   size_t ydig_n = 0, ydig_L = 0;        // key of the cached combine multipliers (v.ydig)
-  int combine_mode = 0;                 // recombination: 0 short vectors for U <= 4, 1 powers of y,
-                                        // 2 short vectors (U <= 4)
+  int combine_mode = 0;                 // recombination: 0 short vectors for U <= 5 (4 with
+                                        // projective addends), 1 powers of y, 2 = 0
   int last_combine = 0;                 // 1: the last verify_device recombined with powers, 2: short vectors
   int last_binomial = 0;                // 1: the last verify_device ran the per-wave binomial
   int step_formula = 0;                 // stepping additions: 0 dedicated + complete redo of marked
@@ -274,6 +274,10 @@ bool stepping_whole_pays(size_t cols, size_t U, size_t L, size_t Lr) {
 // kernels; the check does not depend on U) in SIMD
 // cycles: a SIMD retires one wave instruction per ~4.5 cycles of this mix when it has >= 2 waves,
 // one per ~8 when a lone wave runs a dependent chain (tools/ubench/ilp.hip); 1024 SIMDs.
+// Short multipliers are implemented up to this many pieces (k_combine_aff's digit words; the
+// projective-addend k_combine_short stops at 4)
+constexpr size_t SHORT_MAX = 5;
+
 double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L, bool short_mult) {
   const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAT_ILP = 6, LAUNCH = 3e-3 * 2.4e6;
   const size_t Lr = last_piece_len(N, U, L), off = L - Lr;  // the last piece: Lr positions, starts at step off
@@ -310,7 +314,7 @@ double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L, bool 
     // product (253 doublings + ~85 NAF additions), then (ceil(U/2) - 1) joint y^2 / y steps (253
     // doublings + ~170 additions)
     const double bits = 253.0 * (U - 1) / U;
-    const double per = short_mult && U <= 4 ? bits * 950 + U * bits / 3 * ADD
+    const double per = short_mult && U <= SHORT_MAX ? bits * 950 + U * bits / 3 * ADD
                                             : (U % 2 == 0 ? 253 * 950 + 85 * ADD : 0.0) +
                                                   ((U + 1) / 2 - 1) * (253 * 950 + 170 * ADD);
     const double waves = (double)cols / 64 * n;
@@ -347,7 +351,7 @@ size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
   size_t umax = 1;
   for (size_t U = 2; U <= 16; U++) {
     if (N < 64 * U) break;  // pieces of degree < 63: the binomial is cheap already
-    ms[U] = split_model_ms(cols, n, N, U, sm);
+    ms[U] = split_model_ms(cols, n, N, U, sm && (ctx->addend_mode == 0 || U <= 4));
     best_ms = std::min(best_ms, ms[U]);
     umax = U;
   }
@@ -440,7 +444,7 @@ void short_vectors(size_t n, size_t L, size_t K, std::vector<uint8_t>& mag, std:
 
 void split_short(dkg_ctx* ctx, size_t n, size_t L, size_t K, const uint32_t** digits, const int16_t** top,
                  const uint32_t** scale) {
-  uint32_t* dd = buf<uint32_t>(ctx, "v.sdig", 4 * 256 * n);
+  uint32_t* dd = buf<uint32_t>(ctx, "v.sdig", 2 * 4 * 256 * n);  // word 0: pieces 0..3, word 1: 4..
   int16_t* dt = buf<int16_t>(ctx, "v.stop", 2 * n);
   uint32_t* ds = buf<uint32_t>(ctx, "v.sscale", 32 * n);
   *digits = dd;
@@ -450,7 +454,7 @@ void split_short(dkg_ctx* ctx, size_t n, size_t L, size_t K, const uint32_t** di
   std::vector<uint8_t> mag;
   std::vector<int8_t> sign;
   short_vectors(n, L, K, mag, sign);
-  std::vector<uint32_t> hd(256 * n, 0), hs(8 * n, 0);
+  std::vector<uint32_t> hd(2 * 256 * n, 0), hs(8 * n, 0);
   std::vector<int16_t> ht(n, -1);
   uint8_t r256[33] = {0};
   r256[32] = 1;
@@ -462,7 +466,7 @@ void split_short(dkg_ctx* ctx, size_t n, size_t L, size_t K, const uint32_t** di
       naf_digits(&mag[(j * K + u) * 32], d, &tp);
       ht[j] = std::max(ht[j], tp);
       for (int b = 0; b < 256; b++)
-        hd[256 * j + b] |= (uint32_t)(uint8_t)(int8_t)(d[b] * sign[j * K + u]) << (8 * u);
+        hd[(u / 4) * 256 * n + 256 * j + b] |= (uint32_t)(uint8_t)(int8_t)(d[b] * sign[j * K + u]) << (8 * (u % 4));
     }
     const dkgh::Zl b = dkgh::zl_from_bytes_wide(&mag[j * K * 32], 32);  // b > 0
     uint8_t w[32];
@@ -526,7 +530,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const int16_t* ytop = nullptr;
   const uint32_t *sdig = nullptr, *sscale = nullptr;  // short multipliers: R holds b_j P(j)
   const int16_t* stop = nullptr;
-  const bool short_mult = U > 1 && U <= 4 && ctx->combine_mode != 1;
+  // short multipliers up to SHORT_MAX pieces with affine addends, 4 with projective ones
+  const bool short_mult = U > 1 && U <= (ctx->addend_mode == 0 ? SHORT_MAX : 4) && ctx->combine_mode != 1;
   // stepping flags of the dedicated additions: chunk c0's words start at stepping_flag_words(c0, U)
   uint32_t* sflags = ctx->step_formula == 0
                          ? buf<uint32_t>(ctx, "v.sflags", 4 * dkgk::stepping_flag_words(npad, U)) : nullptr;
@@ -1651,7 +1656,7 @@ int dkg_ctx_set_addends(dkg_ctx* ctx, int mode) {
   return DKG_OK;
 }
 int dkg_split_multipliers(size_t n, size_t L, int pieces, uint8_t* mag, int8_t* sign) {
-  if (!n || !L || pieces < 2 || pieces > 4 || !mag || !sign) return DKG_E_ARG;
+  if (!n || !L || pieces < 2 || pieces > (int)SHORT_MAX || !mag || !sign) return DKG_E_ARG;
   try {
     std::vector<uint8_t> m;
     std::vector<int8_t> sg;

@@ -100,10 +100,11 @@ size_t dkg_ctx_last_split_len(const dkg_ctx *ctx);
 double dkg_split_model_ms(size_t columns, size_t n, size_t t, int pieces);
 /* The piece length L the runtime uses for a `pieces`-way split of such tables (0 on bad input). */
 size_t dkg_split_len(size_t columns, size_t n, size_t t, int pieces);
-/* Recombination of a degree split: 0 (default) short multipliers for 2..4 pieces -- receiver j's
- * pieces are combined as b_j P(j) = b_j Q_0(j) + a_j1 Q_1(j) + .. with a short lattice vector
- * (b_j, a_j1, ..), a_ju = b_j j^(uL) mod l (126 / 168 / 189-bit scalars for 2 / 3 / 4 pieces
- * instead of 253), and the checks compare with g*(b_j s) + h*(b_j s'); 1 powers of y = j^L (253-bit
+/* Recombination of a degree split: 0 (default) short multipliers for 2..5 pieces (2..4 with
+ * projective addends) -- receiver j's pieces are combined as b_j P(j) = b_j Q_0(j) + a_j1 Q_1(j) + ..
+ * with a short lattice vector (b_j, a_j1, ..), a_ju = b_j j^(uL) mod l (126 / 168 / 189 / 202-bit
+ * scalars for 2 / 3 / 4 / 5 pieces instead of 253), and the checks compare with g*(b_j s) +
+ * h*(b_j s'); 1 powers of y = j^L (253-bit
  * NAFs, pairwise Horner in y^2, any number of pieces); 2 = 0.  Decisions do not depend on it
  * (DESIGN.md section 2). */
 int dkg_ctx_set_combine(dkg_ctx *ctx, int mode);
@@ -125,7 +126,7 @@ int dkg_ctx_set_stepping_formula(dkg_ctx *ctx, int mode);
  * (synchronises the context's stream; 0 in mode 1; -1 on error). */
 long long dkg_ctx_stepping_redos(dkg_ctx *ctx);
 /* The short multipliers (b_j, a_j1, .., a_j(U-1)) of receivers j = 1..n for a `pieces`-way split of
- * piece length L (2 <= pieces <= 4): magnitudes mag[n][pieces][32] (little-endian), signs
+ * piece length L (2 <= pieces <= 5): magnitudes mag[n][pieces][32] (little-endian), signs
  * sign[n][pieces] (+1 / -1); a_ju = b_j j^(uL) mod l and b_j > 0.  DKG_E_ARG on bad input. */
 int dkg_split_multipliers(size_t n, size_t L, int pieces, uint8_t *mag, int8_t *sign);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
