@@ -492,6 +492,102 @@ class Backend:
         _check(self._ctx, _lib.lib().dkg_point_sum_device(self._ctx, count, vp(d_points), vp(d_mask), vp(d_out)))
 
 
+class _ShardView(Backend):
+    """A shard's dkg_ctx inside a MultiBackend (owned by the multi-device context: close is a no-op)."""
+
+    def __init__(self, ctx, owner):
+        self._ctx, self.h, self._owner = ctx, None, owner
+
+    def close(self):
+        self._ctx = None
+
+
+class MultiBackend:
+    """Several GPUs driven from ONE process (dkg_multi_*, SURVEY.md section 8(b) threading row): the
+    ceremony sharded by dealer over `devices`, exchanged by peer copies into devices[0], combined and
+    finalised there.  Results equal Backend.ceremony / ceremony_verify's except that E, A, s,
+    s_prime are not returned (they stay on the shards' devices).  A device may repeat."""
+
+    def __init__(self, devices):
+        L = _lib.lib()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        rc = L.dkg_multi_create(devs, len(devices), ctypes.byref(h))
+        if rc != _lib.DKG_OK:
+            raise DkgError(rc, f"dkg_multi_create(devices={list(devices)}) failed (are gfx950 GPUs visible?)")
+        self._m = h
+        self.devices = list(devices)
+        self.h: Optional[bytes] = None
+
+    def close(self):
+        if self._m:
+            _lib.lib().dkg_multi_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != _lib.DKG_OK:
+            raise DkgError(rc, _lib.lib().dkg_multi_last_error(self._m).decode())
+
+    def __len__(self):
+        return _lib.lib().dkg_multi_size(self._m)
+
+    def shard(self, i: int) -> Backend:
+        """Shard i's context, for its tuning knobs (set_split, set_streams, ...)."""
+        ctx = _lib.lib().dkg_multi_ctx(self._m, i)
+        if not ctx:
+            raise DkgError(_lib.DKG_E_ARG, f"no shard {i}")
+        return _ShardView(ctypes.c_void_p(ctx), self)
+
+    def phase_ms(self) -> dict:
+        L = _lib.lib()
+        return {k: L.dkg_multi_phase_ms(self._m, k.encode())
+                for k in ("shard_max", "shard_min", "exchange", "combine", "recon", "finalise")}
+
+    def env_init(self, threshold: int, nr_members: int, ck_gen_bytes: bytes = CK_DEFAULT) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        self._check(_lib.lib().dkg_multi_env_init(self._m, threshold, nr_members, ck_gen_bytes, len(ck_gen_bytes),
+                                                  out))
+        self.h = out.raw
+        return out.raw
+
+    def _out(self, n, t):
+        o, bufs = Backend._ceremony_out(None, n, t, True)
+        for k in ("E", "A", "s", "s_prime"):
+            setattr(o, k, None)
+        return o, bufs
+
+    def _result(self, n, t, o, bufs):
+        r = Backend._result(None, n, t, o, bufs, False)
+        for k in ("dec2", "dec4", "final_share", "public_share"):
+            setattr(r, k, bufs[k].raw)
+        return r
+
+    def ceremony(self, a: bytes, b: bytes, n: int, t: int) -> CeremonyResult:
+        o, bufs = self._out(n, t)
+        self._check(_lib.lib().dkg_multi_ceremony_run(self._m, n, t, a, b, ctypes.byref(o)))
+        return self._result(n, t, o, bufs)
+
+    def ceremony_device(self, d_as, d_bs, n: int, t: int) -> CeremonyResult:
+        """d_as[i], d_bs[i]: device pointers on devices[i] to shard i's dealers' coefficients."""
+        k = len(self.devices)
+        pa = (ctypes.c_void_p * k)(*d_as)
+        pb = (ctypes.c_void_p * k)(*d_bs)
+        o, bufs = self._out(n, t)
+        self._check(_lib.lib().dkg_multi_ceremony_run_device(self._m, n, t, pa, pb, ctypes.byref(o)))
+        return self._result(n, t, o, bufs)
+
+    def ceremony_verify(self, E: bytes, A: bytes, s: bytes, s_prime: bytes, n: int, t: int) -> CeremonyResult:
+        o, bufs = self._out(n, t)
+        self._check(_lib.lib().dkg_multi_ceremony_verify(self._m, n, t, E, A, s, s_prime, ctypes.byref(o)))
+        return self._result(n, t, o, bufs)
+
+
 @dataclass
 class ShardOutcome:
     """The common outcome of a sharded ceremony (dkg_shard_combine_device), identical on every rank."""

@@ -326,6 +326,43 @@ int dkg_shard_finalise_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_siz
                               const void *d_partials_g, const uint8_t *qualified, int phase4_error,
                               void *d_final_share, void *d_public_share, uint8_t *mpk);
 
+/* ---- in-library multi-device context: ONE process, several GPUs (SURVEY.md section 8(b),
+ * threading row; dkg_amd/csrc/multi.cpp) ----
+ * The same dealer sharding as the one-process-per-GPU protocol above, driven inside the library:
+ * shard i (on devices[i]) owns dealers dkg_shard_range(n, ndev, i) and runs them on its own host
+ * thread; the exchange is a gather of every shard's rows, master-key terms and partial shares into
+ * devices[0] by peer copies over xGMI; the combine, the round-4 reconstruction (on the owning
+ * shards) and the finalise are the dkg_shard_* steps.  Outputs equal dkg_ceremony_run /
+ * dkg_ceremony_verify's.  A device may be listed more than once (its shards share the GPU).
+ * The reference is single-threaded and has no transport (src/lib.rs:91-115); this replaces the
+ * caller's loop over parties (committee.rs:1518-1656) spread over a node's GPUs.  Not re-entrant
+ * on the same context. */
+typedef struct dkg_multi dkg_multi;
+int dkg_multi_create(const int *devices, int ndev, dkg_multi **out);
+void dkg_multi_destroy(dkg_multi *m);
+int dkg_multi_size(const dkg_multi *m);
+/* shard i's dkg_ctx (its tuning knobs: dkg_ctx_set_split, _set_streams, ...); owned by m */
+dkg_ctx *dkg_multi_ctx(dkg_multi *m, int shard);
+const char *dkg_multi_last_error(const dkg_multi *m);
+/* host wall milliseconds of the last ceremony's steps: "shard_max" / "shard_min" (the shards' device
+ * times), "exchange", "combine", "recon", "finalise"; -1 if unknown */
+double dkg_multi_phase_ms(const dkg_multi *m, const char *name);
+/* Environment::init (committee.rs:72-83) on every shard's context */
+int dkg_multi_env_init(dkg_multi *m, size_t threshold, size_t nr_members, const uint8_t *ck_bytes, size_t ck_len,
+                       uint8_t h_out[32]);
+/* dkg_ceremony_run over the shards: a, b host [n][t+1][32].  out->E, A, s, s_prime must be NULL
+ * (they stay on the shards' devices); every other output as dkg_ceremony_run.  Times: ms_round2 =
+ * the slowest shard, ms_round3 = exchange, ms_round4 = combine + reconstruction, ms_finalise,
+ * ms_total = host wall from the shards' start (after the uploads) to the outputs. */
+int dkg_multi_ceremony_run(dkg_multi *m, size_t n, size_t t, const uint8_t *a, const uint8_t *b,
+                           dkg_ceremony_out *out);
+/* d_a[i], d_b[i]: device pointers on devices[i] to shard i's dealers' coefficients [D_i][t+1][32] */
+int dkg_multi_ceremony_run_device(dkg_multi *m, size_t n, size_t t, const void *const *d_a, const void *const *d_b,
+                                  dkg_ceremony_out *out);
+/* dkg_ceremony_verify over the shards (received broadcasts, host arrays as there) */
+int dkg_multi_ceremony_verify(dkg_multi *m, size_t n, size_t t, const uint8_t *E, const uint8_t *A, const uint8_t *s,
+                              const uint8_t *s_prime, dkg_ceremony_out *out);
+
 /* ---- per-party finalise: Phases<Phase5>::finalise (committee.rs:726-805) as EVERY party p runs it ----
  * Inputs are the ceremony's common outcome (host arrays [n]): qualified, reconstruct (round 4,
  * committee.rs:660-670), r2_error / r4_error (may be NULL: a party whose Phase1 / Phase3 proceed failed

@@ -60,6 +60,8 @@ def test_no_gpu_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(dkg_amd.DkgError):
         dkg_amd.Backend(0)
+    with pytest.raises(dkg_amd.DkgError):
+        dkg_amd.MultiBackend([0, 0])
 
 
 @pytest.mark.parametrize("name", ["full_n4_t1.json", "full_n10_t4.json"])

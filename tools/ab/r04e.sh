@@ -4,7 +4,7 @@ set -o pipefail
 R=$(pwd)
 O=$R/gpurun_out/r04e
 mkdir -p $O
-timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu.py tests/test_gpu_scale.py -k "batch or config5 or stepping_tail or binomial_schedules or combine_modes or split or recombination_modes or faults_baseline" > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_multi.py tests/test_gpu.py tests/test_gpu_scale.py -k "multi or batch or config5 or stepping_tail or binomial_schedules or combine_modes or split or recombination_modes or faults_baseline" > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for v in "" "--no-overlap"; do
   tag=b5$(echo $v | tr -d ' -')
