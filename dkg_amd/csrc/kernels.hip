@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void k_share_eval(size_t D, size_t n, size_t N
   size_t i = e / n;
   const size_t j = e % n;
   // n % 64 == 0: a wave's lanes share the dealer, so its coefficients are scalar (broadcast) loads
-  if (n % 64 == 0) i = (size_t)__builtin_amdgcn_readfirstlane((uint32_t)i);
+  if (n % 64 == 0) i = (size_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)i);
   const uint32_t x = (uint32_t)(j + 1);
   const uint32_t* ai = a + 8 * i * N;
   const uint32_t* bi = b + 8 * i * N;
@@ -580,8 +580,11 @@ __global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t 
   const uint32_t lane = threadIdx.x;
   const size_t S = (size_t)L * npad;
   const int off = piece == last_piece ? last_off : 0;
+  // one position: no step follows, so the top coefficient goes straight into the column-major
+  // table (with L = 1 both layouts are [40][npad])
+  uint32_t* e_top = (L == 1 && eT) ? eT + col0 : eb;
 #pragma unroll 8
-  for (int w = 0; w < PT_WORDS; w++) eb[w * S + lane] = cb[w * S + (size_t)(L - 1) * npad + lane];
+  for (int w = 0; w < PT_WORDS; w++) e_top[w * S + lane] = cb[w * S + (size_t)(L - 1) * npad + lane];
 #pragma unroll 1
   for (int r = 1; r < L; r++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores land before it rereads them
@@ -1430,8 +1433,10 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
   ge_identity(acc);
 #pragma unroll 1
   for (int b = tp; b >= 0; b--) {
-    uint64_t w = __builtin_amdgcn_readfirstlane(dw[b]);
-    if constexpr (K > 4) w |= (uint64_t)__builtin_amdgcn_readfirstlane(dw1[b]) << 32;
+    // readfirstlane returns a signed int: zero-extend, or a negative piece-3 digit would sign-fill
+    // the bytes of pieces 4..7
+    uint64_t w = (uint32_t)__builtin_amdgcn_readfirstlane(dw[b]);
+    if constexpr (K > 4) w |= (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(dw1[b]) << 32;
     if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
     aff_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
