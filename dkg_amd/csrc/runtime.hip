@@ -277,6 +277,9 @@ bool stepping_whole_pays(size_t cols, size_t U, size_t L, size_t Lr) {
 // Short multipliers are implemented up to this many pieces (k_combine_aff's digit words; the
 // projective-addend k_combine_short stops at 4)
 constexpr size_t SHORT_MAX = 5;
+#ifndef DKG_AUTO_SHORT5
+#define DKG_AUTO_SHORT5 0
+#endif
 
 double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L, bool short_mult) {
   const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAT_ILP = 6, LAUNCH = 3e-3 * 2.4e6;
@@ -351,7 +354,11 @@ size_t choose_split(dkg_ctx* ctx, size_t cols, size_t n, size_t N) {
   size_t umax = 1;
   for (size_t U = 2; U <= 16; U++) {
     if (N < 64 * U) break;  // pieces of degree < 63: the binomial is cheap already
-    ms[U] = split_model_ms(cols, n, N, U, sm && (ctx->addend_mode == 0 || U <= 4));
+    // five-piece short multipliers are priced for the automatic choice only with DKG_AUTO_SHORT5:
+    // they are parity-tested (forced splits) but their shard timings are unmeasured, so by default
+    // the model ranks U = 5 with powers as before (it then never wins) -- dkg_ctx_set_split(5)
+    // runs them
+    ms[U] = split_model_ms(cols, n, N, U, sm && (U <= 4 || (ctx->addend_mode == 0 && DKG_AUTO_SHORT5)));
     best_ms = std::min(best_ms, ms[U]);
     umax = U;
   }

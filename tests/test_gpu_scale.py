@@ -116,13 +116,14 @@ def _check_rows(n, dec2, dec4, qualified, exp, ctx):
 
 
 @pytest.mark.parametrize("n,t,split,combine", [(256, 127, 0, 0), (1024, 511, 0, 0), (1024, 511, 2, 0),
-                                               (1024, 511, 3, 0), (1024, 511, 3, 1), (1024, 511, 5, 0)])
+                                               (1024, 511, 3, 0), (1024, 511, 3, 1), (1024, 511, 5, 0),
+                                               (1024, 511, 5, 1), (1024, 511, 6, 0)])
 def test_faults_baseline_sizes(be, n, t, split, combine):
     """Configs 2 and 3 with the default schedule (for n=1024 the headline one: U=4 from the cost
     model, pieces of 128 positions recombined with short lattice multipliers, every piece of a
     column in one 512-lane stepping workgroup, two dealer-chunk streams, rounds 2 and 4 fused), and
     forced U=2 / U=3 (171 + 171 + 170, the last piece a step late; short multipliers and powers of
-    j^L) / U=5 (powers, pairwise Horner in y^2): tampered shares, randomness, E and A
+    j^L) / U=5 (five-piece short multipliers, and powers) / U=6 (powers, pairwise Horner in y^2): tampered shares, randomness, E and A
     coefficients, an undecodable E row and a tampered self-share.  Whole rows of every tampered
     dealer equal the oracle's per-pair MSM checks; qualification, reconstruction, final shares and
     the final parties' mpk follow the reference's rules (committee.rs:311-398, 454-467, 660-805)."""
@@ -144,7 +145,7 @@ def test_faults_baseline_sizes(be, n, t, split, combine):
         assert U == split
     elif n == 1024:
         assert U == 4, "the headline schedule uses the cost model's U=4 at n=1024"
-    assert comb == (0 if U == 1 else 1 if (combine == 1 or U > 4) else 2)
+    assert comb == (0 if U == 1 else 1 if (combine == 1 or U > 5) else 2)
     assert sorted(faulty) == [0, 1, 2, 3, 4]
     exp = _expected_rows(n, t, h, E, A, s, sp)
     qualified = [0 if i in (0, 1, 3, 4) else 1 for i in range(n)]
@@ -322,7 +323,7 @@ def test_batch_faulty_members_at_scale(be, golden):
 @pytest.mark.parametrize("n,t", [(130, 64), (300, 149), (517, 258)])
 def test_recombination_modes_agree_on_faults(be, n, t):
     """Ragged sizes with tampered dealers (shares, E, A, an undecodable row, randomness): every split
-    U = 2..4 recombined with short lattice multipliers, U = 3..4 with powers of j^L and U = 5 give the
+    U = 2..5 recombined with short lattice multipliers, U = 3..5 with powers of j^L and U = 6 give the
     same decision matrices, qualification and mpk as the unsplit tables."""
     be.env_init(t, n, CK)
     a, b = dkg_amd.dealer_coefficients(bytes([t % 251]) * 32, 5, 0, n, t)
@@ -331,13 +332,14 @@ def test_recombination_modes_agree_on_faults(be, n, t):
     runs = {}
     try:
         for split, comb, add in ((1, 0, 0), (2, 0, 0), (3, 0, 0), (4, 0, 0), (2, 0, 1), (3, 0, 1), (4, 0, 1),
-                                 (3, 1, 0), (4, 1, 0), (5, 0, 0)):
+                                 (3, 1, 0), (4, 1, 0), (5, 0, 0), (5, 1, 0), (5, 0, 1), (6, 0, 0)):
             be.set_split(split)
             be.set_combine(comb)
             be.set_addends(add)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             assert be.last_split() == split
-            assert be.last_combine() == (0 if split == 1 else 1 if (comb == 1 or split > 4) else 2)
+            short = split <= 4 or (split == 5 and add == 0)  # five pieces: affine addends only
+            assert be.last_combine() == (0 if split == 1 else 2 if (comb == 0 and short) else 1)
             runs[(split, comb, add)] = r
     finally:
         be.set_split(0)
