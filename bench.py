@@ -190,13 +190,17 @@ def pmc_traffic(kernel, n, t, U, plen=None, batch=1, mode="plain"):
     taken on this workload (n, t, split, piece length, batch, mode); else None."""
     want = {"n": n, "t": t, "split": U, "split_len": plen if plen is not None else split_pieces(t, U)[1],
             "batch": batch, "mode": mode}
-    try:
-        names = sorted(os.listdir(TRAFFIC_DIR))
-    except OSError:
-        return None
-    for name in names:
+    # DKG_PMC_TRAFFIC_DIR (a profile pass of the same GPU call, not yet committed) first, then the
+    # committed files, newest round first (names start with the round tag)
+    paths = []
+    for d in [os.environ.get("DKG_PMC_TRAFFIC_DIR"), TRAFFIC_DIR]:
         try:
-            with open(os.path.join(TRAFFIC_DIR, name)) as f:
+            paths += [os.path.join(d, x) for x in sorted(os.listdir(d), reverse=True) if x.endswith(".json")]
+        except (OSError, TypeError):
+            pass
+    for path in paths:
+        try:
+            with open(path) as f:
                 doc = json.load(f)
         except (OSError, ValueError):
             continue

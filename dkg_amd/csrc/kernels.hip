@@ -906,7 +906,13 @@ double stepping_waves_per_simd(size_t cols, size_t N, size_t pieces, size_t last
   return wgs / std::ceil(wgs / cap) * (s.bs / 64.0) / 1024;
 }
 
-size_t stepping_flag_words(size_t ndealers, size_t pieces) { return ndealers * (pieces + 1); }
+// Flag words one stepping() call may use.  A grid has at most ndealers x pieces workgroups, plus one
+// launch for a short last piece; the dead-position repack of an unsplit table (stepping_tail_phases)
+// runs up to TAIL_MAX_PHASES launches of at most ndealers workgroups each (512 -> 4 lanes: 8).
+constexpr size_t TAIL_MAX_PHASES = 8;
+size_t stepping_flag_words(size_t ndealers, size_t pieces) {
+  return ndealers * (pieces == 1 ? TAIL_MAX_PHASES : pieces + 1);
+}
 
 struct ColReal {  // which table columns belong to real dealers (k_stepping's `real`); Rz: dense Z copy
   size_t col0, dreal;
@@ -957,6 +963,7 @@ int stepping_tail_phases(size_t N, size_t nrecv, size_t pieces) {
   if (pieces != 1 || N > 512 || N < 2 * TAIL_MIN_P || 10 * N < 2 * nrecv || nrecv + 1 < N) return 1;
   int k = 1;
   for (size_t P = N / 2; P >= TAIL_MIN_P; P /= 2) k++;
+  static_assert(TAIL_MIN_P << (TAIL_MAX_PHASES - 1) >= 512, "flag words of the tail phases");
   return k;
 }
 size_t stepping_tail_words(size_t ndealers, size_t N) { return PT_WORDS * ndealers * (N / 2); }
@@ -969,8 +976,11 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
   const ColReal cr{col0, dreal, gw ? gw : 64u, Rz};
   if (!last_len || last_len > N) last_len = N;
   // with flags (stepping_flag_words zeroed words): every launch below runs dedicated, then again
-  // complete in its marked workgroups (its own flag words: a grid has at most ndealers x pieces)
+  // complete in its marked workgroups (its own flag words: a grid has at most ndealers x pieces);
+  // a layout that would pass stepping_flag_words fails the call before anything is launched
   size_t foff = 0;
+  const size_t fcap = flags ? stepping_flag_words(ndealers, pieces) : 0;
+  auto fits = [&](size_t words) { return !flags || foff + words <= fcap; };
   auto run = [&](int maxbs, dim3 grid, dim3 block, size_t pos0, int P, const uint32_t* up, uint32_t* down,
                  uint32_t* Rout, size_t Nlive, unsigned piece0, int nseg, int Plast, uint32_t* f) {
     if (f) {
@@ -982,9 +992,11 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
   };
   auto launch = [&](const StepShape& s, size_t Nlive, unsigned piece0, size_t np, int nseg, int Plast) {
     const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), (unsigned)np), block((unsigned)s.bs);
+    if (!fits((size_t)grid.x * grid.y)) return false;
     uint32_t* f = flags ? flags + foff : nullptr;
     foff += (size_t)grid.x * grid.y;
     run((int)s.maxbs, grid, block, 0, (int)s.P, nullptr, nullptr, R, Nlive, piece0, nseg, Plast, f);
+    return true;
   };
   const int phases = (tail_a && tail_b) ? stepping_tail_phases(N, nrecv, pieces) : 1;
   if (phases > 1) {
@@ -997,6 +1009,7 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
       const size_t Pn = P / 2, j1 = k + 1 < phases ? nrecv - Pn + 1 : nrecv;
       const StepShape s = stepping_shape(P);
       const dim3 grid((unsigned)((ndealers + s.per - 1) / s.per), 1u), block((unsigned)s.bs);
+      if (!fits(grid.x)) return false;
       uint32_t* f = flags ? flags + foff : nullptr;
       foff += grid.x;
       // the states are laid out for the whole table ([40][npad][P], word-row stride P npad): this
@@ -1021,8 +1034,7 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
     // (a column), so a launch of ndealers columns has no tail of lone pieces
     StepShape s = stepping_shape((pieces - 1) * N + last_len);
     s.P = N;
-    launch(s, N, 0u, 1, (int)pieces, (int)last_len);
-    return true;
+    return launch(s, N, 0u, 1, (int)pieces, (int)last_len);
   }
   const StepShape sh = stepping_shape(N);
   if (sh.nblk > 1) {  // one dealer per workgroup, top block first, block values streamed down
@@ -1030,6 +1042,7 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
     // pass runs all blocks top-down, then the complete pass redoes all blocks of marked columns
     auto blocks = [&](size_t Nlive, unsigned piece0, size_t np) {
       const dim3 grid((unsigned)ndealers, (unsigned)np), block((unsigned)sh.bs);
+      if (!fits((size_t)grid.x * grid.y)) return false;
       uint32_t* f = flags ? flags + foff : nullptr;
       foff += (size_t)grid.x * grid.y;
       for (int pass = f ? 0 : 1; pass < 2; pass++) {
@@ -1047,26 +1060,18 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
           up = down;
         }
       }
+      return true;
     };
     // a short last piece runs the same blocks with its positions >= last_len as the identity
-    if (last_len == N || pieces == 1) {
-      blocks(last_len, 0u, pieces);
-    } else {
-      blocks(N, 0u, pieces - 1);
-      blocks(last_len, (unsigned)(pieces - 1), 1);
-    }
-    return true;
+    if (last_len == N || pieces == 1) return blocks(last_len, 0u, pieces);
+    return blocks(N, 0u, pieces - 1) && blocks(last_len, (unsigned)(pieces - 1), 1);
   }
   // whole table in one segment of N lanes, sh.per tables per workgroup; a short last piece in its
   // own launch with segments of last_len lanes (the same column-major stride N)
-  if (last_len == N) {
-    launch(sh, N, 0u, pieces, 1, (int)sh.P);
-    return true;
-  }
-  if (pieces > 1) launch(sh, N, 0u, pieces - 1, 1, (int)sh.P);
+  if (last_len == N) return launch(sh, N, 0u, pieces, 1, (int)sh.P);
+  if (pieces > 1 && !launch(sh, N, 0u, pieces - 1, 1, (int)sh.P)) return false;
   const StepShape sl = stepping_shape(last_len);
-  launch(sl, last_len, (unsigned)(pieces - 1), 1, 1, (int)sl.P);
-  return true;
+  return launch(sl, last_len, (unsigned)(pieces - 1), 1, 1, (int)sl.P);
 }
 
 // Degree split: P(x) = sum_u x^(uL) Q_u(x).  With the stepped values Q_u(j) of

@@ -204,6 +204,12 @@ int finish(dkg_multi* m, size_t n, size_t t, dkg_ceremony_out* out, double t_sta
                                              nullptr, m->A0[i].p, &fail[i]);
     });
     if (rc != DKG_OK) return rc;
+    // every shard derives the verdict from the same gathered outcome: they must agree
+    for (int i = 1; i < ws; i++)
+      if (fail[i] != fail[0]) {
+        m->err = "recon: shards disagree on the recovery outcome";
+        return DKG_E_DEVICE;
+      }
     no_mpk = fail[0];
     if (!no_mpk) gather_blocks(m, n, m->A0, m->g_A0, 32, 0, R * 32);
   }

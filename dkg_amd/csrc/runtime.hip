@@ -645,9 +645,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     auto step = step_ilp ? dkgk_ilp::stepping : dkgk::stepping;
-    step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
-         sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw,
-         Rz ? Rz + c0 * n * 10 : nullptr, tail_a, tail_b);
+    if (!step(w, W, L, eT + c0 * L, n, R + c0 * n * PT_WORDS_H, sa ? sa + c0 * n * 40 : nullptr,
+              sb ? sb + c0 * n * 40 : nullptr, st, U, npad, Lr, whole, fl, c0, D, (unsigned)gw,
+              Rz ? Rz + c0 * n * 10 : nullptr, tail_a, tail_b))
+      throw Fail{DKG_E_ARG};  // stepping flag words: an internal layout error, never silently dropped
     if (tm) HCK(hipEventRecord(ctx->pev[2], st));
     if (short_mult && Aff) {
       dkgk::affine_pieces(w, npad, U, n, R + c0 * n * PT_WORDS_H, Aff + c0 * n * AFFP_WORDS_H, st, Rz + c0 * n * 10);
@@ -1214,6 +1215,9 @@ struct BatchRound1 {
   }
   bool deferred() const { return ctx->overlap && ctx->verify_mode == 0; }
   ~BatchRound1() {
+    // after an exception the shares kernel may still be writing s / sp on the side stream: make the
+    // home stream (every later call's) wait for it before the state that tracks it is dropped
+    if (ctx->shares_pending) (void)hipStreamWaitEvent(ctx->stream, ctx->shares_done, 0);
     ctx->r1_a = ctx->r1_b = nullptr;
     ctx->r1_D = 0;
     ctx->r1_A0 = nullptr;

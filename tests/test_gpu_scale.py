@@ -545,6 +545,45 @@ def test_stepping_tail_repack_faults(be, n, t):
     assert bytes(d2[7 * n:8 * n]).count(REJECT) == n - 1 and bytes(d4[9 * n:10 * n]).count(REJECT) == n - 1
 
 
+def test_stepping_tail_repack_unsplit_n1024(be):
+    """n=1024, t=511 forced unsplit runs the repack on 512-lane tables, 8 phases
+    of one table per workgroup at first (grid.x = columns for P = 512 and 256): the redo flag words
+    of every phase must fit the allocation (kernels.hip stepping_flag_words), or a dropped flag
+    would skip the complete-formula redo of an exceptional addition.  Identity E and A rows make
+    every phase's additions exceptional; the repack and the plain stepping (mode 3) must agree,
+    and the tampered dealers' rows equal the oracle's per-pair MSM checks (committee.rs:287-305,
+    532-548)."""
+    n, t = 1024, 511
+    h = be.env_init(t, n, CK)
+    a, b = dkg_amd.dealer_coefficients(bytes([77]) * 32, 6, 0, n, t)
+    E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
+    _inject(random.Random(1024 + 17), n, t, E, A, s, sp)
+    N = t + 1
+    for d, buf in ((7, E), (9, A), (n - 1, E)):  # identity rows, one in the last dealer group
+        buf[32 * N * d:32 * N * (d + 1)] = bytes(32 * N)
+    out = []
+    try:
+        be.set_split(1)
+        for mode in (3, 0):
+            be.set_stepping(mode)
+            r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            assert be.last_split() == 1
+            out.append((r.dec2, r.dec4, r.qualified, r.reconstruct, r.mpk, r.final_share, be.stepping_redos()))
+    finally:
+        be.set_stepping(0)
+        be.set_split(0)
+    assert out[0][:6] == out[1][:6]
+    assert out[1][6] > 0
+    exp = _expected_rows(n, t, h, E, A, s, sp)
+    d2, d4, q = out[1][0], out[1][1], out[1][2]
+    for i in range(5):
+        assert bytes(d2[i * n:(i + 1) * n]) == exp[(i, 2)], (i, "round 2")
+        want4 = exp[(i, 4)] if q[i] else bytes(SELF if j == i else SKIPPED for j in range(n))
+        assert bytes(d4[i * n:(i + 1) * n]) == want4, (i, "round 4")
+    for d, dd in ((7, d2), (9, d4), (n - 1, d2)):
+        assert bytes(dd[d * n:(d + 1) * n]).count(REJECT) == n - 1, d
+
+
 @pytest.mark.parametrize("n,t,split", [(1024, 511, 4), (1024, 511, 3), (1100, 549, 2), (300, 149, 1)])
 def test_binomial_schedules_match_at_scale(be, n, t, split):
     """The binomial schedules (dkg_ctx_set_binomial: lane pairs for no / every / the latency-bound
