@@ -730,8 +730,8 @@ def main():
                     help="short-multiplier recombination addends: 0 affine Niels, 1 cached projective")
     ap.add_argument("--field", type=int, default=0,
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
-    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4],
-                    help="binomial schedule (dkg_ctx_set_binomial): 0 default (per-wave Horner loops for tables of many column groups, else per step with lane pairs for the latency-bound steps), 1 per step without lane pairs, 2 per step with lane pairs for every step, 3 per step as 0, 4 per wave always")
+    ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
+                    help="binomial schedule (dkg_ctx_set_binomial): 0 default (per-wave Horner loops for tables of many column groups, else per step with lane pairs for the latency-bound steps), 1 per step without lane pairs, 2 per step with lane pairs for every step, 3 per step as 0, 4 per wave always, 5 per wave with operands prefetched one item ahead")
     ap.add_argument("--stepping", type=int, default=0, choices=[0, 1, 2, 3],
                     help="stepping slots (dkg_ctx_set_stepping): 0 cost model, 1 per column, 2 per piece, 3 no dead-position repack")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
@@ -950,6 +950,14 @@ def main():
             out["gpu_vs_cpu"] = value / out["cpu_baseline"]["value"]
     if shard_stats is not None:
         out.update(shard_stats)
+        # the all-gathered decisions are packed bitmaps (dkg_decisions_pack_device): bytes one rank
+        # contributes per ceremony, against the n-byte rows, here and at BASELINE config 4
+        R4, W4 = dkg_amd.shard_rows(4096, 8), dkg_amd.packed_row_words(4096)
+        out["exchange"] = {"decisions": "packed bitmaps" if sc.packed else "bytes",
+                           "bytes_per_rank": sc.exchange_bytes(),
+                           "bytes_per_rank_byte_rows": 2 * sc.R * n + sc.A0.numel() + sc.part.numel(),
+                           "n4096_ws8_bytes_per_rank": 2 * R4 * 4 * W4 + 32 * R4 + 32 * 4096,
+                           "n4096_ws8_bytes_per_rank_byte_rows": 2 * R4 * 4096 + 32 * R4 + 32 * 4096}
     if ws > 1 and args.mode != "full" and args.verify == "group":
         # per-GPU roofline of this rank's shard: one extra serialised pass (every rank joins its
         # collectives); the rank's work is its D dealers' share of the closed form

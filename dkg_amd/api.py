@@ -155,7 +155,7 @@ class Backend:
         """Binomial schedule (dkg_ctx_set_binomial): 0 (default) per-wave Horner loops for tables of
         many column groups, else one launch per step with lane pairs for the latency-bound steps; 1
         per step without lane pairs; 2 per step with lane pairs everywhere; 3 per step as 0; 4 per
-        wave always."""
+        wave always; 5 per wave always with each item's operand prefetched during the previous item."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
     def set_stepping(self, mode: int):
@@ -455,20 +455,31 @@ class Backend:
         return PartyFinalise([m[32 * p:32 * p + 32] for p in range(n)], list(st)[:n], list(ri)[:n])
 
     def shard_combine_device(self, n: int, t: int, world_size: int, d_dec2_g: int, d_dec4_g: int,
-                             d_dec2: Optional[int] = None, d_dec4: Optional[int] = None) -> "ShardOutcome":
+                             d_dec2: Optional[int] = None, d_dec4: Optional[int] = None,
+                             packed: bool = False) -> "ShardOutcome":
         """Combine step of the sharded run (dkg_shard_combine_device): the common round-2/4 outcome
-        from the all-gathered [ws][R][n] decision blocks (device pointers); d_dec2 / d_dec4 optionally
-        receive the compacted [n][n] matrices (dec4 with SKIPPED rows)."""
+        from the all-gathered [ws][R][n] decision blocks (device pointers; with packed, the
+        [ws][R][packed_row_words(n)] bitmaps of dkg_shard_combine_packed_device); d_dec2 / d_dec4
+        optionally receive the compacted [n][n] matrices (dec4 with SKIPPED rows)."""
         q, r2e, rc, r4e = (ctypes.create_string_buffer(max(n, 1)) for _ in range(4))
         c = (ctypes.c_int32 * max(n, 1))()
         o = _lib.ShardOutcome(ctypes.cast(q, ctypes.c_void_p), ctypes.cast(c, ctypes.c_void_p),
                               ctypes.cast(r2e, ctypes.c_void_p), ctypes.cast(rc, ctypes.c_void_p),
                               ctypes.cast(r4e, ctypes.c_void_p), 0, 0)
         vp = ctypes.c_void_p
-        _check(self._ctx, _lib.lib().dkg_shard_combine_device(self._ctx, n, t, world_size, vp(d_dec2_g), vp(d_dec4_g),
-                                                               vp(d_dec2), vp(d_dec4), ctypes.byref(o)))
+        fn = _lib.lib().dkg_shard_combine_packed_device if packed else _lib.lib().dkg_shard_combine_device
+        _check(self._ctx, fn(self._ctx, n, t, world_size, vp(d_dec2_g), vp(d_dec4_g), vp(d_dec2), vp(d_dec4),
+                             ctypes.byref(o)))
         return ShardOutcome(list(q.raw[:n]), list(c)[:n], list(r2e.raw[:n]), list(rc.raw[:n]), list(r4e.raw[:n]),
                             o.n_qualified, bool(o.phase4_error))
+
+    def decisions_pack_device(self, rows: int, nvalid: int, n: int, d0: int, d_dec: int, d_packed: int):
+        """Raw decision rows of dealers d0.. (device [nvalid][n] bytes) -> the packed bitmaps the ranks
+        all-gather (device [rows][packed_row_words(n)] u32; dkg_decisions_pack_device).  Raises if a
+        row holds values the encoding cannot carry."""
+        vp = ctypes.c_void_p
+        _check(self._ctx, _lib.lib().dkg_decisions_pack_device(self._ctx, rows, nvalid, n, d0, vp(d_dec),
+                                                                vp(d_packed)))
 
     def shard_finalise_device(self, n: int, t: int, world_size: int, d_terms_g: int, d_partials_g: int, qualified,
                               phase4_error: bool, d_final_share: int, d_public_share: Optional[int] = None) -> bytes:
@@ -610,6 +621,11 @@ def shard_range(n: int, world_size: int, rank: int):
 def shard_rows(n: int, world_size: int) -> int:
     """Padded per-rank block height R of the all-gathers (dkg_shard_rows)."""
     return _lib.lib().dkg_shard_rows(n, world_size)
+
+
+def packed_row_words(n: int) -> int:
+    """u32 words of one packed decision row (dkg_packed_row_words: ceil(n/32) ACCEPT-bit words + a kind word)."""
+    return _lib.lib().dkg_packed_row_words(n)
 
 
 @dataclass

@@ -566,10 +566,16 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
 #ifndef DKG_BINOM_WAVE_CARRY
 #define DKG_BINOM_WAVE_CARRY 1
 #endif
-template <bool CARRY>
-__global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t npad, const uint32_t* __restrict__ C,
-                                                                uint32_t* e, size_t pstride, unsigned gx,
-                                                                unsigned last_piece, int last_off, uint32_t* eT) {
+// PF (with CARRY): the next item's e_{m-2} is loaded before this item's chain starts, so the load
+// latency hides behind the chain instead of behind the other waves of the SIMD (40 more VGPRs: 2
+// waves per SIMD instead of 3).
+template <bool CARRY, bool PF>
+__global__ __launch_bounds__(64, PF ? 2 : (CARRY ? 3 : 4)) void k_binom_wave(int L, size_t npad,
+                                                                           const uint32_t* __restrict__ C,
+                                                                           uint32_t* e, size_t pstride, unsigned gx,
+                                                                           unsigned last_piece, int last_off,
+                                                                           uint32_t* eT) {
+  static_assert(!PF || CARRY, "the prefetch runs on the carried schedule");
   __shared__ uint32_t qs[PT_WORDS * 64];
   uint32_t* q = qs + threadIdx.x;
   const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
@@ -589,8 +595,11 @@ __global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t 
   for (int r = 1; r < L; r++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores land before it rereads them
     const int re = r - off;  // a short last piece joins late (as k_binom_step)
-    ge_p3 carry;
+    ge_p3 carry, nx;
     if constexpr (CARRY) ge_identity(carry);  // position re is still the identity
+    if constexpr (PF) {
+      if (re >= 1) pt_load(nx, eb, S, (size_t)(re - 1) * npad + lane);
+    }
 #pragma unroll 1
     for (int m = re; m >= 1; m--) {
       {
@@ -611,7 +620,13 @@ __global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t 
       }
       __builtin_amdgcn_sched_barrier(0);
       ge_p3 x;
-      pt_load(x, eb, S, (size_t)(m - 1) * npad + lane);
+      if constexpr (PF) {
+        x = nx;
+        // item m-1's operand: position m-2 is rewritten only by item m-2, after this load
+        if (m >= 2) pt_load(nx, eb, S, (size_t)(m - 2) * npad + lane);
+      } else {
+        pt_load(x, eb, S, (size_t)(m - 1) * npad + lane);
+      }
       if constexpr (CARRY) carry = x;    // the old e_{m-1}: the next item's e_m
       ge_add_lds(x, x, q, false);        // e_{m-1} + e_m
       mul_small_lds(x, (uint32_t)m, q);  // * m
@@ -640,11 +655,15 @@ __global__ __launch_bounds__(64, CARRY ? 3 : 4) void k_binom_wave(int L, size_t 
 }
 
 uint32_t* binomial_wave(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e, hipStream_t stream,
-                        size_t pieces, size_t pstride, size_t last_len, uint32_t* eT) {
+                        size_t pieces, size_t pstride, size_t last_len, uint32_t* eT, bool prefetch) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
-  hipLaunchKernelGGL(k_binom_wave<DKG_BINOM_WAVE_CARRY != 0>, dim3((unsigned)(width / 64 * pieces)), dim3(64), 0,
-                     stream, (int)N, npad, C, e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off,
-                     eT);
+  const dim3 grid((unsigned)(width / 64 * pieces));
+  if (prefetch)
+    hipLaunchKernelGGL((k_binom_wave<true, true>), grid, dim3(64), 0, stream, (int)N, npad, C, e, pstride,
+                       (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, eT);
+  else
+    hipLaunchKernelGGL((k_binom_wave<DKG_BINOM_WAVE_CARRY != 0, false>), grid, dim3(64), 0, stream, (int)N, npad, C,
+                       e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, eT);
   return e;
 }
 
@@ -2041,6 +2060,91 @@ void compact_ranks(size_t n, size_t ws, size_t R, size_t width, const void* in, 
     hipLaunchKernelGGL(k_compact_ranks<uint8_t>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, n, ws,
                        R, width, (const uint8_t*)in, (uint8_t*)out);
   }
+}
+
+// Packed decision rows: what the ranks of a sharded ceremony all-gather instead of n bytes per row
+// (north_star: the complaint / verification bitmaps).  A rank's raw rows hold
+// REJECT / ACCEPT (round 4 as well: SKIPPED is applied after the exchange), SELF on the global
+// diagonal and, in round 2, whole rows of MISSING (an undecodable broadcast), so row r becomes
+// W = ceil(n / 32) words of ACCEPT bits plus one kind word (0 checked, 1 MISSING row, 2 SKIPPED
+// row); the diagonal is implied by the dealer index.  Rows past nvalid (the padding of a rank block)
+// are zero.  A row the encoding cannot hold sets err[0] (vector store: lanes are divergent).
+__global__ __launch_bounds__(64) void k_pack_rows(size_t nvalid, size_t n, size_t d0, const uint8_t* __restrict__ dec,
+                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+  const size_t r = blockIdx.y, W = (n + 31) / 32, w = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (w > W) return;
+  uint32_t* o = out + r * (W + 1);
+  if (r >= nvalid) {
+    o[w] = 0;
+    return;
+  }
+  const uint8_t* row = dec + r * n;
+  const size_t self = d0 + r;
+  const uint8_t ref = n > 1 ? row[self == 0 ? 1 : 0] : 1;  // any entry off the diagonal
+  const uint32_t kind = ref == 4 ? 1u : ref == 3 ? 2u : 0u;
+  if (w == W) {
+    o[w] = kind;
+    return;
+  }
+  uint32_t bits = 0, bad = 0;
+  for (int b = 0; b < 32; b++) {
+    const size_t j = w * 32 + b;
+    if (j >= n) break;
+    const uint32_t v = row[j];
+    if (j == self) bad |= v != 2;
+    else if (kind == 0) {
+      bad |= v > 1;
+      bits |= (v & 1u) << b;
+    } else {
+      bad |= v != (kind == 1 ? 4u : 3u);
+    }
+  }
+  o[w] = bits;
+  if (bad) err[0] = 1u;
+}
+
+void pack_rows(size_t rows, size_t nvalid, size_t n, size_t d0, const uint8_t* dec, uint32_t* out, uint32_t* err,
+               hipStream_t stream) {
+  if (!rows || !n) return;
+  const size_t W1 = (n + 31) / 32 + 1;
+  hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((W1 + 63) / 64), (unsigned)rows), dim3(64), 0, stream, nvalid, n,
+                     d0, dec, out, err);
+}
+
+// All-gathered packed blocks [ws][R][W + 1] -> the dense decision matrix [n][n]: one thread per
+// (global row i, word w), 32 entries each (eight 4-byte stores when rows are 4-byte aligned).
+__global__ __launch_bounds__(256) void k_unpack_ranks(size_t n, size_t ws, size_t R, const uint32_t* __restrict__ in,
+                                                      uint8_t* __restrict__ out) {
+  const size_t W = (n + 31) / 32, e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * W) return;
+  const size_t i = e / W, w = e % W;
+  size_t r = (i * ws) / n;  // the rank owning row i (as k_compact_ranks)
+  while (r + 1 < ws && ((r + 1) * n) / ws <= i) r++;
+  while (r > 0 && (r * n) / ws > i) r--;
+  const uint32_t* src = in + (r * R + (i - (r * n) / ws)) * (W + 1);
+  const uint32_t kind = src[W], bits = src[w];
+  const uint32_t fill = kind == 1 ? 4u : kind == 2 ? 3u : 0u;
+  uint8_t* o = out + i * n;
+  const size_t j0 = w * 32;
+  auto val = [&](size_t j, int b) -> uint32_t { return j == i ? 2u : kind ? fill : (bits >> b) & 1u; };
+  if (n % 4 == 0 && j0 + 32 <= n) {
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(o + j0);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) v |= val(j0 + 4 * q + b, 4 * q + b) << (8 * b);
+      o4[q] = v;
+    }
+  } else {
+    for (int b = 0; b < 32 && j0 + b < n; b++) o[j0 + b] = (uint8_t)val(j0 + b, b);
+  }
+}
+
+void unpack_ranks(size_t n, size_t ws, size_t R, const uint32_t* in, uint8_t* out, hipStream_t stream) {
+  const size_t total = n * ((n + 31) / 32);
+  if (!total) return;
+  hipLaunchKernelGGL(k_unpack_ranks, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, n, ws, R, in, out);
 }
 
 void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,

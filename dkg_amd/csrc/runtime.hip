@@ -50,7 +50,8 @@ struct dkg_ctx {
                                         // tables of many column groups, else one launch per step
                                         // with lane pairs (k_binom_pair) for the steps under one
                                         // wave per SIMD; 1 per step, no lane pairs; 2 per step, lane
-                                        // pairs for every step; 3 per step as 0; 4 per wave always
+                                        // pairs for every step; 3 per step as 0; 4 per wave always;
+                                        // 5 per wave always, operands prefetched one item ahead
   int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece,
                                         // 3 as 0 without the dead-position repack
   int fe_mode = 0;                      // field multiplication per launch: 0 by occupancy, 1 product
@@ -237,6 +238,9 @@ struct VerifySeg {
 // launch of per-wave Horner loops (kernels.hip k_binom_wave): each wave then has a long private
 // chain, and 4 rounds of a chip's resident waves keep the last round's tail small.  Fewer groups
 // (n=1024: 128; n=4096: 512) keep one launch per step.
+#ifndef DKG_BINOM_WAVE_PF  // the per-wave binomial's default: operands prefetched one item ahead
+#define DKG_BINOM_WAVE_PF 0
+#endif
 #ifndef DKG_BINOM_WAVE_GROUPS
 #define DKG_BINOM_WAVE_GROUPS 16384
 #endif
@@ -601,7 +605,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const bool long_stepping = (double)W * (double)L * (double)n >= 5e7 && npad >= 512;
   const size_t nsub = (saturating || long_stepping) ? std::min<size_t>(ctx->nsub, groups) : 1;
   // the binomial as per-wave Horner loops (k_binom_wave) for tables of many column groups
-  const bool per_wave = ctx->binom_mode == 4 ||
+  const bool per_wave = ctx->binom_mode == 4 || ctx->binom_mode == 5 ||
                         (ctx->binom_mode == 0 && L > 1 && (double)npad / 64 * U >= DKG_BINOM_WAVE_GROUPS);
   ctx->last_binomial = per_wave ? 1 : 0;
   // dead-position repack of an unsplit table (kernels.hip stepping_tail_phases): two scratch states
@@ -618,7 +622,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
     const uint32_t* e;
     if (per_wave) {  // its last step writes the column-major table itself
-      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr, eT + c0 * L);
+      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr, eT + c0 * L,
+                              ctx->binom_mode == 5 || (ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF));
     } else {
       dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
       uint32_t *bin = e0 + c0, *bout = e1 + c0;
@@ -1616,7 +1621,7 @@ int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
 }
 
 int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 4) return DKG_E_ARG;
+  if (!ctx || mode < 0 || mode > 5) return DKG_E_ARG;
   ctx->binom_mode = mode;
   return DKG_OK;
 }
@@ -2375,35 +2380,83 @@ size_t dkg_shard_rows(size_t n, size_t world_size) {
   return R;
 }
 
+}  // extern "C"
+
+// The combine of the sharded run from the gathered rank blocks: `dense` materialises them as the
+// [n][n] matrices (compacted bytes or unpacked bitmaps), then the single-GPU drivers' outcome code.
+template <typename F>
+int shard_combine(dkg_ctx* ctx, size_t n, size_t t, void* d_dec2, void* d_dec4, dkg_shard_outcome* out, F&& dense) {
+  uint8_t* dec2 = d_dec2 ? (uint8_t*)d_dec2 : buf<uint8_t>(ctx, "sc.dec2", n * n);
+  uint8_t* dec4 = d_dec4 ? (uint8_t*)d_dec4 : buf<uint8_t>(ctx, "sc.dec4", n * n);
+  uint8_t* qmask = buf<uint8_t>(ctx, "sc.qmask", n);
+  dense(dec2, dec4);
+  check_launch(ctx);
+  std::vector<uint8_t> q(n), r2e(n), recon(n), r4e(n);
+  std::vector<int32_t> c(n);
+  round2_outcome(ctx, 1, n, t, dec2, qmask, q.data(), c.data(), r2e.data());
+  round4_outcome(ctx, 1, n, t, dec4, qmask, q.data(), recon.data(), r4e.data());
+  int32_t nq = 0, nr = 0;
+  for (size_t i = 0; i < n; i++) {
+    nq += q[i];
+    nr += recon[i];
+  }
+  if (out->qualified) memcpy(out->qualified, q.data(), n);
+  if (out->complaints2) memcpy(out->complaints2, c.data(), 4 * n);
+  if (out->r2_error) memcpy(out->r2_error, r2e.data(), n);
+  if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
+  if (out->r4_error) memcpy(out->r4_error, r4e.data(), n);
+  out->n_qualified = nq;
+  out->phase4_error = nq - nr <= (int32_t)t;  // committee.rs:673-677
+  return DKG_OK;
+}
+
+extern "C" {
+
 int dkg_shard_combine_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_size, const void* d_dec2_g,
                              const void* d_dec4_g, void* d_dec2, void* d_dec4, dkg_shard_outcome* out) {
   return guarded(ctx, [&] {
     if (!out || !d_dec2_g || !d_dec4_g || !world_size || world_size > n || dkg_env_check(t, n) != DKG_OK)
       return DKG_E_ARG;
     const size_t R = dkg_shard_rows(n, world_size);
-    uint8_t* dec2 = d_dec2 ? (uint8_t*)d_dec2 : buf<uint8_t>(ctx, "sc.dec2", n * n);
-    uint8_t* dec4 = d_dec4 ? (uint8_t*)d_dec4 : buf<uint8_t>(ctx, "sc.dec4", n * n);
-    uint8_t* qmask = buf<uint8_t>(ctx, "sc.qmask", n);
-    dkgk::compact_ranks(n, world_size, R, n, d_dec2_g, dec2, ctx->stream);
-    dkgk::compact_ranks(n, world_size, R, n, d_dec4_g, dec4, ctx->stream);
+    return shard_combine(ctx, n, t, d_dec2, d_dec4, out, [&](uint8_t* dec2, uint8_t* dec4) {
+      dkgk::compact_ranks(n, world_size, R, n, d_dec2_g, dec2, ctx->stream);
+      dkgk::compact_ranks(n, world_size, R, n, d_dec4_g, dec4, ctx->stream);
+    });
+  });
+}
+
+size_t dkg_packed_row_words(size_t n) { return (n + 31) / 32 + 1; }
+
+int dkg_decisions_pack_device(dkg_ctx* ctx, size_t rows, size_t nvalid, size_t n, size_t d0, const void* d_dec,
+                              void* d_packed) {
+  return guarded(ctx, [&] {
+    if (!n || nvalid > rows || (nvalid && !d_dec) || (rows && !d_packed) || d0 + nvalid > n) return DKG_E_ARG;
+    if (!rows) return DKG_OK;
+    uint32_t* err = buf<uint32_t>(ctx, "pk.err", 4);
+    HCK(hipMemsetAsync(err, 0, 4, ctx->stream));
+    dkgk::pack_rows(rows, nvalid, n, d0, (const uint8_t*)d_dec, (uint32_t*)d_packed, err, ctx->stream);
     check_launch(ctx);
-    std::vector<uint8_t> q(n), r2e(n), recon(n), r4e(n);
-    std::vector<int32_t> c(n);
-    round2_outcome(ctx, 1, n, t, dec2, qmask, q.data(), c.data(), r2e.data());
-    round4_outcome(ctx, 1, n, t, dec4, qmask, q.data(), recon.data(), r4e.data());
-    int32_t nq = 0, nr = 0;
-    for (size_t i = 0; i < n; i++) {
-      nq += q[i];
-      nr += recon[i];
+    uint32_t e = 0;
+    d2h(ctx, &e, err, 4);
+    sync(ctx);
+    if (e) {
+      ctx->err = "decisions_pack: a row holds values the packed encoding cannot carry";
+      return DKG_E_ARG;
     }
-    if (out->qualified) memcpy(out->qualified, q.data(), n);
-    if (out->complaints2) memcpy(out->complaints2, c.data(), 4 * n);
-    if (out->r2_error) memcpy(out->r2_error, r2e.data(), n);
-    if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
-    if (out->r4_error) memcpy(out->r4_error, r4e.data(), n);
-    out->n_qualified = nq;
-    out->phase4_error = nq - nr <= (int32_t)t;  // committee.rs:673-677
     return DKG_OK;
+  });
+}
+
+int dkg_shard_combine_packed_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_size, const void* d_pack2_g,
+                                    const void* d_pack4_g, void* d_dec2, void* d_dec4, dkg_shard_outcome* out) {
+  return guarded(ctx, [&] {
+    if (!out || !d_pack2_g || !d_pack4_g || !world_size || world_size > n || dkg_env_check(t, n) != DKG_OK)
+      return DKG_E_ARG;
+    const size_t R = dkg_shard_rows(n, world_size);
+    return shard_combine(ctx, n, t, d_dec2, d_dec4, out, [&](uint8_t* dec2, uint8_t* dec4) {
+      dkgk::unpack_ranks(n, world_size, R, (const uint32_t*)d_pack2_g, dec2, ctx->stream);
+      dkgk::unpack_ranks(n, world_size, R, (const uint32_t*)d_pack4_g, dec4, ctx->stream);
+    });
   });
 }
 

@@ -5,7 +5,9 @@ shares and checks their rows against all n receivers on its GPU (dkg_ceremony_sh
 protocol's exchange step -- every party learns every complaint (committee.rs:311-331, 370-398) and
 the round-3/5 broadcasts (committee.rs:454-467, 790-795) -- is a set of all-gathers (RCCL over xGMI
 with the "nccl" backend, gloo in the CPU tests) of:
-  * the round-2 / round-4 decision rows,
+  * the round-2 / round-4 decision rows, packed as bitmaps (dkg_decisions_pack_device: one ACCEPT
+    bit per pair plus a row-kind word -- SELF, MISSING rows and SKIPPED are implied; n=4096: 516
+    bytes per row instead of 4096),
   * every dealer's compressed master-key term (A_i0, or g * a_i0 recovered by Lagrange
     interpolation on the owning rank for dealers accused in round 4),
   * each rank's partial final shares (sum over its qualified dealers of s_ij).
@@ -63,11 +65,12 @@ class ShardedCeremony:
     `dist` an initialised torch.distributed, `device` the torch device the exchanged buffers live on
     (cuda:local for RCCL; cpu works with gloo)."""
 
-    def __init__(self, be, dist, n: int, t: int, device):
+    def __init__(self, be, dist, n: int, t: int, device, packed: bool = True):
         import torch
 
         self.torch = torch
         self.be, self.dist, self.n, self.t, self.dev = be, dist, n, t, device
+        self.packed = packed
         self.ws, self.rank = dist.get_world_size(), dist.get_rank()
         self.staged = dist.get_backend() == "gloo" and getattr(device, "type", str(device)) != "cpu"
         self.d0, self.d1 = dealer_range(self.rank, self.ws, n)
@@ -77,8 +80,17 @@ class ShardedCeremony:
         self.dec4 = torch.zeros(R * n, **u8)
         self.A0 = torch.zeros(R * 32, **u8)
         self.part = torch.zeros(n * 32, **u8)
-        self.g_dec2 = torch.empty(self.ws * R * n, **u8)
-        self.g_dec4 = torch.empty(self.ws * R * n, **u8)
+        if packed:  # [R][W+1] u32 bitmaps (dkg_packed_row_words), gathered as [ws][R][W+1]
+            from .api import packed_row_words
+
+            self.W1 = packed_row_words(n)
+            i32 = dict(dtype=torch.int32, device=device)
+            self.p2, self.p4 = torch.zeros(R * self.W1, **i32), torch.zeros(R * self.W1, **i32)
+            self.g_dec2 = torch.empty(self.ws * R * self.W1, **i32)
+            self.g_dec4 = torch.empty(self.ws * R * self.W1, **i32)
+        else:
+            self.g_dec2 = torch.empty(self.ws * R * n, **u8)
+            self.g_dec4 = torch.empty(self.ws * R * n, **u8)
         self.g_A0 = torch.empty(self.ws * R * 32, **u8)
         self.g_part = torch.empty(self.ws * n * 32, **u8)
         self.c_dec2 = torch.empty(n * n, **u8)   # compacted by the combine
@@ -103,11 +115,28 @@ class ShardedCeremony:
         else:
             self.dist.all_gather_into_tensor(out, inp)
 
+    def _pack(self, dec, out):
+        """This rank's raw rows [D][n] -> its packed block [R][W+1] (dkg_decisions_pack_device)."""
+        self.be.decisions_pack_device(self.R, self.D, self.n, self.d0, dec.data_ptr(), out.data_ptr())
+
+    def exchange_bytes(self) -> int:
+        """Bytes one rank contributes to the all-gathers of one ceremony (without the round-4
+        reconstruction's second gather of the master-key terms)."""
+        rows = 2 * self.R * (4 * self.W1 if self.packed else self.n)
+        return rows + self.A0.numel() + self.part.numel()
+
     def exchange(self):
-        """All-gather every rank's padded blocks: the decision rows [ws][R][n] (round 2, round 4),
-        the master-key terms [ws][R][32] and the partial final shares [ws][n][32]."""
-        self._all_gather(self.g_dec2, self.dec2)
-        self._all_gather(self.g_dec4, self.dec4)
+        """All-gather every rank's padded blocks: the decision rows (round 2, round 4; packed bitmaps
+        [ws][R][W+1] or bytes [ws][R][n]), the master-key terms [ws][R][32] and the partial final
+        shares [ws][n][32]."""
+        if self.packed:
+            self._pack(self.dec2, self.p2)
+            self._pack(self.dec4, self.p4)
+            self._all_gather(self.g_dec2, self.p2)
+            self._all_gather(self.g_dec4, self.p4)
+        else:
+            self._all_gather(self.g_dec2, self.dec2)
+            self._all_gather(self.g_dec4, self.dec4)
         self._all_gather(self.g_A0, self.A0)
         self._all_gather(self.g_part, self.part)
         return self.g_dec2, self.g_dec4, self.g_A0, self.g_part
@@ -139,7 +168,7 @@ class ShardedCeremony:
         c1 = time.perf_counter()
         steps["exchange"] = (c1 - c0) * 1e3
         o = self.be.shard_combine_device(n, t, ws, self.g_dec2.data_ptr(), self.g_dec4.data_ptr(),
-                                         self.c_dec2.data_ptr(), self.c_dec4.data_ptr())
+                                         self.c_dec2.data_ptr(), self.c_dec4.data_ptr(), packed=self.packed)
         dec = Decisions(self.c_dec2.view(n, n), self.c_dec4.view(n, n), np.array(o.qualified, dtype=np.uint8),
                         np.array(o.complaints2, dtype=np.int32), np.array(o.r2_error, dtype=np.uint8),
                         np.array(o.reconstruct, dtype=np.uint8), np.array(o.r4_error, dtype=np.uint8),

@@ -77,7 +77,8 @@ int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
  * groups (config 5) as ONE launch in which every wave runs all steps of its 64 columns in place,
  * others one grid launch per step with the steps under one wave per SIMD on lane pairs (each point
  * on two lanes sharing its field products); 1 -- per step, no lane pairs; 2 -- per step, lane pairs
- * for every step; 3 -- per step as 0's; 4 -- per wave always.  Outputs do not depend on it. */
+ * for every step; 3 -- per step as 0's; 4 -- per wave always; 5 -- per wave always, each item's
+ * operand loaded during the previous item's chain.  Outputs do not depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and
@@ -316,6 +317,24 @@ typedef struct {
  * dealers applied (:522). */
 int dkg_shard_combine_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_size, const void *d_dec2_g,
                              const void *d_dec4_g, void *d_dec2, void *d_dec4, dkg_shard_outcome *out);
+/* Packed decision rows: the complaint / verification bitmaps a multi-rank driver all-gathers instead
+ * of n bytes per row (committee.rs:311-347: every party learns every complaint).  A rank's raw rows
+ * hold REJECT / ACCEPT (round 4 too: SKIPPED is applied by the combine), SELF on the global diagonal
+ * and, in round 2, whole rows of MISSING; row r becomes dkg_packed_row_words(n) = ceil(n/32) + 1
+ * little-endian u32 words: bit j % 32 of word j / 32 set iff entry j is ACCEPT, then a kind word (0
+ * checked, 1 MISSING row, 2 SKIPPED row).  n = 4096: 516 bytes per row instead of 4096. */
+size_t dkg_packed_row_words(size_t n);
+/* d_dec device [nvalid][n] raw rows of dealers d0 .. d0+nvalid-1 (dkg_ceremony_shard_device's
+ * output) -> d_packed device [rows][dkg_packed_row_words(n)] u32, rows past nvalid zero (the padded
+ * rank block, rows = dkg_shard_rows).  DKG_E_ARG if a row holds values the encoding cannot carry
+ * (nothing is lost silently). */
+int dkg_decisions_pack_device(dkg_ctx *ctx, size_t rows, size_t nvalid, size_t n, size_t d0, const void *d_dec,
+                              void *d_packed);
+/* dkg_shard_combine_device on the gathered packed blocks: d_pack2_g, d_pack4_g device
+ * [ws][R][dkg_packed_row_words(n)] u32; outputs as dkg_shard_combine_device (d_dec2 / d_dec4 are the
+ * unpacked matrices, bit-identical to the byte exchange's). */
+int dkg_shard_combine_packed_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_size, const void *d_pack2_g,
+                                    const void *d_pack4_g, void *d_dec2, void *d_dec4, dkg_shard_outcome *out);
 /* Finalise of the sharded run: d_terms_g device [ws][R][32] the gathered master-key terms (A_i0, or
  * g * a_i0 for reconstructed dealers after dkg_ceremony_shard_recon_device), d_partials_g device
  * [ws][n][32] the gathered partial final shares, qualified host [n] (the combine's).  Outputs:

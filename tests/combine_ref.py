@@ -45,6 +45,55 @@ def pad(dense, ws, n, width, fill=0xEE):
     return out.reshape(-1)
 
 
+def packed_words(n):
+    """u32 words per packed decision row (include/dkg_amd.h dkg_packed_row_words)."""
+    return (n + 31) // 32 + 1
+
+
+def pack_rows(dec, rows, nvalid, n, d0):
+    """Raw decision rows of dealers d0..d0+nvalid-1 ([nvalid][n] uint8) -> [rows][W+1] uint32, the
+    encoding of dkg_decisions_pack_device restated: ACCEPT bits (bit j % 32 of word j // 32), then the
+    row kind (0 checked, 1 MISSING row, 2 SKIPPED row); the diagonal is implied; padding rows zero.
+    Raises ValueError on a row the encoding cannot carry."""
+    W = (n + 31) // 32
+    out = np.zeros((rows, W + 1), dtype=np.uint32)
+    d = _u8(dec).reshape(-1)[:nvalid * n].reshape(nvalid, n)
+    for r in range(nvalid):
+        row, self_ = d[r], d0 + r
+        off = np.ones(n, dtype=bool)
+        off[self_] = False
+        if row[self_] != SELF:
+            raise ValueError(f"row {r}: diagonal is not SELF")
+        vals = set(row[off].tolist())
+        kind = 1 if vals == {MISSING} else 2 if vals == {SKIPPED} else 0
+        if kind == 0 and not vals <= {REJECT, ACCEPT}:
+            raise ValueError(f"row {r}: values {sorted(vals)} do not fit the packed encoding")
+        if kind == 0:
+            bits = np.zeros(32 * W, dtype=np.uint64)
+            bits[:n] = (row == ACCEPT) & off
+            out[r, :W] = (bits.reshape(W, 32) << np.arange(32, dtype=np.uint64)).sum(axis=1).astype(np.uint32)
+        out[r, W] = kind
+    return out
+
+
+def unpack_ranks(gathered, ws, n):
+    """All-gathered packed blocks [ws][R][W+1] (flat uint32) -> dense [n][n] uint8 decisions."""
+    R, W = rows_per_rank(ws, n), (n + 31) // 32
+    g = np.asarray(gathered, dtype=np.uint32).reshape(ws, R, W + 1)
+    out = np.empty((n, n), dtype=np.uint8)
+    for r in range(ws):
+        a, b = dealer_range(r, ws, n)
+        for k in range(b - a):
+            i, kind = a + k, int(g[r, k, W])
+            if kind:
+                out[i] = MISSING if kind == 1 else SKIPPED
+            else:
+                bits = (g[r, k, :W, None].astype(np.uint64) >> np.arange(32, dtype=np.uint64)) & 1
+                out[i] = bits.reshape(-1)[:n].astype(np.uint8)
+            out[i, i] = SELF
+    return out
+
+
 @dataclass
 class Outcome:
     dec2: np.ndarray

@@ -53,7 +53,10 @@ def test_pmc_traffic_matches_workload():
             per_wave = kern == "binomial" and doc["kernels"][kern]["fetch_launches"] <= 2 * B and B > 1
             alg, _ = bench.algorithmic_bytes(kern, n, t, U, plen, per_wave, B)
             if alg and not (kern == "stepping" and B > 1):  # the repacked tail phases: not in the closed form
-                assert 0.9 < got[0] / alg < 1.1, (nm, kern, got[0] / alg)
+                # the per-step binomial's model counts both operand reads of an item (3 x 160 B); the
+                # second read of a position (items m and m+1 share e_m) may hit L2: down to 2/3 (n=4096)
+                lo = 0.6 if kern == "binomial" and not per_wave else 0.9
+                assert lo < got[0] / alg < 1.1, (nm, kern, got[0] / alg)
         assert bench.pmc_traffic("binomial", n + 1, t, U, plen, B, mode) is None
         assert bench.pmc_traffic("binomial", n, t, U, plen, B, "other") is None
 

@@ -37,12 +37,15 @@ def _rank_main(rank, ws, port, names, errq):
 
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
-        for name in names:
+        for name, packed in [(x, p) for x in names for p in (False, True)]:
             with open(os.path.join(ROOT, "tests", "golden", name)) as f:
                 c = json.load(f)
             n, t = c["n"], c["t"]
             N = t + 1
-            sc = ShardedCeremony(None, dist, n, t, torch.device("cpu"))
+            sc = ShardedCeremony(None, dist, n, t, torch.device("cpu"), packed=packed)
+            if packed:  # the library's packing restated (tests/combine_ref.py pack_rows)
+                sc._pack = lambda dec, out, sc=sc: out.copy_(torch.from_numpy(
+                    CR.pack_rows(dec.numpy()[:sc.D * sc.n], sc.R, sc.D, sc.n, sc.d0).view(np.int32).reshape(-1)))
             d0, d1 = dealer_range(rank, ws, n)
             assert (sc.d0, sc.d1) == (d0, d1)
             rng = random.Random(rank)
@@ -64,7 +67,11 @@ def _rank_main(rank, ws, port, names, errq):
                 sc.A0[:len(A0)] = torch.frombuffer(bytearray(A0), dtype=torch.uint8)
             sc.part[:] = torch.frombuffer(bytearray(part), dtype=torch.uint8)
             g2, g4, gA0, gpart = sc.exchange()
-            g2, g4 = CR.compact(g2.numpy(), ws, n, n), CR.compact(g4.numpy(), ws, n, n)
+            if packed:
+                assert g2.numel() == ws * sc.R * CR.packed_words(n)
+                g2, g4 = (CR.unpack_ranks(g.numpy().view(np.uint32), ws, n) for g in (g2, g4))
+            else:
+                g2, g4 = CR.compact(g2.numpy(), ws, n, n), CR.compact(g4.numpy(), ws, n, n)
             gA0 = CR.compact(gA0.numpy(), ws, n, 32)
             assert bytes(g2) == bytes(int(x) for x in c["dec2"]), name
             assert bytes(gA0) == b"".join(A[32 * N * i:32 * N * i + 32] for i in range(n)), name
@@ -201,12 +208,22 @@ class OracleBackend:
                 self._wr(d_terms + 32 * (i - d0), FR.g_mul(FR.lagrange_at_zero(ys, xs)))
         return False
 
-    def shard_combine_device(self, n, t, ws, d_dec2_g, d_dec4_g, d_dec2=None, d_dec4=None):
+    def decisions_pack_device(self, rows, nvalid, n, d0, d_dec, d_packed):
+        from tests import combine_ref as CR
+        raw = np.frombuffer(self._rd(d_dec, nvalid * n), dtype=np.uint8) if nvalid else np.zeros(0, np.uint8)
+        self._wr(d_packed, CR.pack_rows(raw, rows, nvalid, n, d0).tobytes())
+
+    def shard_combine_device(self, n, t, ws, d_dec2_g, d_dec4_g, d_dec2=None, d_dec4=None, packed=False):
         from dkg_amd.api import ShardOutcome
         from tests import combine_ref as CR
         R = CR.rows_per_rank(ws, n)
-        g2 = CR.compact(np.frombuffer(self._rd(d_dec2_g, ws * R * n), dtype=np.uint8), ws, n, n)
-        g4 = CR.compact(np.frombuffer(self._rd(d_dec4_g, ws * R * n), dtype=np.uint8), ws, n, n)
+        if packed:
+            sz = 4 * ws * R * CR.packed_words(n)
+            g2, g4 = (CR.unpack_ranks(np.frombuffer(self._rd(d, sz), dtype=np.uint32), ws, n)
+                      for d in (d_dec2_g, d_dec4_g))
+        else:
+            g2 = CR.compact(np.frombuffer(self._rd(d_dec2_g, ws * R * n), dtype=np.uint8), ws, n, n)
+            g4 = CR.compact(np.frombuffer(self._rd(d_dec4_g, ws * R * n), dtype=np.uint8), ws, n, n)
         d = CR.combine(g2, g4, n, t)
         if d_dec2:
             self._wr(d_dec2, bytes(d.dec2))

@@ -856,8 +856,9 @@ def test_binomial_schedules_goldens(be, golden, name, field):
     be.env_init(t, n, CK)
     try:
         be.set_field_mode(field)
-        # default; no lane pairs; lane pairs for every step; no mixed order; mixed order everywhere
-        for mode in (0, 1, 2, 3, 4):
+        # default; no lane pairs; lane pairs for every step; per step as default; per wave; per wave
+        # with the operands prefetched one item ahead
+        for mode in (0, 1, 2, 3, 4, 5):
             be.set_binomial(mode)
             for pieces, streams in ((1, 2), (min(3, t + 1), 1), (min(2, t + 1), 2)):
                 be.set_split(pieces)

@@ -41,5 +41,7 @@ def test_bench_multi_rank_gloo_on_one_gpu(gpus):
     for k, v in rm.items():
         assert 0 <= v["min"] <= v["max"], (k, v)
     assert rm["shard_device"]["min"] > 0
+    ex = out["exchange"]  # the decisions travel as packed bitmaps (dkg_decisions_pack_device)
+    assert ex["decisions"] == "packed bitmaps" and ex["bytes_per_rank"] < ex["bytes_per_rank_byte_rows"]
     rl = out["roofline"]
     assert rl["bound"] and rl["peak"] > 0 and 0 < rl["frac"] <= 1.2, rl

@@ -112,6 +112,7 @@ def write_traffic(d, out, key):
     doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
                      f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
            "key": key, "kernels": kern}
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
 
