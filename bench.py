@@ -577,6 +577,7 @@ def bench_batch(args, ws, rank, local):
     be.set_overlap(not args.no_overlap)
     be.set_verify_mode(args.verify)
     be.set_binomial(args.binomial)
+    be.set_check(args.check)
     be.set_stepping(args.stepping)
     be.env_init(t, n)
     dev = torch.device("cuda", local)
@@ -732,6 +733,8 @@ def main():
                     help="field multiply of the checks: 0 per launch by occupancy, 1 product scanning, 2 column sums")
     ap.add_argument("--binomial", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
                     help="binomial schedule (dkg_ctx_set_binomial): 0 default (per-wave Horner loops for tables of many column groups, else per step with lane pairs for the latency-bound steps), 1 per step without lane pairs, 2 per step with lane pairs for every step, 3 per step as 0, 4 per wave always, 5 per wave with operands prefetched one item ahead")
+    ap.add_argument("--check", type=int, default=0, choices=[0, 1],
+                    help="fused checks (dkg_ctx_set_check): 0 one launch, 1 one launch per fixed-base comb")
     ap.add_argument("--stepping", type=int, default=0, choices=[0, 1, 2, 3],
                     help="stepping slots (dkg_ctx_set_stepping): 0 cost model, 1 per column, 2 per piece, 3 no dead-position repack")
     ap.add_argument("--no-overlap", action="store_true", help="verify round 4 after round 3 (protocol order) instead of fused with round 2")
@@ -766,6 +769,7 @@ def main():
     be.set_addends(args.addends)
     be.set_stepping_formula(args.step_formula)
     be.set_binomial(args.binomial)
+    be.set_check(args.check)
     be.set_stepping(args.stepping)
     be.set_verify_mode(args.verify)
     h = be.env_init(t, n)

@@ -158,6 +158,11 @@ class Backend:
         wave always; 5 per wave always with each item's operand prefetched during the previous item."""
         _check(self._ctx, _lib.lib().dkg_ctx_set_binomial(self._ctx, mode))
 
+    def set_check(self, mode: int):
+        """Fused round-2/4 checks: 0 one launch over both combs (default), 1 one launch per comb with
+        g*s parked between them (dkg_ctx_set_check); decisions are identical."""
+        _check(self._ctx, _lib.lib().dkg_ctx_set_check(self._ctx, mode))
+
     def set_stepping(self, mode: int):
         """Stepping slots: 0 cost model, 1 one per column (all pieces of a split table), 2 one per
         piece, 3 as 0 without the dead-position repack of short unsplit tables; results are identical."""

@@ -1539,6 +1539,10 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
 // and its A row the column 64 after it.  g*s_ij is computed ONCE: compared with R_A (round 4,
 // committee.rs:537-541), then h*s'_ij is added and the sum compared with R_E (round 2,
 // committee.rs:292-305) -- the same group elements the two rounds compute separately.
+// PASS 0: both in one launch (the two radix-2^11 combs, 6.3 MB, share each XCD's 4-MB L2).  PASS 1 /
+// 2: the same work as two launches that each read ONE comb (3.1 MB): pass 1 computes g*s, decides
+// round 4 and parks g*s in acc[p] (160 B), pass 2 adds h*s' to it and decides round 2.
+template <int PASS>
 __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
                                                     uint32_t nmod, const uint32_t* __restrict__ s,
                                                     const uint32_t* __restrict__ sp, const uint32_t* __restrict__ R,
@@ -1546,7 +1550,7 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
                                                     const uint32_t* __restrict__ tab_h,
                                                     const uint8_t* __restrict__ dok, uint8_t* __restrict__ dec2,
                                                     uint8_t* __restrict__ dec4, const uint32_t* __restrict__ scale,
-                                                    size_t j0, size_t jn) {
+                                                    size_t j0, size_t jn, uint32_t* __restrict__ accb) {
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ndealers * jn) return;
   const size_t i = dealer0 + p / jn, j = j0 + p % jn;
@@ -1554,32 +1558,48 @@ __global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t n
   const size_t q = i * nrecv + j;  // share / decision index
   const bool self = (uint32_t)((i + dealer_base) % nmod) == (uint32_t)j;
   ge_p3 acc, r;
-  ge_identity(acc);
   sc x, f;
   if (scale) sc_load(f, scale + 8 * j);            // R holds b_j P(j): compare with g*(b_j s) + h*(b_j s')
-  sc_load(x, s + 8 * q);
-  if (scale) sc_mont_mul(x, x, f);
-  combw_mul_add(acc, x, tab_g);                    // G::generator() * s   (committee.rs:294, :537)
-  pt_load_aos(r, R, cA * nrecv + j);
-  bool eq = ristretto_eq(acc, r);                  // round 4 (:541)
-  dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);    // missing A: accusation (committee.rs:549-555)
+  if constexpr (PASS != 2) {
+    ge_identity(acc);
+    sc_load(x, s + 8 * q);
+    if (scale) sc_mont_mul(x, x, f);
+    combw_mul_add(acc, x, tab_g);                  // G::generator() * s   (committee.rs:294, :537)
+    pt_load_aos(r, R, cA * nrecv + j);
+    const bool eq = ristretto_eq(acc, r);          // round 4 (:541)
+    dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);  // missing A: accusation (committee.rs:549-555)
+    if constexpr (PASS == 1) {
+      pt_store_aos(accb, p, acc);
+      return;
+    }
+  } else {
+    pt_load_aos(acc, accb, p);
+  }
   sc_load(x, sp + 8 * q);
   if (scale) sc_mont_mul(x, x, f);
   combw_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
   pt_load_aos(r, R, cE * nrecv + j);
-  eq = ristretto_eq(acc, r);                       // round 2 (:305)
+  const bool eq = ristretto_eq(acc, r);            // round 2 (:305)
   dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)
 }
 
 void check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base, size_t nmod, const uint32_t* s,
                 const uint32_t* sp, const uint32_t* R, const uint32_t* tab_g, const uint32_t* tab_h,
                 const uint8_t* dok, uint8_t* dec2, uint8_t* dec4, hipStream_t stream, const uint32_t* scale, size_t j0,
-                size_t jn) {
+                size_t jn, uint32_t* acc) {
   if (!jn) jn = nrecv - j0;
   const size_t total = ndealers * jn;
   if (!total) return;
-  hipLaunchKernelGGL(k_check_both, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ndealers, nrecv,
-                     dealer0, dealer_base, (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale, j0, jn);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (!acc) {
+    hipLaunchKernelGGL(k_check_both<0>, grid, dim3(256), 0, stream, ndealers, nrecv, dealer0, dealer_base,
+                       (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale, j0, jn, acc);
+    return;
+  }
+  hipLaunchKernelGGL(k_check_both<1>, grid, dim3(256), 0, stream, ndealers, nrecv, dealer0, dealer_base,
+                     (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale, j0, jn, acc);
+  hipLaunchKernelGGL(k_check_both<2>, grid, dim3(256), 0, stream, ndealers, nrecv, dealer0, dealer_base,
+                     (uint32_t)nmod, s, sp, R, tab_g, tab_h, dok, dec2, dec4, scale, j0, jn, acc);
 }
 
 // Identity in every column of a position-major table [40][S] (S = N * npad words apart).

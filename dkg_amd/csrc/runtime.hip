@@ -54,6 +54,8 @@ struct dkg_ctx {
                                         // 5 per wave always, operands prefetched one item ahead
   int step_mode = 0;                    // stepping slots: 0 cost model, 1 whole columns, 2 per piece,
                                         // 3 as 0 without the dead-position repack
+  int check_mode = 0;                   // fused round-2/4 checks: 0 one launch, 1 the g and h combs
+                                        // in two launches (g*s parked between them)
   int fe_mode = 0;                      // field multiplication per launch: 0 by occupancy, 1 product
                                         // scanning (dkgk), 2 column sums (dkgk_ilp)
   int verify_mode = 0;                  // 0: difference tables (every P_i(j) in the group); 1: interpolation
@@ -582,8 +584,10 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
         if (segs[k].extra_ok) dkgk::and_dealer_mask(d1 - d0, nseg, k, segs[k].extra_ok + d0, dok + d0 * nseg, st);
     const VerifySeg& g = segs[0];
     if (nseg == 2) {
+      // split combs: every chunk parks its pairs' g*s at its own dealers' offset
+      uint32_t* acc = ctx->check_mode == 1 ? buf<uint32_t>(ctx, "v.acc", PTB * D * n) + d0 * n * PT_WORDS_H : nullptr;
       dkgk::check_both(d1 - d0, n, d0, g.dealer_base, g.self_mod ? g.self_mod : n, g.s, g.sp, R,
-                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st, sscale, j0, jn);
+                       ctx->tab_gw, ctx->tab_hw, dok, g.dec, segs[1].dec, st, sscale, j0, jn, acc);
     } else {
       dkgk::check(d1 - d0, n, g.dealer_base + d0, 0, g.self_mod ? g.self_mod : n, g.round, g.s + d0 * n * 8,
                   g.round == 2 ? g.sp + d0 * n * 8 : nullptr, R + d0 * n * PT_WORDS_H, ctx->tab_gw, ctx->tab_hw,
@@ -1623,6 +1627,12 @@ int dkg_ctx_set_split(dkg_ctx* ctx, int pieces) {
 int dkg_ctx_set_binomial(dkg_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 5) return DKG_E_ARG;
   ctx->binom_mode = mode;
+  return DKG_OK;
+}
+
+int dkg_ctx_set_check(dkg_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
+  ctx->check_mode = mode;
   return DKG_OK;
 }
 

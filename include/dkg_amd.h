@@ -80,6 +80,10 @@ int dkg_ctx_set_field_mode(dkg_ctx *ctx, int mode);
  * for every step; 3 -- per step as 0's; 4 -- per wave always; 5 -- per wave always, each item's
  * operand loaded during the previous item's chain.  Outputs do not depend on it. */
 int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
+/* The fused round-2/4 checks (g*s compared in round 4, + h*s' in round 2): 0 (default) one launch
+ * reading both fixed-base combs; 1 two launches that each read one comb (3.1 MB, an XCD's L2 holds
+ * it), g*s parked in device memory between them.  Outputs do not depend on it. */
+int dkg_ctx_set_check(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
  *  0 (default) -- difference tables: every P_i(j) = sum_k j^k C_k is computed as a group element and
  *                 compared with g s_ij + h s'_ij, as each receiver of the reference does;

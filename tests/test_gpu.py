@@ -496,6 +496,30 @@ def test_batch_verify_goldens(be, golden, overlap):
         _check_batch_member(c, r.ceremony(k), n)
 
 
+@pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json", "ceremony_n11_t5.json"])
+def test_check_split_combs_goldens(be, golden, name):
+    """The fused round-2/4 check as two launches, one per fixed-base comb (dkg_ctx_set_check 1: g*s
+    parked in device memory between them), unsplit and split tables, one and two chunk streams,
+    alone and batched: every output bit-exact against the fixture (committee.rs:287-305, 532-548)."""
+    c = golden(name)
+    n, t = c["n"], c["t"]
+    be.env_init(t, n, CK)
+    try:
+        be.set_check(1)
+        for pieces, streams in ((1, 2), (min(3, t + 1), 1), (0, 2)):
+            be.set_split(pieces)
+            be.set_streams(streams)
+            r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+            _check_ceremony(c, r, n)
+        rb = dkg_amd.ceremony_batch_verify(be, 3, n, t, *(H(c[k]) * 3 for k in ("E", "A", "s", "s_prime")))
+        for k in range(3):
+            _check_batch_member(c, rb.ceremony(k), n)
+    finally:
+        be.set_check(0)
+        be.set_split(0)
+        be.set_streams(2)
+
+
 def test_batch_verify_disclosure_goldens(be, golden):
     """Final parties with round-2 errors never disclose in phase 5 (committee.rs:340-347, 684): a batch
     of the n=16, t=3 fixtures in which they leave exactly t disclosures (a wrong recovered secret, as

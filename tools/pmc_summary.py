@@ -86,6 +86,8 @@ def phase(name):
         return "stepping_redo" if m.group(1) == "false" else "stepping"
     if re.match(r"void k_combine(_aff|_short)?<", name):
         return "combine"
+    if re.match(r"(void )?k_check_both(<\d>)?$", name):  # <0> fused; <1> / <2> the g and h comb passes
+        return "check"
     return {"k_affine_pieces": "affine", "k_check_both": "check", "k_check": "check", "k_commit": "commit",
             "k_enc_mul": "enc_mul", "k_dec_mul_w4": "dec_mul", "k_sym_xor": "sym"}.get(name)
 
