@@ -208,7 +208,8 @@ def pmc_traffic(kernel, n, t, U, plen=None, batch=1, mode="plain"):
         if key.get("split_len") is None:
             key["split_len"] = split_pieces(t, U)[1]
         if key == want and kernel in doc.get("kernels", {}):
-            return doc["kernels"][kernel]["bytes_per_launch"], doc["source"]
+            k = doc["kernels"][kernel]
+            return k["bytes_per_launch"], doc["source"], k.get("valu_int64_share")
     return None
 
 
@@ -226,6 +227,11 @@ def add_traffic(line, dom, ms_pass, n, t, U, plen, per_wave=False, batch=1, mode
         rl["traffic_source"] = pmc[1]
         if alg:
             rl["traffic_over_algorithmic"] = pmc[0] / alg
+        if pmc[2] is not None:
+            # the counters' own lower bound on the slot fraction: every SQ_INSTS_VALU_INT64 instruction
+            # is half rate (2 slots), the rest counted as full rate
+            rl["valu_int64_share"] = pmc[2]
+            rl["frac_counter_lower_bound"] = rl["instr_frac"] * (1 + pmc[2])
 
 
 def spawn_ranks(args, poll_s=0.2):

@@ -111,6 +111,20 @@ def write_traffic(d, out, key):
     for e in kern.values():
         e["bytes_per_launch"] = (e["fetch_bytes_x2"] / max(e["fetch_launches"], 1)
                                  + e["write_bytes"] / max(e["write_launches"], 1))
+    # the share of 64-bit VALU instructions (all half rate: the 64-bit mads and shifts) per phase, from
+    # the pmc_valu pass: slots >= instructions x (1 + share), the counters' own lower bound on the
+    # roofline's issue-slot unit (bench.py reports it beside frac and instr_frac)
+    va, _ = load_counters(os.path.join(d, "pmc_valu", "run_counter_collection.csv"))
+    agg = {}
+    for k, c in va.items():
+        ph = phase(k)
+        if ph in kern:
+            a = agg.setdefault(ph, [0.0, 0.0])
+            a[0] += c.get("SQ_INSTS_VALU", 0)
+            a[1] += c.get("SQ_INSTS_VALU_INT64", 0)
+    for ph, (ins, i64) in agg.items():
+        if ins:
+            kern[ph]["valu_int64_share"] = i64 / ins
     doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
                      f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
            "key": key, "kernels": kern}
