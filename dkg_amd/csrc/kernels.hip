@@ -381,11 +381,13 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
   }
 }
 
-// Radix-2^10 comb of point e0 + blockIdx.y of ext: block (window w = blockIdx.x, 512 threads),
-// thread d-1 writes d * 2^(10 w) B in affine Niels form (points.h combw_mul_add).
-__global__ __launch_bounds__(COMBW_ENTRIES) void k_build_combw(const uint32_t* __restrict__ ext, size_t stride,
+// Radix-2^COMBW_BITS comb of point e0 + blockIdx.y of ext: block (window w = blockIdx.x, entries
+// blockIdx.z * COMBW_BUILD_BS ..), thread d-1 writes d * 2^(COMBW_BITS w) B in affine Niels form
+// (points.h combw_mul_add).
+constexpr int COMBW_BUILD_BS = COMBW_ENTRIES < 512 ? COMBW_ENTRIES : 512;  // entries per block (grid.z: chunks)
+__global__ __launch_bounds__(COMBW_BUILD_BS) void k_build_combw(const uint32_t* __restrict__ ext, size_t stride,
                                                                size_t e0, uint32_t* __restrict__ tab) {
-  const int w = blockIdx.x, d = threadIdx.x + 1;
+  const int w = blockIdx.x, d = blockIdx.z * COMBW_BUILD_BS + threadIdx.x + 1;
   tab += (size_t)blockIdx.y * COMBW_WORDS;
   ge_p3 b, m;
   pt_load(b, ext, stride, e0 + blockIdx.y);
@@ -418,8 +420,8 @@ static_assert(COMBW_WORDS * 4 == (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW
 
 void build_combw(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
   if (!count) return;
-  hipLaunchKernelGGL(k_build_combw, dim3((unsigned)COMBW_WINDOWS, (unsigned)count), dim3(COMBW_ENTRIES), 0, stream,
-                     ext, stride, e0, tab);
+  hipLaunchKernelGGL(k_build_combw, dim3((unsigned)COMBW_WINDOWS, (unsigned)count, COMBW_ENTRIES / COMBW_BUILD_BS),
+                     dim3(COMBW_BUILD_BS), 0, stream, ext, stride, e0, tab);
 }
 
 __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, size_t N, const uint32_t* __restrict__ C,
