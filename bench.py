@@ -56,7 +56,17 @@ def add_cost(VALU, name, with_t=True):
     if name in NO_T:
         return VALU[NO_T[name]]
     return VALU[name] - (VALU["ge_add_signed"] - VALU["ge_add_signed_not"])
-COMBW_WINDOWS = 24  # points.h: radix-2^11 fixed-base comb, one mixed addition per window
+def combw_windows():
+    """Mixed additions per scalar of the fixed-base combs of g and h (points.h, radix 2^DKG_COMBW_BITS
+    of the loaded build: dkg_fixed_base_windows)."""
+    global _COMBW
+    if _COMBW is None:
+        import dkg_amd
+        _COMBW = dkg_amd.lib().dkg_fixed_base_windows()
+    return _COMBW
+
+
+_COMBW = None
 SLOTS = {k: v[1] for k, v in VALU.items()}
 
 
@@ -123,7 +133,7 @@ def hybrid_valu(n, sk, VALU=SLOTS):
     top, an addition per nonzero digit, the odd multiples), the encode / decode kernels and k_sym_xor
     (model above)."""
     items = 2 * n * n
-    enc = items * (COMBW_WINDOWS * VALU["combw_window"] + 64 * VALU["comb_window"])
+    enc = items * (combw_windows() * VALU["combw_window"] + 64 * VALU["comb_window"])
     dec = 0
     for q in range(n):
         ds = _wnaf(int.from_bytes(sk[32 * q:32 * q + 32], "little"), 4)
@@ -454,7 +464,7 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
             combine += c
     nsc = 2 if rnd == 2 else 1
     scale = nsc * VALU["sc_mont_mul"] if mults is not None else 0
-    check = n * (nsc * COMBW_WINDOWS * VALU["combw_window"] + VALU["eq"] + scale)  # radix-2^11 combs
+    check = n * (nsc * combw_windows() * VALU["combw_window"] + VALU["eq"] + scale)
     return {"binomial": binom * n, "stepping": stepping * n, "combine": combine * n, "check": check * n}
 
 
@@ -466,7 +476,7 @@ def fused_valu(n, t, U=1, VALU=SLOTS, plen=None, mults=None, affine=True, ded=Tr
     w4 = algorithmic_valu(n, t, 4, U, VALU, plen, mults, affine, ded)
     out = {k: w2[k] + w4[k] for k in ("binomial", "stepping", "combine")}
     scale = 2 * VALU["sc_mont_mul"] if mults is not None else 0
-    out["check"] = n * n * (2 * COMBW_WINDOWS * VALU["combw_window"] + 2 * VALU["eq"] + scale)
+    out["check"] = n * n * (2 * combw_windows() * VALU["combw_window"] + 2 * VALU["eq"] + scale)
     return out
 
 

@@ -418,6 +418,8 @@ __global__ __launch_bounds__(COMBW_BUILD_BS) void k_build_combw(const uint32_t* 
 static_assert(COMBW_WORDS * 4 == (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW_BITS) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4,
               "runtime.hip COMBW_BYTES must match points.h");
 
+int fixed_base_windows() { return COMBW_WINDOWS; }
+
 void build_combw(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
   if (!count) return;
   hipLaunchKernelGGL(k_build_combw, dim3((unsigned)COMBW_WINDOWS, (unsigned)count, COMBW_ENTRIES / COMBW_BUILD_BS),
@@ -1024,7 +1026,11 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
     // phase k: steps [J_k, J_{k+1}) on P_k-lane segments, J_k = nrecv - P_k + 1; it starts from the
     // state phase k-1 left (P_k positions, stride P_k) and leaves P_{k+1} positions for phase k+1.
     // Each phase's redo launch restarts from its unchanged starting state (the other buffer).
+    // the compact states keep ONE layout for every phase, [40][npad][N/2] (positions past a phase's
+    // segment unused): the chunks of a verification run their phases on their own streams at their
+    // own pace, and a phase-dependent stride would let one chunk's state overlap another's columns
     uint32_t* st[2] = {tail_a, tail_b};
+    const size_t Nh = N / 2;
     size_t P = N, j0 = 0;
     for (int k = 0; k < phases; k++) {
       const size_t Pn = P / 2, j1 = k + 1 < phases ? nrecv - Pn + 1 : nrecv;
@@ -1033,17 +1039,17 @@ bool stepping(size_t ndealers, size_t npad, size_t N, const uint32_t* e, size_t 
       if (!fits(grid.x)) return false;
       uint32_t* f = flags ? flags + foff : nullptr;
       foff += grid.x;
-      // the states are laid out for the whole table ([40][npad][P], word-row stride P npad): this
+      // the states are laid out for the whole table ([40][npad][Nh], word-row stride Nh npad): this
       // call's columns start at col0
-      const uint32_t* sin = k ? st[(k - 1) % 2] + col0 * P : nullptr;
-      uint32_t* sout = k + 1 < phases ? st[k % 2] + col0 * Pn : nullptr;
+      const uint32_t* sin = k ? st[(k - 1) % 2] + col0 * Nh : nullptr;
+      uint32_t* sout = k + 1 < phases ? st[k % 2] + col0 * Nh : nullptr;
       for (int pass = f ? 0 : 1; pass < 2; pass++) {
         if (pass == 0)
           step_launch_p<true, true>((int)s.maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, 0, (int)P,
-                                    nullptr, nullptr, R, 0, N, 0u, 1, (int)P, f, cr, j0, j1, sin, sout, P, Pn);
+                                    nullptr, nullptr, R, 0, N, 0u, 1, (int)P, f, cr, j0, j1, sin, sout, Nh, Nh);
         else
           step_launch_p<false, true>((int)s.maxbs, grid, block, stream, ndealers, npad, N, e, nrecv, 0, (int)P,
-                                     nullptr, nullptr, R, 0, N, 0u, 1, (int)P, f, cr, j0, j1, sin, sout, P, Pn);
+                                     nullptr, nullptr, R, 0, N, 0u, 1, (int)P, f, cr, j0, j1, sin, sout, Nh, Nh);
       }
       P = Pn;
       j0 = j1;

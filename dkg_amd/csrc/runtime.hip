@@ -241,8 +241,11 @@ struct VerifySeg {
 // chain, and 4 rounds of a chip's resident waves keep the last round's tail small.  Fewer groups
 // (n=1024: 128; n=4096: 512) keep one launch per step.
 #ifndef DKG_BINOM_WAVE_PF  // the per-wave binomial's default: operands prefetched one item ahead
-#define DKG_BINOM_WAVE_PF 0
+#define DKG_BINOM_WAVE_PF 0   // (2 waves per SIMD: config 5 +5.5 ms, profiles/r05_b5_ab.txt)
 #endif
+#ifndef DKG_BINOM_WAVE_COLMAJOR  // its last step writing the stepping's column-major table itself:
+#define DKG_BINOM_WAVE_COLMAJOR 0  // 4-B stores 128 B apart, +10 ms against k_to_column_major's 3.3
+#endif                             // (config 5, profiles/r05_b5_ab.txt)
 #ifndef DKG_BINOM_WAVE_GROUPS
 #define DKG_BINOM_WAVE_GROUPS 16384
 #endif
@@ -625,8 +628,9 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     }
     if (tm) HCK(hipEventRecord(ctx->pev[0], st));
     const uint32_t* e;
-    if (per_wave) {  // its last step writes the column-major table itself
-      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr, eT + c0 * L,
+    if (per_wave) {
+      e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr,
+                              DKG_BINOM_WAVE_COLMAJOR ? eT + c0 * L : nullptr,
                               ctx->binom_mode == 5 || (ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF));
     } else {
       dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
@@ -650,7 +654,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       e = bin;
     }
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
-    if (!per_wave) dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);  // timed with the stepping
+    if (!per_wave || !DKG_BINOM_WAVE_COLMAJOR)  // timed with the stepping
+      dkgk::to_column_major(w, W, L, e, eT + c0 * L, U, npad, st);
     uint32_t* fl = sflags ? sflags + dkgk::stepping_flag_words(c0, U) : nullptr;
     if (fl) HCK(hipMemsetAsync(fl, 0, 4 * dkgk::stepping_flag_words(w, U), st));
     auto step = step_ilp ? dkgk_ilp::stepping : dkgk::stepping;
@@ -2436,6 +2441,8 @@ int dkg_shard_combine_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_size
 }
 
 size_t dkg_packed_row_words(size_t n) { return (n + 31) / 32 + 1; }
+
+int dkg_fixed_base_windows(void) { return dkgk::fixed_base_windows(); }
 
 int dkg_decisions_pack_device(dkg_ctx* ctx, size_t rows, size_t nvalid, size_t n, size_t d0, const void* d_dec,
                               void* d_packed) {

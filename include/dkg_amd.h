@@ -328,6 +328,9 @@ int dkg_shard_combine_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_size
  * little-endian u32 words: bit j % 32 of word j / 32 set iff entry j is ACCEPT, then a kind word (0
  * checked, 1 MISSING row, 2 SKIPPED row).  n = 4096: 516 bytes per row instead of 4096. */
 size_t dkg_packed_row_words(size_t n);
+/* Windows (one mixed addition each) per scalar of the fixed-base combs of g and h the checks and
+ * commitments use (radix 2^DKG_COMBW_BITS, a build-time choice): the closed-form work of bench.py. */
+int dkg_fixed_base_windows(void);
 /* d_dec device [nvalid][n] raw rows of dealers d0 .. d0+nvalid-1 (dkg_ceremony_shard_device's
  * output) -> d_packed device [rows][dkg_packed_row_words(n)] u32, rows past nvalid zero (the padded
  * rank block, rows = dkg_shard_rows).  DKG_E_ARG if a row holds values the encoding cannot carry
