@@ -415,7 +415,7 @@ __global__ __launch_bounds__(COMBW_BUILD_BS) void k_build_combw(const uint32_t* 
   out[31] = 0;
 }
 
-static_assert(COMBW_WORDS * 4 == (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW_BITS) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4,
+static_assert(COMBW_WORDS * 4 == (size_t)(256 / DKG_COMBW_BITS + 1) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4,
               "runtime.hip COMBW_BYTES must match points.h");
 
 int fixed_base_windows() { return COMBW_WINDOWS; }
@@ -1645,6 +1645,19 @@ void and_dealer_mask(size_t D, int nseg, int seg, const uint8_t* extra, uint8_t*
   if (!D) return;
   hipLaunchKernelGGL(k_and_dealer_mask, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, D, (uint32_t)nseg,
                      (uint32_t)seg, extra, dok);
+}
+
+// out[i] = !a[i] && (b == NULL || b[i]): the qualified set from the rows that reject (b = NULL), the
+// honest set from the qualified set and the round-4 rejections (a = rej4, b = qualified)
+__global__ __launch_bounds__(256) void k_mask_not_and(size_t V, const uint8_t* __restrict__ a,
+                                                      const uint8_t* __restrict__ b, uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < V) out[i] = !a[i] && (!b || b[i]);
+}
+
+void mask_not_and(size_t V, const uint8_t* a, const uint8_t* b, uint8_t* out, hipStream_t stream) {
+  if (!V) return;
+  hipLaunchKernelGGL(k_mask_not_and, dim3((unsigned)((V + 255) / 256)), dim3(256), 0, stream, V, a, b, out);
 }
 
 void dealer_ok(size_t ndealers, size_t N, const uint8_t* point_ok, uint8_t* ok, hipStream_t stream) {

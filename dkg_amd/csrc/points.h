@@ -124,17 +124,19 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
   }
 }
 
-// Radix-2^11 comb in global memory (L2 / Infinity-Cache resident: 3.1 MB per base): 24 windows
-// B_w = 2^(11 w) B of 1024 affine Niels entries d B_w (d = 1..1024), entry-major, 32 words per entry
-// (ypx | ymx | xy2d | 2 pad).  Signed digits in [-1024, 1023]: one mixed addition per 11 scalar bits
-// (24 per 253-bit scalar; radix 2^10 took 26, 2^8 32, the LDS radix-16 comb 64), for the bases every
-// kernel shares (g, h).  The checks and commitments are VALU-bound: the two windows fewer pay more
-// than the table's extra L2 misses cost (radix 2^9 / 2^10 / 2^11: profiles/r04_comb_radix_ab.txt).
+// Radix-2^15 comb in global memory (37.7 MB per base: HBM, cached by L2 and the 256-MB Infinity
+// Cache): 18 windows B_w = 2^(15 w) B of 16,384 affine Niels entries d B_w (d = 1..16384),
+// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-16384, 16383]: one
+// mixed addition per 15 scalar bits (18 per scalar; radix 2^11 took 24, 2^8 32, the LDS radix-16
+// comb 64), for the bases every kernel shares (g, h).  The checks and commitments are VALU-bound:
+// fewer windows pay more than the misses on the larger tables cost (radix 2^9 .. 2^11:
+// profiles/r04_comb_radix_ab.txt; 2^11 .. 2^17: profiles/r05_comb_radix_ab.txt -- config 5 307.0 ->
+// 286.5 ms per batch at 2^15).
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 11  // -DDKG_COMBW_BITS=9 / 10: the A/B builds
+#define DKG_COMBW_BITS 15  // -DDKG_COMBW_BITS=11 .. 17: the A/B builds
 #endif
 constexpr int COMBW_BITS = DKG_COMBW_BITS;
-constexpr int COMBW_WINDOWS = (256 + COMBW_BITS - 1) / COMBW_BITS;  // 26: bits 250..259 absorb the top carry
+constexpr int COMBW_WINDOWS = 256 / COMBW_BITS + 1;  // the top window absorbs the signed recoding's carry
 constexpr int COMBW_ENTRIES = 1 << (COMBW_BITS - 1);
 constexpr int COMBW_STRIDE = 32;
 constexpr size_t COMBW_WORDS = (size_t)COMBW_WINDOWS * COMBW_ENTRIES * COMBW_STRIDE;

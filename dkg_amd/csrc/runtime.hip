@@ -103,11 +103,11 @@ constexpr size_t PT_WORDS_H = 40;
 constexpr size_t AFFP_WORDS_H = 32;  // affine addend slot of kernels.hip affine_pieces
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 11
+#define DKG_COMBW_BITS 15
 #endif
-// points.h COMBW_WORDS x 4 (radix 2^11: 24 windows x 1024 entries x 128 B)
+// points.h COMBW_WORDS x 4 (radix 2^15: 18 windows x 16,384 entries x 128 B = 37.7 MB)
 constexpr size_t COMBW_BYTES =
-    (size_t)((256 + DKG_COMBW_BITS - 1) / DKG_COMBW_BITS) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4;
+    (size_t)(256 / DKG_COMBW_BITS + 1) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4;
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
                                0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
                                0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
@@ -706,16 +706,21 @@ void verify_one(dkg_ctx* ctx, size_t n, size_t t, int round, size_t D, size_t de
 // e_ok (may be null): per-dealer device mask, 0 = the dealer's round-1 data is missing (round 2:
 // DKG_MISSING); a_ok (may be null): 0 = its phase-3 commitments are missing (round 4: accusation)
 // (full mode), folded into the round-2 decisions like an undecodable commitment.
+// host_between = false (fused rounds only): `between` only queues device work, so it follows the
+// checks on the stream without a host round trip; the caller syncs and calls collect_phases.
 template <typename F>
 void verify_rounds_group(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
                          const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
-                         hipEvent_t after2, F&& between, const uint8_t* e_ok, const uint8_t* a_ok) {
+                         hipEvent_t after2, F&& between, const uint8_t* e_ok, const uint8_t* a_ok,
+                         bool host_between) {
   if (ctx->overlap) {
     VerifySeg g[2] = {{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok}, {4, D, dealer_base, Acomp, s, nullptr, dec4, a_ok}};
     verify_device(ctx, n, t, g, 2, true, "r24");
     if (after2) HCK(hipEventRecord(after2, ctx->stream));
-    sync(ctx);
-    collect_phases(ctx);
+    if (host_between) {
+      sync(ctx);
+      collect_phases(ctx);
+    }
     between();
   } else {
     VerifySeg g2{2, D, dealer_base, Ecomp, s, sp, dec2, e_ok};
@@ -909,14 +914,16 @@ void verify_rounds_interp(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dea
 template <typename F>
 void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_base, const uint32_t* Ecomp,
                    const uint32_t* Acomp, const uint32_t* s, const uint32_t* sp, uint8_t* dec2, uint8_t* dec4,
-                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
+                   hipEvent_t after2, F&& between, const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr,
+                   bool host_between = true) {
   // dkg_ctx_stepping_redos reports THIS verification's stepping (none if it builds no tables)
   ctx->last_step_flags = nullptr;
   ctx->last_step_flag_words = 0;
   if (ctx->verify_mode == 1)
     verify_rounds_interp(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok);
   else
-    verify_rounds_group(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok);
+    verify_rounds_group(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok,
+                        host_between);
 }
 
 double ev_ms(dkg_ctx* ctx, int a, int b) {
@@ -1251,34 +1258,77 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   uint8_t* dec2 = buf<uint8_t>(ctx, "b.dec2", V * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "b.dec4", V * n);
   uint8_t* qmask = buf<uint8_t>(ctx, "b.qmask", V);
+  uint8_t* rej2 = buf<uint8_t>(ctx, "b.rej2", V);
+  uint8_t* rej4 = buf<uint8_t>(ctx, "b.rej4", V);
+  uint8_t* r4d = buf<uint8_t>(ctx, "b.r4err", V);
+  uint8_t* hmask = buf<uint8_t>(ctx, "b.hmask", V);
+  int32_t* cnt = buf<int32_t>(ctx, "b.cnt", 4 * V);
   uint32_t* fs = buf<uint32_t>(ctx, "b.final", 32 * V);
   uint32_t* pub = buf<uint32_t>(ctx, "b.pub_ext", PTB * V);
   uint32_t* pubc = buf<uint32_t>(ctx, "b.pub_comp", 32 * V);
-  std::vector<uint8_t> qualified(V), r2err(V), recon(V, 0), honest(V);
+  std::vector<uint8_t> qualified(V), r2err(V), recon(V, 0), honest(V), r4e(V), h_rej4(V);
   std::vector<int32_t> complaints(V);
+  // The outcomes stay on the device until the end (one host round trip per batch): the rows that
+  // reject or miss disqualify (committee.rs:311-316, 331-335, 370-398), round 3 sums the qualified
+  // dealers' shares (:433-476), round 4's rejections reconstruct qualified dealers (:660-670) and the
+  // honest set -- qualified, not reconstructed -- sums the master key (:726-805).
   auto round3 = [&] {
-    // round-2 outcome per ceremony (committee.rs:311-316, 340-347, 370-398)
-    round2_outcome(ctx, B, n, t, dec2, qmask, qualified.data(), complaints.data(), r2err.data());
-    // round 3 (committee.rs:433-476) per ceremony
+    dkgk::decision_summary(B, n, dec2, rej2, cnt, ctx->stream);
+    dkgk::mask_not_and(V, rej2, nullptr, qmask, ctx->stream);
     wait_shares(ctx, ctx->stream);  // shares evaluated on the side stream (BatchRound1)
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
     dkgk::fixed_base(V, fs, ctx->tab_gw, pub, ctx->stream);
     dkgk::encode_points(pub, V, V, pubc, ctx->stream);
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
-  verify_rounds(ctx, n, t, V, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3);
-  // round-4 outcome: a qualified dealer rejected by someone is reconstructed (committee.rs:660-670),
-  // disqualified dealers' rows SKIPPED (:522)
-  std::vector<uint8_t> r4e(V);
-  round4_outcome(ctx, B, n, t, dec4, qmask, qualified.data(), recon.data(), r4e.data());
+  verify_rounds(ctx, n, t, V, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, nullptr, nullptr, false);
+  // round 4 (committee.rs:515-522, 567-569, 660-670): rows of disqualified dealers SKIPPED
+  dkgk::decision_summary(B, n, dec4, rej4, nullptr, ctx->stream);
+  dkgk::r4_error(B, n, t, dec4, qmask, r4d, ctx->stream);
+  dkgk::apply_skipped(B, n, dec4, qmask, ctx->stream);
+  dkgk::mask_not_and(V, rej4, qmask, hmask, ctx->stream);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
+  // finalise (committee.rs:726-805): mpk_c = sum of the honest A_i0 (+ g * reconstructed secrets)
+  uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
+  if (ctx->r1_A0) {  // written by the deferred commitments (k_commit_pm), [40][V]
+    HCK(hipMemcpyAsync(A0, ctx->r1_A0, PTB * V, hipMemcpyDeviceToDevice, ctx->stream));
+  } else if (ctx->ext_A) {
+    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, V, A0, V, ctx->stream);
+  } else {
+    uint32_t* A0c = buf<uint32_t>(ctx, "b.A0c", 32 * V);
+    HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, V, hipMemcpyDeviceToDevice, ctx->stream));
+    uint8_t* a0ok = buf<uint8_t>(ctx, "b.A0ok", V);
+    dkgk::decode_points(A0c, V, A0, V, a0ok, ctx->stream);
+  }
+  uint32_t* mpk_ext = buf<uint32_t>(ctx, "b.mpk_ext", PTB * B);
+  dkgk::sum_points(n, A0, V, hmask, mpk_ext, B, 0, ctx->stream, B);
+  uint32_t* mpk_c = buf<uint32_t>(ctx, "b.mpk_comp", 32 * B);
+  dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
+  check_launch(ctx);
+  d2h(ctx, qualified.data(), rej2, V);  // inverted below
+  d2h(ctx, complaints.data(), cnt, 4 * V);
+  d2h(ctx, h_rej4.data(), rej4, V);
+  d2h(ctx, r4e.data(), r4d, V);
+  if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
+  if (out->final_share) d2h(ctx, out->final_share, fs, 32 * V);
+  if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * V);
+  if (out->dec2) d2h(ctx, out->dec2, dec2, V * n);
+  if (out->dec4) d2h(ctx, out->dec4, dec4, V * n);  // SKIPPED rows applied
+  HCK(hipEventRecord(ctx->ev[5], ctx->stream));
+  sync(ctx);
+  collect_phases(ctx);
+  for (size_t i = 0; i < V; i++) {
+    qualified[i] = !qualified[i];
+    r2err[i] = complaints[i] > (int32_t)t;  // committee.rs:340-347
+    recon[i] = qualified[i] && h_rej4[i];
+    honest[i] = qualified[i] && !recon[i];
+  }
   std::vector<size_t> recon_cer, nompk;
   std::vector<uint8_t> p4err(B, 0);
   for (size_t c = 0; c < B; c++) {
     bool any = false;
     int32_t h = 0;
     for (size_t i = c * n; i < (c + 1) * n; i++) {
-      honest[i] = qualified[i] && !recon[i];
       any |= recon[i] != 0;
       h += honest[i];
     }
@@ -1291,23 +1341,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
         recon_cer.push_back(c);
     }
   }
-  // finalise (committee.rs:726-805): mpk_c = sum of honest A_i0 (+ g * reconstructed secrets)
-  uint32_t* A0 = buf<uint32_t>(ctx, "b.A0ext", PTB * V);
-  if (ctx->r1_A0) {  // written by the deferred commitments (k_commit_pm), [40][V]
-    HCK(hipMemcpyAsync(A0, ctx->r1_A0, PTB * V, hipMemcpyDeviceToDevice, ctx->stream));
-  } else if (ctx->ext_A) {
-    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, V, A0, V, ctx->stream);
-  } else {
-    uint32_t* A0c = buf<uint32_t>(ctx, "b.A0c", 32 * V);
-    HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, V, hipMemcpyDeviceToDevice, ctx->stream));
-    uint8_t* a0ok = buf<uint8_t>(ctx, "b.A0ok", V);
-    dkgk::decode_points(A0c, V, A0, V, a0ok, ctx->stream);
-  }
-  uint8_t* hmask = buf<uint8_t>(ctx, "b.hmask", V);
-  h2d(ctx, hmask, honest.data(), V);
-  uint32_t* mpk_ext = buf<uint32_t>(ctx, "b.mpk_ext", PTB * B);
-  dkgk::sum_points(n, A0, V, hmask, mpk_ext, B, 0, ctx->stream, B);
-  if (!recon_cer.empty()) {
+  if (!recon_cer.empty()) {  // ceremonies with round-4 accusations: + g * the reconstructed secrets
     uint32_t* extra = buf<uint32_t>(ctx, "b.mpk_extra", PTB * B);
     std::vector<uint8_t> hs(32 * n * n);
     for (size_t c : recon_cer) {
@@ -1327,17 +1361,11 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
       dkgk::add_points(1, mpk_ext + c, extra + c, B, mpk_ext + c, ctx->stream);
       sync(ctx);  // sec / gsec are reused by the next ceremony
     }
+    dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
+    check_launch(ctx);
+    if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
+    sync(ctx);
   }
-  uint32_t* mpk_c = buf<uint32_t>(ctx, "b.mpk_comp", 32 * B);
-  dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
-  check_launch(ctx);
-  if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
-  if (out->final_share) d2h(ctx, out->final_share, fs, 32 * V);
-  if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * V);
-  if (out->dec2) d2h(ctx, out->dec2, dec2, V * n);
-  if (out->dec4) d2h(ctx, out->dec4, dec4, V * n);  // SKIPPED rows applied (round4_outcome)
-  HCK(hipEventRecord(ctx->ev[5], ctx->stream));
-  sync(ctx);
   if (out->r4_error) memcpy(out->r4_error, r4e.data(), V);
   if (out->qualified) memcpy(out->qualified, qualified.data(), V);
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), V);
