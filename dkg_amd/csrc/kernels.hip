@@ -269,16 +269,28 @@ __global__ __launch_bounds__(256) void k_share_eval(size_t D, size_t n, size_t N
   sc_load(fa, ai + 8 * (N - 1));
   sc_load(fb, bi + 8 * (N - 1));
   size_t k = N - 1;
-  if (x < 2048) {  // two Horner steps per reduction (sc_horner2)
-    sc c0;
-    for (; k >= 2; k -= 2) {
-      sc_load(c, ai + 8 * (k - 1));
-      sc_load(c0, ai + 8 * (k - 2));
-      sc_horner2(fa, fa, x, c, c0);
-      sc_load(c, bi + 8 * (k - 1));
-      sc_load(c0, bi + 8 * (k - 2));
-      sc_horner2(fb, fb, x, c, c0);
+  if (x < 8192) {  // lazy reduction: one fold per SC_LAZY_STEPS Horner steps (sc25519.h)
+    uint32_t va[10], vb[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      va[i] = i < 8 ? fa.v[i] : 0u;
+      vb[i] = i < 8 ? fb.v[i] : 0u;
     }
+    while (k > 0) {
+      const int steps = k < (size_t)SC_LAZY_STEPS ? (int)k : SC_LAZY_STEPS;
+#pragma unroll 1
+      for (int u = 0; u < steps; u++) {
+        k--;
+        sc_load(c, ai + 8 * k);
+        sc_lazy_step(va, x, c);
+        sc_load(c, bi + 8 * k);
+        sc_lazy_step(vb, x, c);
+      }
+      sc_lazy_fold(va);
+      sc_lazy_fold(vb);
+    }
+    sc_lazy_final(fa, va);
+    sc_lazy_final(fb, vb);
   }
   while (k-- > 0) {
     sc_load(c, ai + 8 * k);

@@ -124,16 +124,16 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
   }
 }
 
-// Radix-2^15 comb in global memory (37.7 MB per base: HBM, cached by L2 and the 256-MB Infinity
-// Cache): 18 windows B_w = 2^(15 w) B of 16,384 affine Niels entries d B_w (d = 1..16384),
-// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-16384, 16383]: one
-// mixed addition per 15 scalar bits (18 per scalar; radix 2^11 took 24, 2^8 32, the LDS radix-16
+// Radix-2^17 comb in global memory (134 MB per base: HBM, read through L2 and the 256-MB Infinity
+// Cache): 16 windows B_w = 2^(17 w) B of 65,536 affine Niels entries d B_w (d = 1..65536),
+// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-65536, 65535]: one
+// mixed addition per 17 scalar bits (16 per scalar; radix 2^11 took 24, 2^8 32, the LDS radix-16
 // comb 64), for the bases every kernel shares (g, h).  The checks and commitments are VALU-bound:
-// fewer windows pay more than the misses on the larger tables cost (radix 2^9 .. 2^11:
-// profiles/r04_comb_radix_ab.txt; 2^11 .. 2^17: profiles/r05_comb_radix_ab.txt -- config 5 307.0 ->
-// 286.5 ms per batch at 2^15).
+// each window fewer pays more than the misses on the larger tables cost (radix 2^9 .. 2^11:
+// profiles/r04_comb_radix_ab.txt; 2^11 .. 2^17: profiles/r05_comb_radix_ab.txt -- config 5 device
+// time 2^11 -> 2^15 -> 2^17: 303.6 -> 282.2 -> 273.3 ms per batch).
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 15  // -DDKG_COMBW_BITS=11 .. 17: the A/B builds
+#define DKG_COMBW_BITS 17  // -DDKG_COMBW_BITS=11 .. 17: the A/B builds
 #endif
 constexpr int COMBW_BITS = DKG_COMBW_BITS;
 constexpr int COMBW_WINDOWS = 256 / COMBW_BITS + 1;  // the top window absorbs the signed recoding's carry

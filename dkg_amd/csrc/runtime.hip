@@ -103,9 +103,9 @@ constexpr size_t PT_WORDS_H = 40;
 constexpr size_t AFFP_WORDS_H = 32;  // affine addend slot of kernels.hip affine_pieces
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 15
+#define DKG_COMBW_BITS 17
 #endif
-// points.h COMBW_WORDS x 4 (radix 2^15: 18 windows x 16,384 entries x 128 B = 37.7 MB)
+// points.h COMBW_WORDS x 4 (radix 2^17: 16 windows x 65,536 entries x 128 B = 134 MB)
 constexpr size_t COMBW_BYTES =
     (size_t)(256 / DKG_COMBW_BITS + 1) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4;
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,

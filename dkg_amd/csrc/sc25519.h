@@ -112,6 +112,63 @@ DKG_DEV void sc_horner2(sc& r, const sc& a, uint32_t x, const sc& c1, const sc& 
   sc_reduce9(r, w);
 }
 
+// Horner at a small point with lazy reduction (share evaluation, x < 2^13): the accumulator is ten
+// 32-bit limbs and takes up to SC_LAZY_STEPS steps acc * x + c (13 bits each) from below 2^254
+// before one fold with 2^252 = -delta mod l:
+//   V = H 2^252 + Lo  ->  Lo + l - H delta,
+// H < 2^68 so H delta < 2^193 < l: never negative, below 2^254 again.  One fold per five steps
+// instead of a full reduction per one or two (sc_mul_small_add / sc_horner2).
+constexpr int SC_LAZY_STEPS = 5;  // 2^254 * (2^13)^5 + the coefficients < 2^320
+DKG_DEV void sc_lazy_step(uint32_t (&v)[10], uint32_t x, const sc& c) {
+  uint64_t t = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    t = (uint64_t)v[i] * x + (i < 8 ? c.v[i] : 0u) + (t >> 32);
+    v[i] = (uint32_t)t;
+  }
+}
+
+DKG_DEV void sc_lazy_fold(uint32_t (&v)[10]) {
+  const uint32_t h[3] = {(v[7] >> 28) | (v[8] << 4), (v[8] >> 28) | (v[9] << 4), v[9] >> 28};
+  // P = H delta (7 limbs, < 2^193), column by column
+  uint32_t p[7];
+  uint64_t acc = 0, hiacc = 0;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 4) {
+        const uint64_t m = (uint64_t)h[i] * sc_const::DELTA[j];
+        acc += (uint32_t)m;
+        hiacc += m >> 32;
+      }
+    }
+    p[k] = (uint32_t)acc;
+    acc = (acc >> 32) + hiacc;
+    hiacc = 0;
+  }
+  // Lo + l - P over 8 limbs (the result is positive and below 2^254)
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t lo = i < 7 ? v[i] : (v[7] & 0x0fffffffu);
+    c += (int64_t)lo + sc_const::L[i] - (i < 7 ? p[i] : 0u);
+    v[i] = (uint32_t)c;
+    c >>= 32;  // arithmetic: a borrow is -1
+  }
+  v[8] = 0;
+  v[9] = 0;
+}
+
+// the canonical value of a folded accumulator (< 2^254)
+DKG_DEV void sc_lazy_final(sc& r, const uint32_t (&v)[10]) {
+  uint32_t w[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) w[i] = v[i];
+  sc_reduce9(r, w);
+}
+
 // r = a + b mod l
 DKG_DEV void sc_add(sc& r, const sc& a, const sc& b) {
   uint32_t w[9];
