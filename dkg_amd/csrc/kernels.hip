@@ -190,7 +190,7 @@ __device__ __forceinline__ void lds_fill(uint32_t* lds, const uint32_t* __restri
 
 
 // ------------------------------------------------------------------ K2 commitments
-__global__ __launch_bounds__(256, 4) void k_commit(size_t count, const uint32_t* __restrict__ a,
+__global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_commit(size_t count, const uint32_t* __restrict__ a,
                                                 const uint32_t* __restrict__ b,
                                                 const uint32_t* __restrict__ tab_g,
                                                 const uint32_t* __restrict__ tab_h,
@@ -221,7 +221,7 @@ void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* 
 // coefficient k), lanes = dealers, so the E and A columns of a group (columns 128 g + lane and
 // 128 g + 64 + lane, piece k / L at position k % L) are written coalesced; no extended-form E/A
 // arrays and no placement pass.  The lanes of k = 0 also write A_i0 (A0 [40][A0stride], finalise).
-__global__ __launch_bounds__(64, 4) void k_commit_pm(size_t D, size_t N, const uint32_t* __restrict__ a,
+__global__ __launch_bounds__(64, DKG_COMB_WAVES) void k_commit_pm(size_t D, size_t N, const uint32_t* __restrict__ a,
                                                    const uint32_t* __restrict__ b,
                                                    const uint32_t* __restrict__ tab_g,
                                                    const uint32_t* __restrict__ tab_h, uint32_t* __restrict__ out,
@@ -1513,7 +1513,7 @@ void combine(size_t width, size_t pstride, size_t pieces, size_t nrecv, const in
 }
 
 // ------------------------------------------------------------------ K3c check
-__global__ __launch_bounds__(256, 4) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base,
+__global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base,
                                                uint32_t nmod, int round,
                                                const uint32_t* __restrict__ s, const uint32_t* __restrict__ sp,
                                                const uint32_t* __restrict__ R,
@@ -1563,7 +1563,7 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
 // 2: the same work as two launches that each read ONE comb (3.1 MB): pass 1 computes g*s, decides
 // round 4 and parks g*s in acc[p] (160 B), pass 2 adds h*s' to it and decides round 2.
 template <int PASS>
-__global__ __launch_bounds__(256, 4) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
+__global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
                                                     uint32_t nmod, const uint32_t* __restrict__ s,
                                                     const uint32_t* __restrict__ sp, const uint32_t* __restrict__ R,
                                                     const uint32_t* __restrict__ tab_g,

@@ -143,64 +143,83 @@ constexpr size_t COMBW_WORDS = (size_t)COMBW_WINDOWS * COMBW_ENTRIES * COMBW_STR
 static_assert(COMBW_WINDOWS * COMBW_BITS > 256 && (1 << (256 - (COMBW_WINDOWS - 1) * COMBW_BITS)) < COMBW_ENTRIES,
               "the top window must absorb the signed recoding's carry for any 256-bit scalar");
 
+// Window w's signed digit (carry in / out) and its entry in the comb of base `tab`.
+DKG_DEV const uint32_t* combw_entry(const sc& s, int w, int& carry, bool& neg, bool& zero,
+                                    const uint32_t* __restrict__ tab) {
+  // bits [B w, B w + B) of the scalar: words wi and wi + 1 (wave-uniform selects)
+  const int bit = COMBW_BITS * w, wi = bit >> 5, sh = bit & 31;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    lo = (wi == k) ? s.v[k] : lo;
+    hi = (wi + 1 == k) ? s.v[k] : hi;
+  }
+  const uint32_t raw = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh) & ((1u << COMBW_BITS) - 1);
+  int d = (int)raw + carry;
+  carry = (d + COMBW_ENTRIES) >> COMBW_BITS;
+  d -= carry << COMBW_BITS;
+  const int ad = d < 0 ? -d : d;
+  neg = d < 0;
+  zero = ad == 0;
+  return tab + ((size_t)w * COMBW_ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMBW_STRIDE;
+}
+
+// The entry's 30 words as an affine Niels addend: -Q = (y-x, y+x, -2dxy), 0 = (1, 1, 0).
+DKG_DEV void combw_select(ge_aff& r, const uint4 (&e)[8], bool neg, bool zero) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(e);  // ypx 0..9 | ymx 10..19 | xy2d 20..29
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t ypx = q[i], ymx = q[10 + i];
+    r.ypx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? ymx : ypx);
+    r.ymx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? ypx : ymx);
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t p2 = i == 0 ? fe_const::P2_0 : ((i & 1) ? fe_const::P2_O : fe_const::P2_E);
+    r.xy2d.v[i] = zero ? 0u : (neg ? p2 - q[20 + i] : q[20 + i]);
+  }
+}
+
+// acc += s * B with the radix-2^COMBW_BITS comb of B.  The digits are known up front, so each
+// window's entry is loaded one window ahead (DKG_COMBW_PF, 32 VGPRs): the load of a 128-B entry
+// from tables far beyond L2 lands during the previous window's mixed addition.
+#ifndef DKG_COMBW_PF
+#define DKG_COMBW_PF 1
+#endif
+// minimum resident waves per SIMD of the fixed-base kernels (check, commitments, fixed_base): 4 caps
+// them at 128 VGPRs, 3 at 168, 2 at 256
+#ifndef DKG_COMB_WAVES
+#define DKG_COMB_WAVES 4
+#endif
 DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
   int carry = 0;
+  bool neg, zero;
+  uint4 e[8];
+  if constexpr (DKG_COMBW_PF) {
+    const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, 0, carry, neg, zero, tab));
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = p[k];
+  }
 #pragma unroll 1
   for (int w = 0; w < COMBW_WINDOWS; w++) {
-    // bits [10 w, 10 w + 10) of the scalar: words wi and wi + 1 (wave-uniform selects)
-    const int bit = COMBW_BITS * w, wi = bit >> 5, sh = bit & 31;
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      lo = (wi == k) ? s.v[k] : lo;
-      hi = (wi + 1 == k) ? s.v[k] : hi;
-    }
-    const uint32_t raw = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh) & ((1u << COMBW_BITS) - 1);
-    int d = (int)raw + carry;
-    carry = (d + COMBW_ENTRIES) >> COMBW_BITS;
-    d -= carry << COMBW_BITS;
-    const int ad = d < 0 ? -d : d;
-    const uint32_t* ep = tab + ((size_t)w * COMBW_ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMBW_STRIDE;
-    const bool neg = d < 0, zero = ad == 0;
-    // the entry's 30 words, selected as they arrive: -Q = (y-x, y+x, -2dxy), 0 = (1, 1, 0)
     ge_aff r;
-    {
-      uint32_t qa[12], qb[12];
-      const uint4* e4 = reinterpret_cast<const uint4*>(ep);
+    if constexpr (DKG_COMBW_PF) {
+      combw_select(r, e, neg, zero);
+      if (w + 1 < COMBW_WINDOWS) {
+        const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, w + 1, carry, neg, zero, tab));
 #pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const uint4 u = e4[k], v = e4[k + 2];  // words 4k..4k+3 (ypx...) and 8+4k.. (ymx...)
-        qa[4 * k] = u.x; qa[4 * k + 1] = u.y; qa[4 * k + 2] = u.z; qa[4 * k + 3] = u.w;
-        (void)v;
+        for (int k = 0; k < 8; k++) e[k] = p[k];
       }
+    } else {
+      const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, w, carry, neg, zero, tab));
 #pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const uint4 v = e4[2 + k];  // words 8..19
-        qb[4 * k] = v.x; qb[4 * k + 1] = v.y; qb[4 * k + 2] = v.z; qb[4 * k + 3] = v.w;
-      }
-      // qa[0..9] = ypx, qa[10..11] = ymx[0..1]; qb = words 8..19: ymx = qa[10..11] ++ qb[4..11]
-#pragma unroll
-      for (int i = 0; i < 10; i++) {
-        const uint32_t ypx = qa[i], ymx = i < 2 ? qa[10 + i] : qb[2 + i];
-        r.ypx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? ymx : ypx);
-        r.ymx.v[i] = zero ? (i == 0 ? 1u : 0u) : (neg ? ypx : ymx);
-      }
-      const uint4* x4 = reinterpret_cast<const uint4*>(ep + 20);
-      uint32_t xw[12];
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const uint4 v = x4[k];
-        xw[4 * k] = v.x; xw[4 * k + 1] = v.y; xw[4 * k + 2] = v.z; xw[4 * k + 3] = v.w;
-      }
-#pragma unroll
-      for (int i = 0; i < 10; i++) {
-        const uint32_t p2 = i == 0 ? fe_const::P2_0 : ((i & 1) ? fe_const::P2_O : fe_const::P2_E);
-        r.xy2d.v[i] = zero ? 0u : (neg ? p2 - xw[i] : xw[i]);
-      }
+      for (int k = 0; k < 8; k++) e[k] = p[k];
+      combw_select(r, e, neg, zero);
     }
     ge_madd(acc, acc, r);
   }
 }
+
 
 // Register-lean variants for the m-chains: the cached addend lives in LDS (lane-interleaved,
 // word w of lane l at q[w * 64 + l], conflict-free) and is read field by field when the addition

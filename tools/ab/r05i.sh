@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 5: profiles of the round's tree (headline and config 5: kernel trace + SQ / FETCH / WRITE /
+# VALU passes, traffic files), and the 2/4/8-way n=1024 shard with five short pieces against four.
+set -o pipefail
+R=$(pwd)
+O=$R/gpurun_out/r05i
+mkdir -p $O
+bash tools/profile.sh r05i_D || { echo PROFILE D FAILED; exit 1; }
+python tools/pmc_summary.py gpurun_out/prof_r05i_D --traffic $O/traffic/r05i_D.json --n 1024 --t 511 --split 4 \
+  --split-len 128 > $O/prof_D_summary.txt 2>&1 || { echo SUMMARY D FAILED; tail -5 $O/prof_D_summary.txt; exit 1; }
+head -12 $O/prof_D_summary.txt
+bash tools/profile.sh r05i_B5 --config B5 || { echo PROFILE B5 FAILED; exit 1; }
+python tools/pmc_summary.py gpurun_out/prof_r05i_B5 --traffic $O/traffic/r05i_B5.json --n 64 --t 31 --split 1 \
+  --split-len 32 --batch 10000 > $O/prof_B5_summary.txt 2>&1 || { echo SUMMARY B5 FAILED; tail -5 $O/prof_B5_summary.txt; exit 1; }
+head -12 $O/prof_B5_summary.txt
+bash tools/ab/ab.sh r05i_shard 2 300 "python tools/shard_time.py --ws 2,4,8 --reps 3" "u4=--split 4" "u5=--split 5" \
+  || { echo AB SHARD FAILED; exit 1; }
+python tools/ab/summary.py gpurun_out/ab_r05i_shard > $O/ab_shard.txt 2>&1; cat $O/ab_shard.txt
+bash tools/ab/ab.sh r05i_E 2 300 "python bench.py --config E --steps 2 --warmup 1 --no-cpu --no-interp" "u4=--split 4" "u5=--split 5" \
+  || { echo AB E FAILED; exit 1; }
+python tools/ab/summary.py gpurun_out/ab_r05i_E > $O/ab_E.txt 2>&1; cat $O/ab_E.txt
+echo ALL DONE
