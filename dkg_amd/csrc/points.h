@@ -180,42 +180,26 @@ DKG_DEV void combw_select(ge_aff& r, const uint4 (&e)[8], bool neg, bool zero) {
   }
 }
 
-// acc += s * B with the radix-2^COMBW_BITS comb of B.  The digits are known up front, so each
-// window's entry is loaded one window ahead (DKG_COMBW_PF, 32 VGPRs): the load of a 128-B entry
-// from tables far beyond L2 lands during the previous window's mixed addition.
-#ifndef DKG_COMBW_PF
-#define DKG_COMBW_PF 1
-#endif
-// minimum resident waves per SIMD of the fixed-base kernels (check, commitments, fixed_base): 4 caps
-// them at 128 VGPRs, 3 at 168, 2 at 256
+// minimum resident waves per SIMD of the fixed-base kernels (check, commitments): 4 caps them at 128
+// VGPRs, 3 at 168, 2 at 256
 #ifndef DKG_COMB_WAVES
 #define DKG_COMB_WAVES 4
 #endif
+
+// acc += s * B with the radix-2^COMBW_BITS comb of B.  (Loading each window's entry one window ahead
+// measured no gain -- check 48.0 vs 47.7 ms on config 5 -- and pushed the kernels into scratch at 128
+// VGPRs: profiles/r05_comb_radix_ab.txt.)
 DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
   int carry = 0;
   bool neg, zero;
-  uint4 e[8];
-  if constexpr (DKG_COMBW_PF) {
-    const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, 0, carry, neg, zero, tab));
-#pragma unroll
-    for (int k = 0; k < 8; k++) e[k] = p[k];
-  }
 #pragma unroll 1
   for (int w = 0; w < COMBW_WINDOWS; w++) {
+    const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, w, carry, neg, zero, tab));
+    uint4 e[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = p[k];
     ge_aff r;
-    if constexpr (DKG_COMBW_PF) {
-      combw_select(r, e, neg, zero);
-      if (w + 1 < COMBW_WINDOWS) {
-        const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, w + 1, carry, neg, zero, tab));
-#pragma unroll
-        for (int k = 0; k < 8; k++) e[k] = p[k];
-      }
-    } else {
-      const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, w, carry, neg, zero, tab));
-#pragma unroll
-      for (int k = 0; k < 8; k++) e[k] = p[k];
-      combw_select(r, e, neg, zero);
-    }
+    combw_select(r, e, neg, zero);
     ge_madd(acc, acc, r);
   }
 }
