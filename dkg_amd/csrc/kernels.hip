@@ -198,14 +198,14 @@ __global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_commit(size_t count, co
                                                 size_t stride) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
-  sc sa, sb;
-  sc_load(sa, a + 8 * e);
-  sc_load(sb, b + 8 * e);
+  sc x;  // one scalar live at a time: b is loaded after a's comb (fewer VGPRs across the chain)
+  sc_load(x, a + 8 * e);
   ge_p3 acc;
   ge_identity(acc);
-  combw_mul_add(acc, sa, tab_g);               // apub = G::generator() * a   (committee.rs:155)
+  combw_mul_add(acc, x, tab_g);                // apub = G::generator() * a   (committee.rs:155)
   pt_store(A_ext, stride, e, acc);
-  combw_mul_add(acc, sb, tab_h);               // coeff_comm = h * b + apub   (committee.rs:156)
+  sc_load(x, b + 8 * e);
+  combw_mul_add(acc, x, tab_h);                // coeff_comm = h * b + apub   (committee.rs:156)
   pt_store(E_ext, stride, e, acc);
 }
 
@@ -221,25 +221,29 @@ void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* 
 // coefficient k), lanes = dealers, so the E and A columns of a group (columns 128 g + lane and
 // 128 g + 64 + lane, piece k / L at position k % L) are written coalesced; no extended-form E/A
 // arrays and no placement pass.  The lanes of k = 0 also write A_i0 (A0 [40][A0stride], finalise).
-__global__ __launch_bounds__(64, DKG_COMB_WAVES) void k_commit_pm(size_t D, size_t N, const uint32_t* __restrict__ a,
+// 3 waves per SIMD: at 128 VGPRs it spills 260 B per lane (config 5 -2 ms, profiles/r05_b5_ab.txt).
+__global__ __launch_bounds__(64, 3) void k_commit_pm(size_t D, size_t N, const uint32_t* __restrict__ a,
                                                    const uint32_t* __restrict__ b,
                                                    const uint32_t* __restrict__ tab_g,
                                                    const uint32_t* __restrict__ tab_h, uint32_t* __restrict__ out,
                                                    size_t W, size_t L, size_t pstride,
                                                    uint32_t* __restrict__ A0, size_t A0stride) {
-  const size_t g = blockIdx.x, k = blockIdx.y, i = g * 64 + threadIdx.x;
+  const size_t g = blockIdx.x, i = g * 64 + threadIdx.x;
+  const uint32_t k = blockIdx.y, Lu = (uint32_t)L;  // 32-bit: uniform position arithmetic
   if (i >= D) return;
-  sc sa, sb;
-  sc_load(sa, a + 8 * (i * N + k));
-  sc_load(sb, b + 8 * (i * N + k));
+  sc x;  // one scalar live at a time (b loaded after a's comb)
+  sc_load(x, a + 8 * (i * N + k));
   ge_p3 acc;
   ge_identity(acc);
-  combw_mul_add(acc, sa, tab_g);                    // apub = G::generator() * a   (committee.rs:155)
-  uint32_t* o = out + (k % L) * W + (k / L) * pstride + g * 128 + threadIdx.x;
-  pt_store(o + 64, L * W, 0, acc);                  // the A column (round 4)
+  combw_mul_add(acc, x, tab_g);                     // apub = G::generator() * a   (committee.rs:155)
+  // this (position, piece) row of the table: a wave-uniform base
+  uint32_t* o = out + (size_t)(k % Lu) * W + (size_t)(k / Lu) * pstride + g * 128;
+  asm volatile("" : "+s"(o));
+  pt_store(o + 64, L * W, threadIdx.x, acc);        // the A column (round 4)
   if (k == 0) pt_store(A0, A0stride, i, acc);
-  combw_mul_add(acc, sb, tab_h);                    // coeff_comm = h * b + apub   (committee.rs:156)
-  pt_store(o, L * W, 0, acc);                       // the E column (round 2)
+  sc_load(x, b + 8 * (i * N + k));
+  combw_mul_add(acc, x, tab_h);                     // coeff_comm = h * b + apub   (committee.rs:156)
+  pt_store(o, L * W, threadIdx.x, acc);             // the E column (round 2)
 }
 
 void commit_position_major(size_t D, size_t N, const uint32_t* a, const uint32_t* b, const uint32_t* tab_g,
@@ -585,8 +589,11 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
 // PF (with CARRY): the next item's e_{m-2} is loaded before this item's chain starts, so the load
 // latency hides behind the chain instead of behind the other waves of the SIMD (40 more VGPRs: 2
 // waves per SIMD instead of 3).
+#ifndef DKG_BINOM_WAVE_WAVES  // resident waves per SIMD of the carried schedule (168 VGPRs at 3)
+#define DKG_BINOM_WAVE_WAVES 3
+#endif
 template <bool CARRY, bool PF>
-__global__ __launch_bounds__(64, PF ? 2 : (CARRY ? 3 : 4)) void k_binom_wave(int L, size_t npad,
+__global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) void k_binom_wave(int L, size_t npad,
                                                                            const uint32_t* __restrict__ C,
                                                                            uint32_t* e, size_t pstride, unsigned gx,
                                                                            unsigned last_piece, int last_off,
