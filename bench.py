@@ -67,6 +67,12 @@ def combw_windows():
 
 
 _COMBW = None
+
+
+def key_comb_windows():
+    """Mixed additions per scalar of the member keys' combs (full mode's encryption; dkg_key_comb_windows)."""
+    import dkg_amd
+    return dkg_amd.lib().dkg_key_comb_windows()
 SLOTS = {k: v[1] for k, v in VALU.items()}
 
 
@@ -128,12 +134,12 @@ HY_SYM_SLOTS = 12 * 8 * (6 * 3 + 4 * 2 + 3 * 4) + 20 * 4 * (4 + 4 + 4 * 2) + 64
 
 def hybrid_valu(n, sk, VALU=SLOTS):
     """Closed-form VALU work of full mode's encryption and decryption of all 2 n^2 items (n dealers x n
-    recipients x {randomness, share}): k_enc_mul (24 radix-2^11 windows of g + 64 radix-16 windows of
-    pk_q per item), k_dec_mul_w4 (sk_q's width-4 window, wave-uniform: a doubling per digit below the
+    recipients x {randomness, share}): k_enc_mul (the windows of g's comb and of pk_q's own global comb
+    per item: dkg_fixed_base_windows + dkg_key_comb_windows), k_dec_mul_w4 (sk_q's width-4 window, wave-uniform: a doubling per digit below the
     top, an addition per nonzero digit, the odd multiples), the encode / decode kernels and k_sym_xor
     (model above)."""
     items = 2 * n * n
-    enc = items * (combw_windows() * VALU["combw_window"] + 64 * VALU["comb_window"])
+    enc = items * (combw_windows() + key_comb_windows()) * VALU["combw_window"]
     dec = 0
     for q in range(n):
         ds = _wnaf(int.from_bytes(sk[32 * q:32 * q + 32], "little"), 4)

@@ -160,6 +160,7 @@ def lib():
     L.dkg_shard_combine_device.argtypes = [p, sz, sz, sz, p, p, p, p, ctypes.POINTER(ShardOutcome)]
     L.dkg_shard_combine_packed_device.argtypes = [p, sz, sz, sz, p, p, p, p, ctypes.POINTER(ShardOutcome)]
     L.dkg_fixed_base_windows.argtypes = []
+    L.dkg_key_comb_windows.argtypes = []
     L.dkg_packed_row_words.argtypes = [sz]
     L.dkg_packed_row_words.restype = sz
     L.dkg_decisions_pack_device.argtypes = [p, sz, sz, sz, sz, p, p]
@@ -197,7 +198,7 @@ EXPORTED = [
     "dkg_ceremony_verify_full", "dkg_misbehaviour_prove", "dkg_complaint1_verify", "dkg_complaint3_verify", "dkg_dealer_coeffs", "dkg_dealer_coeffs_device",
     "dkg_scalar_sum_device", "dkg_point_sum_device", "dkg_ceremony_shard_recon_device", "dkg_finalise_parties",
     "dkg_share_gen_device", "dkg_shard_range", "dkg_shard_rows", "dkg_shard_combine_device",
-    "dkg_shard_combine_packed_device", "dkg_packed_row_words", "dkg_fixed_base_windows", "dkg_decisions_pack_device",
+    "dkg_shard_combine_packed_device", "dkg_packed_row_words", "dkg_fixed_base_windows", "dkg_key_comb_windows", "dkg_decisions_pack_device",
     "dkg_shard_finalise_device", "dkg_multi_create", "dkg_multi_destroy", "dkg_multi_size", "dkg_multi_ctx",
     "dkg_multi_last_error", "dkg_multi_phase_ms", "dkg_multi_env_init", "dkg_multi_ceremony_run",
     "dkg_multi_ceremony_run_device", "dkg_multi_ceremony_verify",

@@ -19,22 +19,15 @@
 
 namespace dkgk {
 
-constexpr int HY_COMB_WORDS = AFF_WORDS * COMB_ENTRIES;
-
-// grid (ceil(2D / 1024), n): recipient q = blockIdx.y; the recipient's comb table in LDS (60 KB),
-// the generator's radix-2^11 comb (24 mixed additions instead of 64) from global memory / L2.
+// grid (ceil(2D / 1024), n): recipient q = blockIdx.y.  The generator's comb (radix 2^DKG_COMBW_BITS)
+// and the recipient's own comb (radix 2^DKG_KEY_COMB_BITS, 26 windows at 2^10: 1.7 MB per key, every
+// dealer of the block reads the same table through L2; the radix-16 LDS comb it replaces took 64).
 __global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
                                                   const uint32_t* __restrict__ tab_gw,
                                                   const uint32_t* __restrict__ tabs_pk, uint32_t* __restrict__ R_ext,
                                                   uint32_t* __restrict__ K_ext) {
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   const size_t q = blockIdx.y;
-  {
-    const uint4* sp = reinterpret_cast<const uint4*>(tabs_pk + q * HY_COMB_WORDS);
-    for (int i = threadIdx.x; i < HY_COMB_WORDS / 4; i += blockDim.x) lds4[i] = sp[i];
-  }
-  __syncthreads();
+  const uint32_t* tab_pk = tabs_pk + q * CombGeo<DKG_KEY_COMB_BITS>::WORDS;
   const size_t item = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // i * 2 + w
   if (item >= 2 * D) return;
   const size_t i = item >> 1, w = item & 1;
@@ -47,15 +40,15 @@ __global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint
   combw_mul_add(acc, x, tab_gw);               // e1 = G::generator() * r      (elgamal.rs:141)
   pt_store(R_ext, count, idx, acc);
   ge_identity(acc);
-  comb_mul_add(acc, x, lds);                   // symmetric key = pk * r       (elgamal.rs:138-140)
+  combw_mul_add_r<DKG_KEY_COMB_BITS>(acc, x, tab_pk);  // symmetric key = pk * r  (elgamal.rs:138-140)
   pt_store(K_ext, count, idx, acc);
 }
 
 void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_gw, const uint32_t* tabs_pk, uint32_t* R_ext,
              uint32_t* K_ext, hipStream_t stream) {
   if (!D || !n) return;
-  hipLaunchKernelGGL(k_enc_mul, dim3((unsigned)((2 * D + 1023) / 1024), (unsigned)n), dim3(1024),
-                     HY_COMB_WORDS * 4, stream, D, n, r, tab_gw, tabs_pk, R_ext, K_ext);
+  hipLaunchKernelGGL(k_enc_mul, dim3((unsigned)((2 * D + 1023) / 1024), (unsigned)n), dim3(1024), 0, stream, D, n,
+                     r, tab_gw, tabs_pk, R_ext, K_ext);
 }
 
 // grid (ceil(D / 64), n, 2): recipient q = blockIdx.y, w = blockIdx.z; lanes = dealers.

@@ -400,21 +400,25 @@ __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint
 // Radix-2^COMBW_BITS comb of point e0 + blockIdx.y of ext: block (window w = blockIdx.x, entries
 // blockIdx.z * COMBW_BUILD_BS ..), thread d-1 writes d * 2^(COMBW_BITS w) B in affine Niels form
 // (points.h combw_mul_add).
-constexpr int COMBW_BUILD_BS = COMBW_ENTRIES < 512 ? COMBW_ENTRIES : 512;  // entries per block (grid.z: chunks)
-__global__ __launch_bounds__(COMBW_BUILD_BS) void k_build_combw(const uint32_t* __restrict__ ext, size_t stride,
-                                                               size_t e0, uint32_t* __restrict__ tab) {
-  const int w = blockIdx.x, d = blockIdx.z * COMBW_BUILD_BS + threadIdx.x + 1;
-  tab += (size_t)blockIdx.y * COMBW_WORDS;
+template <int BITS>
+constexpr int comb_build_bs() { return CombGeo<BITS>::ENTRIES < 512 ? CombGeo<BITS>::ENTRIES : 512; }
+template <int BITS>
+__global__ __launch_bounds__(comb_build_bs<BITS>()) void k_build_combw(const uint32_t* __restrict__ ext,
+                                                                        size_t stride, size_t e0,
+                                                                        uint32_t* __restrict__ tab) {
+  using G = CombGeo<BITS>;
+  const int w = blockIdx.x, d = blockIdx.z * comb_build_bs<BITS>() + threadIdx.x + 1;
+  tab += (size_t)blockIdx.y * G::WORDS;
   ge_p3 b, m;
   pt_load(b, ext, stride, e0 + blockIdx.y);
-  for (int i = 0; i < COMBW_BITS * w; i++) ge_dbl<true>(b, b);
+  for (int i = 0; i < BITS * w; i++) ge_dbl<true>(b, b);
   mul_small_uniform(m, b, (uint32_t)d);
   fe zi, x, y, t, d2;
   fe_ld(d2, ge_const::D2);
   fe_invert(zi, m.Z);
   fe_mul(x, m.X, zi);
   fe_mul(y, m.Y, zi);
-  uint32_t* out = tab + ((size_t)w * COMBW_ENTRIES + (d - 1)) * COMBW_STRIDE;
+  uint32_t* out = tab + ((size_t)w * G::ENTRIES + (d - 1)) * COMBW_STRIDE;
   fe_add(t, y, x);
   fe_carry(t, t);
 #pragma unroll
@@ -433,13 +437,28 @@ __global__ __launch_bounds__(COMBW_BUILD_BS) void k_build_combw(const uint32_t* 
 
 static_assert(COMBW_WORDS * 4 == (size_t)(256 / DKG_COMBW_BITS + 1) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4,
               "runtime.hip COMBW_BYTES must match points.h");
+static_assert(CombGeo<COMBW_BITS>::WORDS == COMBW_WORDS, "one comb geometry");
 
 int fixed_base_windows() { return COMBW_WINDOWS; }
 
-void build_combw(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
+template <int BITS>
+void build_combw_r(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
   if (!count) return;
-  hipLaunchKernelGGL(k_build_combw, dim3((unsigned)COMBW_WINDOWS, (unsigned)count, COMBW_ENTRIES / COMBW_BUILD_BS),
-                     dim3(COMBW_BUILD_BS), 0, stream, ext, stride, e0, tab);
+  using G = CombGeo<BITS>;
+  hipLaunchKernelGGL(k_build_combw<BITS>, dim3((unsigned)G::WINDOWS, (unsigned)count, G::ENTRIES / comb_build_bs<BITS>()),
+                     dim3(comb_build_bs<BITS>()), 0, stream, ext, stride, e0, tab);
+}
+
+void build_combw(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream, size_t count) {
+  build_combw_r<COMBW_BITS>(ext, stride, e0, tab, stream, count);
+}
+
+size_t key_comb_words() { return CombGeo<DKG_KEY_COMB_BITS>::WORDS; }
+int key_comb_windows() { return CombGeo<DKG_KEY_COMB_BITS>::WINDOWS; }
+
+void build_key_combs(const uint32_t* ext, size_t stride, size_t e0, uint32_t* tab, hipStream_t stream,
+                     size_t count) {
+  build_combw_r<DKG_KEY_COMB_BITS>(ext, stride, e0, tab, stream, count);
 }
 
 __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, size_t N, const uint32_t* __restrict__ C,

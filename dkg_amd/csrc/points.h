@@ -143,25 +143,43 @@ constexpr size_t COMBW_WORDS = (size_t)COMBW_WINDOWS * COMBW_ENTRIES * COMBW_STR
 static_assert(COMBW_WINDOWS * COMBW_BITS > 256 && (1 << (256 - (COMBW_WINDOWS - 1) * COMBW_BITS)) < COMBW_ENTRIES,
               "the top window must absorb the signed recoding's carry for any 256-bit scalar");
 
-// Window w's signed digit (carry in / out) and its entry in the comb of base `tab`.
-DKG_DEV const uint32_t* combw_entry(const sc& s, int w, int& carry, bool& neg, bool& zero,
-                                    const uint32_t* __restrict__ tab) {
+// Radix of the member keys' combs (full mode's encryption, K = pk_q r: one table per recipient key,
+// shared by the wave's dealers, read through L2).
+#ifndef DKG_KEY_COMB_BITS
+#define DKG_KEY_COMB_BITS 10
+#endif
+
+// The comb geometry of radix 2^BITS: 256/BITS + 1 windows of 2^(BITS-1) entries of 32 words.
+template <int BITS>
+struct CombGeo {
+  static constexpr int WINDOWS = 256 / BITS + 1;  // the top window absorbs the signed recoding's carry
+  static constexpr int ENTRIES = 1 << (BITS - 1);
+  static constexpr size_t WORDS = (size_t)WINDOWS * ENTRIES * 32;
+  static_assert(WINDOWS * BITS > 256 && (1 << (256 - (WINDOWS - 1) * BITS)) < ENTRIES,
+                "the top window must absorb the signed recoding's carry for any 256-bit scalar");
+};
+
+// Window w's signed digit (carry in / out) and its entry in the radix-2^BITS comb of base `tab`.
+template <int BITS>
+DKG_DEV const uint32_t* combw_entry_r(const sc& s, int w, int& carry, bool& neg, bool& zero,
+                                      const uint32_t* __restrict__ tab) {
+  constexpr int ENTRIES = CombGeo<BITS>::ENTRIES;
   // bits [B w, B w + B) of the scalar: words wi and wi + 1 (wave-uniform selects)
-  const int bit = COMBW_BITS * w, wi = bit >> 5, sh = bit & 31;
+  const int bit = BITS * w, wi = bit >> 5, sh = bit & 31;
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     lo = (wi == k) ? s.v[k] : lo;
     hi = (wi + 1 == k) ? s.v[k] : hi;
   }
-  const uint32_t raw = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh) & ((1u << COMBW_BITS) - 1);
+  const uint32_t raw = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh) & ((1u << BITS) - 1);
   int d = (int)raw + carry;
-  carry = (d + COMBW_ENTRIES) >> COMBW_BITS;
-  d -= carry << COMBW_BITS;
+  carry = (d + ENTRIES) >> BITS;
+  d -= carry << BITS;
   const int ad = d < 0 ? -d : d;
   neg = d < 0;
   zero = ad == 0;
-  return tab + ((size_t)w * COMBW_ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMBW_STRIDE;
+  return tab + ((size_t)w * ENTRIES + (ad == 0 ? 0 : ad - 1)) * COMBW_STRIDE;
 }
 
 // The entry's 30 words as an affine Niels addend: -Q = (y-x, y+x, -2dxy), 0 = (1, 1, 0).
@@ -186,15 +204,16 @@ DKG_DEV void combw_select(ge_aff& r, const uint4 (&e)[8], bool neg, bool zero) {
 #define DKG_COMB_WAVES 4
 #endif
 
-// acc += s * B with the radix-2^COMBW_BITS comb of B.  (Loading each window's entry one window ahead
+// acc += s * B with the radix-2^BITS comb of B.  (Loading each window's entry one window ahead
 // measured no gain -- check 48.0 vs 47.7 ms on config 5 -- and pushed the kernels into scratch at 128
 // VGPRs: profiles/r05_comb_radix_ab.txt.)
-DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
+template <int BITS>
+DKG_DEV void combw_mul_add_r(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
   int carry = 0;
   bool neg, zero;
 #pragma unroll 1
-  for (int w = 0; w < COMBW_WINDOWS; w++) {
-    const uint4* p = reinterpret_cast<const uint4*>(combw_entry(s, w, carry, neg, zero, tab));
+  for (int w = 0; w < CombGeo<BITS>::WINDOWS; w++) {
+    const uint4* p = reinterpret_cast<const uint4*>(combw_entry_r<BITS>(s, w, carry, neg, zero, tab));
     uint4 e[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) e[k] = p[k];
@@ -202,6 +221,10 @@ DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__
     combw_select(r, e, neg, zero);
     ge_madd(acc, acc, r);
   }
+}
+// the shared bases' combs (g, h: radix 2^DKG_COMBW_BITS)
+DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
+  combw_mul_add_r<COMBW_BITS>(acc, s, tab);
 }
 
 

@@ -1405,13 +1405,13 @@ void encrypt_device(dkg_ctx* ctx, size_t D, size_t n, const uint32_t* pkc, const
   if (!st) st = ctx->stream;
   uint32_t* pk_ext = buf<uint32_t>(ctx, "hy.pk_ext", PTB * n);
   uint8_t* pk_ok = buf<uint8_t>(ctx, "hy.pk_ok", n);
-  uint32_t* tabs = buf<uint32_t>(ctx, "hy.tabs", COMB_BYTES * n);
+  uint32_t* tabs = buf<uint32_t>(ctx, "hy.tabs", 4 * dkgk::key_comb_words() * n);
   const bool cached = pk_host && ctx->key_tabs_pk.size() == 32 * n &&
                       memcmp(ctx->key_tabs_pk.data(), pk_host, 32 * n) == 0;
   if (!cached) {
     ctx->key_tabs_pk.clear();  // invalid until this build is queued
     dkgk::decode_points(pkc, n, pk_ext, n, pk_ok, st);
-    dkgk::build_comb(pk_ext, n, 0, tabs, st, n);  // one comb per recipient key: r * pk_q is fixed-base
+    dkgk::build_key_combs(pk_ext, n, 0, tabs, st, n);  // one comb per recipient key: r * pk_q is fixed-base
     if (pk_host) ctx->key_tabs_pk.assign(pk_host, pk_host + 32 * n);
   }
   uint32_t* R = buf<uint32_t>(ctx, "hy.R", PTB * items);
@@ -2471,6 +2471,7 @@ int dkg_shard_combine_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_size
 size_t dkg_packed_row_words(size_t n) { return (n + 31) / 32 + 1; }
 
 int dkg_fixed_base_windows(void) { return dkgk::fixed_base_windows(); }
+int dkg_key_comb_windows(void) { return dkgk::key_comb_windows(); }
 
 int dkg_decisions_pack_device(dkg_ctx* ctx, size_t rows, size_t nvalid, size_t n, size_t d0, const void* d_dec,
                               void* d_packed) {

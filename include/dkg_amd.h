@@ -331,6 +331,8 @@ size_t dkg_packed_row_words(size_t n);
 /* Windows (one mixed addition each) per scalar of the fixed-base combs of g and h the checks and
  * commitments use (radix 2^DKG_COMBW_BITS, a build-time choice): the closed-form work of bench.py. */
 int dkg_fixed_base_windows(void);
+/* The same for the member keys' combs (full mode's K = pk_q r, radix 2^DKG_KEY_COMB_BITS). */
+int dkg_key_comb_windows(void);
 /* d_dec device [nvalid][n] raw rows of dealers d0 .. d0+nvalid-1 (dkg_ceremony_shard_device's
  * output) -> d_packed device [rows][dkg_packed_row_words(n)] u32, rows past nvalid zero (the padded
  * rank block, rows = dkg_shard_rows).  DKG_E_ARG if a row holds values the encoding cannot carry

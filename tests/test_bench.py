@@ -138,7 +138,7 @@ def test_hybrid_valu_closed_form():
     assert bench._wnaf(23, 4) == [7, 0, 0, 0, 1]  # 23 = 16 + 7
     w = bench.hybrid_valu(n, sk)
     S = bench.SLOTS
-    assert w["enc_mul"] == 2 * n * n * (bench.combw_windows() * S["combw_window"] + 64 * S["comb_window"])
+    assert w["enc_mul"] == 2 * n * n * (bench.combw_windows() + bench.key_comb_windows()) * S["combw_window"]
     pre = S["ge_dbl_t"] + 3 * S["ge_add"] + 5 * S["ge_to_cached"]
     c5 = pre + S["ge_add_signed"]  # one digit: one addition onto the identity
     c1 = pre + S["ge_add_signed"]
