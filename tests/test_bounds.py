@@ -75,3 +75,53 @@ def test_tight_zero_representations():
     z = F.fe_mul([F.MASK[i] for i in range(10)], [F.MASK[i] for i in range(10)], "x")
     for i in range(10):
         assert z[i] < (1 << W[i]) + p_limbs[i] if i in (1, 5) else z[i] <= F.MASK[i]
+
+
+def test_lazy_horner_bounds():
+    """The share evaluation's lazy reduction (sc25519.h sc_lazy_step / sc_lazy_fold, k_share_eval
+    for x < 2^13), restated limb by limb: at the worst case -- accumulator just below 2^254,
+    coefficients l - 1, x = 8191, SC_LAZY_STEPS = 5 steps between folds -- no 64-bit limb sum or
+    10-limb accumulator overflows, the fold never goes negative and lands below 2^254 again, and
+    the value stays congruent to the Horner value mod l."""
+    L = 2**252 + 27742317777372353535851937790883648493
+    D = L - 2**252
+    limbs = lambda v, k: [(v >> (32 * i)) & 0xffffffff for i in range(k)]  # noqa: E731
+    val = lambda l: sum(x << (32 * i) for i, x in enumerate(l))  # noqa: E731
+
+    def step(v, x, c):
+        t, out, cl = 0, [], limbs(c, 8)
+        for i in range(10):
+            t = v[i] * x + (cl[i] if i < 8 else 0) + (t >> 32)
+            assert t < 2**64
+            out.append(t & 0xffffffff)
+        assert t >> 32 == 0, "10-limb accumulator overflow"
+        return out
+
+    def fold(v):
+        h = [(v[7] >> 28) | ((v[8] << 4) & 0xffffffff), (v[8] >> 28) | ((v[9] << 4) & 0xffffffff), v[9] >> 28]
+        dl, p, acc, hiacc = limbs(D, 4), [], 0, 0
+        for k in range(7):
+            for i in range(3):
+                if 0 <= k - i < 4:
+                    m = h[i] * dl[k - i]
+                    acc += m & 0xffffffff
+                    hiacc += m >> 32
+            assert acc < 2**64
+            p.append(acc & 0xffffffff)
+            acc, hiacc = (acc >> 32) + hiacc, 0
+        Ll, c, out = limbs(L, 8), 0, []
+        for i in range(8):
+            c += (v[i] if i < 7 else v[7] & 0x0fffffff) + Ll[i] - (p[i] if i < 7 else 0)
+            out.append(c & 0xffffffff)
+            c >>= 32
+        assert c == 0, "fold went negative or past 2^256"
+        return out + [0, 0]
+
+    x = 8191
+    for start in (2**254 - 1, L - 1, 0):
+        v, want = limbs(start, 10), start
+        for _ in range(5):
+            v = step(v, x, L - 1)
+            want = want * x + L - 1
+        v = fold(v)
+        assert val(v) < 2**254 and val(v) % L == want % L
