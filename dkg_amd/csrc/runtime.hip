@@ -22,6 +22,7 @@ struct dkg_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   std::map<std::string, std::pair<void*, size_t>> bufs;
+  std::map<std::string, std::pair<void*, size_t>> hbufs;  // pinned host staging (hbuf), grow-only
   uint32_t* tab_g = nullptr;  // comb table of the generator (15360 words)
   uint32_t* tab_h = nullptr;  // comb table of the commitment key h
   uint32_t* tab_gw = nullptr;  // radix-2^11 combs (global, L2 / MALL-resident) of g and h: commit, check,
@@ -142,6 +143,29 @@ T* buf(dkg_ctx* ctx, const char* name, size_t bytes) {
     throw Fail{DKG_E_NOMEM};
   }
   ctx->bufs[name] = {p, bytes};
+  return reinterpret_cast<T*>(p);
+}
+
+// Pinned host staging, name-keyed and grow-only like buf(): device-to-host copies into it are plain
+// DMA transfers that complete with the stream, where a copy into pageable memory makes the runtime
+// stage it through its own buffers on the calling thread.
+template <typename T = void>
+T* hbuf(dkg_ctx* ctx, const char* name, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  auto it = ctx->hbufs.find(name);
+  if (it != ctx->hbufs.end() && it->second.second >= bytes) return reinterpret_cast<T*>(it->second.first);
+  if (it != ctx->hbufs.end()) {
+    HCK(hipDeviceSynchronize());  // a copy into the old buffer may still be queued
+    HCK(hipHostFree(it->second.first));
+    ctx->hbufs.erase(it);
+  }
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    ctx->err = std::string("hipHostMalloc(") + name + ", " + std::to_string(bytes) + "): " + hipGetErrorString(e);
+    throw Fail{DKG_E_NOMEM};
+  }
+  ctx->hbufs[name] = {p, bytes};
   return reinterpret_cast<T*>(p);
 }
 
@@ -1305,17 +1329,34 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   uint32_t* mpk_c = buf<uint32_t>(ctx, "b.mpk_comp", 32 * B);
   dkgk::encode_points(mpk_ext, B, B, mpk_c, ctx->stream);
   check_launch(ctx);
-  d2h(ctx, qualified.data(), rej2, V);  // inverted below
-  d2h(ctx, complaints.data(), cnt, 4 * V);
-  d2h(ctx, h_rej4.data(), rej4, V);
-  d2h(ctx, r4e.data(), r4d, V);
-  if (out->mpk) d2h(ctx, out->mpk, mpk_c, 32 * B);
-  if (out->final_share) d2h(ctx, out->final_share, fs, 32 * V);
-  if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * V);
-  if (out->dec2) d2h(ctx, out->dec2, dec2, V * n);
-  if (out->dec4) d2h(ctx, out->dec4, dec4, V * n);  // SKIPPED rows applied
+  // every outcome through pinned staging, one sync: copies into the caller's pageable buffers were
+  // staged by the runtime on this thread, 1-27 ms of host time per 10,000-ceremony batch beyond the
+  // device span (tools/batch_gap.py)
+  struct Out {
+    void* host;
+    const void* dev;
+    size_t bytes;
+    const char* name;
+  };
+  const Out outs[] = {{qualified.data(), rej2, V, "hb.rej2"},  // inverted below
+                      {complaints.data(), cnt, 4 * V, "hb.cnt"},
+                      {h_rej4.data(), rej4, V, "hb.rej4"},
+                      {r4e.data(), r4d, V, "hb.r4err"},
+                      {out->mpk, mpk_c, 32 * B, "hb.mpk"},
+                      {out->final_share, fs, 32 * V, "hb.final"},
+                      {out->public_share, pubc, 32 * V, "hb.pub"},
+                      {out->dec2, dec2, V * n, "hb.dec2"},
+                      {out->dec4, dec4, V * n, "hb.dec4"}};  // SKIPPED rows applied
+  void* staged[sizeof(outs) / sizeof(outs[0])] = {};
+  for (size_t k = 0; k < sizeof(outs) / sizeof(outs[0]); k++)
+    if (outs[k].host) {
+      staged[k] = hbuf(ctx, outs[k].name, outs[k].bytes);
+      d2h(ctx, staged[k], outs[k].dev, outs[k].bytes);
+    }
   HCK(hipEventRecord(ctx->ev[5], ctx->stream));
   sync(ctx);
+  for (size_t k = 0; k < sizeof(outs) / sizeof(outs[0]); k++)
+    if (staged[k]) memcpy(outs[k].host, staged[k], outs[k].bytes);
   collect_phases(ctx);
   for (size_t i = 0; i < V; i++) {
     qualified[i] = !qualified[i];
@@ -1606,6 +1647,7 @@ void dkg_ctx_destroy(dkg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipDeviceSynchronize();
   for (auto& kv : ctx->bufs) (void)hipFree(kv.second.first);
+  for (auto& kv : ctx->hbufs) (void)hipHostFree(kv.second.first);
   if (ctx->tab_g) (void)hipFree(ctx->tab_g);
   if (ctx->tab_h) (void)hipFree(ctx->tab_h);
   if (ctx->tab_gw) (void)hipFree(ctx->tab_gw);
