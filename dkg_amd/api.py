@@ -461,11 +461,13 @@ class Backend:
 
     def shard_combine_device(self, n: int, t: int, world_size: int, d_dec2_g: int, d_dec4_g: int,
                              d_dec2: Optional[int] = None, d_dec4: Optional[int] = None,
-                             packed: bool = False) -> "ShardOutcome":
+                             packed: bool = False, arrays: bool = False) -> "ShardOutcome":
         """Combine step of the sharded run (dkg_shard_combine_device): the common round-2/4 outcome
         from the all-gathered [ws][R][n] decision blocks (device pointers; with packed, the
         [ws][R][packed_row_words(n)] bitmaps of dkg_shard_combine_packed_device); d_dec2 / d_dec4
-        optionally receive the compacted [n][n] matrices (dec4 with SKIPPED rows)."""
+        optionally receive the compacted [n][n] matrices (dec4 with SKIPPED rows).  arrays: the
+        per-party outcomes as numpy arrays (uint8 / int32) instead of lists -- no per-element
+        conversion on the multi-GPU driver's path."""
         q, r2e, rc, r4e = (ctypes.create_string_buffer(max(n, 1)) for _ in range(4))
         c = (ctypes.c_int32 * max(n, 1))()
         o = _lib.ShardOutcome(ctypes.cast(q, ctypes.c_void_p), ctypes.cast(c, ctypes.c_void_p),
@@ -475,6 +477,12 @@ class Backend:
         fn = _lib.lib().dkg_shard_combine_packed_device if packed else _lib.lib().dkg_shard_combine_device
         _check(self._ctx, fn(self._ctx, n, t, world_size, vp(d_dec2_g), vp(d_dec4_g), vp(d_dec2), vp(d_dec4),
                              ctypes.byref(o)))
+        if arrays:
+            import numpy as np
+
+            u8 = lambda b: np.frombuffer(b.raw, dtype=np.uint8, count=n).copy()  # noqa: E731
+            return ShardOutcome(u8(q), np.frombuffer(c, dtype=np.int32, count=n).copy(), u8(r2e), u8(rc), u8(r4e),
+                                o.n_qualified, bool(o.phase4_error))
         return ShardOutcome(list(q.raw[:n]), list(c)[:n], list(r2e.raw[:n]), list(rc.raw[:n]), list(r4e.raw[:n]),
                             o.n_qualified, bool(o.phase4_error))
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <map>
@@ -1042,39 +1043,59 @@ std::vector<uint8_t> recon_secrets(size_t n, const std::vector<uint8_t>& fin, co
 // complaints raise MisbehaviourHigherThreshold for j (:340-347).  Host outputs [groups*n]; qmask
 // (device [groups*n]) receives the qualified set.  The single-GPU drivers, the batches and the
 // sharded combine all decide through this function.
+// Each outcome has a device half (kernels queued on ctx->stream, per-dealer / per-receiver results
+// left in `rej`, `cnt`, `r4d`) and a host half (applied to their copies after a sync), so that a
+// caller can queue both rounds' device halves and copy everything back in one round trip.
+void round2_device(dkg_ctx* ctx, size_t groups, size_t n, const uint8_t* dec2, uint8_t* qmask, uint8_t* rej,
+                   int32_t* cnt) {
+  dkgk::decision_summary(groups, n, dec2, rej, cnt, ctx->stream);
+  dkgk::mask_not_and(groups * n, rej, nullptr, qmask, ctx->stream);  // qualified = no rejecting row
+}
+// host half: `qualified` holds the copied rej flags on entry
+void round2_host(size_t V, size_t t, uint8_t* qualified, const int32_t* complaints, uint8_t* r2err) {
+  for (size_t i = 0; i < V; i++) {
+    qualified[i] = !qualified[i];
+    r2err[i] = complaints[i] > (int32_t)t;  // committee.rs:340-347
+  }
+}
 void round2_outcome(dkg_ctx* ctx, size_t groups, size_t n, size_t t, const uint8_t* dec2, uint8_t* qmask,
                     uint8_t* qualified, int32_t* complaints, uint8_t* r2err) {
   const size_t V = groups * n;
   uint8_t* rej = buf<uint8_t>(ctx, "o.rej2", V);
   int32_t* cnt = buf<int32_t>(ctx, "o.cnt", 4 * V);
-  dkgk::decision_summary(groups, n, dec2, rej, cnt, ctx->stream);
+  round2_device(ctx, groups, n, dec2, qmask, rej, cnt);
+  check_launch(ctx);
   d2h(ctx, qualified, rej, V);
   d2h(ctx, complaints, cnt, 4 * V);
   sync(ctx);
-  for (size_t i = 0; i < V; i++) {
-    qualified[i] = !qualified[i];
-    r2err[i] = complaints[i] > (int32_t)t;
-  }
-  h2d(ctx, qmask, qualified, V);
+  round2_host(V, t, qualified, complaints, r2err);
 }
 
 // Round-4 outcome (committee.rs:515-522, 567-569, 660-670) from dec4 [groups*n][n] on the device and
 // the round-2 qualified set (host `qualified`, device `qmask`): the rows of disqualified dealers
 // become SKIPPED in place (:522); a qualified dealer some receiver rejects is reconstructed; receiver
-// j's round-4 error (r4err, may be NULL) counts itself and the qualified dealers it accepted.
+// j's round-4 error (r4d / r4err, may be NULL) counts itself and the qualified dealers it accepted.
+void round4_device(dkg_ctx* ctx, size_t groups, size_t n, size_t t, uint8_t* dec4, const uint8_t* qmask,
+                   uint8_t* rej, uint8_t* r4d) {
+  dkgk::decision_summary(groups, n, dec4, rej, nullptr, ctx->stream);
+  if (r4d) dkgk::r4_error(groups, n, t, dec4, qmask, r4d, ctx->stream);
+  dkgk::apply_skipped(groups, n, dec4, qmask, ctx->stream);
+}
+// host half: `recon` holds the copied rej flags on entry
+void round4_host(size_t V, const uint8_t* qualified, uint8_t* recon) {
+  for (size_t i = 0; i < V; i++) recon[i] = qualified[i] && recon[i];
+}
 void round4_outcome(dkg_ctx* ctx, size_t groups, size_t n, size_t t, uint8_t* dec4, const uint8_t* qmask,
                     const uint8_t* qualified, uint8_t* recon, uint8_t* r4err) {
   const size_t V = groups * n;
   uint8_t* rej = buf<uint8_t>(ctx, "o.rej4", V);
-  uint8_t* r4d = buf<uint8_t>(ctx, "o.r4err", V);
-  dkgk::decision_summary(groups, n, dec4, rej, nullptr, ctx->stream);
-  if (r4err) dkgk::r4_error(groups, n, t, dec4, qmask, r4d, ctx->stream);
-  dkgk::apply_skipped(groups, n, dec4, qmask, ctx->stream);
+  uint8_t* r4d = r4err ? buf<uint8_t>(ctx, "o.r4err", V) : nullptr;
+  round4_device(ctx, groups, n, t, dec4, qmask, rej, r4d);
   check_launch(ctx);
   d2h(ctx, recon, rej, V);
   if (r4err) d2h(ctx, r4err, r4d, V);
   sync(ctx);
-  for (size_t i = 0; i < V; i++) recon[i] = qualified[i] && recon[i];
+  round4_host(V, qualified, recon);
 }
 
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
@@ -2475,11 +2496,25 @@ int shard_combine(dkg_ctx* ctx, size_t n, size_t t, void* d_dec2, void* d_dec4, 
   uint8_t* dec4 = d_dec4 ? (uint8_t*)d_dec4 : buf<uint8_t>(ctx, "sc.dec4", n * n);
   uint8_t* qmask = buf<uint8_t>(ctx, "sc.qmask", n);
   dense(dec2, dec4);
+  // both rounds' device halves, then one copy-back (pinned) and one sync
+  uint8_t* rej2 = buf<uint8_t>(ctx, "sc.rej2", n);
+  int32_t* cnt = buf<int32_t>(ctx, "sc.cnt", 4 * n);
+  uint8_t* rej4 = buf<uint8_t>(ctx, "sc.rej4", n);
+  uint8_t* r4d = buf<uint8_t>(ctx, "sc.r4err", n);
+  round2_device(ctx, 1, n, dec2, qmask, rej2, cnt);
+  round4_device(ctx, 1, n, t, dec4, qmask, rej4, r4d);
   check_launch(ctx);
-  std::vector<uint8_t> q(n), r2e(n), recon(n), r4e(n);
+  uint8_t* h = hbuf<uint8_t>(ctx, "sc.out", 7 * n);  // rej2 | rej4 | r4err | cnt
+  d2h(ctx, h, rej2, n);
+  d2h(ctx, h + n, rej4, n);
+  d2h(ctx, h + 2 * n, r4d, n);
+  d2h(ctx, h + 3 * n, cnt, 4 * n);
+  sync(ctx);
+  std::vector<uint8_t> q(h, h + n), r2e(n), recon(h + n, h + 2 * n), r4e(h + 2 * n, h + 3 * n);
   std::vector<int32_t> c(n);
-  round2_outcome(ctx, 1, n, t, dec2, qmask, q.data(), c.data(), r2e.data());
-  round4_outcome(ctx, 1, n, t, dec4, qmask, q.data(), recon.data(), r4e.data());
+  memcpy(c.data(), h + 3 * n, 4 * n);
+  round2_host(n, t, q.data(), c.data(), r2e.data());
+  round4_host(n, q.data(), recon.data());
   int32_t nq = 0, nr = 0;
   for (size_t i = 0; i < n; i++) {
     nq += q[i];
@@ -2602,9 +2637,9 @@ int dkg_shard_finalise_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_siz
           ctx->err = "shard_finalise: a qualified dealer's master-key term does not decode";
           return DKG_E_DECODE;
         }
-    } else {
-      join_public();
+      return DKG_OK;  // synced above, the public shares joined
     }
+    join_public();
     check_launch(ctx);
     sync(ctx);
     return DKG_OK;

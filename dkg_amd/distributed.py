@@ -17,7 +17,7 @@ rows, reconstruction set, r4 errors, Phase4 failure) with the single-GPU drivers
 dkg_shard_finalise_device the final shares, public shares and mpk (include/dkg_amd.h).
 """
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -47,17 +47,36 @@ class Decisions:
     phase4_error: bool        # qualified minus reconstructable <= t: Phase4::proceed fails (:673-677)
 
 
-@dataclass
 class ShardResult:
-    decisions: Decisions
-    final_share: Optional[bytes]   # [n][32] s_j (committee.rs:454-462)
-    public_share: Optional[bytes]  # [n][32] g * s_j (committee.rs:463-467)
-    mpk: Optional[bytes]           # 32 bytes (committee.rs:790-795); None when Phase4 fails
-    ms_shard: float                # device time of this rank's share gen + checks
-    # host wall ms of the steps after the shard: "exchange" (the all-gathers, fenced), "combine"
-    # (dkg_shard_combine_device + outcome copies), "recon" (round-4 reconstruction + its gather; 0
-    # when nobody was accused), "finalise" (dkg_shard_finalise_device + the share copies)
-    ms_steps: Dict[str, float] = field(default_factory=dict)
+    """One rank's outputs of a sharded ceremony.
+    final_share  [n][32] s_j (committee.rs:454-462) and public_share [n][32] g * s_j (:463-467): bytes,
+                 copied from the device when first read (a device copy is kept, so a later run does
+                 not change them; a timed loop that never reads them pays no host round trip)
+    mpk          32 bytes (committee.rs:790-795); None when Phase4 fails
+    ms_shard     device time of this rank's share gen + checks
+    ms_steps     host wall ms of the steps after the shard: "exchange" (the all-gather, fenced),
+                 "combine" (dkg_shard_combine_device + outcome copies), "recon" (round-4
+                 reconstruction + its gather; 0 when nobody was accused), "finalise"
+                 (dkg_shard_finalise_device)"""
+
+    def __init__(self, decisions: Decisions, final_share, public_share, mpk: Optional[bytes], ms_shard: float,
+                 ms_steps: Optional[Dict[str, float]] = None):
+        self.decisions, self._fs, self._pub = decisions, final_share, public_share
+        self.mpk, self.ms_shard, self.ms_steps = mpk, ms_shard, dict(ms_steps or {})
+
+    @staticmethod
+    def _host(v):
+        return v if v is None or isinstance(v, (bytes, bytearray)) else bytes(v.cpu().numpy())
+
+    @property
+    def final_share(self) -> Optional[bytes]:
+        self._fs = self._host(self._fs)
+        return self._fs
+
+    @property
+    def public_share(self) -> Optional[bytes]:
+        self._pub = self._host(self._pub)
+        return self._pub
 
 
 class ShardedCeremony:
@@ -76,21 +95,33 @@ class ShardedCeremony:
         self.d0, self.d1 = dealer_range(self.rank, self.ws, n)
         D, R = self.d1 - self.d0, max_rows(self.ws, n)
         u8 = dict(dtype=torch.uint8, device=device)
-        self.dec2 = torch.zeros(R * n, **u8)
-        self.dec4 = torch.zeros(R * n, **u8)
-        self.A0 = torch.zeros(R * 32, **u8)
-        self.part = torch.zeros(n * 32, **u8)
-        if packed:  # [R][W+1] u32 bitmaps (dkg_packed_row_words), gathered as [ws][R][W+1]
+        # One send block per rank, gathered in ONE collective: [round-2 rows | round-4 rows | master-key
+        # terms [R][32] | partial final shares [n][32]], the rows packed ([R][W+1] u32 bitmaps,
+        # dkg_packed_row_words) or raw ([R][n] bytes).  The library writes straight into its views.
+        if packed:
             from .api import packed_row_words
 
             self.W1 = packed_row_words(n)
+            S2 = 4 * R * self.W1
+        else:
+            S2 = R * n
+        self.S2, self.S = S2, 2 * S2 + R * 32 + n * 32
+        self.send = torch.zeros(self.S, **u8)
+        self.A0 = self.send[2 * S2:2 * S2 + R * 32]
+        self.part = self.send[2 * S2 + R * 32:]
+        if packed:
+            self.dec2 = torch.zeros(R * n, **u8)  # raw rows, packed into the send block
+            self.dec4 = torch.zeros(R * n, **u8)
+            self.p2 = self.send[:S2].view(torch.int32)
+            self.p4 = self.send[S2:2 * S2].view(torch.int32)
             i32 = dict(dtype=torch.int32, device=device)
-            self.p2, self.p4 = torch.zeros(R * self.W1, **i32), torch.zeros(R * self.W1, **i32)
             self.g_dec2 = torch.empty(self.ws * R * self.W1, **i32)
             self.g_dec4 = torch.empty(self.ws * R * self.W1, **i32)
         else:
+            self.dec2, self.dec4 = self.send[:S2], self.send[S2:2 * S2]
             self.g_dec2 = torch.empty(self.ws * R * n, **u8)
             self.g_dec4 = torch.empty(self.ws * R * n, **u8)
+        self.g_all = torch.empty(self.ws * self.S, **u8)
         self.g_A0 = torch.empty(self.ws * R * 32, **u8)
         self.g_part = torch.empty(self.ws * n * 32, **u8)
         self.c_dec2 = torch.empty(n * n, **u8)   # compacted by the combine
@@ -120,25 +151,24 @@ class ShardedCeremony:
         self.be.decisions_pack_device(self.R, self.D, self.n, self.d0, dec.data_ptr(), out.data_ptr())
 
     def exchange_bytes(self) -> int:
-        """Bytes one rank contributes to the all-gathers of one ceremony (without the round-4
+        """Bytes one rank contributes to the all-gather of one ceremony (without the round-4
         reconstruction's second gather of the master-key terms)."""
-        rows = 2 * self.R * (4 * self.W1 if self.packed else self.n)
-        return rows + self.A0.numel() + self.part.numel()
+        return self.S
 
     def exchange(self):
-        """All-gather every rank's padded blocks: the decision rows (round 2, round 4; packed bitmaps
-        [ws][R][W+1] or bytes [ws][R][n]), the master-key terms [ws][R][32] and the partial final
-        shares [ws][n][32]."""
+        """All-gather every rank's send block (one collective), then split the gathered [ws][S] blocks
+        on the device into the decision rows (round 2, round 4; packed bitmaps [ws][R][W+1] or bytes
+        [ws][R][n]), the master-key terms [ws][R][32] and the partial final shares [ws][n][32]."""
         if self.packed:
             self._pack(self.dec2, self.p2)
             self._pack(self.dec4, self.p4)
-            self._all_gather(self.g_dec2, self.p2)
-            self._all_gather(self.g_dec4, self.p4)
-        else:
-            self._all_gather(self.g_dec2, self.dec2)
-            self._all_gather(self.g_dec4, self.dec4)
-        self._all_gather(self.g_A0, self.A0)
-        self._all_gather(self.g_part, self.part)
+        self._all_gather(self.g_all, self.send)
+        S2, R, ws = self.S2, self.R, self.ws
+        g = self.g_all.view(ws, self.S)
+        self.g_dec2.view(self.torch.uint8).view(ws, S2).copy_(g[:, :S2])
+        self.g_dec4.view(self.torch.uint8).view(ws, S2).copy_(g[:, S2:2 * S2])
+        self.g_A0.view(ws, R * 32).copy_(g[:, 2 * S2:2 * S2 + R * 32])
+        self.g_part.view(ws, self.n * 32).copy_(g[:, 2 * S2 + R * 32:])
         return self.g_dec2, self.g_dec4, self.g_A0, self.g_part
 
     def run(self, d_a: int, d_b: int, finalise: bool = True) -> ShardResult:
@@ -168,7 +198,8 @@ class ShardedCeremony:
         c1 = time.perf_counter()
         steps["exchange"] = (c1 - c0) * 1e3
         o = self.be.shard_combine_device(n, t, ws, self.g_dec2.data_ptr(), self.g_dec4.data_ptr(),
-                                         self.c_dec2.data_ptr(), self.c_dec4.data_ptr(), packed=self.packed)
+                                         self.c_dec2.data_ptr(), self.c_dec4.data_ptr(), packed=self.packed,
+                                         arrays=True)
         dec = Decisions(self.c_dec2.view(n, n), self.c_dec4.view(n, n), np.array(o.qualified, dtype=np.uint8),
                         np.array(o.complaints2, dtype=np.int32), np.array(o.r2_error, dtype=np.uint8),
                         np.array(o.reconstruct, dtype=np.uint8), np.array(o.r4_error, dtype=np.uint8),
@@ -192,6 +223,7 @@ class ShardedCeremony:
         steps["recon"] = (c3 - c2) * 1e3
         mpk = self.be.shard_finalise_device(n, t, ws, self.g_A0.data_ptr(), self.g_part.data_ptr(), dec.qualified,
                                             no_mpk, self.fs.data_ptr(), self.pub.data_ptr())
-        fs, pub = bytes(self.fs.cpu().numpy()), bytes(self.pub.cpu().numpy())
+        # device copies of this run's shares (the buffers are reused), read back only when asked for
+        fs, pub = self.fs.clone(), self.pub.clone()
         steps["finalise"] = (time.perf_counter() - c3) * 1e3
         return ShardResult(dec, fs, pub, None if no_mpk else mpk, ms, steps)

@@ -213,7 +213,8 @@ class OracleBackend:
         raw = np.frombuffer(self._rd(d_dec, nvalid * n), dtype=np.uint8) if nvalid else np.zeros(0, np.uint8)
         self._wr(d_packed, CR.pack_rows(raw, rows, nvalid, n, d0).tobytes())
 
-    def shard_combine_device(self, n, t, ws, d_dec2_g, d_dec4_g, d_dec2=None, d_dec4=None, packed=False):
+    def shard_combine_device(self, n, t, ws, d_dec2_g, d_dec4_g, d_dec2=None, d_dec4=None, packed=False,
+                             arrays=False):
         from dkg_amd.api import ShardOutcome
         from tests import combine_ref as CR
         R = CR.rows_per_rank(ws, n)
@@ -229,8 +230,9 @@ class OracleBackend:
             self._wr(d_dec2, bytes(d.dec2))
         if d_dec4:
             self._wr(d_dec4, bytes(d.dec4))
-        return ShardOutcome(d.qualified.tolist(), d.complaints2.tolist(), d.r2_error.tolist(), d.reconstruct.tolist(),
-                            d.r4_error.tolist(), int(d.qualified.sum()), d.phase4_error)
+        cv = (lambda a: np.asarray(a).copy()) if arrays else (lambda a: a.tolist())
+        return ShardOutcome(cv(d.qualified), cv(d.complaints2), cv(d.r2_error), cv(d.reconstruct), cv(d.r4_error),
+                            int(d.qualified.sum()), d.phase4_error)
 
     def shard_finalise_device(self, n, t, ws, d_terms_g, d_partials_g, qualified, phase4_error, d_fs, d_pub=None):
         from tests import combine_ref as CR

@@ -63,9 +63,12 @@ def main():
         timed("shard_device", lambda: be.ceremony_shard_device(n, t, sc.d0, sc.d1, ta.data_ptr(), tb.data_ptr(),
                                                                sc.dec2.data_ptr(), sc.dec4.data_ptr(),
                                                                sc.A0.data_ptr(), sc.part.data_ptr()))
-        timed("all_gathers", sc.exchange)
+        if sc.packed:
+            timed("pack", lambda: (sc._pack(sc.dec2, sc.p2), sc._pack(sc.dec4, sc.p4)))
+        timed("all_gathers", sc.exchange)  # packs again when packed
         o = timed("combine", lambda: be.shard_combine_device(n, t, 1, sc.g_dec2.data_ptr(), sc.g_dec4.data_ptr(),
-                                                             sc.c_dec2.data_ptr(), sc.c_dec4.data_ptr()))
+                                                             sc.c_dec2.data_ptr(), sc.c_dec4.data_ptr(),
+                                                             packed=sc.packed))
         q = [int(x) for x in o.qualified]
         timed("finalise", lambda: be.shard_finalise_device(n, t, 1, sc.g_A0.data_ptr(), sc.g_part.data_ptr(), q,
                                                            bool(o.phase4_error), sc.fs.data_ptr(), sc.pub.data_ptr()))
