@@ -2226,6 +2226,11 @@ void unpack_ranks(size_t n, size_t ws, size_t R, const uint32_t* in, uint8_t* ou
   hipLaunchKernelGGL(k_unpack_ranks, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, n, ws, R, in, out);
 }
 
+void row_reject(size_t rows, size_t n, const uint8_t* dec, uint8_t* out, hipStream_t stream) {
+  if (!rows) return;
+  hipLaunchKernelGGL(k_row_reject, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, rows, n, dec, out);
+}
+
 void decision_summary(size_t groups, size_t n, const uint8_t* dec, uint8_t* row_reject, int32_t* complaints,
                       hipStream_t stream) {
   const size_t rows = groups * n;

@@ -44,6 +44,7 @@ struct dkg_ctx {
   // (round1_device with overlap_shares): the checks and round 3 wait for shares_done
   hipStream_t side = nullptr;
   hipEvent_t side_fork = nullptr, shares_done = nullptr, pub_done = nullptr;
+  hipEvent_t terms_done = nullptr;      // a shard's master-key terms, encoded on the side stream
   bool shares_pending = false;
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
@@ -1240,6 +1241,17 @@ void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a
 
 // Verify what round1_device just generated from its extended-form commitments (no encode/decode
 // round trip); restores the ctx on exit.
+// Shares evaluated on the side stream (round1_device with overlap_shares) that a call leaves pending
+// when it throws: the home stream -- every later call's -- waits for them, then the flag is dropped.
+struct SharesScope {
+  dkg_ctx* ctx;
+  explicit SharesScope(dkg_ctx* c) : ctx(c) {}
+  ~SharesScope() {
+    if (ctx->shares_pending) (void)hipStreamWaitEvent(ctx->stream, ctx->shares_done, 0);
+    ctx->shares_pending = false;
+  }
+};
+
 struct ExtScope {
   dkg_ctx* ctx;
   ExtScope(dkg_ctx* c, size_t D, size_t N) : ctx(c) {
@@ -1640,6 +1652,7 @@ int dkg_ctx_create(int device, dkg_ctx** out) {
     HCK(hipEventCreateWithFlags(&ctx->side_fork, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->shares_done, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->pub_done, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&ctx->terms_done, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
     for (auto& e : ctx->join) HCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCK(hipMalloc(&ctx->tab_g, COMB_BYTES));
@@ -2163,32 +2176,40 @@ void shard_rows(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_t D, const uin
     HCK(hipMemsetAsync(d_partial, 0, 32 * n, ctx->stream));
     return;
   }
-  // Qualification of a dealer depends only on its own decision row (any REJECT disqualifies,
-  // committee.rs:370-398; missing data disqualifies, :331-335), so each rank decides it for its
-  // dealers with no exchange.
-  std::vector<uint8_t> rows(D * n), q(D, 1);
-  verify_rounds(ctx, n, t, D, d0, Ec, Ac, ds, dsp, (uint8_t*)d_dec2, (uint8_t*)d_dec4, nullptr, [&] {
-    d2h(ctx, rows.data(), d_dec2, D * n);
-    sync(ctx);
-    for (size_t i = 0; i < D; i++)
-      for (size_t j = 0; j < n; j++)
-        if (rows[i * n + j] == DKG_REJECT || rows[i * n + j] == DKG_MISSING) q[i] = 0;
-  });
-  if (ctx->ext_A) {  // the exchanged A_i0 encodings
+  // the exchanged A_i0 encodings depend only on round 1: encoded on the side stream beside the checks
+  // (a latency-bound chain of D lanes that otherwise ends the call), joined before it returns
+  const bool side_terms = ctx->ext_A != nullptr;
+  if (side_terms) {
     uint32_t* a0 = buf<uint32_t>(ctx, "sh_a0ext", PTB * D);
-    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, D, a0, D, ctx->stream);
-    dkgk::encode_points(a0, D, D, (uint32_t*)d_A0, ctx->stream);
+    HCK(hipEventRecord(ctx->side_fork, ctx->stream));
+    HCK(hipStreamWaitEvent(ctx->side, ctx->side_fork, 0));
+    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, D, a0, D, ctx->side);
+    dkgk::encode_points(a0, D, D, (uint32_t*)d_A0, ctx->side);
+    HCK(hipEventRecord(ctx->terms_done, ctx->side));
   } else {
     HCK(hipMemcpy2DAsync(d_A0, 32, Ac, 32 * N, 32, D, hipMemcpyDeviceToDevice, ctx->stream));
   }
+  // Qualification of a dealer depends only on its own decision row (any REJECT disqualifies,
+  // committee.rs:370-398; missing data disqualifies, :331-335), so each rank decides it for its
+  // dealers with no exchange -- on the device, queued after the checks (no host round trip)
+  uint8_t* rej = buf<uint8_t>(ctx, "sh_rej", D);
+  uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
+  verify_rounds(
+      ctx, n, t, D, d0, Ec, Ac, ds, dsp, (uint8_t*)d_dec2, (uint8_t*)d_dec4, nullptr,
+      [&] {
+        dkgk::row_reject(D, n, (const uint8_t*)d_dec2, rej, ctx->stream);
+        dkgk::mask_not_and(D, rej, nullptr, qm, ctx->stream);
+      },
+      nullptr, nullptr, false);
+  if (side_terms) HCK(hipStreamWaitEvent(ctx->stream, ctx->terms_done, 0));
+  wait_shares(ctx, ctx->stream);  // shares evaluated on the side stream (round1_device)
+  ctx->shares_pending = false;
   // A dealer accused in round 4 (committee.rs:660-670) has its term replaced after the exchange,
   // once the final parties are known (dkg_ceremony_shard_recon_device): its shares stay here.
   ctx->shard_s = ds;
   ctx->shard_n = n;
   ctx->shard_d0 = d0;
   ctx->shard_D = D;
-  uint8_t* qm = buf<uint8_t>(ctx, "sh_q", D);
-  h2d(ctx, qm, q.data(), D);
   dkgk::sum_shares(D, n, ds, qm, (uint32_t*)d_partial, ctx->stream);  // partial of :454-462
 }
 
@@ -2207,12 +2228,16 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     uint32_t* Ac = buf<uint32_t>(ctx, "sh_A", 32 * D * N);
     uint32_t* ds = buf<uint32_t>(ctx, "sh_s", 32 * D * n);
     uint32_t* dsp = buf<uint32_t>(ctx, "sh_sp", 32 * D * n);
-    if (D) round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false);
+    // the shares on the side stream beside the checks, which wait for them (one-stream runs: back to back);
+    // on an exception the home stream still waits for them before the state is dropped
+    SharesScope pending(ctx);
+    if (D) round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false, ctx->nsub > 1);
     ExtScope ext(ctx, D, N);
     shard_rows(ctx, n, t, d0, D, Ec, Ac, ds, dsp, d_dec2, d_dec4, d_A0, d_partial);
     check_launch(ctx);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     sync(ctx);
+    collect_phases(ctx);  // the checks' serialised phases (shard_rows queues no host round trip)
     if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
     return DKG_OK;
   });
@@ -2239,6 +2264,7 @@ int dkg_ceremony_shard_verify_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0
     check_launch(ctx);
     HCK(hipEventRecord(ctx->ev[1], ctx->stream));
     sync(ctx);
+    collect_phases(ctx);  // the checks' serialised phases (shard_rows queues no host round trip)
     if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
     return DKG_OK;
   });
