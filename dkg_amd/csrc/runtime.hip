@@ -1041,12 +1041,12 @@ std::vector<uint8_t> recon_secrets(size_t n, const std::vector<uint8_t>& fin, co
 // dec2 [groups*n][n] on the device, as every party derives it (committee.rs:311-347, 370-398): a
 // REJECT by receiver j is a complaint of j against dealer i, and a valid complaint disqualifies i for
 // everyone; MISSING (no decodable broadcast) disqualifies without a complaint (:331-335); more than t
-// complaints raise MisbehaviourHigherThreshold for j (:340-347).  Host outputs [groups*n]; qmask
-// (device [groups*n]) receives the qualified set.  The single-GPU drivers, the batches and the
-// sharded combine all decide through this function.
-// Each outcome has a device half (kernels queued on ctx->stream, per-dealer / per-receiver results
-// left in `rej`, `cnt`, `r4d`) and a host half (applied to their copies after a sync), so that a
-// caller can queue both rounds' device halves and copy everything back in one round trip.
+// complaints raise MisbehaviourHigherThreshold for j (:340-347); qmask (device [groups*n]) receives
+// the qualified set.  Each round's outcome has a device half (kernels queued on ctx->stream, the
+// per-dealer / per-receiver results left in `rej`, `cnt`, `r4d`) and a host half (applied to their
+// copies after a sync), so that a caller queues both rounds' device halves and copies everything back
+// in one round trip.  The single-GPU drivers, the batches and the sharded combine all decide through
+// these four functions.
 void round2_device(dkg_ctx* ctx, size_t groups, size_t n, const uint8_t* dec2, uint8_t* qmask, uint8_t* rej,
                    int32_t* cnt) {
   dkgk::decision_summary(groups, n, dec2, rej, cnt, ctx->stream);
@@ -1059,19 +1059,6 @@ void round2_host(size_t V, size_t t, uint8_t* qualified, const int32_t* complain
     r2err[i] = complaints[i] > (int32_t)t;  // committee.rs:340-347
   }
 }
-void round2_outcome(dkg_ctx* ctx, size_t groups, size_t n, size_t t, const uint8_t* dec2, uint8_t* qmask,
-                    uint8_t* qualified, int32_t* complaints, uint8_t* r2err) {
-  const size_t V = groups * n;
-  uint8_t* rej = buf<uint8_t>(ctx, "o.rej2", V);
-  int32_t* cnt = buf<int32_t>(ctx, "o.cnt", 4 * V);
-  round2_device(ctx, groups, n, dec2, qmask, rej, cnt);
-  check_launch(ctx);
-  d2h(ctx, qualified, rej, V);
-  d2h(ctx, complaints, cnt, 4 * V);
-  sync(ctx);
-  round2_host(V, t, qualified, complaints, r2err);
-}
-
 // Round-4 outcome (committee.rs:515-522, 567-569, 660-670) from dec4 [groups*n][n] on the device and
 // the round-2 qualified set (host `qualified`, device `qmask`): the rows of disqualified dealers
 // become SKIPPED in place (:522); a qualified dealer some receiver rejects is reconstructed; receiver
@@ -1086,35 +1073,28 @@ void round4_device(dkg_ctx* ctx, size_t groups, size_t n, size_t t, uint8_t* dec
 void round4_host(size_t V, const uint8_t* qualified, uint8_t* recon) {
   for (size_t i = 0; i < V; i++) recon[i] = qualified[i] && recon[i];
 }
-void round4_outcome(dkg_ctx* ctx, size_t groups, size_t n, size_t t, uint8_t* dec4, const uint8_t* qmask,
-                    const uint8_t* qualified, uint8_t* recon, uint8_t* r4err) {
-  const size_t V = groups * n;
-  uint8_t* rej = buf<uint8_t>(ctx, "o.rej4", V);
-  uint8_t* r4d = r4err ? buf<uint8_t>(ctx, "o.r4err", V) : nullptr;
-  round4_device(ctx, groups, n, t, dec4, qmask, rej, r4d);
-  check_launch(ctx);
-  d2h(ctx, recon, rej, V);
-  if (r4err) d2h(ctx, r4err, r4d, V);
-  sync(ctx);
-  round4_host(V, qualified, recon);
-}
 
 // Rounds 2-5 on device-resident broadcast values (E, A compressed [n][N][8]; s, sp [n][n][8]).
+// The outcomes stay on the device until the end -- one host round trip per ceremony, as the batches
+// (batch_receivers): the round-2 outcome's device half gives the qualified mask for round 3, the
+// round-4 half the reconstruction flags, and the master key is summed over the honest set (qualified,
+// not reconstructed: committee.rs:726-805) speculatively; the host then only zeroes it (Phase4 failure,
+// failed recovery) or, when a dealer is reconstructed, adds g * its recovered secret (a second trip).
 void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
                       const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
                       const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
   const size_t N = t + 1;
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
-  // ---- rounds 2 and 4 (committee.rs:260-366, :508-580), fused or in protocol order (verify_rounds)
-  std::vector<uint8_t> qualified(n, 1), r2err(n, 0);
-  std::vector<int32_t> complaints(n, 0);
   uint32_t* fs = buf<uint32_t>(ctx, "final_share", 32 * n);
   uint32_t* pubc = buf<uint32_t>(ctx, "pub_comp", 32 * n);
   uint8_t* qmask = buf<uint8_t>(ctx, "qmask", n);
+  uint8_t* rej2 = buf<uint8_t>(ctx, "o.rej2", n);
+  int32_t* cnt = buf<int32_t>(ctx, "o.cnt", 4 * n);
+  // ---- rounds 2 and 4 (committee.rs:260-366, :508-580), fused or in protocol order (verify_rounds)
   auto round3 = [&] {
     wait_shares(ctx, ctx->stream);
-    round2_outcome(ctx, 1, n, t, dec2, qmask, qualified.data(), complaints.data(), r2err.data());
+    round2_device(ctx, 1, n, dec2, qmask, rej2, cnt);
     // ---- round 3 (committee.rs:433-476): final share s_j = sum_{i in Q} s_ij, public g s_j
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream);
     // the public shares g s_j are an output only: computed on the side stream, off the path to
@@ -1127,17 +1107,54 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     HCK(hipEventRecord(ctx->pub_done, ctx->side));
     HCK(hipEventRecord(ctx->ev[3], ctx->stream));
   };
-  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok, a_ok);
+  verify_rounds(ctx, n, t, n, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, e_ok, a_ok, false);
   wait_shares(ctx, ctx->stream);
   ctx->shares_pending = false;
   // round-4 outcome on the device: a qualified dealer some receiver rejects is reconstructed
   // (committee.rs:660-670); receiver j's round-4 error (:515-516, 567-569) counts itself and the
   // qualified dealers it accepted
-  std::vector<uint8_t> recon(n, 0), r4e(n, 0);
-  round4_outcome(ctx, 1, n, t, dec4, qmask, qualified.data(), recon.data(), r4e.data());
+  uint8_t* rej4 = buf<uint8_t>(ctx, "o.rej4", n);
+  uint8_t* r4d = buf<uint8_t>(ctx, "o.r4err", n);
+  round4_device(ctx, 1, n, t, dec4, qmask, rej4, r4d);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
-  // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 + sum_{recon} g * L_i(0)
-  std::vector<uint8_t> honest_mask = final_parties(n, qualified.data(), recon.data());
+  // ---- finalise (committee.rs:726-805): mpk = sum_{i in Q \ recon} A_i0 (+ sum_{recon} g * L_i(0))
+  uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
+  if (ctx->ext_A) {
+    dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, n, A0, n, ctx->stream);
+  } else {
+    uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
+    HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
+    uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
+    dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
+  }
+  uint8_t* hmask = buf<uint8_t>(ctx, "hmask", n);
+  dkgk::mask_not_and(n, rej4, qmask, hmask, ctx->stream);  // the final parties: qualified, not accused
+  uint32_t* mpk_ext = buf<uint32_t>(ctx, "mpk_ext", PTB);
+  dkgk::sum_points(n, A0, n, hmask, mpk_ext, 1, 0, ctx->stream);
+  uint32_t* mpk_c = buf<uint32_t>(ctx, "mpk_comp", 32);
+  dkgk::encode_points(mpk_ext, 1, 1, mpk_c, ctx->stream);
+  check_launch(ctx);
+  uint8_t* h = hbuf<uint8_t>(ctx, "rr.out", 8 * n + 32);  // rej2 | rej4 | r4err | cnt | mpk
+  d2h(ctx, h, rej2, n);
+  d2h(ctx, h + n, rej4, n);
+  d2h(ctx, h + 2 * n, r4d, n);
+  d2h(ctx, h + 3 * n, cnt, 4 * n);
+  d2h(ctx, h + 7 * n, mpk_c, 32);
+  HCK(hipEventRecord(ctx->ev[5], ctx->stream));
+  HCK(hipStreamWaitEvent(ctx->stream, ctx->pub_done, 0));  // public shares (round 3, side stream)
+  if (copy_big) {
+    if (out->dec2) d2h(ctx, out->dec2, dec2, n * n);
+    if (out->dec4) d2h(ctx, out->dec4, dec4, n * n);  // SKIPPED rows applied (round4_device)
+    if (out->final_share) d2h(ctx, out->final_share, fs, 32 * n);
+    if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * n);
+  }
+  sync(ctx);
+  collect_phases(ctx);
+  std::vector<uint8_t> qualified(h, h + n), r2err(n), recon(h + n, h + 2 * n), r4e(h + 2 * n, h + 3 * n);
+  std::vector<int32_t> complaints(n);
+  memcpy(complaints.data(), h + 3 * n, 4 * n);
+  round2_host(n, t, qualified.data(), complaints.data(), r2err.data());
+  round4_host(n, qualified.data(), recon.data());
   const std::vector<uint8_t> disc = disclosing_parties(n, qualified.data(), recon.data(), r2err.data(), r4e.data());
   size_t nrecon = 0;
   int32_t nq = 0;
@@ -1146,24 +1163,12 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     nq += qualified[i];
   }
   // Phases<Phase4>::proceed fails for every party when qualified minus reconstructable <= t
-  // (committee.rs:673-677): nobody finalises, so there is no master public key (mpk zeroed)
+  // (committee.rs:673-677): nobody finalises, so there is no master public key (mpk zeroed); with
+  // reconstructions and fewer than t disclosing parties nobody recovers (:779-781): none either
   const bool phase4_error = nq - (int32_t)nrecon <= (int32_t)t;
   memset(out->mpk, 0, 32);
   if (!phase4_error && !(nrecon && recovery_fails(disc, t))) {
-    uint32_t* A0 = buf<uint32_t>(ctx, "A0ext", PTB * n);
-    if (ctx->ext_A) {
-      dkgk::gather_points(ctx->ext_A, ctx->ext_stride, N, 0, n, A0, n, ctx->stream);
-    } else {
-      uint32_t* A0c = buf<uint32_t>(ctx, "A0c", 32 * n);
-      HCK(hipMemcpy2DAsync(A0c, 32, Acomp, 32 * N, 32, n, hipMemcpyDeviceToDevice, ctx->stream));
-      uint8_t* a0ok = buf<uint8_t>(ctx, "A0ok", n);
-      dkgk::decode_points(A0c, n, A0, n, a0ok, ctx->stream);
-    }
-    uint8_t* hmask = buf<uint8_t>(ctx, "hmask", n);
-    h2d(ctx, hmask, honest_mask.data(), n);
-    uint32_t* parts = buf<uint32_t>(ctx, "mpk_parts", PTB * 2);
-    dkgk::sum_points(n, A0, n, hmask, parts, 2, 0, ctx->stream);
-    if (nrecon) {
+    if (nrecon) {  // + g * the reconstructed secrets, interpolated over the disclosing final parties
       std::vector<size_t> rows;
       std::vector<uint8_t> hs(32 * n * nrecon);
       for (size_t i = 0; i < n; i++)
@@ -1176,19 +1181,17 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
       uint32_t* sec = buf<uint32_t>(ctx, "recon_sec", 32 * nrecon);
       h2d(ctx, sec, secrets.data(), secrets.size());
       uint32_t* gsec = buf<uint32_t>(ctx, "recon_ext", PTB * nrecon);
+      uint32_t* extra = buf<uint32_t>(ctx, "recon_sum", PTB);
       dkgk::fixed_base(nrecon, sec, ctx->tab_gw, gsec, ctx->stream);
-      dkgk::sum_points(nrecon, gsec, nrecon, nullptr, parts, 2, 1, ctx->stream);
-    } else {
-      dkgk::sum_points(0, A0, n, nullptr, parts, 2, 1, ctx->stream);  // identity
+      dkgk::sum_points(nrecon, gsec, nrecon, nullptr, extra, 1, 0, ctx->stream);
+      dkgk::add_points(1, mpk_ext, extra, 1, mpk_ext, ctx->stream);
+      dkgk::encode_points(mpk_ext, 1, 1, mpk_c, ctx->stream);
+      check_launch(ctx);
+      d2h(ctx, h + 7 * n, mpk_c, 32);
+      sync(ctx);
     }
-    uint32_t* mpk_ext = buf<uint32_t>(ctx, "mpk_ext", PTB);
-    dkgk::sum_points(2, parts, 2, nullptr, mpk_ext, 1, 0, ctx->stream);
-    uint32_t* mpk_c = buf<uint32_t>(ctx, "mpk_comp", 32);
-    dkgk::encode_points(mpk_ext, 1, 1, mpk_c, ctx->stream);
-    check_launch(ctx);
-    d2h(ctx, out->mpk, mpk_c, 32);
+    memcpy(out->mpk, h + 7 * n, 32);
   }
-  HCK(hipEventRecord(ctx->ev[5], ctx->stream));
   // ---- outputs
   if (out->qualified) memcpy(out->qualified, qualified.data(), n);
   if (out->r2_error) memcpy(out->r2_error, r2err.data(), n);
@@ -1197,14 +1200,6 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
   out->n_qualified = nq;
   out->phase4_error = phase4_error;  // committee.rs:673-677
-  HCK(hipStreamWaitEvent(ctx->stream, ctx->pub_done, 0));  // public shares (round 3, side stream)
-  if (copy_big) {
-    if (out->dec2) d2h(ctx, out->dec2, dec2, n * n);
-    if (out->dec4) d2h(ctx, out->dec4, dec4, n * n);  // SKIPPED rows applied (round4_outcome)
-    if (out->final_share) d2h(ctx, out->final_share, fs, 32 * n);
-    if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * n);
-  }
-  sync(ctx);
 }
 
 // Round 1 for D dealers on device: a, b canonical [D][N][8] -> Ecomp, Acomp [D][N][8], s, sp [D][n][8].
@@ -1330,8 +1325,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   // dealers' shares (:433-476), round 4's rejections reconstruct qualified dealers (:660-670) and the
   // honest set -- qualified, not reconstructed -- sums the master key (:726-805).
   auto round3 = [&] {
-    dkgk::decision_summary(B, n, dec2, rej2, cnt, ctx->stream);
-    dkgk::mask_not_and(V, rej2, nullptr, qmask, ctx->stream);
+    round2_device(ctx, B, n, dec2, qmask, rej2, cnt);
     wait_shares(ctx, ctx->stream);  // shares evaluated on the side stream (BatchRound1)
     dkgk::sum_shares(n, n, s, qmask, fs, ctx->stream, B);
     dkgk::fixed_base(V, fs, ctx->tab_gw, pub, ctx->stream);
@@ -1340,9 +1334,7 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   };
   verify_rounds(ctx, n, t, V, 0, Ecomp, Acomp, s, sp, dec2, dec4, ctx->ev[2], round3, nullptr, nullptr, false);
   // round 4 (committee.rs:515-522, 567-569, 660-670): rows of disqualified dealers SKIPPED
-  dkgk::decision_summary(B, n, dec4, rej4, nullptr, ctx->stream);
-  dkgk::r4_error(B, n, t, dec4, qmask, r4d, ctx->stream);
-  dkgk::apply_skipped(B, n, dec4, qmask, ctx->stream);
+  round4_device(ctx, B, n, t, dec4, qmask, rej4, r4d);
   dkgk::mask_not_and(V, rej4, qmask, hmask, ctx->stream);
   HCK(hipEventRecord(ctx->ev[4], ctx->stream));
   // finalise (committee.rs:726-805): mpk_c = sum of the honest A_i0 (+ g * reconstructed secrets)
@@ -1391,12 +1383,10 @@ void batch_receivers(dkg_ctx* ctx, size_t B, size_t n, size_t t, const uint32_t*
   for (size_t k = 0; k < sizeof(outs) / sizeof(outs[0]); k++)
     if (staged[k]) memcpy(outs[k].host, staged[k], outs[k].bytes);
   collect_phases(ctx);
-  for (size_t i = 0; i < V; i++) {
-    qualified[i] = !qualified[i];
-    r2err[i] = complaints[i] > (int32_t)t;  // committee.rs:340-347
-    recon[i] = qualified[i] && h_rej4[i];
-    honest[i] = qualified[i] && !recon[i];
-  }
+  round2_host(V, t, qualified.data(), complaints.data(), r2err.data());
+  recon = h_rej4;
+  round4_host(V, qualified.data(), recon.data());
+  for (size_t i = 0; i < V; i++) honest[i] = qualified[i] && !recon[i];
   std::vector<size_t> recon_cer, nompk;
   std::vector<uint8_t> p4err(B, 0);
   for (size_t c = 0; c < B; c++) {

@@ -316,7 +316,7 @@ typedef struct {
 
 /* Combine step after the decision all-gathers: d_dec2_g, d_dec4_g device [ws][R][n] (rank blocks as
  * gathered, rows past a rank's dealer count ignored).  Derives the common outcome with the same code
- * as the single-GPU drivers (runtime.hip round2_outcome / round4_outcome).  d_dec2, d_dec4 (device
+ * as the single-GPU drivers (runtime.hip round2_device / round4_device and their host halves).  d_dec2, d_dec4 (device
  * [n][n], may be NULL): the compacted decision matrices, dec4 with the SKIPPED rows of disqualified
  * dealers applied (:522). */
 int dkg_shard_combine_device(dkg_ctx *ctx, size_t n, size_t t, size_t world_size, const void *d_dec2_g,
