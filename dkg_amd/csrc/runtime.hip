@@ -1234,8 +1234,6 @@ void round1_device(dkg_ctx* ctx, size_t D, size_t n, size_t t, const uint32_t* a
 }
 
 
-// Verify what round1_device just generated from its extended-form commitments (no encode/decode
-// round trip); restores the ctx on exit.
 // Shares evaluated on the side stream (round1_device with overlap_shares) that a call leaves pending
 // when it throws: the home stream -- every later call's -- waits for them, then the flag is dropped.
 struct SharesScope {
@@ -1247,6 +1245,8 @@ struct SharesScope {
   }
 };
 
+// Verify what round1_device just generated from its extended-form commitments (no encode/decode
+// round trip); restores the ctx on exit.
 struct ExtScope {
   dkg_ctx* ctx;
   ExtScope(dkg_ctx* c, size_t D, size_t N) : ctx(c) {
