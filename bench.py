@@ -1006,6 +1006,16 @@ def main():
             dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
             out["roofline"] = roofline_line(rl, dom, f"rank 0's shard ({D} dealers): {work[dom]:.4g} VALU issue "
                                                      f"slots per pass (closed form); device time in a serialised pass")
+            # the counters' lower bound needs the kernel's INT64 share, a per-lane instruction mix that
+            # does not depend on the dealer count: the one-GPU profile of the same (n, t, U, L) gives it
+            # (its byte count does depend on D, so `traffic` stays unmeasured here)
+            pmc = pmc_traffic(dom, n, t, U, Ls)
+            if pmc is not None and pmc[2] is not None:
+                r = out["roofline"]
+                r["valu_int64_share"] = pmc[2]
+                r["valu_int64_share_source"] = (pmc[1] + " -- the same kernel at the one-GPU workload "
+                                                "(n, t, U, L); the instruction mix per lane is independent of D")
+                r["frac_counter_lower_bound"] = r["instr_frac"] * (1 + pmc[2])
     if rank == 0:
         emit(out)
     be.close()

@@ -45,3 +45,6 @@ def test_bench_multi_rank_gloo_on_one_gpu(gpus):
     assert ex["decisions"] == "packed bitmaps" and ex["bytes_per_rank"] < ex["bytes_per_rank_byte_rows"]
     rl = out["roofline"]
     assert rl["bound"] and rl["peak"] > 0 and 0 < rl["frac"] <= 1.2, rl
+    assert 0 < rl["instr_frac"] < rl["frac"], rl
+    if gpus == 2 and rl["kernel"] == "stepping":  # the one-GPU profile's (n, t, U, L) = this shard's
+        assert rl["instr_frac"] < rl["frac_counter_lower_bound"] <= rl["frac"] * 1.01, rl
