@@ -367,6 +367,41 @@ __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q)
   }
 }
 
+// mul_small_lds with the dedicated additions (k_binom_wave<.., DED>): the base's cached form needs no
+// product by d; `bad` is set when an addition's Z vanished (then the caller redoes the column group
+// with the complete formula)
+__device__ __forceinline__ void mul_small_ded_lds(ge_p3& y, uint32_t m, uint32_t* q, bool& bad) {
+  uint32_t pos = 0, neg = 0;
+  int len = 0;
+  for (uint32_t v = m; v; v >>= 1, len++) {
+    if (v & 1u) {
+      if ((v & 3u) == 1u) {
+        pos |= 1u << len;
+        v -= 1;
+      } else {
+        neg |= 1u << len;
+        v += 1;
+      }
+    }
+  }
+  if (len <= 1) return;
+  {
+    ge_cached xc;
+    ge_to_cached_ded(xc, y);
+    lds_put_cached(q, xc);
+  }
+#pragma unroll 1
+  for (int i = len - 2; i >= 0; i--) {
+    const uint32_t bit = 1u << i;
+    const bool nz = ((pos | neg) & bit) != 0;
+    ge_dbl_lean(y, y, nz || i == 0);
+    if (nz) {
+      ge_add_ded_lds_s(y, y, q, (neg & bit) != 0, 64, i == 0);  // T only for the result
+      bad |= fe_tight_zero(y.Z);
+    }
+  }
+}
+
 // y = m * x for a wave-uniform small m (non-adjacent form, left to right).
 __device__ __forceinline__ void mul_small_uniform(ge_p3& y, const ge_p3& x, uint32_t m) {
   uint32_t pos = 0, neg = 0;
@@ -611,16 +646,26 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
 #ifndef DKG_BINOM_WAVE_WAVES  // resident waves per SIMD of the carried schedule (168 VGPRs at 3)
 #define DKG_BINOM_WAVE_WAVES 3
 #endif
-template <bool CARRY, bool PF>
+// DED: the dedicated additions (no product by d in the cached forms: two fewer products per item);
+// a wave whose real columns met an addition with Z = 0 marks flags[its group], and the same grid
+// relaunched with DED = false and the flags redoes only the marked groups with the complete formula,
+// from the coefficients (every position is rebuilt from C, so the first pass's table is irrelevant).
+// Identity padding columns (past `dreal` dealers, `gw` columns per dealer group) never mark.
+template <bool CARRY, bool PF, bool DED>
 __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) void k_binom_wave(int L, size_t npad,
                                                                            const uint32_t* __restrict__ C,
                                                                            uint32_t* e, size_t pstride, unsigned gx,
                                                                            unsigned last_piece, int last_off,
-                                                                           uint32_t* eT) {
+                                                                           uint32_t* eT, uint32_t* __restrict__ flags,
+                                                                           size_t col_base, size_t dreal, unsigned gw) {
   static_assert(!PF || CARRY, "the prefetch runs on the carried schedule");
+  static_assert(!DED || (CARRY && !PF), "the dedicated pass runs on the carried schedule");
   __shared__ uint32_t qs[PT_WORDS * 64];
   uint32_t* q = qs + threadIdx.x;
   const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
+  // this group's flag word: one per (piece, dealer-column group) over the whole table
+  const size_t fidx = (size_t)piece * (pstride / 64) + (col_base / 64) + grp;
+  if (!DED && flags && !flags[fidx]) return;  // a redo launch: this group's table was exact
   // wave-uniform bases (SGPRs) and a 32-bit lane index: no 64-bit per-lane address stays live
   const size_t col0 = piece * pstride + (size_t)grp * 64;
   uint32_t* eb = e + col0;
@@ -628,6 +673,9 @@ __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) vo
   const uint32_t lane = threadIdx.x;
   const size_t S = (size_t)L * npad;
   const int off = piece == last_piece ? last_off : 0;
+  bool bad = false;
+  const size_t gcol = col_base + (size_t)grp * 64 + lane;  // the column within its piece
+  const bool real = (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
   // one position: no step follows, so the top coefficient goes straight into the column-major
   // table (with L = 1 both layouts are [40][npad])
   uint32_t* e_top = (L == 1 && eT) ? eT + col0 : eb;
@@ -647,7 +695,8 @@ __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) vo
       {
         ge_cached cc;
         if constexpr (CARRY) {
-          ge_to_cached(cc, carry);
+          if constexpr (DED) ge_to_cached_ded(cc, carry);
+          else ge_to_cached(cc, carry);
         } else {
           ge_p3 cur;
           pt_load(cur, eb, S, (size_t)m * npad + lane);
@@ -670,8 +719,14 @@ __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) vo
         pt_load(x, eb, S, (size_t)(m - 1) * npad + lane);
       }
       if constexpr (CARRY) carry = x;    // the old e_{m-1}: the next item's e_m
-      ge_add_lds(x, x, q, false);        // e_{m-1} + e_m
-      mul_small_lds(x, (uint32_t)m, q);  // * m
+      if constexpr (DED) {
+        ge_add_ded_lds(x, x, q);         // e_{m-1} + e_m
+        bad |= fe_tight_zero(x.Z);
+        mul_small_ded_lds(x, (uint32_t)m, q, bad);  // * m
+      } else {
+        ge_add_lds(x, x, q, false);        // e_{m-1} + e_m
+        mul_small_lds(x, (uint32_t)m, q);  // * m
+      }
       // an opaque copy of the base: otherwise the compiler keeps the 40 addresses of the `cur` load
       // (the same words) live across the chain for this store, and spills them
       if (r + 1 < L || !eT) {
@@ -694,18 +749,30 @@ __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) vo
       for (int w = 0; w < PT_WORDS; w++) eo[w * S + (size_t)lane * L] = cb[w * S + lane];
     }
   }
+  if constexpr (DED) {
+    if (__ballot(bad && real) != 0 && lane == 0) flags[fidx] = 1u;
+  }
 }
 
 uint32_t* binomial_wave(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e, hipStream_t stream,
-                        size_t pieces, size_t pstride, size_t last_len, uint32_t* eT, bool prefetch) {
+                        size_t pieces, size_t pstride, size_t last_len, uint32_t* eT, bool prefetch,
+                        uint32_t* flags, size_t col_base, size_t dreal, unsigned gw) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   const dim3 grid((unsigned)(width / 64 * pieces));
-  if (prefetch)
-    hipLaunchKernelGGL((k_binom_wave<true, true>), grid, dim3(64), 0, stream, (int)N, npad, C, e, pstride,
-                       (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, eT);
-  else
-    hipLaunchKernelGGL((k_binom_wave<DKG_BINOM_WAVE_CARRY != 0, false>), grid, dim3(64), 0, stream, (int)N, npad, C,
-                       e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, eT);
+  const unsigned gx = (unsigned)(width / 64), lp = (unsigned)(pieces - 1);
+  if (!gw) gw = 64;
+  if (prefetch) {
+    hipLaunchKernelGGL((k_binom_wave<true, true, false>), grid, dim3(64), 0, stream, (int)N, npad, C, e, pstride, gx,
+                       lp, last_off, eT, nullptr, col_base, dreal, gw);
+  } else if (flags && DKG_BINOM_WAVE_CARRY) {  // dedicated pass, then the complete redo of marked groups
+    hipLaunchKernelGGL((k_binom_wave<true, false, true>), grid, dim3(64), 0, stream, (int)N, npad, C, e, pstride, gx,
+                       lp, last_off, eT, flags, col_base, dreal, gw);
+    hipLaunchKernelGGL((k_binom_wave<true, false, false>), grid, dim3(64), 0, stream, (int)N, npad, C, e, pstride,
+                       gx, lp, last_off, eT, flags, col_base, dreal, gw);
+  } else {
+    hipLaunchKernelGGL((k_binom_wave<DKG_BINOM_WAVE_CARRY != 0, false, false>), grid, dim3(64), 0, stream, (int)N,
+                       npad, C, e, pstride, gx, lp, last_off, eT, nullptr, col_base, dreal, gw);
+  }
   return e;
 }
 

@@ -307,6 +307,34 @@ DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int str
   fe_mul(r.Z, h, e);             // Z3 = F G  (x19 operands F and H, computed once each)
 }
 
+// The dedicated addition with a signed addend and an optional T (the m-chains of the per-wave
+// binomial): r = p +/- Q, Q as ge_to_cached_ded in LDS, -Q = (Y-X, Y+X, 2Z, -2T) -- the fields
+// swapped and C negated exactly as ge_add_lds does (the same bounds).  `neg` wave-uniform.  Not
+// complete (above): the caller tests r.Z.
+DKG_DEV void ge_add_ded_lds_s(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,
+                              bool with_t = true) {
+  fe a, b, e, h, t, qv;
+  fe_sub(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 1 : 0, stride);
+  fe_mul(a, t, qv);              // A
+  fe_add(t, p.Y, p.X);
+  lds_get_fe(qv, q, neg ? 0 : 1, stride);
+  fe_mul(b, t, qv);              // B
+  fe_sub(e, b, a);               // F
+  fe_add(h, b, a);               // G
+  lds_get_fe(qv, q, 3, stride);
+  fe_mul(a, p.Z, qv);            // C = 2 Z1 T2
+  if (neg) fe_neg(a, a);         // 2p - C <= 2p limbwise: a valid fe_sub subtrahend
+  lds_get_fe(qv, q, 2, stride);
+  fe_mul(b, p.T, qv);            // D = 2 T1 Z2
+  fe_add(t, b, a);               // E = D + C
+  fe_sub(b, b, a);               // H = D - C
+  fe_mul(r.X, t, e);             // X3 = E F
+  fe_mul(r.Y, h, b);             // Y3 = G H
+  fe_mul(r.Z, h, e);             // Z3 = F G
+  if (with_t) fe_mul(r.T, t, b); // T3 = E H
+}
+
 // r = p +/- Q with Q affine Niels (y+x, y-x, 2dxy) in LDS, read like the cached form above (fields
 // 0, 1, 2): 7M, d = 2Z carried as in ge_madd_signed.  `neg` must be wave-uniform.
 DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,

@@ -269,6 +269,9 @@ struct VerifySeg {
 #ifndef DKG_BINOM_WAVE_PF  // the per-wave binomial's default: operands prefetched one item ahead
 #define DKG_BINOM_WAVE_PF 0   // (2 waves per SIMD: config 5 +5.5 ms, profiles/r05_b5_ab.txt)
 #endif
+#ifndef DKG_BINOM_WAVE_DED  // the per-wave binomial with dedicated additions (+ complete redo)
+#define DKG_BINOM_WAVE_DED 1
+#endif
 #ifndef DKG_BINOM_WAVE_COLMAJOR  // its last step writing the stepping's column-major table itself:
 #define DKG_BINOM_WAVE_COLMAJOR 0  // 4-B stores 128 B apart, +10 ms against k_to_column_major's 3.3
 #endif                             // (config 5, profiles/r05_b5_ab.txt)
@@ -641,6 +644,14 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   const bool per_wave = ctx->binom_mode == 4 || ctx->binom_mode == 5 ||
                         (ctx->binom_mode == 0 && L > 1 && (double)npad / 64 * U >= DKG_BINOM_WAVE_GROUPS);
   ctx->last_binomial = per_wave ? 1 : 0;
+  // the per-wave binomial's dedicated additions (with the stepping's formula setting): one redo flag
+  // per (piece, 64-column group), zeroed before the chunks fork
+  uint32_t* bflags = nullptr;
+  if (per_wave && ctx->step_formula == 0 && DKG_BINOM_WAVE_DED && ctx->binom_mode != 5 &&
+      !(ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF)) {
+    bflags = buf<uint32_t>(ctx, "v.bflags", 4 * (W / 64));
+    HCK(hipMemsetAsync(bflags, 0, 4 * (W / 64), home));
+  }
   // dead-position repack of an unsplit table (kernels.hip stepping_tail_phases): two scratch states
   const bool tails = ctx->step_mode != 3 && dkgk::stepping_tail_phases(L, n, U) > 1;
   uint32_t* tail_a = tails ? buf<uint32_t>(ctx, "v.tail_a", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
@@ -657,7 +668,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
     if (per_wave) {
       e = dkgk::binomial_wave(w, W, L, Cpm + c0, e0 + c0, st, U, npad, Lr,
                               DKG_BINOM_WAVE_COLMAJOR ? eT + c0 * L : nullptr,
-                              ctx->binom_mode == 5 || (ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF));
+                              ctx->binom_mode == 5 || (ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF), bflags, c0, D,
+                              (unsigned)gw);
     } else {
       dkgk::binom_init(w, W, L, Cpm + c0, e0 + c0, st, U, npad);
       uint32_t *bin = e0 + c0, *bout = e1 + c0;

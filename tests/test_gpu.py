@@ -896,6 +896,42 @@ def test_binomial_schedules_goldens(be, golden, name, field):
         be.set_streams(2)
 
 
+@pytest.mark.parametrize("field", [1, 2])
+def test_binomial_dedicated_redo(be, golden, field):
+    """The per-wave binomial's dedicated additions (runtime.hip DKG_BINOM_WAVE_DED) meet Z = 0 on a
+    dealer whose commitments are all the identity (the fault of committee.rs:1127): e_{m-1} + e_m of
+    two identities gives the all-zero quadruple, which the projective equality test would find equal
+    to ANY point -- a false accept of that dealer's honest shares.  Its column group must be redone
+    with the complete formula: every receiver rejects it (identity != g*s + h*s'), and every output
+    equals the per-step schedule's (complete additions in the binomial).  A build without the redo
+    launch fails here (profiles/r05_binom_ded_ab.txt)."""
+    c = golden("ceremony_n64_t31.json")
+    n, t = c["n"], c["t"]
+    N = t + 1
+    be.env_init(t, n, CK)
+    E, A = bytearray(H(c["E"])), bytearray(H(c["A"]))
+    s, sp = bytearray(H(c["s"])), bytearray(H(c["s_prime"]))
+    bad = 5
+    for buf in (E, A):
+        buf[32 * N * bad:32 * N * (bad + 1)] = bytes(32 * N)  # the identity's encoding, every coefficient
+    outs = {}
+    try:
+        be.set_field_mode(field)
+        be.set_split(1)
+        for mode in (1, 4):  # one launch per step (complete) / per-wave loops (dedicated + redo)
+            be.set_binomial(mode)
+            r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            row = list(r.dec2[bad * n:(bad + 1) * n])  # round 4 then skips the disqualified dealer
+            assert row == [SELF if j == bad else REJECT for j in range(n)], (mode, row)
+            assert not r.qualified[bad]
+            outs[mode] = (bytes(r.dec2), bytes(r.dec4), list(r.qualified), r.final_share, r.public_share, r.mpk)
+    finally:
+        be.set_field_mode(0)
+        be.set_binomial(0)
+        be.set_split(0)
+    assert outs[1] == outs[4]
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("name", FAULTS + ["ceremony_n64_t31.json"])
 def test_stepping_modes_goldens(be, golden, name, mode):
