@@ -512,11 +512,16 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 // pieces, r+1) with m = r - blockIdx.y: workgroups are dispatched x-fastest, so the longest NAF
 // chains (largest m) of EVERY piece start first and the launch tail is made of the short ones.
 
+// DED: the dedicated additions (no product by d in the cached forms); a wave whose real columns met
+// Z = 0 marks flags[its (piece, column group)], and after the last step binomial_wave_redo rebuilds
+// the marked groups' whole tables with the complete formula (per-wave loops, from the coefficients).
+template <bool DED>
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
                                                     size_t pstride, unsigned gx, unsigned last_piece,
-                                                    int last_off) {
+                                                    int last_off, uint32_t* __restrict__ flags, size_t col_base,
+                                                    size_t dreal, unsigned gw) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
   const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
@@ -544,14 +549,26 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
 #pragma unroll
     for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
     ge_cached cc;
-    ge_to_cached(cc, cur);
+    if constexpr (DED) ge_to_cached_ded(cc, cur);
+    else ge_to_cached(cc, cur);
     lds_put_cached(q, cc);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the second point's loads after the first is retired
   ge_p3 x;
   pt_load(x, ein, S, (size_t)(m - 1) * npad + d);
-  ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
-  mul_small_lds(x, (uint32_t)m, q);        // * m
+  if constexpr (DED) {
+    bool bad = false;
+    ge_add_ded_lds(x, x, q);                   // e_{m-1} + e_m
+    bad |= fe_tight_zero(x.Z);
+    mul_small_ded_lds(x, (uint32_t)m, q, bad);  // * m
+    const size_t gcol = col_base + (size_t)grp * blockDim.x + threadIdx.x;
+    const bool real = (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
+    if (__ballot(bad && real) != 0 && threadIdx.x == 0)
+      flags[(size_t)piece * (pstride / 64) + (col_base / 64) + grp] = 1u;
+  } else {
+    ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
+    mul_small_lds(x, (uint32_t)m, q);        // * m
+  }
   pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
@@ -613,12 +630,19 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 }
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
-                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len) {
+                hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* flags, size_t col_base,
+                size_t dreal, unsigned gw) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
-  hipLaunchKernelGGL(k_binom_step, dim3((unsigned)(width / 64 * pieces), (unsigned)(r + 1)), dim3(64), 0, stream,
-                     (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride, (unsigned)(width / 64),
-                     (unsigned)(pieces - 1), last_off);
+  const dim3 grid((unsigned)(width / 64 * pieces), (unsigned)(r + 1));
+  if (flags)
+    hipLaunchKernelGGL(k_binom_step<true>, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out,
+                       pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, flags, col_base, dreal,
+                       gw ? gw : 64u);
+  else
+    hipLaunchKernelGGL(k_binom_step<false>, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out,
+                       pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, nullptr, col_base, dreal,
+                       gw ? gw : 64u);
 }
 
 // Every Horner step of one column group in ONE wave (short tables of many columns: config 5's
@@ -774,6 +798,15 @@ uint32_t* binomial_wave(size_t width, size_t npad, size_t N, const uint32_t* C, 
                        npad, C, e, pstride, gx, lp, last_off, eT, nullptr, col_base, dreal, gw);
   }
   return e;
+}
+
+void binomial_wave_redo(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e, hipStream_t stream,
+                        size_t pieces, size_t pstride, size_t last_len, uint32_t* flags, size_t col_base,
+                        size_t dreal, unsigned gw) {
+  const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
+  hipLaunchKernelGGL((k_binom_wave<true, false, false>), dim3((unsigned)(width / 64 * pieces)), dim3(64), 0, stream,
+                     (int)N, npad, C, e, pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, nullptr,
+                     flags, col_base, dreal, gw ? gw : 64u);
 }
 
 uint32_t* binomial(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t* e0, uint32_t* e1,

@@ -272,6 +272,9 @@ struct VerifySeg {
 #ifndef DKG_BINOM_WAVE_DED  // the per-wave binomial with dedicated additions (+ complete redo)
 #define DKG_BINOM_WAVE_DED 1
 #endif
+#ifndef DKG_BINOM_STEP_DED  // the per-step binomial's steps without lane pairs likewise (redone per wave)
+#define DKG_BINOM_STEP_DED 1
+#endif
 #ifndef DKG_BINOM_WAVE_COLMAJOR  // its last step writing the stepping's column-major table itself:
 #define DKG_BINOM_WAVE_COLMAJOR 0  // 4-B stores 128 B apart, +10 ms against k_to_column_major's 3.3
 #endif                             // (config 5, profiles/r05_b5_ab.txt)
@@ -646,9 +649,11 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   ctx->last_binomial = per_wave ? 1 : 0;
   // the per-wave binomial's dedicated additions (with the stepping's formula setting): one redo flag
   // per (piece, 64-column group), zeroed before the chunks fork
+  // (and of the per-step binomial's steps without lane pairs: DKG_BINOM_STEP_DED, redone per wave)
   uint32_t* bflags = nullptr;
-  if (per_wave && ctx->step_formula == 0 && DKG_BINOM_WAVE_DED && ctx->binom_mode != 5 &&
-      !(ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF)) {
+  const bool wave_ded = per_wave && DKG_BINOM_WAVE_DED && ctx->binom_mode != 5 &&
+                        !(ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF);
+  if (ctx->step_formula == 0 && (wave_ded || (!per_wave && DKG_BINOM_STEP_DED))) {
     bflags = buf<uint32_t>(ctx, "v.bflags", 4 * (W / 64));
     HCK(hipMemsetAsync(bflags, 0, 4 * (W / 64), home));
   }
@@ -686,10 +691,12 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
           (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad,
                                                                     Lr);
         else
-          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr);
+          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr, bflags,
+                                                          c0, D, (unsigned)gw);
         std::swap(bin, bout);
       }
       e = bin;
+      if (bflags) dkgk::binomial_wave_redo(w, W, L, Cpm + c0, bin, st, U, npad, Lr, bflags, c0, D, (unsigned)gw);
     }
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     if (!per_wave || !DKG_BINOM_WAVE_COLMAJOR)  // timed with the stepping

@@ -903,8 +903,9 @@ def test_binomial_dedicated_redo(be, golden, field):
     two identities gives the all-zero quadruple, which the projective equality test would find equal
     to ANY point -- a false accept of that dealer's honest shares.  Its column group must be redone
     with the complete formula: every receiver rejects it (identity != g*s + h*s'), and every output
-    equals the per-step schedule's (complete additions in the binomial).  A build without the redo
-    launch fails here (profiles/r05_binom_ded_ab.txt)."""
+    equals the complete formula's.  The per-step schedule (steps without lane pairs) marks its groups
+    the same way and redoes them with the per-wave loops after its last step.  A build without the
+    redo launch fails here (profiles/r05_binom_ded_ab.txt)."""
     c = golden("ceremony_n64_t31.json")
     n, t = c["n"], c["t"]
     N = t + 1
@@ -918,18 +919,23 @@ def test_binomial_dedicated_redo(be, golden, field):
     try:
         be.set_field_mode(field)
         be.set_split(1)
-        for mode in (1, 4):  # one launch per step (complete) / per-wave loops (dedicated + redo)
+        # formula 0: dedicated additions in the per-step (mode 1, no lane pairs) and the per-wave
+        # (mode 4) binomial, each with its redo; formula 1: the complete formula throughout (reference)
+        for formula, mode in ((0, 1), (0, 4), (1, 1)):
+            be.set_stepping_formula(formula)
             be.set_binomial(mode)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             row = list(r.dec2[bad * n:(bad + 1) * n])  # round 4 then skips the disqualified dealer
-            assert row == [SELF if j == bad else REJECT for j in range(n)], (mode, row)
+            assert row == [SELF if j == bad else REJECT for j in range(n)], (formula, mode, row)
             assert not r.qualified[bad]
-            outs[mode] = (bytes(r.dec2), bytes(r.dec4), list(r.qualified), r.final_share, r.public_share, r.mpk)
+            outs[(formula, mode)] = (bytes(r.dec2), bytes(r.dec4), list(r.qualified), r.final_share,
+                                     r.public_share, r.mpk)
     finally:
+        be.set_stepping_formula(0)
         be.set_field_mode(0)
         be.set_binomial(0)
         be.set_split(0)
-    assert outs[1] == outs[4]
+    assert outs[(0, 1)] == outs[(1, 1)] and outs[(0, 4)] == outs[(1, 1)]
 
 
 @pytest.mark.parametrize("mode", [1, 2])
