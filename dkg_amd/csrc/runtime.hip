@@ -272,8 +272,12 @@ struct VerifySeg {
 #ifndef DKG_BINOM_WAVE_DED  // the per-wave binomial with dedicated additions (+ complete redo)
 #define DKG_BINOM_WAVE_DED 1
 #endif
-#ifndef DKG_BINOM_STEP_DED  // the per-step binomial's steps without lane pairs likewise (redone per wave)
-#define DKG_BINOM_STEP_DED 1
+// the per-step binomial's steps without lane pairs likewise, redone per wave: off -- it gains 0.4 ms
+// on the headline and 29 ms on config 4, but a crafted identity row would then cost one per-wave
+// loop over a whole 128- (512-) position triangle, ~0.1 (~2) s, where the per-wave binomial's redo
+// costs at most its own pass again (profiles/r05_binom_ded_ab.txt)
+#ifndef DKG_BINOM_STEP_DED
+#define DKG_BINOM_STEP_DED 0
 #endif
 #ifndef DKG_BINOM_WAVE_COLMAJOR  // its last step writing the stepping's column-major table itself:
 #define DKG_BINOM_WAVE_COLMAJOR 0  // 4-B stores 128 B apart, +10 ms against k_to_column_major's 3.3
