@@ -73,13 +73,18 @@ def main(d):
                   f"{c.get('SQ_ACTIVE_INST_VALU2', 0) / (c.get('SQ_ACTIVE_INST_VALU', 0) or 1):12.4f}")
 
 
-def phase(name):
+def phase(name, ded_binomial=False):
     """Pipeline phase of a kernel-trace name (template arguments as rocprofv3 prints them): the
     dedicated stepping (k_stepping<MAXBS, true, PARTS>) and its complete-formula redo launches
     (<MAXBS, false, ..>: near-empty when no workgroup was marked, kept apart so that they do not
     halve the per-launch average), the recombination, the normalisation, the binomial (per step or
-    per wave), the check and full mode's hybrid kernels."""
-    if name == "k_binom_step" or re.match(r"(void )?k_binom_wave<", name):
+    per wave; with ded_binomial -- the run had a dedicated k_binom_wave<.., .., true> / k_binom_step<true>
+    -- the complete variants are its redo launches, "binomial_redo"), the check and full mode's
+    hybrid kernels."""
+    m = re.match(r"(?:void )?k_binom_(?:wave<\w+, \w+, (true|false)>|step<(true|false)>)", name)
+    if m and ded_binomial:
+        return "binomial" if "true" in (m.group(1), m.group(2)) else "binomial_redo"
+    if name == "k_binom_step" or re.match(r"(void )?k_binom_(wave|step)<", name):
         return "binomial"
     m = re.match(r"void k_stepping<\d+(?:, (true|false))?", name)
     if m:
@@ -99,8 +104,9 @@ def write_traffic(d, out, key):
     fe, fcalls = load_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
     wr, wcalls = load_counters(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
     kern = {}
+    ded = any(re.match(r"(?:void )?k_binom_(?:wave<\w+, \w+, true>|step<true>)", k) for k in fe)
     for k in fe:
-        ph = phase(k)
+        ph = phase(k, ded)
         if ph is None or k not in wr:
             continue
         e = kern.setdefault(ph, {"fetch_bytes_x2": 0.0, "write_bytes": 0.0, "fetch_launches": 0, "write_launches": 0})
