@@ -903,9 +903,9 @@ def test_binomial_dedicated_redo(be, golden, field):
     two identities gives the all-zero quadruple, which the projective equality test would find equal
     to ANY point -- a false accept of that dealer's honest shares.  Its column group must be redone
     with the complete formula: every receiver rejects it (identity != g*s + h*s'), and every output
-    equals the complete formula's.  The per-step schedule (steps without lane pairs) marks its groups
-    the same way and redoes them with the per-wave loops after its last step.  A build without the
-    redo launch fails here (profiles/r05_binom_ded_ab.txt)."""
+    equals the complete formula's.  With -DDKG_BINOM_STEP_DED=1 the per-step schedule (mode 1) marks
+    its groups the same way and redoes them with the per-wave loops after its last step (off by
+    default).  Builds without either redo fail here (profiles/r05_binom_ded_ab.txt)."""
     c = golden("ceremony_n64_t31.json")
     n, t = c["n"], c["t"]
     N = t + 1
