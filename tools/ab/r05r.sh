@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd)
-O=$R/gpurun_out/r05r
+O=$R/gpurun_out/r05r2
 mkdir -p $O
 (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/tools/shard_time.py --ws 8 --reps 3 > $O/shard.log 2>&1) \
   || { echo TRACE FAILED; tail -20 $O/shard.log; exit 1; }
