@@ -521,7 +521,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
                                                     size_t pstride, unsigned gx, unsigned last_piece,
                                                     int last_off, uint32_t* __restrict__ flags, size_t col_base,
-                                                    size_t dreal, unsigned gw) {
+                                                    size_t dreal, unsigned gw, int fany) {
   __shared__ uint32_t qs[PT_WORDS * 64];  // this wave's cached addend (lane-interleaved)
   uint32_t* q = qs + threadIdx.x;
   const unsigned piece = blockIdx.x / gx, grp = blockIdx.x - piece * gx;
@@ -563,8 +563,8 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
     mul_small_ded_lds(x, (uint32_t)m, q, bad);  // * m
     const size_t gcol = col_base + (size_t)grp * blockDim.x + threadIdx.x;
     const bool real = (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
-    if (__ballot(bad && real) != 0 && threadIdx.x == 0)
-      flags[(size_t)piece * (pstride / 64) + (col_base / 64) + grp] = 1u;
+    if (__ballot(bad && real) != 0 && threadIdx.x == 0)  // fany: one word for the whole table
+      flags[fany ? 0 : (size_t)piece * (pstride / 64) + (col_base / 64) + grp] = 1u;
   } else {
     ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
     mul_small_lds(x, (uint32_t)m, q);        // * m
@@ -631,18 +631,18 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
                 hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* flags, size_t col_base,
-                size_t dreal, unsigned gw) {
+                size_t dreal, unsigned gw, bool flag_any) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
   const dim3 grid((unsigned)(width / 64 * pieces), (unsigned)(r + 1));
   if (flags)
     hipLaunchKernelGGL(k_binom_step<true>, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out,
                        pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, flags, col_base, dreal,
-                       gw ? gw : 64u);
+                       gw ? gw : 64u, flag_any ? 1 : 0);
   else
     hipLaunchKernelGGL(k_binom_step<false>, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out,
                        pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, nullptr, col_base, dreal,
-                       gw ? gw : 64u);
+                       gw ? gw : 64u, 0);
 }
 
 // Every Horner step of one column group in ONE wave (short tables of many columns: config 5's

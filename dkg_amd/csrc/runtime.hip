@@ -75,6 +75,13 @@ struct dkg_ctx {
                                         // workgroups, 1 complete formula only
   uint32_t* last_step_flags = nullptr;  // the last verify_device's stepping flags (dedicated mode)
   size_t last_step_flag_words = 0;
+  // the per-step binomial's dedicated additions: only inside the drivers that check its group flags
+  // after their sync and rerun the verification with the complete formula when one is set
+  // (receivers_rounds, shard_rows: binom_step_ded = true around the call)
+  bool binom_step_ded = false;
+  uint32_t* binom_any = nullptr;        // device word: a dedicated per-step binomial marked a group
+                                        // since the last verify_rounds began (null: none ran)
+  const uint32_t* binom_any_host = nullptr;  // its pinned copy, queued before the caller's sync
   int addend_mode = 0;                  // short vectors' addends: 0 affine Niels (affine_pieces, mixed
                                         // additions), 1 cached projective (read from R)
   size_t sdig_n = 0, sdig_L = 0, sdig_K = 0;  // key of the cached short multipliers (v.sdig)
@@ -272,12 +279,12 @@ struct VerifySeg {
 #ifndef DKG_BINOM_WAVE_DED  // the per-wave binomial with dedicated additions (+ complete redo)
 #define DKG_BINOM_WAVE_DED 1
 #endif
-// the per-step binomial's steps without lane pairs likewise, redone per wave: off -- it gains 0.4 ms
-// on the headline and 29 ms on config 4, but a crafted identity row would then cost one per-wave
-// loop over a whole 128- (512-) position triangle, ~0.1 (~2) s, where the per-wave binomial's redo
-// costs at most its own pass again (profiles/r05_binom_ded_ab.txt)
+// the per-step binomial's steps without lane pairs likewise (0.5 ms on the headline, 22 ms on config
+// 4, profiles/r05_binom_ded_ab.txt): in the drivers that rerun the verification with the complete
+// formula when a step marked the guard word (with_binom_ded: at most twice the honest time); 2 = redo
+// per wave after the last step instead (a slow worst case: a per-wave loop over a whole triangle)
 #ifndef DKG_BINOM_STEP_DED
-#define DKG_BINOM_STEP_DED 0
+#define DKG_BINOM_STEP_DED 1
 #endif
 #ifndef DKG_BINOM_WAVE_COLMAJOR  // its last step writing the stepping's column-major table itself:
 #define DKG_BINOM_WAVE_COLMAJOR 0  // 4-B stores 128 B apart, +10 ms against k_to_column_major's 3.3
@@ -653,14 +660,19 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
   ctx->last_binomial = per_wave ? 1 : 0;
   // the per-wave binomial's dedicated additions (with the stepping's formula setting): one redo flag
   // per (piece, 64-column group), zeroed before the chunks fork
-  // (and of the per-step binomial's steps without lane pairs: DKG_BINOM_STEP_DED, redone per wave)
+  // (and of the per-step binomial's steps without lane pairs under DKG_BINOM_STEP_DED=2, redone per
+  // wave; =1 marks the one guard word of with_binom_ded instead)
   uint32_t* bflags = nullptr;
   const bool wave_ded = per_wave && DKG_BINOM_WAVE_DED && ctx->binom_mode != 5 &&
                         !(ctx->binom_mode == 0 && DKG_BINOM_WAVE_PF);
-  if (ctx->step_formula == 0 && (wave_ded || (!per_wave && DKG_BINOM_STEP_DED))) {
+  const bool step_ded = !per_wave && ((DKG_BINOM_STEP_DED == 1 && ctx->binom_step_ded && ctx->binom_any) ||
+                                      DKG_BINOM_STEP_DED == 2);
+  if (ctx->step_formula == 0 && (wave_ded || (step_ded && DKG_BINOM_STEP_DED == 2))) {
     bflags = buf<uint32_t>(ctx, "v.bflags", 4 * (W / 64));
     HCK(hipMemsetAsync(bflags, 0, 4 * (W / 64), home));
   }
+  // the rerun guard's word (with_binom_ded): zeroed when the verification began (verify_rounds)
+  uint32_t* bany = step_ded && DKG_BINOM_STEP_DED == 1 && ctx->step_formula == 0 ? ctx->binom_any : nullptr;
   // dead-position repack of an unsplit table (kernels.hip stepping_tail_phases): two scratch states
   const bool tails = ctx->step_mode != 3 && dkgk::stepping_tail_phases(L, n, U) > 1;
   uint32_t* tail_a = tails ? buf<uint32_t>(ctx, "v.tail_a", 4 * dkgk::stepping_tail_words(npad, L)) : nullptr;
@@ -695,12 +707,13 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
           (ilp ? dkgk_ilp::binom_step_pair : dkgk::binom_step_pair)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad,
                                                                     Lr);
         else
-          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr, bflags,
-                                                          c0, D, (unsigned)gw);
+          (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr,
+                                                          bany ? bany : bflags, c0, D, (unsigned)gw, bany != nullptr);
         std::swap(bin, bout);
       }
       e = bin;
-      if (bflags) dkgk::binomial_wave_redo(w, W, L, Cpm + c0, bin, st, U, npad, Lr, bflags, c0, D, (unsigned)gw);
+      if (bflags && DKG_BINOM_STEP_DED == 2)
+        dkgk::binomial_wave_redo(w, W, L, Cpm + c0, bin, st, U, npad, Lr, bflags, c0, D, (unsigned)gw);
     }
     if (tm) HCK(hipEventRecord(ctx->pev[1], st));
     if (!per_wave || !DKG_BINOM_WAVE_COLMAJOR)  // timed with the stepping
@@ -968,11 +981,53 @@ void verify_rounds(dkg_ctx* ctx, size_t n, size_t t, size_t D, size_t dealer_bas
   // dkg_ctx_stepping_redos reports THIS verification's stepping (none if it builds no tables)
   ctx->last_step_flags = nullptr;
   ctx->last_step_flag_words = 0;
+  ctx->binom_any = nullptr;
+  ctx->binom_any_host = nullptr;
+  if (ctx->binom_step_ded && DKG_BINOM_STEP_DED == 1) {  // both rounds' binomials mark one word
+    ctx->binom_any = buf<uint32_t>(ctx, "v.bany", 4);
+    HCK(hipMemsetAsync(ctx->binom_any, 0, 4, ctx->stream));
+  }
   if (ctx->verify_mode == 1)
     verify_rounds_interp(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok);
   else
     verify_rounds_group(ctx, n, t, D, dealer_base, Ecomp, Acomp, s, sp, dec2, dec4, after2, between, e_ok, a_ok,
                         host_between);
+}
+
+// Queues the copy of the rerun guard's word into pinned memory ahead of the caller's own sync, so
+// that reading it costs no round trip of its own.
+void binom_mark_copy(dkg_ctx* ctx) {
+  if (!ctx->binom_any) return;
+  uint32_t* h = hbuf<uint32_t>(ctx, "bany.h", 4);
+  d2h(ctx, h, ctx->binom_any, 4);
+  ctx->binom_any_host = h;
+}
+
+// After a sync: did the last verification's per-step binomial mark a group (a dedicated addition met
+// Z = 0)?  Then its tables are not the complete formula's and the caller reruns the verification.
+// (A caller that queued no copy pays a blocking read.)
+bool binom_marked(dkg_ctx* ctx) {
+  if (!ctx->binom_any) return false;
+  uint32_t v = 0;
+  if (ctx->binom_any_host)
+    v = *ctx->binom_any_host;
+  else
+    HCK(hipMemcpy(&v, ctx->binom_any, 4, hipMemcpyDeviceToHost));
+  return v != 0;
+}
+
+// Runs f() -- a verification and its outcomes, ending in a sync -- with the per-step binomial's
+// dedicated additions allowed; when a group was marked, f() runs again with the complete formula.
+template <typename F>
+void with_binom_ded(dkg_ctx* ctx, F&& f) {
+  struct Off {
+    dkg_ctx* c;
+    ~Off() { c->binom_step_ded = false; }
+  } off{ctx};
+  ctx->binom_step_ded = true;
+  f();
+  ctx->binom_step_ded = false;
+  if (binom_marked(ctx)) f();
 }
 
 double ev_ms(dkg_ctx* ctx, int a, int b) {
@@ -1103,9 +1158,9 @@ void round4_host(size_t V, const uint8_t* qualified, uint8_t* recon) {
 // round-4 half the reconstruction flags, and the master key is summed over the honest set (qualified,
 // not reconstructed: committee.rs:726-805) speculatively; the host then only zeroes it (Phase4 failure,
 // failed recovery) or, when a dealer is reconstructed, adds g * its recovered secret (a second trip).
-void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
-                      const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
-                      const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
+void receivers_rounds_once(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
+                           const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
+                           const uint8_t* e_ok, const uint8_t* a_ok) {
   const size_t N = t + 1;
   uint8_t* dec2 = buf<uint8_t>(ctx, "dec2", n * n);
   uint8_t* dec4 = buf<uint8_t>(ctx, "dec4", n * n);
@@ -1171,6 +1226,7 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
     if (out->final_share) d2h(ctx, out->final_share, fs, 32 * n);
     if (out->public_share) d2h(ctx, out->public_share, pubc, 32 * n);
   }
+  binom_mark_copy(ctx);
   sync(ctx);
   collect_phases(ctx);
   std::vector<uint8_t> qualified(h, h + n), r2err(n), recon(h + n, h + 2 * n), r4e(h + 2 * n, h + 3 * n);
@@ -1223,6 +1279,14 @@ void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, c
   if (out->reconstruct) memcpy(out->reconstruct, recon.data(), n);
   out->n_qualified = nq;
   out->phase4_error = phase4_error;  // committee.rs:673-677
+}
+
+// receivers_rounds_once with the per-step binomial's dedicated additions, rerun with the complete
+// formula when they marked a group (with_binom_ded)
+void receivers_rounds(dkg_ctx* ctx, size_t n, size_t t, const uint32_t* Ecomp, const uint32_t* Acomp,
+                      const uint32_t* s, const uint32_t* sp, dkg_ceremony_out* out, bool copy_big,
+                      const uint8_t* e_ok = nullptr, const uint8_t* a_ok = nullptr) {
+  with_binom_ded(ctx, [&] { receivers_rounds_once(ctx, n, t, Ecomp, Acomp, s, sp, out, copy_big, e_ok, a_ok); });
 }
 
 // Round 1 for D dealers on device: a, b canonical [D][N][8] -> Ecomp, Acomp [D][N][8], s, sp [D][n][8].
@@ -2246,10 +2310,13 @@ int dkg_ceremony_shard_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0, size_
     SharesScope pending(ctx);
     if (D) round1_device(ctx, D, n, t, (const uint32_t*)d_a, (const uint32_t*)d_b, Ec, Ac, ds, dsp, false, ctx->nsub > 1);
     ExtScope ext(ctx, D, N);
-    shard_rows(ctx, n, t, d0, D, Ec, Ac, ds, dsp, d_dec2, d_dec4, d_A0, d_partial);
-    check_launch(ctx);
-    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
-    sync(ctx);
+    with_binom_ded(ctx, [&] {
+      shard_rows(ctx, n, t, d0, D, Ec, Ac, ds, dsp, d_dec2, d_dec4, d_A0, d_partial);
+      check_launch(ctx);
+      HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+      binom_mark_copy(ctx);
+      sync(ctx);
+    });
     collect_phases(ctx);  // the checks' serialised phases (shard_rows queues no host round trip)
     if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
     return DKG_OK;
@@ -2272,11 +2339,14 @@ int dkg_ceremony_shard_verify_device(dkg_ctx* ctx, size_t n, size_t t, size_t d0
       dkgk::reduce_scalars(D * n, (const uint32_t*)d_s, ds, ctx->stream);
       dkgk::reduce_scalars(D * n, (const uint32_t*)d_s_prime, dsp, ctx->stream);
     }
-    shard_rows(ctx, n, t, d0, D, (const uint32_t*)d_E, (const uint32_t*)d_A, ds, dsp, d_dec2, d_dec4, d_A0,
-               d_partial);
-    check_launch(ctx);
-    HCK(hipEventRecord(ctx->ev[1], ctx->stream));
-    sync(ctx);
+    with_binom_ded(ctx, [&] {
+      shard_rows(ctx, n, t, d0, D, (const uint32_t*)d_E, (const uint32_t*)d_A, ds, dsp, d_dec2, d_dec4, d_A0,
+                 d_partial);
+      check_launch(ctx);
+      HCK(hipEventRecord(ctx->ev[1], ctx->stream));
+      binom_mark_copy(ctx);
+      sync(ctx);
+    });
     collect_phases(ctx);  // the checks' serialised phases (shard_rows queues no host round trip)
     if (ms_total) *ms_total = ev_ms(ctx, 0, 1);
     return DKG_OK;

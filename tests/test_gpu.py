@@ -903,9 +903,11 @@ def test_binomial_dedicated_redo(be, golden, field):
     two identities gives the all-zero quadruple, which the projective equality test would find equal
     to ANY point -- a false accept of that dealer's honest shares.  Its column group must be redone
     with the complete formula: every receiver rejects it (identity != g*s + h*s'), and every output
-    equals the complete formula's.  With -DDKG_BINOM_STEP_DED=1 the per-step schedule (mode 1) marks
-    its groups the same way and redoes them with the per-wave loops after its last step (off by
-    default).  Builds without either redo fail here (profiles/r05_binom_ded_ab.txt)."""
+    equals the complete formula's.  The per-step schedule (mode 1; DKG_BINOM_STEP_DED=1, the default)
+    marks one word instead and its driver reruns the whole verification with the complete formula --
+    here through the ceremony and the dealer-shard entry point alike.  Builds without the per-wave
+    redo or the rerun fail here (profiles/r05_binom_ded_ab.txt)."""
+    import torch
     c = golden("ceremony_n64_t31.json")
     n, t = c["n"], c["t"]
     N = t + 1
@@ -930,12 +932,23 @@ def test_binomial_dedicated_redo(be, golden, field):
             assert not r.qualified[bad]
             outs[(formula, mode)] = (bytes(r.dec2), bytes(r.dec4), list(r.qualified), r.final_share,
                                      r.public_share, r.mpk)
+            if mode == 1:  # one rank holding every dealer: dkg_ceremony_shard_verify_device's rows
+                dev = torch.device("cuda", 0)
+                ins = [torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev) for x in (E, A, s, sp)]
+                o2, o4 = (torch.zeros(n * n, dtype=torch.uint8, device=dev) for _ in range(2))
+                oA, op = (torch.zeros(32 * n, dtype=torch.uint8, device=dev) for _ in range(2))
+                be.ceremony_shard_verify_device(n, t, 0, n, *(x.data_ptr() for x in ins), o2.data_ptr(),
+                                                o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+                srow = o2[bad * n:(bad + 1) * n].tolist()
+                assert srow == [SELF if j == bad else REJECT for j in range(n)], (formula, "shard", srow)
+                outs[(formula, "shard")] = (bytes(o2.cpu().numpy()), bytes(op.cpu().numpy()))
     finally:
         be.set_stepping_formula(0)
         be.set_field_mode(0)
         be.set_binomial(0)
         be.set_split(0)
     assert outs[(0, 1)] == outs[(1, 1)] and outs[(0, 4)] == outs[(1, 1)]
+    assert outs[(0, "shard")] == outs[(1, "shard")]
 
 
 @pytest.mark.parametrize("mode", [1, 2])
