@@ -513,8 +513,9 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 // chains (largest m) of EVERY piece start first and the launch tail is made of the short ones.
 
 // DED: the dedicated additions (no product by d in the cached forms); a wave whose real columns met
-// Z = 0 marks flags[its (piece, column group)], and after the last step binomial_wave_redo rebuilds
-// the marked groups' whole tables with the complete formula (per-wave loops, from the coefficients).
+// Z = 0 marks flags[0] (fany: the driver's guard word, runtime.hip with_binom_ded, which reruns the
+// verification with the complete formula) or flags[its (piece, column group)] (binomial_wave_redo
+// rebuilds the marked groups after the last step, DKG_BINOM_STEP_DED=2).
 template <bool DED>
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
