@@ -2729,23 +2729,25 @@ int dkg_shard_finalise_device(dkg_ctx* ctx, size_t n, size_t t, size_t world_siz
       uint8_t* qm = buf<uint8_t>(ctx, "sf.q", n);
       uint32_t* sum = buf<uint32_t>(ctx, "sf.sum", PTB);
       uint32_t* mc = buf<uint32_t>(ctx, "sf.mpk", 32);
+      // small host transfers through pinned staging ([qualified | ok | mpk]): no pageable bounce
+      uint8_t* h = hbuf<uint8_t>(ctx, "sf.host", 2 * n + 32);
+      memcpy(h, qualified, n);
       dkgk::compact_ranks(n, world_size, R, 32, d_terms_g, terms, ctx->stream);
-      h2d(ctx, qm, qualified, n);
+      h2d(ctx, qm, h, n);
       dkgk::decode_points(terms, n, ext, n, ok, ctx->stream);
       dkgk::sum_points(n, ext, n, qm, sum, 1, 0, ctx->stream);
       dkgk::encode_points(sum, 1, 1, mc, ctx->stream);
       join_public();
       check_launch(ctx);
-      std::vector<uint8_t> okh(n);
-      d2h(ctx, okh.data(), ok, n);
-      d2h(ctx, mpk, mc, 32);
+      d2h(ctx, h + n, ok, n);
+      d2h(ctx, h + 2 * n, mc, 32);
       sync(ctx);
       for (size_t i = 0; i < n; i++)
-        if (qualified[i] && !okh[i]) {
-          memset(mpk, 0, 32);
+        if (qualified[i] && !h[n + i]) {
           ctx->err = "shard_finalise: a qualified dealer's master-key term does not decode";
           return DKG_E_DECODE;
         }
+      memcpy(mpk, h + 2 * n, 32);
       return DKG_OK;  // synced above, the public shares joined
     }
     join_public();

@@ -73,8 +73,11 @@ def main():
         timed("finalise", lambda: be.shard_finalise_device(n, t, 1, sc.g_A0.data_ptr(), sc.g_part.data_ptr(), q,
                                                            bool(o.phase4_error), sc.fs.data_ptr(), sc.pub.data_ptr()))
         timed("copy_out", lambda: (bytes(sc.fs.cpu().numpy()), bytes(sc.pub.cpu().numpy())))
+    after = sorted(f - s for f, s in zip(full, shard))  # per run: wall minus the shard's device span
     print(json.dumps({"n": n, "t": t, "run_ms": round(min(full), 3), "shard_device_ms": round(min(shard), 3),
                       "exchange_and_combine_ms": round(min(full) - min(shard), 3),
+                      "after_shard_ms_median": round(after[len(after) // 2], 3),
+                      "after_shard_ms_min": round(after[0], 3),
                       "parts_ms": {k: round(v, 3) for k, v in parts.items()}}))
     be.close()
     dist.destroy_process_group()
