@@ -185,6 +185,11 @@ class Backend:
             raise DkgError(_lib.DKG_E_DEVICE, "dkg_ctx_stepping_redos failed")
         return r
 
+    def binomial_reruns(self) -> int:
+        """1 when the last ceremony / shard call reran its verification with the complete formula
+        (a dedicated addition of the per-step binomial met an exceptional pair), else 0."""
+        return _lib.lib().dkg_ctx_binomial_reruns(self._ctx)
+
     def set_addends(self, mode: int):
         """Addends of the short-multiplier recombination: 0 affine Niels (default), 1 cached
         projective; decisions are identical (dkg_ctx_set_addends)."""

@@ -82,6 +82,7 @@ struct dkg_ctx {
   uint32_t* binom_any = nullptr;        // device word: a dedicated per-step binomial marked a group
                                         // since the last verify_rounds began (null: none ran)
   const uint32_t* binom_any_host = nullptr;  // its pinned copy, queued before the caller's sync
+  int last_binom_rerun = 0;             // the last guarded driver reran its verification (1) or not
   int addend_mode = 0;                  // short vectors' addends: 0 affine Niels (affine_pieces, mixed
                                         // additions), 1 cached projective (read from R)
   size_t sdig_n = 0, sdig_L = 0, sdig_K = 0;  // key of the cached short multipliers (v.sdig)
@@ -1025,9 +1026,13 @@ void with_binom_ded(dkg_ctx* ctx, F&& f) {
     ~Off() { c->binom_step_ded = false; }
   } off{ctx};
   ctx->binom_step_ded = true;
+  ctx->last_binom_rerun = 0;
   f();
   ctx->binom_step_ded = false;
-  if (binom_marked(ctx)) f();
+  if (binom_marked(ctx)) {
+    ctx->last_binom_rerun = 1;
+    f();
+  }
 }
 
 double ev_ms(dkg_ctx* ctx, int a, int b) {
@@ -1862,6 +1867,7 @@ long long dkg_ctx_stepping_redos(dkg_ctx* ctx) {
     return -1;
   }
 }
+int dkg_ctx_binomial_reruns(dkg_ctx* ctx) { return ctx ? ctx->last_binom_rerun : -1; }
 int dkg_ctx_set_addends(dkg_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 1) return DKG_E_ARG;
   ctx->addend_mode = mode;

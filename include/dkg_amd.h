@@ -130,6 +130,10 @@ int dkg_ctx_set_stepping_formula(dkg_ctx *ctx, int mode);
 /* Workgroups of the last verification's stepping that were recomputed by the complete formula
  * (synchronises the context's stream; 0 in mode 1; -1 on error). */
 long long dkg_ctx_stepping_redos(dkg_ctx *ctx);
+/* 1 when the last single-ceremony or dealer-shard call reran its verification with the complete
+ * formula because a dedicated addition of the per-step binomial met Z = 0 (an exceptional pair, e.g.
+ * a crafted all-identity commitment row), else 0 (-1 on a NULL ctx). */
+int dkg_ctx_binomial_reruns(dkg_ctx *ctx);
 /* The short multipliers (b_j, a_j1, .., a_j(U-1)) of receivers j = 1..n for a `pieces`-way split of
  * piece length L (2 <= pieces <= 5): magnitudes mag[n][pieces][32] (little-endian), signs
  * sign[n][pieces] (+1 / -1); a_ju = b_j j^(uL) mod l and b_j > 0.  DKG_E_ARG on bad input. */

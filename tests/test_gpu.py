@@ -921,12 +921,18 @@ def test_binomial_dedicated_redo(be, golden, field):
     try:
         be.set_field_mode(field)
         be.set_split(1)
+        be.set_binomial(1)  # the honest broadcasts: the dedicated per-step binomial needs no rerun
+        r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), n, t)
+        _check_ceremony(c, r, n)
+        assert be.binomial_reruns() == 0
         # formula 0: dedicated additions in the per-step (mode 1, no lane pairs) and the per-wave
         # (mode 4) binomial, each with its redo; formula 1: the complete formula throughout (reference)
         for formula, mode in ((0, 1), (0, 4), (1, 1)):
             be.set_stepping_formula(formula)
             be.set_binomial(mode)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+            # only the dedicated per-step schedule reran (the per-wave one redoes its groups in place)
+            assert be.binomial_reruns() == (1 if (formula, mode) == (0, 1) else 0), (formula, mode)
             row = list(r.dec2[bad * n:(bad + 1) * n])  # round 4 then skips the disqualified dealer
             assert row == [SELF if j == bad else REJECT for j in range(n)], (formula, mode, row)
             assert not r.qualified[bad]
@@ -939,6 +945,7 @@ def test_binomial_dedicated_redo(be, golden, field):
                 oA, op = (torch.zeros(32 * n, dtype=torch.uint8, device=dev) for _ in range(2))
                 be.ceremony_shard_verify_device(n, t, 0, n, *(x.data_ptr() for x in ins), o2.data_ptr(),
                                                 o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+                assert be.binomial_reruns() == (1 if formula == 0 else 0), (formula, "shard")
                 srow = o2[bad * n:(bad + 1) * n].tolist()
                 assert srow == [SELF if j == bad else REJECT for j in range(n)], (formula, "shard", srow)
                 outs[(formula, "shard")] = (bytes(o2.cpu().numpy()), bytes(op.cpu().numpy()))

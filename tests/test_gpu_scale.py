@@ -633,3 +633,4 @@ def test_honest_ragged_no_stepping_redo(be, n, t, split):
         be.set_split(0)
     assert r.qualified == [1] * n and r.n_qualified == n
     assert be.stepping_redos() == 0, (n, t, be.last_split())
+    assert be.binomial_reruns() == 0, (n, t, be.last_split())
