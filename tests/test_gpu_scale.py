@@ -503,6 +503,46 @@ def test_shard_ranks_n1024_all_match_single(be):
     assert o.reconstruct == [int(i in {dkg_amd.shard_range(n, ws, r)[0] + 2 for r in range(ws)}) for i in range(n)]
 
 
+def test_shard_stepping_redo_n1024(be):
+    """The 8-way n=1024 shard's stepping (256 columns x 4 pieces, 2 waves per SIMD) with identity E
+    and A rows inside rank 0's dealers: their columns' dedicated additions are exceptional, the
+    complete-formula redo must run, and every output of the rank equals the complete formula's
+    (dkg_ctx_set_stepping_formula 1); the identity rows are rejected by every other receiver, honest
+    rows accepted (committee.rs:287-305, 532-548).  (A lane-pair variant of the dedicated pass was
+    built against this test and measured slower: profiles/r05_step_pair_ab.txt.)"""
+    import torch
+
+    n, t, ws = 1024, 511, 8
+    N = t + 1
+    be.env_init(t, n, CK)
+    _, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([59]) * 32, 3)
+    d0, d1 = dkg_amd.shard_range(n, ws, 0)
+    D = d1 - d0
+    for d, buf in ((7, tE), (9, tA)):  # identity rows (committee.rs:1127 style)
+        buf[32 * N * d:32 * N * (d + 1)] = 0
+    outs = []
+    try:
+        for formula in (0, 1):
+            be.set_stepping_formula(formula)
+            o2 = torch.zeros(D * n, dtype=torch.uint8, device=ts.device)
+            o4 = torch.zeros_like(o2)
+            oA = torch.zeros(D * 32, dtype=torch.uint8, device=ts.device)
+            op = torch.zeros(n * 32, dtype=torch.uint8, device=ts.device)
+            be.ceremony_shard_verify_device(n, t, d0, d1, tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr(),
+                                            o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+            assert be.last_split() == 4, be.last_split()
+            outs.append((bytes(o2.cpu().numpy()), bytes(o4.cpu().numpy()), bytes(oA.cpu().numpy()),
+                         bytes(op.cpu().numpy()), be.stepping_redos()))
+    finally:
+        be.set_stepping_formula(0)
+    assert outs[0][:4] == outs[1][:4]
+    assert outs[0][4] > 0 and outs[1][4] == 0  # the dedicated pass marked the identity rows' workgroups
+    d2, d4 = outs[0][0], outs[0][1]
+    row = lambda m, i, v: bytes(SELF if j == i else v for j in range(n)) == m[i * n:(i + 1) * n]  # noqa: E731
+    assert row(d2, 7, REJECT) and row(d4, 9, REJECT)  # identity rows: every other receiver rejects
+    assert all(row(d2, i, ACCEPT) for i in (0, 8, 9, D - 1)) and all(row(d4, i, ACCEPT) for i in (0, 8, D - 1))
+
+
 @pytest.mark.parametrize("n,t", [(64, 31), (100, 49), (41, 20)])
 def test_stepping_tail_repack_faults(be, n, t):
     """The dead-position repack of short unsplit tables (kernels.hip stepping_tail_phases: the last
