@@ -243,6 +243,8 @@ def add_traffic(line, dom, ms_pass, n, t, U, plen, per_wave=False, batch=1, mode
         rl["traffic"] = pmc[0]
         rl["traffic_unit"] = "HBM-side bytes per launch (average)"
         rl["traffic_source"] = pmc[1]
+        rl["traffic_measured_on"] = (f"profile box ({pmc[1]}): PMC FETCH_SIZE/WRITE_SIZE passes of the same "
+                                     "workload, not counters taken during this run")
         if alg:
             rl["traffic_over_algorithmic"] = pmc[0] / alg
         if pmc[2] is not None:
@@ -290,6 +292,15 @@ def spawn_ranks(args, poll_s=0.2):
                 p.wait()
         return failed if failed > 0 else 1
     return 0
+
+
+def clock_fields(before, after):
+    """The shader clock just before and just after the timed region (Backend.clock_probe: 4 waves per
+    SIMD on every CU, s_memtime against s_memrealtime): boxes differ by several percent in clock,
+    and the line says which clock its number was taken at."""
+    return {"sclk_mhz": {"before": round(before["sclk_mhz"], 1), "after": round(after["sclk_mhz"], 1)},
+            "sclk_probe": "median over 4 waves/SIMD x all CUs of s_memtime cycles per s_memrealtime us, "
+                          f"{before['busy_ms']:.2f} ms probe launches outside the timed region"}
 
 
 def dist_env():
@@ -615,6 +626,7 @@ def bench_batch(args, ws, rank, local):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    clk0 = be.clock_probe()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -627,6 +639,7 @@ def bench_batch(args, ws, rank, local):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    clk1 = be.clock_probe()
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -657,6 +670,7 @@ def bench_batch(args, ws, rank, local):
            "phases_ms": {k: round(v, 3) for k, v in res.ms.items()}}
     out["config"]["degree_split"] = U
     out["ref_equiv"] = ref_equiv(n, t, out["value"])
+    out.update(clock_fields(clk0, clk1))
     out["config"]["binomial"] = "per-wave loops" if be.last_binomial() else "one launch per step"
     if rl:
         dom = max(rl, key=lambda k: rl[k]["ms_per_pass"])
@@ -696,6 +710,17 @@ def sharded_self_check(args, dist, be, res, ta, D, N, dev):
     secret = sum(int.from_bytes(raw[32 * r:32 * r + 32], "little") for r in range(dist.get_world_size())) % L
     expect = be.fixed_base_batch(secret.to_bytes(32, "little"))
     assert res.mpk == expect, "sharded mpk != g * sum of the dealers' a_i0"
+    # which device each rank ran on: the N > 1 line must show N distinct GPUs under RCCL (under the
+    # gloo rehearsal ranks share one GPU and the count is 1)
+    bus = be.pci_bus_id().encode()[:31].ljust(32, b"\0")
+    mine = torch.frombuffer(bytearray(bus), dtype=torch.uint8).to(xdev)
+    allb = torch.empty(32 * dist.get_world_size(), dtype=torch.uint8, device=xdev)
+    dist.all_gather_into_tensor(allb, mine)
+    rawb = bytes(allb.cpu().numpy())
+    rank_devices = [rawb[32 * r:32 * r + 32].rstrip(b"\0").decode() for r in range(dist.get_world_size())]
+    distinct = len(set(rank_devices))
+    if args.dist_backend == "nccl" and distinct != dist.get_world_size():
+        raise SystemExit(f"RCCL ranks share devices: {rank_devices}")
     keys = ["shard_device", "exchange", "combine", "recon", "finalise"]
     vals = [res.ms_shard] + [res.ms_steps.get(k, 0.0) for k in keys[1:]]
     mine = torch.tensor(vals, dtype=torch.float64, device=xdev)
@@ -703,6 +728,8 @@ def sharded_self_check(args, dist, be, res, ta, D, N, dev):
     dist.all_gather_into_tensor(allv, mine)
     per = allv.cpu().view(-1, len(vals)).tolist()
     return {"mpk_check": "mpk == g * sum_i a_i0 (partial sums all-gathered)",
+            "rank_devices": rank_devices, "distinct_devices": distinct,
+            "dist": {"backend": args.dist_backend, "world_size": dist.get_world_size()},
             "rank_ms": {k: {"min": round(min(r[i] for r in per), 3), "max": round(max(r[i] for r in per), 3)}
                         for i, k in enumerate(keys)},
             "rank_ms_note": "last timed step; shard_device = HIP-event time of the rank's share gen + checks, the "
@@ -831,6 +858,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    clk0 = be.clock_probe()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -843,6 +871,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    clk1 = be.clock_probe()
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -869,6 +898,7 @@ def main():
                    "parallelism": f"dealer-sharded x{ws}" if ws > 1 else "single GPU"},
     }
     out["ref_equiv"] = ref_equiv(n, t, value)
+    out.update(clock_fields(clk0, clk1))
     if args.mode == "full":
         out["config"]["mode"] = "full: shares hybrid-encrypted (elgamal.rs) and decrypted by each receiver"
     if rank == 0 and ws == 1 and res is not None and args.mode == "full":

@@ -115,6 +115,8 @@ def lib():
     L.dkg_ctx_stepping_redos.argtypes = [p]
     L.dkg_ctx_stepping_redos.restype = ctypes.c_longlong
     L.dkg_ctx_binomial_reruns.argtypes = [p]
+    L.dkg_ctx_clock_probe.argtypes = [p, ctypes.c_uint, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    L.dkg_device_pci_bus_id.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     L.dkg_split_multipliers.argtypes = [sz, sz, ctypes.c_int, p, p]
     L.dkg_ctx_phase_ms.argtypes = [p, ctypes.c_char_p]
     L.dkg_ctx_phase_ms.restype = ctypes.c_double
@@ -192,6 +194,7 @@ EXPORTED = [
     "dkg_points_valid_batch", "dkg_share_gen", "dkg_verify_pairs", "dkg_verify_receiver",
     "dkg_ctx_set_split", "dkg_ctx_set_stepping", "dkg_ctx_set_field_mode", "dkg_ctx_set_binomial", "dkg_ctx_set_check", "dkg_ctx_last_split", "dkg_ctx_last_split_len", "dkg_ctx_set_verify_mode", "dkg_ctx_fallback_rows", "dkg_split_model_ms", "dkg_split_len",
     "dkg_ctx_set_combine", "dkg_ctx_last_combine", "dkg_ctx_last_binomial", "dkg_ctx_set_addends", "dkg_ctx_set_stepping_formula", "dkg_ctx_stepping_redos", "dkg_ctx_binomial_reruns", "dkg_split_multipliers",
+    "dkg_ctx_clock_probe", "dkg_device_pci_bus_id",
     "dkg_ceremony_run", "dkg_ceremony_verify", "dkg_ceremony_verify_fetched", "dkg_ceremony_run_device", "dkg_ceremony_shard_device",
     "dkg_ceremony_shard_verify_device",
     "dkg_ceremony_batch_device", "dkg_ceremony_batch_verify", "dkg_member_keys", "dkg_enc_randomness",

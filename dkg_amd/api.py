@@ -112,6 +112,7 @@ class Backend:
         if rc != _lib.DKG_OK:
             raise DkgError(rc, f"dkg_ctx_create(device={device}) failed (is a gfx950 GPU visible?)")
         self._ctx = h
+        self.device = device
         self.h: Optional[bytes] = None
 
     def close(self):
@@ -189,6 +190,16 @@ class Backend:
         """1 when the last ceremony / shard call reran its verification with the complete formula
         (a dedicated addition of the per-step binomial met an exceptional pair), else 0."""
         return _lib.lib().dkg_ctx_binomial_reruns(self._ctx)
+
+    def clock_probe(self, iters: int = 200_000) -> dict:
+        """Shader clock under full VALU occupancy (dkg_ctx_clock_probe): {"sclk_mhz", "busy_ms"}."""
+        mhz, ms = ctypes.c_double(), ctypes.c_double()
+        _check(self._ctx, _lib.lib().dkg_ctx_clock_probe(self._ctx, iters, ctypes.byref(mhz), ctypes.byref(ms)))
+        return {"sclk_mhz": mhz.value, "busy_ms": ms.value}
+
+    def pci_bus_id(self) -> str:
+        """PCI bus id of this context's device ("dddd:bb:dd.f")."""
+        return device_pci_bus_id(self.device)
 
     def set_addends(self, mode: int):
         """Addends of the short-multiplier recombination: 0 affine Niels (default), 1 cached
@@ -634,6 +645,15 @@ def shard_range(n: int, world_size: int, rank: int):
     d0, d1 = ctypes.c_size_t(), ctypes.c_size_t()
     _lib.lib().dkg_shard_range(n, world_size, rank, ctypes.byref(d0), ctypes.byref(d1))
     return d0.value, d1.value
+
+
+def device_pci_bus_id(device: int) -> str:
+    """PCI bus id ("dddd:bb:dd.f") of HIP device `device` (dkg_device_pci_bus_id)."""
+    b = ctypes.create_string_buffer(64)
+    rc = _lib.lib().dkg_device_pci_bus_id(device, b, len(b))
+    if rc != _lib.DKG_OK:
+        raise DkgError(rc, f"dkg_device_pci_bus_id({device}) failed")
+    return b.value.decode()
 
 
 def shard_rows(n: int, world_size: int) -> int:

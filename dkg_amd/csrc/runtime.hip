@@ -49,6 +49,8 @@ struct dkg_ctx {
   bool overlap = true;                  // rounds 2 and 4 as one fused pipeline (verify_rounds)
   int split = 0;                        // degree split U of the difference tables (0: cost model)
   std::vector<uint8_t> key_tabs_pk;     // member keys whose decoded points and combs sit in hy.* (encrypt)
+  uint8_t fb_base[32] = {0};            // dkg_fixed_base_batch: the caller base whose comb sits in fb_tabw
+  bool fb_valid = false;
   int binom_mode = 0;                   // binomial: 0 per-wave Horner loops (k_binom_wave) for
                                         // tables of many column groups, else one launch per step
                                         // with lane pairs (k_binom_pair) for the steps under one
@@ -1707,12 +1709,60 @@ int need_env(dkg_ctx* ctx) {
 
 }  // namespace
 
+// dkg_ctx_clock_probe: a dependent integer chain per lane between two reads of each clock; lane 0
+// of every wave writes (shader cycles, constant-clock ticks) with vector stores.
+__global__ __launch_bounds__(256) void k_clock_probe(unsigned iters, unsigned long long* out) {
+  uint32_t x = threadIdx.x * 2654435761u + blockIdx.x;
+  const unsigned long long c0 = clock64(), r0 = wall_clock64();
+  for (unsigned i = 0; i < iters; i++) x = x * 1664525u + 1013904223u;
+  asm volatile("" : "+v"(x));
+  const unsigned long long c1 = clock64(), r1 = wall_clock64();
+  const size_t w = (size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    out[2 * w] = (c1 - c0) + (x == 0xffffffffu ? 1 : 0);  // x kept live: the chain is not dead code
+    out[2 * w + 1] = r1 - r0;
+  }
+}
+
 extern "C" {
 
 int dkg_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int dkg_device_pci_bus_id(int device, char* buf, int len) {
+  if (!buf || len < 13) return DKG_E_ARG;
+  return hipDeviceGetPCIBusId(buf, len, device) == hipSuccess ? DKG_OK : DKG_E_DEVICE;
+}
+
+int dkg_ctx_clock_probe(dkg_ctx* ctx, unsigned iters, double* sclk_mhz, double* busy_ms) {
+  return guarded(ctx, [&] {
+    if (!sclk_mhz || !busy_ms || !iters) return DKG_E_ARG;
+    int cus = 0, wall_khz = 0;
+    HCK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HCK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, ctx->device));
+    if (cus <= 0 || wall_khz <= 0) return DKG_E_DEVICE;
+    const size_t waves = (size_t)cus * 16;  // 4 workgroups of 4 waves per CU: 4 waves per SIMD
+    unsigned long long* d = buf<unsigned long long>(ctx, "clock_probe", 2 * 8 * waves);
+    hipLaunchKernelGGL(k_clock_probe, dim3((unsigned)(waves / 4)), dim3(256), 0, ctx->stream, iters, d);
+    check_launch(ctx);
+    std::vector<unsigned long long> h(2 * waves);
+    d2h(ctx, h.data(), d, 2 * 8 * waves);
+    sync(ctx);
+    std::vector<double> mhz(waves), ms(waves);
+    for (size_t w = 0; w < waves; w++) {
+      const double real_us = (double)h[2 * w + 1] / wall_khz * 1e3;
+      mhz[w] = real_us > 0 ? (double)h[2 * w] / real_us : 0.0;
+      ms[w] = real_us / 1e3;
+    }
+    std::nth_element(mhz.begin(), mhz.begin() + waves / 2, mhz.end());
+    std::nth_element(ms.begin(), ms.begin() + waves / 2, ms.end());
+    *sclk_mhz = mhz[waves / 2];
+    *busy_ms = ms[waves / 2];
+    return DKG_OK;
+  });
 }
 
 int dkg_ctx_create(int device, dkg_ctx** out) {
@@ -1972,13 +2022,26 @@ int dkg_fixed_base_batch(dkg_ctx* ctx, const uint8_t base[32], size_t count, con
   return guarded(ctx, [&] {
     if (count == 0) return DKG_OK;
     const uint32_t* tab = ctx->tab_gw;
+    // the generator and the commitment key have their combs already; another base's comb (134 MB,
+    // ~1M entry threads) is built once and kept while the caller passes the same base bytes
+    if (base && memcmp(base, BASEPOINT, 32) == 0) {
+      base = nullptr;
+    } else if (base && ctx->have_h && ctx->tab_hw && memcmp(base, ctx->h, 32) == 0) {
+      tab = ctx->tab_hw;
+      base = nullptr;
+    }
     if (base) {
       uint32_t* t = buf<uint32_t>(ctx, "fb_tabw", COMBW_BYTES);
-      bool ok = false;
-      comb_for_point(ctx, base, nullptr, &ok, t);
-      if (!ok) {
-        ctx->err = "fixed_base: base point failed to decode";
-        return DKG_E_DECODE;
+      if (!ctx->fb_valid || memcmp(ctx->fb_base, base, 32) != 0) {
+        ctx->fb_valid = false;
+        bool ok = false;
+        comb_for_point(ctx, base, nullptr, &ok, t);
+        if (!ok) {
+          ctx->err = "fixed_base: base point failed to decode";
+          return DKG_E_DECODE;
+        }
+        memcpy(ctx->fb_base, base, 32);
+        ctx->fb_valid = true;
       }
       tab = t;
     }
@@ -2919,7 +2982,8 @@ int dkg_encrypt_shares(dkg_ctx* ctx, size_t D, size_t n, const uint8_t* pk, cons
     uint32_t* dr = upload_scalars(ctx, "hx_r", r, items);
     uint32_t* de1 = buf<uint32_t>(ctx, "hx_e1", 32 * items);
     uint32_t* dct = buf<uint32_t>(ctx, "hx_ct", 32 * items);
-    encrypt_device(ctx, D, n, dpk, ds, dsp, dr, de1, dct);
+    // the host keys: a repeated key set reuses its decoded points and combs (1.7 MB per key)
+    encrypt_device(ctx, D, n, dpk, ds, dsp, dr, de1, dct, nullptr, pk);
     d2h(ctx, ok.data(), buf<uint8_t>(ctx, "hy.pk_ok", n), n);
     d2h(ctx, e1, de1, 32 * items);
     d2h(ctx, ct, dct, 32 * items);

@@ -140,6 +140,15 @@ int dkg_ctx_binomial_reruns(dkg_ctx *ctx);
 int dkg_split_multipliers(size_t n, size_t L, int pieces, uint8_t *mag, int8_t *sign);
 /* Number of GPUs visible to this process (counts only; does not create a context). */
 int dkg_device_count(void);
+/* Measurement aids (bench.py; no reference counterpart).
+ * dkg_ctx_clock_probe: 4 waves per SIMD on every CU of the ctx's device each run `iters` dependent
+ * VALU iterations, reading the shader clock (s_memtime) and the constant-rate clock (s_memrealtime,
+ * hipDeviceAttributeWallClockRate) around them; *sclk_mhz = the median over waves of shader cycles
+ * per real-time microsecond (the clock the VALU ran at under full occupancy), *busy_ms = the
+ * probe's real-time span (median).  dkg_device_pci_bus_id: the device's PCI bus id
+ * ("dddd:bb:dd.f", hipDeviceGetPCIBusId) into buf[len]. */
+int dkg_ctx_clock_probe(dkg_ctx *ctx, unsigned iters, double *sclk_mhz, double *busy_ms);
+int dkg_device_pci_bus_id(int device, char *buf, int len);
 
 /* ---- Environment::init (committee.rs:72-83) ----
  * Checks threshold < (nr_members + 1) / 2 (DKG_E_ARG otherwise, where the reference asserts) and

@@ -38,7 +38,7 @@ def test_all_ranks_succeed():
     assert p.returncode == 0, p.stderr[-2000:]
 
 
-def _self_check_rank(rank, ws, port, wrong, errq, outq):
+def _self_check_rank(rank, ws, port, wrong, errq, outq, backend="gloo", shared=False):
     """One gloo rank of bench.sharded_self_check on a stand-in sharded result: the rank's dealers'
     coefficients, the honest outcome, the mpk g * sum_i a_i0 (or a wrong one) and step times."""
     import random
@@ -67,12 +67,16 @@ def _self_check_rank(rank, ws, port, wrong, errq, outq):
                               r4_error=np.zeros(n, np.uint8), phase4_error=False)
         res = SimpleNamespace(decisions=dec, mpk=mpk, ms_shard=1.0 + rank,
                               ms_steps={"exchange": 0.5 * (rank + 1), "combine": 0.2, "recon": 0.0, "finalise": 0.3})
-        be = SimpleNamespace(fixed_base_batch=O.base_mul)
-        args = SimpleNamespace(dist_backend="gloo")
+        bus = "0000:05:00.0" if shared else f"0000:{0x05 + 0x10 * rank:02x}:00.0"
+        be = SimpleNamespace(fixed_base_batch=O.base_mul, pci_bus_id=lambda: bus)
+        # backend "nccl" here only selects bench's RCCL-side checks; the tensors stay on the CPU
+        args = SimpleNamespace(dist_backend=backend)
         try:
             out = bench.sharded_self_check(args, dist, be, res, ta, d1 - d0, N, torch.device("cpu"))
         except AssertionError as e:
             out = {"assertion": str(e)}
+        except SystemExit as e:
+            out = {"exit": str(e)}
         outq.put((rank, out))
         dist.destroy_process_group()
     except BaseException as e:
@@ -80,7 +84,7 @@ def _self_check_rank(rank, ws, port, wrong, errq, outq):
         raise
 
 
-def _self_check(ws, wrong):
+def _self_check(ws, wrong, backend="gloo", shared=False):
     import socket
 
     import torch.multiprocessing as mp
@@ -90,7 +94,8 @@ def _self_check(ws, wrong):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     errq, outq = ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=_self_check_rank, args=(r, ws, port, wrong, errq, outq)) for r in range(ws)]
+    procs = [ctx.Process(target=_self_check_rank, args=(r, ws, port, wrong, errq, outq, backend, shared))
+             for r in range(ws)]
     for p in procs:
         p.start()
     outs = dict(outq.get(timeout=240) for _ in range(ws))
@@ -115,6 +120,22 @@ def test_sharded_self_check_gloo():
         assert rm["shard_device"] == {"min": 1.0, "max": 3.0}
         assert rm["exchange"] == {"min": 0.5, "max": 1.5}
         assert rm["combine"] == {"min": 0.2, "max": 0.2} and rm["recon"] == {"min": 0.0, "max": 0.0}
+        # every rank's device, all-gathered in rank order
+        assert o["rank_devices"] == ["0000:05:00.0", "0000:15:00.0", "0000:25:00.0"], o
+        assert o["distinct_devices"] == 3 and o["dist"] == {"backend": "gloo", "world_size": 3}
+
+
+def test_sharded_self_check_shared_device_gloo_rehearsal():
+    """The gloo rehearsal on one GPU: every rank reports the same device and the line says so."""
+    outs = _self_check(2, wrong=-1, shared=True)
+    for r in range(2):
+        assert outs[r]["rank_devices"] == ["0000:05:00.0"] * 2 and outs[r]["distinct_devices"] == 1
+
+
+def test_sharded_self_check_rccl_refuses_shared_devices():
+    """Under RCCL the N > 1 line must come from N distinct devices: ranks sharing one fail."""
+    outs = _self_check(2, wrong=-1, backend="nccl", shared=True)
+    assert all("share devices" in outs[r].get("exit", "") for r in range(2)), outs
 
 
 def test_sharded_self_check_catches_a_wrong_mpk():

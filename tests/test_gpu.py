@@ -54,6 +54,29 @@ def test_fixed_base_generator(be, golden):
 def test_fixed_base_other_point(be, golden):
     for e in golden("kat_group.json")["mul"]:
         assert be.fixed_base_batch(H(e["k"]), base=H(e["P"])).hex() == e["kP"]
+    # the caller base's comb is cached by its bytes: repeats, alternations, and the generator and the
+    # commitment key passed as explicit bases (their own combs) give the same products
+    muls = golden("kat_group.json")["mul"]
+    for e in muls + muls[::-1] + muls:
+        assert be.fixed_base_batch(H(e["k"]), base=H(e["P"])).hex() == e["kP"]
+    g = golden("kat_group.json")
+    gen = bytes.fromhex("e2f2ae0a6abc4e71a884a961c500515f58e30b6aa582dd8db6a65945e08d2d76")
+    e = g["base_mul"][0]
+    assert be.fixed_base_batch(H(e["k"]), base=gen).hex() == e["P"]
+    h = be.env_init(4, 10, CK)
+    k = (123456789).to_bytes(32, "little")
+    assert be.fixed_base_batch(k, base=h) == bytes(O.msm(k, h))
+    with pytest.raises(dkg_amd.DkgError):
+        be.fixed_base_batch(k, base=b"\xff" * 32)  # does not decode
+    assert be.fixed_base_batch(H(muls[0]["k"]), base=H(muls[0]["P"])).hex() == muls[0]["kP"]
+
+
+def test_clock_probe_and_device_id(be):
+    """bench.py's measurement aids: the shader clock under full occupancy and the PCI bus id."""
+    c = be.clock_probe()
+    assert 500 < c["sclk_mhz"] < 4000 and c["busy_ms"] > 0.05, c
+    bus = be.pci_bus_id()
+    assert len(bus.split(":")) == 3 and "." in bus, bus
 
 
 def test_points_valid(be, golden):

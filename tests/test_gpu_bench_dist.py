@@ -36,6 +36,11 @@ def test_bench_multi_rank_gloo_on_one_gpu(gpus):
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert out["value"] == pytest.approx(out["config"]["pairs_per_step"] / (out["ms_per_step"] / 1e3), rel=1e-6)
     assert out["mpk_check"].startswith("mpk == g")
+    # the rehearsal's ranks share GPU 0: one device, named by its PCI bus id on every rank
+    assert len(out["rank_devices"]) == gpus and len(set(out["rank_devices"])) == 1, out["rank_devices"]
+    assert out["distinct_devices"] == 1 and out["dist"] == {"backend": "gloo", "world_size": gpus}
+    clk = out["sclk_mhz"]
+    assert 500 < clk["before"] < 4000 and 500 < clk["after"] < 4000, clk
     rm = out["rank_ms"]
     assert set(rm) == {"shard_device", "exchange", "combine", "recon", "finalise"}
     for k, v in rm.items():

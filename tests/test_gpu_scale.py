@@ -358,27 +358,37 @@ def test_stepping_redo_at_scale(be, n, t, split):
     slots (U=4), per-piece tables (U=3: 171-position pieces) and 512-lane blocks chained through
     boundary streams (n=1100 unsplit: 550 positions): an E row made the identity (committee.rs:1127)
     makes its dedicated additions exceptional; the marked workgroups are redone by the complete
-    formula, and every output equals the complete formula's run."""
+    formula, and every output equals the complete formula's run.  The same rows trip the per-step
+    binomial's dedicated additions (e_{m-1} + e_m of two identities has Z = 0): its guard word makes
+    the driver rerun the whole verification with the complete formula (binomial_reruns() == 1) -- on
+    the headline schedule at n=1024 (two chunk streams, lane-pair early steps, column-sum copy) --
+    and a committee without them reruns nothing."""
     be.env_init(t, n, CK)
     a, b = dkg_amd.dealer_coefficients(bytes([split]) * 32, 3, 0, n, t)
     E, A, s, sp = (bytearray(x) for x in be.share_gen(a, b, n, n, t))
     N = t + 1
-    for d in (3, n - 2):  # dealers in the first and the last stepping workgroups
-        E[32 * d * N:32 * (d + 1) * N] = bytes(32 * N)
-    _bump(s, 32 * (5 * n + 9))  # and an ordinary fault beside them
+    _bump(s, 32 * (5 * n + 9))  # an ordinary fault
     out = []
     try:
         be.set_split(split)
+        # the honest control: no identity rows, no binomial rerun (and no stepping redo)
+        r0 = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
+        assert be.binomial_reruns() == 0 and be.stepping_redos() == 0
+        assert r0.dec2[5 * n:6 * n].count(REJECT) == 1
+        for d in (3, n - 2):  # dealers in the first and the last stepping workgroups
+            E[32 * d * N:32 * (d + 1) * N] = bytes(32 * N)
         for formula in (0, 1):
             be.set_stepping_formula(formula)
             r = be.ceremony_verify(bytes(E), bytes(A), bytes(s), bytes(sp), n, t)
             assert be.last_split() == split
-            out.append((r.dec2, r.dec4, r.qualified, r.reconstruct, r.mpk, r.final_share, be.stepping_redos()))
+            out.append((r.dec2, r.dec4, r.qualified, r.reconstruct, r.mpk, r.final_share, be.stepping_redos(),
+                        be.binomial_reruns()))
     finally:
         be.set_stepping_formula(0)
         be.set_split(0)
     assert out[0][:6] == out[1][:6]
     assert out[0][6] > 0 and out[1][6] == 0
+    assert out[0][7] == 1 and out[1][7] == 0  # the dedicated binomial's rerun guard fired (formula 0 only)
     dec2 = out[0][0]
     for d in (3, n - 2):
         row = dec2[d * n:(d + 1) * n]
@@ -518,9 +528,22 @@ def test_shard_stepping_redo_n1024(be):
     _, tE, tA, ts, tsp = _device_committee(be, n, t, bytes([59]) * 32, 3)
     d0, d1 = dkg_amd.shard_range(n, ws, 0)
     D = d1 - d0
+    outs = []
+
+    def rows():
+        o2 = torch.zeros(D * n, dtype=torch.uint8, device=ts.device)
+        o4 = torch.zeros_like(o2)
+        oA = torch.zeros(D * 32, dtype=torch.uint8, device=ts.device)
+        op = torch.zeros(n * 32, dtype=torch.uint8, device=ts.device)
+        be.ceremony_shard_verify_device(n, t, d0, d1, tE.data_ptr(), tA.data_ptr(), ts.data_ptr(), tsp.data_ptr(),
+                                        o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
+        return o2, o4
+
+    h2, h4 = rows()  # the honest rank: the binomial's guard word stays clear
+    assert be.binomial_reruns() == 0 and be.stepping_redos() == 0
+    assert h2.view(D, n)[0].eq(ACCEPT).sum().item() == n - 1
     for d, buf in ((7, tE), (9, tA)):  # identity rows (committee.rs:1127 style)
         buf[32 * N * d:32 * N * (d + 1)] = 0
-    outs = []
     try:
         for formula in (0, 1):
             be.set_stepping_formula(formula)
@@ -532,11 +555,14 @@ def test_shard_stepping_redo_n1024(be):
                                             o2.data_ptr(), o4.data_ptr(), oA.data_ptr(), op.data_ptr())
             assert be.last_split() == 4, be.last_split()
             outs.append((bytes(o2.cpu().numpy()), bytes(o4.cpu().numpy()), bytes(oA.cpu().numpy()),
-                         bytes(op.cpu().numpy()), be.stepping_redos()))
+                         bytes(op.cpu().numpy()), be.stepping_redos(), be.binomial_reruns()))
     finally:
         be.set_stepping_formula(0)
     assert outs[0][:4] == outs[1][:4]
     assert outs[0][4] > 0 and outs[1][4] == 0  # the dedicated pass marked the identity rows' workgroups
+    # the shard's per-step binomial (dedicated additions) met Z = 0 and the call reran with the
+    # complete formula; its rows are the complete-formula run's (above)
+    assert outs[0][5] == 1 and outs[1][5] == 0
     d2, d4 = outs[0][0], outs[0][1]
     row = lambda m, i, v: bytes(SELF if j == i else v for j in range(n)) == m[i * n:(i + 1) * n]  # noqa: E731
     assert row(d2, 7, REJECT) and row(d4, 9, REJECT)  # identity rows: every other receiver rejects
