@@ -221,7 +221,7 @@ void commit(size_t count, const uint32_t* a, const uint32_t* b, const uint32_t* 
 // coefficient k), lanes = dealers, so the E and A columns of a group (columns 128 g + lane and
 // 128 g + 64 + lane, piece k / L at position k % L) are written coalesced; no extended-form E/A
 // arrays and no placement pass.  The lanes of k = 0 also write A_i0 (A0 [40][A0stride], finalise).
-// 3 waves per SIMD: at 128 VGPRs it spills 260 B per lane (config 5 -2 ms, profiles/r05_b5_ab.txt).
+// 3 waves per SIMD: the comb's mixed additions need ~140 VGPRs (at 128 it spills 52 B per lane).
 __global__ __launch_bounds__(64, 3) void k_commit_pm(size_t D, size_t N, const uint32_t* __restrict__ a,
                                                    const uint32_t* __restrict__ b,
                                                    const uint32_t* __restrict__ tab_g,
@@ -243,6 +243,10 @@ __global__ __launch_bounds__(64, 3) void k_commit_pm(size_t D, size_t N, const u
   if (k == 0) pt_store(A0, A0stride, i, acc);
   sc_load(x, b + 8 * (i * N + k));
   combw_mul_add(acc, x, tab_h);                     // coeff_comm = h * b + apub   (committee.rs:156)
+  // an opaque copy of the base again: otherwise the 40 store addresses of the A column (the same
+  // words 64 columns on) stay live across h's comb and spill (168 VGPRs + 92 B of scratch per lane;
+  // with it 140 VGPRs and none)
+  asm volatile("" : "+s"(o));
   pt_store(o, L * W, threadIdx.x, acc);             // the E column (round 2)
 }
 
