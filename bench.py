@@ -424,6 +424,25 @@ def short_combine_valu(mults, VALU=SLOTS, affine=True):
     return total
 
 
+def binom_item_valu(m, VALU=SLOTS, ded=True):
+    """One binomial item e_m <- m (e_{m-1} + e_m) (kernels.hip k_binom_step / k_binom_wave): the first
+    addition, then the NAF chain of m on the sum's cached form.  ded (the default with the dedicated
+    stepping additions): the product-free cached forms, dedicated additions and a zero test of every
+    addition's Z (fe_tight_zero); else the complete formula (cached form with the product by 2d)."""
+    cached = VALU["ge_to_cached_ded"] if ded else VALU["ge_to_cached"]
+    zt = VALU["fe_tight_zero"] if ded else 0
+    c = cached + (VALU["ge_add_ded"] if ded else VALU["ge_add"]) + zt  # e_{m-1} + e_m
+    ds = _naf(m)
+    if len(ds) > 1:
+        c += cached
+        for i in range(len(ds) - 2, -1, -1):
+            nz = ds[i] != 0
+            c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
+            if nz:  # a doubling follows unless i = 0: no T (the dedicated signed form costs the same)
+                c += add_cost(VALU, "ge_add_signed", i == 0) + zt
+    return c
+
+
 def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine=True, ded=True):
     """Closed-form VALU work (issue slots, or instructions with VALU=INSTR) of one verification round
     over all n dealers as implemented (DESIGN.md "Work per unit"): binomial-basis Horner on U pieces
@@ -431,18 +450,7 @@ def algorithmic_valu(n, t, rnd=2, U=1, VALU=SLOTS, plen=None, mults=None, affine
     y_j = j^L (U > 1; with `mults`, the short multipliers of api.split_multipliers), fixed-base
     check (with `mults`, of b_j s: one more Montgomery product per scalar)."""
     pieces, L_ = split_pieces(t, U, plen)
-    cost_m = {}
-    for m in range(1, L_):
-        ds = _naf(m)
-        c = VALU["ge_to_cached"] + VALU["ge_add"]          # e_{m-1} + e_m
-        if len(ds) > 1:
-            c += VALU["ge_to_cached"]
-            for i in range(len(ds) - 2, -1, -1):
-                nz = ds[i] != 0
-                c += VALU["ge_dbl_t"] if (nz or i == 0) else VALU["ge_dbl_not"]
-                if nz:  # a doubling follows unless i = 0: no T
-                    c += add_cost(VALU, "ge_add_signed", i == 0)
-        cost_m[m] = c
+    cost_m = {m: binom_item_valu(m, VALU, ded) for m in range(1, L_)}
     # position m of a piece of length Lp is live for Lp-m steps (a short last piece starts late)
     binom = sum(sum(cost_m[m] * (Lp - m) for m in range(1, Lp)) for Lp in pieces)
     # stepping: every lane converts each step; position p adds at step j (0..n-1) only while

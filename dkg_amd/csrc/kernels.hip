@@ -679,7 +679,12 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
 // a wave whose real columns met an addition with Z = 0 marks flags[its group], and the same grid
 // relaunched with DED = false and the flags redoes only the marked groups with the complete formula,
 // from the coefficients (every position is rebuilt from C, so the first pass's table is irrelevant).
-// Identity padding columns (past `dreal` dealers, `gw` columns per dealer group) never mark.
+// Identity padding columns (past `dreal` dealers, `gw` columns per dealer group) never mark, and
+// they are never redone: after a dedicated pass their table entries (and everything the stepping
+// and recombination derive from them) are UNDEFINED (identity + identity has Z = 0).  That is safe
+// because nothing reads a padding column's values: the checks, k_affine_pieces' outputs that reach
+// a decision, the round outcomes and every sum over dealers index real dealers only (the checks'
+// grids run over ndealers, not npad).  A new kernel that reduces across columns must keep to that.
 template <bool CARRY, bool PF, bool DED>
 __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) void k_binom_wave(int L, size_t npad,
                                                                            const uint32_t* __restrict__ C,
@@ -1690,9 +1695,10 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
 // and its A row the column 64 after it.  g*s_ij is computed ONCE: compared with R_A (round 4,
 // committee.rs:537-541), then h*s'_ij is added and the sum compared with R_E (round 2,
 // committee.rs:292-305) -- the same group elements the two rounds compute separately.
-// PASS 0: both in one launch (the two radix-2^11 combs, 6.3 MB, share each XCD's 4-MB L2).  PASS 1 /
-// 2: the same work as two launches that each read ONE comb (3.1 MB): pass 1 computes g*s, decides
-// round 4 and parks g*s in acc[p] (160 B), pass 2 adds h*s' to it and decides round 2.
+// PASS 0: both in one launch (the default).  PASS 1 / 2: the same work as two launches that each
+// read ONE comb: pass 1 computes g*s, decides round 4 and parks g*s in acc[p] (160 B), pass 2 adds
+// h*s' to it and decides round 2 -- a split made for the radix-2^11 combs (3.1 MB per base, one
+// XCD's 4-MB L2); the radix-2^17 combs are 134 MB per base (HBM / Infinity Cache) either way.
 template <int PASS>
 __global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
                                                     uint32_t nmod, const uint32_t* __restrict__ s,

@@ -84,7 +84,9 @@ def test_closed_form_work_per_pair():
         assert 1.6 < w[k] / wi[k] < 2.0
     # the dedicated stepping additions (default) drop the product of the cached form
     wd = bench.algorithmic_valu(n, t, 2, 2)
-    assert 0.88 < wd["stepping"] / w["stepping"] < 0.95 and wd["binomial"] == w["binomial"]
+    assert 0.88 < wd["stepping"] / w["stepping"] < 0.95
+    # and the dedicated binomial items: two product-free cached forms, a zero test per addition
+    assert 0.95 < wd["binomial"] / w["binomial"] < 0.98, wd["binomial"] / w["binomial"]
     # the fused schedule carries both rounds' tables through binomial, stepping and recombination
     f = bench.fused_valu(n, t, 2, ded=False)
     assert f["binomial"] == pytest.approx(2 * w["binomial"])

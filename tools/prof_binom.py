@@ -15,19 +15,8 @@ def main(d, t=128, n=8192):
     rows = [r for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv")))
             if "binom" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    V = bench.SLOTS
-    cost = {}
-    for m in range(1, t):
-        ds = bench._naf(m)
-        cc = V["ge_to_cached"] + V["ge_add"]
-        if len(ds) > 1:
-            cc += V["ge_to_cached"]
-            for i in range(len(ds) - 2, -1, -1):
-                nz = ds[i] != 0
-                cc += V["ge_dbl_t"] if (nz or i == 0) else V["ge_dbl_not"]
-                if nz:
-                    cc += bench.add_cost(V, "ge_add_signed", i == 0)
-        cost[m] = cc
+    ded = os.environ.get("DKG_PROF_BINOM_COMPLETE") is None  # the dedicated items (default schedule)
+    cost = {m: bench.binom_item_valu(m, bench.SLOTS, ded) for m in range(1, t)}
     seg = rows[:t - 1]
     tot = totw = 0
     for i, r in enumerate(seg):

@@ -5,6 +5,7 @@
 //   noload   the two points come from registers (a hash of the lane), no global loads
 //   nostore  loads and chain, the result is folded into one word per lane instead of stored
 //   chain    only the m-chain on a register point: no loads, no first addition, no store
+//   pair2    two column groups per lane (the same m: identical chains, ILP 2), 2 waves per SIMD
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I dkg_amd/csrc tools/ubench/binom.hip -o tools/ubench/binom
 // Output: one line per (variant, r): microseconds per launch (tools/ubench/binom.py prices it).
 #include "../../dkg_amd/csrc/kernels.hip"
@@ -65,6 +66,79 @@ __global__ __launch_bounds__(64, 4) void k_binom_var(int r, size_t npad, size_t 
   }
 }
 
+// pair2: two column groups per lane (ILP 2 over identical chains: the same m), 2 waves per SIMD
+__device__ __forceinline__ void mul_small_ded_lds2(ge_p3 (&y)[2], uint32_t m, uint32_t* q0, uint32_t* q1,
+                                                   bool& bad) {
+  uint32_t pos = 0, neg = 0;
+  int len = 0;
+  for (uint32_t v = m; v; v >>= 1, len++) {
+    if (v & 1u) {
+      if ((v & 3u) == 1u) {
+        pos |= 1u << len;
+        v -= 1;
+      } else {
+        neg |= 1u << len;
+        v += 1;
+      }
+    }
+  }
+  if (len <= 1) return;
+  {
+    ge_cached xc;
+    ge_to_cached_ded(xc, y[0]);
+    lds_put_cached(q0, xc);
+    ge_to_cached_ded(xc, y[1]);
+    lds_put_cached(q1, xc);
+  }
+#pragma unroll 1
+  for (int i = len - 2; i >= 0; i--) {
+    const uint32_t bit = 1u << i;
+    const bool nz = ((pos | neg) & bit) != 0;
+    ge_dbl_lean(y[0], y[0], nz || i == 0);
+    ge_dbl_lean(y[1], y[1], nz || i == 0);
+    if (nz) {
+      ge_add_ded_lds_s(y[0], y[0], q0, (neg & bit) != 0, 64, i == 0);
+      ge_add_ded_lds_s(y[1], y[1], q1, (neg & bit) != 0, 64, i == 0);
+      bad |= fe_tight_zero(y[0].Z) | fe_tight_zero(y[1].Z);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64, 2) void k_binom_pair2(int r, size_t npad, size_t N, const uint32_t* __restrict__ ein,
+                                                       uint32_t* __restrict__ eout, uint32_t* __restrict__ flags) {
+  __shared__ uint32_t qs[2 * PT_WORDS * 64];
+  uint32_t* q0 = qs + threadIdx.x;
+  uint32_t* q1 = qs + PT_WORDS * 64 + threadIdx.x;
+  const size_t d0 = (size_t)blockIdx.x * 128 + threadIdx.x, d1 = d0 + 64;
+  const size_t S = N * npad;
+  const int m = r - (int)blockIdx.y;
+  if (m == 0) return;
+  bool bad = false;
+  ge_p3 x[2];
+  {
+    ge_p3 cur;
+    ge_cached cc;
+    pt_load(cur, ein, S, (size_t)m * npad + d0);
+    ge_to_cached_ded(cc, cur);
+    lds_put_cached(q0, cc);
+    pt_load(cur, ein, S, (size_t)m * npad + d1);
+    ge_to_cached_ded(cc, cur);
+    lds_put_cached(q1, cc);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  pt_load(x[0], ein, S, (size_t)(m - 1) * npad + d0);
+  pt_load(x[1], ein, S, (size_t)(m - 1) * npad + d1);
+  ge_add_ded_lds(x[0], x[0], q0);
+  ge_add_ded_lds(x[1], x[1], q1);
+  bad |= fe_tight_zero(x[0].Z) | fe_tight_zero(x[1].Z);
+  mul_small_ded_lds2(x, (uint32_t)m, q0, q1, bad);
+  if (__ballot(bad) != 0 && threadIdx.x == 0) flags[0] = 1u;
+  pt_store(eout, S, (size_t)m * npad + d0, x[0]);
+  uint32_t* eo = eout;
+  asm volatile("" : "+s"(eo));
+  pt_store(eo, S, (size_t)m * npad + d1, x[1]);
+}
+
 }  // namespace dkgk
 
 int main(int argc, char** argv) {
@@ -87,10 +161,10 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   const int rs[] = {16, 32, 64, 96, 127};
-  const char* names[] = {"full", "noload", "nostore", "chain"};
-  for (int var = 0; var < 4; var++) {
+  const char* names[] = {"full", "noload", "nostore", "chain", "pair2"};
+  for (int var = 0; var < 5; var++) {
     for (int r : rs) {
-      const dim3 grid((unsigned)(npad / 64), (unsigned)(r + 1));
+      const dim3 grid((unsigned)(npad / (var == 4 ? 128 : 64)), (unsigned)(r + 1));
       auto launch = [&] {
         switch (var) {
           case 0:
@@ -99,7 +173,8 @@ int main(int argc, char** argv) {
             break;
           case 1: hipLaunchKernelGGL(dkgk::k_binom_var<1>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
           case 2: hipLaunchKernelGGL(dkgk::k_binom_var<2>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
-          default: hipLaunchKernelGGL(dkgk::k_binom_var<3>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
+          case 3: hipLaunchKernelGGL(dkgk::k_binom_var<3>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
+          default: hipLaunchKernelGGL(dkgk::k_binom_pair2, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
         }
       };
       launch();
