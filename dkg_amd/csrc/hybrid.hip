@@ -22,7 +22,12 @@ namespace dkgk {
 // grid (ceil(2D / 1024), n): recipient q = blockIdx.y.  The generator's comb (radix 2^DKG_COMBW_BITS)
 // and the recipient's own comb (radix 2^DKG_KEY_COMB_BITS, 26 windows at 2^10: 1.7 MB per key, every
 // dealer of the block reads the same table through L2; the radix-16 LDS comb it replaces took 64).
-__global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
+// 256-thread workgroups at 3 waves per SIMD: the two combs' mixed additions need ~138 VGPRs (the
+// 1024-thread blocks capped it at 128 and spilled 32 B per lane)
+#ifndef DKG_ENC_BS
+#define DKG_ENC_BS 256
+#endif
+__global__ __launch_bounds__(DKG_ENC_BS, DKG_ENC_BS == 256 ? 3 : 1) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
                                                   const uint32_t* __restrict__ tab_gw,
                                                   const uint32_t* __restrict__ tabs_pk, uint32_t* __restrict__ R_ext,
                                                   uint32_t* __restrict__ K_ext) {
@@ -47,7 +52,8 @@ __global__ __launch_bounds__(1024) void k_enc_mul(size_t D, size_t n, const uint
 void enc_mul(size_t D, size_t n, const uint32_t* r, const uint32_t* tab_gw, const uint32_t* tabs_pk, uint32_t* R_ext,
              uint32_t* K_ext, hipStream_t stream) {
   if (!D || !n) return;
-  hipLaunchKernelGGL(k_enc_mul, dim3((unsigned)((2 * D + 1023) / 1024), (unsigned)n), dim3(1024), 0, stream, D, n,
+  hipLaunchKernelGGL(k_enc_mul, dim3((unsigned)((2 * D + DKG_ENC_BS - 1) / DKG_ENC_BS), (unsigned)n), dim3(DKG_ENC_BS),
+                     0, stream, D, n,
                      r, tab_gw, tabs_pk, R_ext, K_ext);
 }
 
