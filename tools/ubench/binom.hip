@@ -6,6 +6,9 @@
 //   nostore  loads and chain, the result is folded into one word per lane instead of stored
 //   chain    only the m-chain on a register point: no loads, no first addition, no store
 //   pair2    two column groups per lane (the same m: identical chains, ILP 2), 2 waves per SIMD
+//   tiled    the table tiled [N][npad/64][40][64]: a wave's point is one contiguous 10-KB block
+//   tiled_nt tiled, nontemporal stores;  full_nt  the library layout, nontemporal stores
+// (argv: reps, first variant)
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I dkg_amd/csrc tools/ubench/binom.hip -o tools/ubench/binom
 // Output: one line per (variant, r): microseconds per launch (tools/ubench/binom.py prices it).
 #include "../../dkg_amd/csrc/kernels.hip"
@@ -139,6 +142,59 @@ __global__ __launch_bounds__(64, 2) void k_binom_pair2(int r, size_t npad, size_
   pt_store(eo, S, (size_t)m * npad + d1, x[1]);
 }
 
+// tiled: the same item on a tiled position-major table [N][npad/64][40][64] -- a wave's point is one
+// contiguous 10-KB block instead of 40 rows 4 MB apart (VAR 5; VAR 6 = tiled + nontemporal stores;
+// VAR 7 = the library layout with nontemporal stores)
+DKG_DEV void pt_load_tiled(ge_p3& p, const uint32_t* __restrict__ blk) {
+#pragma unroll
+  for (int w = 0; w < PT_WORDS; w++) pt_word(p, w) = blk[w * 64 + threadIdx.x];
+}
+template <bool NT>
+DKG_DEV void pt_store_tiled(uint32_t* __restrict__ blk, const ge_p3& p) {
+#pragma unroll
+  for (int w = 0; w < PT_WORDS; w++) {
+    if (NT) __builtin_nontemporal_store(pt_word(p, w), blk + w * 64 + threadIdx.x);
+    else blk[w * 64 + threadIdx.x] = pt_word(p, w);
+  }
+}
+template <int VAR>
+__global__ __launch_bounds__(64, 4) void k_binom_tiled(int r, size_t npad, size_t N, const uint32_t* __restrict__ ein,
+                                                       uint32_t* __restrict__ eout, uint32_t* __restrict__ flags) {
+  __shared__ uint32_t qs[PT_WORDS * 64];
+  uint32_t* q = qs + threadIdx.x;
+  const size_t g = blockIdx.x, G = npad / 64;
+  const size_t d = g * 64 + threadIdx.x;
+  const size_t S = N * npad;
+  const int m = r - (int)blockIdx.y;
+  if (m == 0) return;
+  bool bad = false;
+  {
+    ge_p3 cur;
+    if (VAR == 7) pt_load(cur, ein, S, (size_t)m * npad + d);
+    else pt_load_tiled(cur, ein + ((size_t)m * G + g) * (PT_WORDS * 64));
+    ge_cached cc;
+    ge_to_cached_ded(cc, cur);
+    lds_put_cached(q, cc);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  ge_p3 x;
+  if (VAR == 7) pt_load(x, ein, S, (size_t)(m - 1) * npad + d);
+  else pt_load_tiled(x, ein + ((size_t)(m - 1) * G + g) * (PT_WORDS * 64));
+  ge_add_ded_lds(x, x, q);
+  bad |= fe_tight_zero(x.Z);
+  mul_small_ded_lds(x, (uint32_t)m, q, bad);
+  if (__ballot(bad) != 0 && threadIdx.x == 0) flags[0] = 1u;
+  uint32_t* eo = eout;
+  asm volatile("" : "+s"(eo));
+  if (VAR == 7) {
+#pragma unroll
+    for (int w = 0; w < PT_WORDS; w++)
+      __builtin_nontemporal_store(pt_word(x, w), eo + (size_t)w * S + (size_t)m * npad + d);
+  } else {
+    pt_store_tiled<VAR == 6>(eo + ((size_t)m * G + g) * (PT_WORDS * 64), x);
+  }
+}
+
 }  // namespace dkgk
 
 int main(int argc, char** argv) {
@@ -161,8 +217,9 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   const int rs[] = {16, 32, 64, 96, 127};
-  const char* names[] = {"full", "noload", "nostore", "chain", "pair2"};
-  for (int var = 0; var < 5; var++) {
+  const char* names[] = {"full", "noload", "nostore", "chain", "pair2", "tiled", "tiled_nt", "full_nt"};
+  const int first = argc > 2 ? atoi(argv[2]) : 0;
+  for (int var = first; var < 8; var++) {
     for (int r : rs) {
       const dim3 grid((unsigned)(npad / (var == 4 ? 128 : 64)), (unsigned)(r + 1));
       auto launch = [&] {
@@ -174,7 +231,10 @@ int main(int argc, char** argv) {
           case 1: hipLaunchKernelGGL(dkgk::k_binom_var<1>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
           case 2: hipLaunchKernelGGL(dkgk::k_binom_var<2>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
           case 3: hipLaunchKernelGGL(dkgk::k_binom_var<3>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
-          default: hipLaunchKernelGGL(dkgk::k_binom_pair2, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
+          case 4: hipLaunchKernelGGL(dkgk::k_binom_pair2, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
+          case 5: hipLaunchKernelGGL(dkgk::k_binom_tiled<5>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
+          case 6: hipLaunchKernelGGL(dkgk::k_binom_tiled<6>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
+          default: hipLaunchKernelGGL(dkgk::k_binom_tiled<7>, grid, dim3(64), 0, nullptr, r, npad, N, ein, eout, flags); break;
         }
       };
       launch();
