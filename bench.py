@@ -227,7 +227,7 @@ def pmc_traffic(kernel, n, t, U, plen=None, batch=1, mode="plain"):
             key["split_len"] = split_pieces(t, U)[1]
         if key == want and kernel in doc.get("kernels", {}):
             k = doc["kernels"][kernel]
-            return k["bytes_per_launch"], doc["source"], k.get("valu_int64_share")
+            return k["bytes_per_launch"], doc["source"], k.get("valu_int64_share"), k.get("effective_clock_mhz")
     return None
 
 
@@ -252,6 +252,14 @@ def add_traffic(line, dom, ms_pass, n, t, U, plen, per_wave=False, batch=1, mode
             # is half rate (2 slots), the rest counted as full rate
             rl["valu_int64_share"] = pmc[2]
             rl["frac_counter_lower_bound"] = rl["instr_frac"] * (1 + pmc[2])
+    # the clock the chip held during each kernel in the profiled pass (GRBM_GUI_ACTIVE / 8 / time,
+    # MI355X_MICROARCH.md "DVFS give-back"): integer-VALU load is power-limited, so the 2.4-GHz peak
+    # overstates what a kernel could issue; frac_at_profile_clock = frac x 2400 / that clock
+    for name, k in [(dom, rl)] + list(rl.get("all_kernels", {}).items()):
+        got = pmc_traffic(name, n, t, U, plen, batch, mode)
+        if got is not None and got[3]:
+            k["effective_clock_mhz_profile"] = round(got[3], 1)
+            k["frac_at_profile_clock"] = k["frac"] * 2400.0 / got[3]
 
 
 def spawn_ranks(args, poll_s=0.2):

@@ -510,6 +510,36 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
   for (int w = 0; w < PT_WORDS; w++) e[w * S + d] = C[w * S + kpos * npad + d];
 }
 
+// The per-step binomial's table stores (k_binom_step, k_binom_pair): nontemporal by default
+// (DKG_BINOM_NT=0: plain stores, the round-5 kernels).  Every launch rereads the previous step's rows
+// (each position by two items); plain stores of the new rows displaced them from L2: one step of the
+// headline's tables 324 -> 268 us (tools/ubench/binom, profiles/r06_binom_levers_ab.txt).
+#ifndef DKG_BINOM_NT
+#define DKG_BINOM_NT 1
+#endif
+// A/B knobs of the same kind for the other large table writers (0: plain stores): the stepping's
+// evaluations R and dense Z copy, the normalisation's affine addends, the per-wave binomial
+#ifndef DKG_STEP_NT
+#define DKG_STEP_NT 0
+#endif
+#ifndef DKG_AFF_NT
+#define DKG_AFF_NT 0
+#endif
+#ifndef DKG_BINOM_WAVE_NT
+#define DKG_BINOM_WAVE_NT 0
+#endif
+#ifndef DKG_COMB_NT  // the recombination's b_j P(j) (read by the checks)
+#define DKG_COMB_NT 0
+#endif
+DKG_DEV void binom_st(uint32_t* p, uint32_t v) {
+  if (DKG_BINOM_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+DKG_DEV void binom_pt_store(uint32_t* __restrict__ base, size_t stride, size_t e, const ge_p3& p) {
+  if (DKG_BINOM_NT) pt_store_nt(base, stride, e, p);
+  else pt_store(base, stride, e, p);
+}
+
 // One Horner step in the binomial basis: e'_0 = C_k, e'_m = m (e_{m-1} + e_m), m = 1..r.
 // Lanes = dealers (so m is uniform per wave: no divergence in the m-chain); one wave per
 // (position, 64 dealers); position 0 just copies the next coefficient C_k.  Grid (dealer groups x
@@ -535,7 +565,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
   const int m = r - (int)blockIdx.y;
   if (m == 0) {
 #pragma unroll 8
-    for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
+    for (int w = 0; w < PT_WORDS; w++) binom_st(eout + w * S + d, C[w * S + (size_t)k * npad + d]);
     return;
   }
   // A short last piece (last_off = L - its length) holds the identity in its top last_off
@@ -574,7 +604,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
     ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
     mul_small_lds(x, (uint32_t)m, q);        // * m
   }
-  pt_store(eout, S, (size_t)m * npad + d, x);
+  binom_pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
 // k_binom_step with lane pairs (split.h): one wave per (position, 32 columns), each column's point
@@ -595,7 +625,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_pair(int r, int k, size_t npad,
   if (m == 0) {
     if (lane & 1) return;
 #pragma unroll 8
-    for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
+    for (int w = 0; w < PT_WORDS; w++) binom_st(eout + w * S + d, C[w * S + (size_t)k * npad + d]);
     return;
   }
   const int re = r - (piece == last_piece ? last_off : 0);
@@ -616,7 +646,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_pair(int r, int k, size_t npad,
   ge_add_pair(x, x, c, false);             // e_{m-1} + e_m
   mul_small_pair(x, (uint32_t)m, c);       // * m
   if (lane & 1) return;
-  pt_store(eout, S, (size_t)m * npad + d, x);
+  binom_pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
 void binom_step_pair(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in,
@@ -766,7 +796,8 @@ __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) vo
       if (r + 1 < L || !eT) {
         uint32_t* eo = eb;
         asm volatile("" : "+s"(eo));
-        pt_store(eo, S, (size_t)m * npad + lane, x);
+        if (DKG_BINOM_WAVE_NT) pt_store_nt(eo, S, (size_t)m * npad + lane, x);
+        else pt_store(eo, S, (size_t)m * npad + lane, x);
       } else {  // the last step writes the stepping's column-major table (no to_column_major pass):
         // the L positions of a column's word w are one line, filled by this lane within the step
         uint32_t* eo = eT + col0 * L;
@@ -981,12 +1012,16 @@ __global__ __launch_bounds__(MAXBS) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
     __syncthreads();  // every column read before the next step overwrites it
     if (live && q == 0 && R) {
-      pt_store_aos(R, d * nrecv + j, D);
+      pt_store_aos<DKG_STEP_NT != 0>(R, d * nrecv + j, D);
       // Z once more in a dense 40-B record: the affine normalisation reads only Z in its first pass
       if (Rz) {
         uint2* z2 = reinterpret_cast<uint2*>(Rz + (d * nrecv + j) * 10);
 #pragma unroll
-        for (int k = 0; k < 5; k++) z2[k] = make_uint2(D.Z.v[2 * k], D.Z.v[2 * k + 1]);
+        for (int k = 0; k < 5; k++) {
+          if (DKG_STEP_NT) __builtin_nontemporal_store(D.Z.v[2 * k], reinterpret_cast<uint32_t*>(z2 + k));
+          if (DKG_STEP_NT) __builtin_nontemporal_store(D.Z.v[2 * k + 1], reinterpret_cast<uint32_t*>(z2 + k) + 1);
+          if (!DKG_STEP_NT) z2[k] = make_uint2(D.Z.v[2 * k], D.Z.v[2 * k + 1]);
+        }
       }
     }
   }
@@ -1314,7 +1349,7 @@ __global__ __launch_bounds__(64, SLOTS == 1 ? 4 : 2) void k_combine(size_t width
       ge_add_lds(acc, acc, slot_y, false);
     }
   }
-  if (live) pt_store_aos(R, c * nrecv + j, acc);
+  if (live) pt_store_aos<DKG_COMB_NT != 0>(R, c * nrecv + j, acc);
 }
 
 // Recombination with short multipliers (lattice.cpp, U = K <= 4): b_j P(j) = sum_u v_ju Q_u(j) with
@@ -1387,7 +1422,7 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_short(size_t wid
     if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
     short_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
-  if (live) pt_store_aos(R, c * nrecv + j, acc);
+  if (live) pt_store_aos<DKG_COMB_NT != 0>(R, c * nrecv + j, acc);
 }
 
 void combine_short(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* digits,
@@ -1417,15 +1452,15 @@ constexpr int AFF_RUN = 32;     // points per lane
 constexpr int AFF_BLK = 4;      // points per block
 
 DKG_DEV void st_fe3(uint32_t* slot, const fe& a, const fe& b, const fe& c) {
-  uint4* s = reinterpret_cast<uint4*>(slot);
-  s[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
-  s[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
-  s[2] = make_uint4(a.v[8], a.v[9], b.v[0], b.v[1]);
-  s[3] = make_uint4(b.v[2], b.v[3], b.v[4], b.v[5]);
-  s[4] = make_uint4(b.v[6], b.v[7], b.v[8], b.v[9]);
-  s[5] = make_uint4(c.v[0], c.v[1], c.v[2], c.v[3]);
-  s[6] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
-  s[7] = make_uint4(c.v[8], c.v[9], 0u, 0u);
+  constexpr bool NT = DKG_AFF_NT != 0;
+  st16<NT>(slot, a.v[0], a.v[1], a.v[2], a.v[3]);
+  st16<NT>(slot + 4, a.v[4], a.v[5], a.v[6], a.v[7]);
+  st16<NT>(slot + 8, a.v[8], a.v[9], b.v[0], b.v[1]);
+  st16<NT>(slot + 12, b.v[2], b.v[3], b.v[4], b.v[5]);
+  st16<NT>(slot + 16, b.v[6], b.v[7], b.v[8], b.v[9]);
+  st16<NT>(slot + 20, c.v[0], c.v[1], c.v[2], c.v[3]);
+  st16<NT>(slot + 24, c.v[4], c.v[5], c.v[6], c.v[7]);
+  st16<NT>(slot + 28, c.v[8], c.v[9], 0u, 0u);
 }
 
 // f(K-1), f(K-2), .., f(0) with compile-time arguments
@@ -1620,7 +1655,7 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
     if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
     aff_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
-  if (live) pt_store_aos(R, c * nrecv + j, acc);
+  if (live) pt_store_aos<DKG_COMB_NT != 0>(R, c * nrecv + j, acc);
 }
 
 void combine_short_aff(size_t width, size_t pstride, size_t pieces, size_t nrecv, const uint32_t* digits,

@@ -32,6 +32,20 @@ DKG_DEV void pt_store(uint32_t* __restrict__ base, size_t stride, size_t e, cons
   }
 }
 
+// pt_store with nontemporal (streaming) stores: the data goes out without displacing L2 lines the
+// kernel still reads.  The per-step binomial stores one table row per item and rereads its input
+// rows (each position is read by two items of a launch); with plain stores one Horner step of the
+// headline's tables took 324 us, with these 268 us (tools/ubench/binom, profiles/r06_binom_levers_ab.txt).
+DKG_DEV void pt_store_nt(uint32_t* __restrict__ base, size_t stride, size_t e, const ge_p3& p) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    __builtin_nontemporal_store(p.X.v[i], base + (size_t)(i)*stride + e);
+    __builtin_nontemporal_store(p.Y.v[i], base + (size_t)(10 + i) * stride + e);
+    __builtin_nontemporal_store(p.Z.v[i], base + (size_t)(20 + i) * stride + e);
+    __builtin_nontemporal_store(p.T.v[i], base + (size_t)(30 + i) * stride + e);
+  }
+}
+
 // Point-major (AoS) element e: 40 consecutive words, moved as ten 16-B accesses.  Used for the
 // per-(column, receiver) evaluations R, which one lane writes per step (stepping, recombination):
 // a point fills whole cache lines instead of 40 scattered 4-B words.  base must be 16-B aligned.
@@ -43,6 +57,15 @@ DKG_DEV uint32_t& pt_word(ge_p3& p, int w) {
 DKG_DEV uint32_t pt_word(const ge_p3& p, int w) {
   const fe& f = w < 10 ? p.X : (w < 20 ? p.Y : (w < 30 ? p.Z : p.T));
   return f.v[w % 10];
+}
+
+// one 16-B store, nontemporal (streaming) when NT
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+DKG_DEV void st16(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const u32x4_t v = {a, b, c, d};
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+  else *reinterpret_cast<u32x4_t*>(p) = v;
 }
 
 DKG_DEV void pt_load_aos(ge_p3& p, const uint32_t* __restrict__ base, size_t e) {
@@ -57,11 +80,12 @@ DKG_DEV void pt_load_aos(ge_p3& p, const uint32_t* __restrict__ base, size_t e) 
   }
 }
 
+template <bool NT = false>
 DKG_DEV void pt_store_aos(uint32_t* __restrict__ base, size_t e, const ge_p3& p) {
-  uint4* b = reinterpret_cast<uint4*>(base + e * PT_WORDS);
+  uint32_t* b = base + e * PT_WORDS;
 #pragma unroll
   for (int k = 0; k < PT_WORDS / 4; k++)
-    b[k] = make_uint4(pt_word(p, 4 * k), pt_word(p, 4 * k + 1), pt_word(p, 4 * k + 2), pt_word(p, 4 * k + 3));
+    st16<NT>(b + 4 * k, pt_word(p, 4 * k), pt_word(p, 4 * k + 1), pt_word(p, 4 * k + 2), pt_word(p, 4 * k + 3));
 }
 
 DKG_DEV void ld_words8(uint32_t (&w)[8], const uint32_t* __restrict__ p) {

@@ -33,6 +33,24 @@ def load_counters(path):
     return agg, calls
 
 
+def eff_clock(path):
+    """Per kernel: (sum of GRBM_GUI_ACTIVE, sum of dispatch durations in ns) over its dispatches of the
+    pass at `path`.  GRBM_GUI_ACTIVE / 8 / duration is the clock the chip held during the kernel
+    (MI355X_MICROARCH.md "DVFS give-back": rocprofv3 sums the counter over the 8 XCDs; it reads high
+    on dispatches shorter than ~0.3 ms and is within 3 % of the in-kernel clock from 10 ms on)."""
+    out = defaultdict(lambda: [0.0, 0.0])
+    if not os.path.exists(path):
+        return out
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != "GRBM_GUI_ACTIVE":
+                continue
+            e = out[short(row["Kernel_Name"])]
+            e[0] += float(row["Counter_Value"])
+            e[1] += int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+    return out
+
+
 def main(d):
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     print(f"{'kernel':24s} {'calls':>6s} {'total ms':>10s} {'avg us':>10s}")
@@ -40,6 +58,13 @@ def main(d):
         for row in csv.DictReader(f):
             print(f"{short(row['Name']):24s} {int(row['Calls']):6d} {float(row['TotalDurationNs']) / 1e6:10.3f} "
                   f"{float(row['AverageNs']) / 1e3:10.1f}")
+    clk = eff_clock(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
+    if clk:
+        print()
+        print("effective clock under load (pmc_fetch pass: GRBM_GUI_ACTIVE / 8 / dispatch time), kernels >= 1 ms:")
+        for k, (g, ns) in sorted(clk.items(), key=lambda x: -x[1][1]):
+            if ns >= 1e6:
+                print(f"{k:40s} {g / 8 / ns * 1e3:7.0f} MHz over {ns / 1e6:9.3f} ms")
     sq, calls = load_counters(os.path.join(d, "pmc_sq", "run_counter_collection.csv"))
     fe, _ = load_counters(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"))
     wr, _ = load_counters(os.path.join(d, "pmc_write", "run_counter_collection.csv"))
@@ -131,6 +156,19 @@ def write_traffic(d, out, key):
     for ph, (ins, i64) in agg.items():
         if ins:
             kern[ph]["valu_int64_share"] = i64 / ins
+    # the clock each phase ran at in the profiled pass (GRBM_GUI_ACTIVE / 8 / time)
+    # (only where the phase's dispatches average >= 1 ms: the counter reads high on short ones, so the
+    # per-step binomial's ~0.15-ms launches get no figure)
+    ck = {}
+    for k, (g, ns) in eff_clock(os.path.join(d, "pmc_fetch", "run_counter_collection.csv")).items():
+        ph = phase(k, ded)
+        if ph in kern:
+            a = ck.setdefault(ph, [0.0, 0.0])
+            a[0] += g
+            a[1] += ns
+    for ph, (g, ns) in ck.items():
+        if ns and ns / max(kern[ph]["fetch_launches"], 1) >= 1e6:
+            kern[ph]["effective_clock_mhz"] = g / 8 / ns * 1e3
     doc = {"source": f"rocprofv3 --pmc FETCH_SIZE (doubled, MI355X_MICROARCH.md HBM) and --pmc WRITE_SIZE, "
                      f"separate passes of tools/profile.sh ({os.path.basename(os.path.normpath(d))})",
            "key": key, "kernels": kern}
