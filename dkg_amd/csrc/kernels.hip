@@ -510,13 +510,12 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
   for (int w = 0; w < PT_WORDS; w++) e[w * S + d] = C[w * S + kpos * npad + d];
 }
 
-// The per-step binomial's table stores (k_binom_step, k_binom_pair): nontemporal by default
-// (DKG_BINOM_NT=0: plain stores, the round-5 kernels).  Every launch rereads the previous step's rows
-// (each position by two items); plain stores of the new rows displaced them from L2: one step of the
-// headline's tables 324 -> 268 us (tools/ubench/binom, profiles/r06_binom_levers_ab.txt).
-#ifndef DKG_BINOM_NT
-#define DKG_BINOM_NT 1
-#endif
+// The per-step binomial's table stores (k_binom_step<.., NT>): nontemporal for the large steps.
+// A launch rereads the previous step's rows (each position by two items) while writing the new
+// ones; once a step's rows read + written exceed the 256-MB Infinity Cache, plain stores evict the
+// rows still to be read (the steps above r ~ 105 at n=1024 took 290-330 us, bimodal), while below
+// it the next launch finds the plain-stored rows cached.  runtime.hip picks NT per step by that
+// footprint (binom_nt, DKG_BINOM_NT_BYTES; profiles/r06_binom_levers_ab.txt).
 // A/B knobs of the same kind for the other large table writers (0: plain stores): the stepping's
 // evaluations R and dense Z copy, the normalisation's affine addends, the per-wave binomial
 #ifndef DKG_STEP_NT
@@ -531,12 +530,14 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 #ifndef DKG_COMB_NT  // the recombination's b_j P(j) (read by the checks)
 #define DKG_COMB_NT 0
 #endif
+template <bool NT>
 DKG_DEV void binom_st(uint32_t* p, uint32_t v) {
-  if (DKG_BINOM_NT) __builtin_nontemporal_store(v, p);
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
+template <bool NT>
 DKG_DEV void binom_pt_store(uint32_t* __restrict__ base, size_t stride, size_t e, const ge_p3& p) {
-  if (DKG_BINOM_NT) pt_store_nt(base, stride, e, p);
+  if constexpr (NT) pt_store_nt(base, stride, e, p);
   else pt_store(base, stride, e, p);
 }
 
@@ -550,7 +551,7 @@ DKG_DEV void binom_pt_store(uint32_t* __restrict__ base, size_t stride, size_t e
 // Z = 0 marks flags[0] (fany: the driver's guard word, runtime.hip with_binom_ded, which reruns the
 // verification with the complete formula) or flags[its (piece, column group)] (binomial_wave_redo
 // rebuilds the marked groups after the last step, DKG_BINOM_STEP_DED=2).
-template <bool DED>
+template <bool DED, bool NT>
 __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
@@ -565,7 +566,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
   const int m = r - (int)blockIdx.y;
   if (m == 0) {
 #pragma unroll 8
-    for (int w = 0; w < PT_WORDS; w++) binom_st(eout + w * S + d, C[w * S + (size_t)k * npad + d]);
+    for (int w = 0; w < PT_WORDS; w++) binom_st<NT>(eout + w * S + d, C[w * S + (size_t)k * npad + d]);
     return;
   }
   // A short last piece (last_off = L - its length) holds the identity in its top last_off
@@ -604,7 +605,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
     ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
     mul_small_lds(x, (uint32_t)m, q);        // * m
   }
-  binom_pt_store(eout, S, (size_t)m * npad + d, x);
+  binom_pt_store<NT>(eout, S, (size_t)m * npad + d, x);
 }
 
 // k_binom_step with lane pairs (split.h): one wave per (position, 32 columns), each column's point
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_pair(int r, int k, size_t npad,
   if (m == 0) {
     if (lane & 1) return;
 #pragma unroll 8
-    for (int w = 0; w < PT_WORDS; w++) binom_st(eout + w * S + d, C[w * S + (size_t)k * npad + d]);
+    for (int w = 0; w < PT_WORDS; w++) eout[w * S + d] = C[w * S + (size_t)k * npad + d];
     return;
   }
   const int re = r - (piece == last_piece ? last_off : 0);
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_pair(int r, int k, size_t npad,
   ge_add_pair(x, x, c, false);             // e_{m-1} + e_m
   mul_small_pair(x, (uint32_t)m, c);       // * m
   if (lane & 1) return;
-  binom_pt_store(eout, S, (size_t)m * npad + d, x);
+  pt_store(eout, S, (size_t)m * npad + d, x);
 }
 
 void binom_step_pair(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in,
@@ -666,18 +667,19 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
                 hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* flags, size_t col_base,
-                size_t dreal, unsigned gw, bool flag_any) {
+                size_t dreal, unsigned gw, bool flag_any, bool nt) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
   const dim3 grid((unsigned)(width / 64 * pieces), (unsigned)(r + 1));
-  if (flags)
-    hipLaunchKernelGGL(k_binom_step<true>, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out,
-                       pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, flags, col_base, dreal,
-                       gw ? gw : 64u, flag_any ? 1 : 0);
-  else
-    hipLaunchKernelGGL(k_binom_step<false>, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out,
-                       pstride, (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, nullptr, col_base, dreal,
-                       gw ? gw : 64u, 0);
+  auto go = [&](auto kern, uint32_t* fl, int fany) {
+    hipLaunchKernelGGL(kern, grid, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride,
+                       (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, fl, col_base, dreal, gw ? gw : 64u,
+                       fany);
+  };
+  if (flags && nt) go(k_binom_step<true, true>, flags, flag_any ? 1 : 0);
+  else if (flags) go(k_binom_step<true, false>, flags, flag_any ? 1 : 0);
+  else if (nt) go(k_binom_step<false, true>, nullptr, 0);
+  else go(k_binom_step<false, false>, nullptr, 0);
 }
 
 // Every Horner step of one column group in ONE wave (short tables of many columns: config 5's

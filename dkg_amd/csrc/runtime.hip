@@ -235,6 +235,20 @@ uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, si
   return red;
 }
 
+#ifndef DKG_BINOM_NT_BYTES_DEFAULT
+#define DKG_BINOM_NT_BYTES_DEFAULT 1e30  // never; the round-6 A/B sets it
+#endif
+// Nontemporal stores for binomial step r over `columns` table columns (all chunks run their steps
+// together): when the step's rows read + written, 2 (r + 1) columns 160 B, exceed DKG_BINOM_NT_BYTES
+// (kernels.hip binom_pt_store).  The environment variable overrides the default for A/B runs.
+bool binom_nt(size_t r, size_t columns) {
+  static const double lim = [] {
+    const char* e = getenv("DKG_BINOM_NT_BYTES");
+    return e ? atof(e) : DKG_BINOM_NT_BYTES_DEFAULT;
+  }();
+  return 2.0 * (double)(r + 1) * (double)columns * 160.0 > lim;
+}
+
 // After a sync: record the device time of binomial / stepping / check of the last verify_device
 // when it ran serialised and timed (names "<tag>.binomial" etc.; tag r2, r4 or r24 = fused).
 void collect_phases(dkg_ctx* ctx) {
@@ -711,7 +725,8 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
                                                                     Lr);
         else
           (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr,
-                                                          bany ? bany : bflags, c0, D, (unsigned)gw, bany != nullptr);
+                                                          bany ? bany : bflags, c0, D, (unsigned)gw, bany != nullptr,
+                                                          binom_nt(r, npad * U));
         std::swap(bin, bout);
       }
       e = bin;
