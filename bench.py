@@ -432,6 +432,15 @@ def short_combine_valu(mults, VALU=SLOTS, affine=True):
     return total
 
 
+def binom_digits(m):
+    """The kernels' recoding of a binomial multiplier m (points.h small_recode): signed digits, least
+    significant first, top digit +1 -- the NAF with a leading 1 0 -1 turned into 1 1."""
+    ds = _naf(m)
+    if len(ds) >= 3 and ds[-1] == 1 and ds[-2] == 0 and ds[-3] == -1:
+        ds = ds[:-3] + [1, 1]
+    return ds
+
+
 def binom_item_valu(m, VALU=SLOTS, ded=True):
     """One binomial item e_m <- m (e_{m-1} + e_m) (kernels.hip k_binom_step / k_binom_wave): the first
     addition, then the NAF chain of m on the sum's cached form.  ded (the default with the dedicated
@@ -440,7 +449,7 @@ def binom_item_valu(m, VALU=SLOTS, ded=True):
     cached = VALU["ge_to_cached_ded"] if ded else VALU["ge_to_cached"]
     zt = VALU["fe_tight_zero"] if ded else 0
     c = cached + (VALU["ge_add_ded"] if ded else VALU["ge_add"]) + zt  # e_{m-1} + e_m
-    ds = _naf(m)
+    ds = binom_digits(m)
     if len(ds) > 1:
         c += cached
         for i in range(len(ds) - 2, -1, -1):

@@ -343,19 +343,8 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
 // ------------------------------------------------------------------ K3a binomial-basis Horner
 // y = m * y, m wave-uniform; q = this lane's column of the wave's 40 x 64-word LDS slot (clobbered).
 __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q) {
-  uint32_t pos = 0, neg = 0;
-  int len = 0;
-  for (uint32_t v = m; v; v >>= 1, len++) {
-    if (v & 1u) {
-      if ((v & 3u) == 1u) {
-        pos |= 1u << len;
-        v -= 1;
-      } else {
-        neg |= 1u << len;
-        v += 1;
-      }
-    }
-  }
+  uint32_t pos, neg;
+  const int len = small_recode(m, pos, neg);
   if (len <= 1) return;
   {
     ge_cached xc;
@@ -375,19 +364,8 @@ __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q)
 // product by d; `bad` is set when an addition's Z vanished (then the caller redoes the column group
 // with the complete formula)
 __device__ __forceinline__ void mul_small_ded_lds(ge_p3& y, uint32_t m, uint32_t* q, bool& bad) {
-  uint32_t pos = 0, neg = 0;
-  int len = 0;
-  for (uint32_t v = m; v; v >>= 1, len++) {
-    if (v & 1u) {
-      if ((v & 3u) == 1u) {
-        pos |= 1u << len;
-        v -= 1;
-      } else {
-        neg |= 1u << len;
-        v += 1;
-      }
-    }
-  }
+  uint32_t pos, neg;
+  const int len = small_recode(m, pos, neg);
   if (len <= 1) return;
   {
     ge_cached xc;

@@ -59,6 +59,35 @@ DKG_DEV uint32_t pt_word(const ge_p3& p, int w) {
   return f.v[w % 10];
 }
 
+// Signed-digit recoding of a small positive multiplier m for the binomial's chains (mul_small_*):
+// the NAF, except that a leading 1 0 -1 (2^k - 2^(k-2)) becomes 1 1 (2^(k-1) + 2^(k-2)): one
+// doubling fewer for the same additions.  That is the cheapest signed-binary chain of every m < 256
+// under this build's slot costs (checked exhaustively by tests/test_bench.py against all signed-digit
+// representations; bench.py binom_digits): m = 3, 6, 11-13, 22-26, 44-52, ...  pos / neg hold the
+// +1 / -1 digits; returns the length (the top digit is +1 at len - 1).
+DKG_DEV int small_recode(uint32_t m, uint32_t& pos, uint32_t& neg) {
+  pos = 0;
+  neg = 0;
+  int len = 0;
+  for (uint32_t v = m; v; v >>= 1, len++) {
+    if (v & 1u) {
+      if ((v & 3u) == 1u) {
+        pos |= 1u << len;
+        v -= 1;
+      } else {
+        neg |= 1u << len;
+        v += 1;
+      }
+    }
+  }
+  if (len >= 3 && !((pos | neg) >> (len - 2) & 1u) && (neg >> (len - 3) & 1u)) {
+    pos = (pos & ~(1u << (len - 1))) | (3u << (len - 3));
+    neg &= ~(1u << (len - 3));
+    len--;
+  }
+  return len;
+}
+
 // one 16-B store, nontemporal (streaming) when NT
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 template <bool NT>

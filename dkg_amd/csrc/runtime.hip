@@ -235,12 +235,15 @@ uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, si
   return red;
 }
 
-#ifndef DKG_BINOM_NT_BYTES_DEFAULT
-#define DKG_BINOM_NT_BYTES_DEFAULT 1e30  // never; the round-6 A/B sets it
-#endif
 // Nontemporal stores for binomial step r over `columns` table columns (all chunks run their steps
 // together): when the step's rows read + written, 2 (r + 1) columns 160 B, exceed DKG_BINOM_NT_BYTES
 // (kernels.hip binom_pt_store).  The environment variable overrides the default for A/B runs.
+// Default 0 = every step: the serialised n=1024 binomial 21.5-21.8 -> 20.4-20.6 ms, thresholds of
+// 180 / 256 / 320 MB in between; config 4 and the whole ceremony within noise
+// (profiles/r06_binom_levers_ab.txt, recipe r06e).
+#ifndef DKG_BINOM_NT_BYTES_DEFAULT
+#define DKG_BINOM_NT_BYTES_DEFAULT 0.0
+#endif
 bool binom_nt(size_t r, size_t columns) {
   static const double lim = [] {
     const char* e = getenv("DKG_BINOM_NT_BYTES");
@@ -353,17 +356,31 @@ constexpr size_t SHORT_MAX = 5;
 double split_model_ms(size_t cols, size_t n, size_t N, size_t U, size_t L, bool short_mult) {
   const double DBL = 1000, ADD = 1400, SIMDS = 1024, THR = 4.5, LAT = 8, LAT_ILP = 6, LAUNCH = 3e-3 * 2.4e6;
   const size_t Lr = last_piece_len(N, U, L), off = L - Lr;  // the last piece: Lr positions, starts at step off
-  auto cost = [&](size_t m) {  // one binomial position-step: add + NAF multiplication by m
-    int len = 0, nz = 0;  // NAF length and weight of m (as mul_small_lds recodes it)
-    for (size_t v = m; v; v >>= 1, len++) {
+  auto cost = [&](size_t m) {  // one binomial position-step: add + multiplication by m
+    // length and weight of m's recoding as the kernels do it (points.h small_recode: the NAF, a
+    // leading 1 0 -1 turned into 1 1 -- one doubling fewer)
+    uint64_t pos = 0, neg = 0;
+    int len = 0;
+    for (uint64_t v = m; v; v >>= 1, len++) {
       if (v & 1) {
-        nz++;
-        if ((v & 3) == 1) v -= 1;
-        else v += 1;
+        if ((v & 3) == 1) {
+          pos |= 1ull << len;
+          v -= 1;
+        } else {
+          neg |= 1ull << len;
+          v += 1;
+        }
       }
     }
+    if (len >= 3 && !(((pos | neg) >> (len - 2)) & 1) && ((neg >> (len - 3)) & 1)) {
+      pos = (pos & ~(1ull << (len - 1))) | (3ull << (len - 3));
+      neg &= ~(1ull << (len - 3));
+      len--;
+    }
+    const int nz = __builtin_popcountll(pos | neg);
     return ADD + (len > 1 ? (len - 1) * DBL + (nz - 1) * ADD : 0.0);
   };
+
   std::vector<double> pre(L + 1, 0.0);
   for (size_t m = 1; m <= L; m++) pre[m] = pre[m - 1] + cost(m);
   const double waves_col = (double)cols / 64;

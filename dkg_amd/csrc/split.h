@@ -133,19 +133,8 @@ DKG_DEV void ge_add_pair(ge_p3& r, const ge_p3& p, const pair_ctx& c, bool neg) 
 
 // y = m y for a wave-uniform small m (mul_small_lds's NAF chain, with the pair operations)
 DKG_DEV void mul_small_pair(ge_p3& y, uint32_t m, const pair_ctx& c) {
-  uint32_t pos = 0, neg = 0;
-  int len = 0;
-  for (uint32_t v = m; v; v >>= 1, len++) {
-    if (v & 1u) {
-      if ((v & 3u) == 1u) {
-        pos |= 1u << len;
-        v -= 1;
-      } else {
-        neg |= 1u << len;
-        v += 1;
-      }
-    }
-  }
+  uint32_t pos, neg;
+  const int len = small_recode(m, pos, neg);
   if (len <= 1) return;
   pair_put_cached(c, y);
 #pragma unroll 1
