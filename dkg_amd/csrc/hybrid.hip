@@ -19,7 +19,7 @@
 
 namespace dkgk {
 
-// grid (ceil(2D / 1024), n): recipient q = blockIdx.y.  The generator's comb (radix 2^DKG_COMBW_BITS)
+// grid (ceil(2D / DKG_ENC_BS), n): recipient q = blockIdx.y.  The generator's comb (radix 2^DKG_COMBW_BITS)
 // and the recipient's own comb (radix 2^DKG_KEY_COMB_BITS, 26 windows at 2^10: 1.7 MB per key, every
 // dealer of the block reads the same table through L2; the radix-16 LDS comb it replaces took 64).
 // 256-thread workgroups at 3 waves per SIMD: the two combs' mixed additions need ~138 VGPRs (the
