@@ -193,7 +193,7 @@ def algorithmic_bytes(kernel, n, t, U, plen=None, per_wave=False, batch=1):
     if kernel == "combine":  # U affine piece values (128-B slots) in, P(j) out per (column, receiver)
         return 2 * n * n * (U * AFF_BYTES + PT_BYTES), 1
     if kernel == "check":  # s and s' (32 B each), b_j P(j) of the E and A columns (160 B each), 2 decisions,
-        # and one 128-B comb entry per window of g and of h: the radix-2^17 tables (134 MB per base)
+        # and one 128-B comb entry per window of g and of h: the radix-2^19 tables (470 MB per base)
         # live in HBM beyond the Infinity Cache, so every window's entry is a read of the algorithm
         return n * n * (2 * 32 + 2 * PT_BYTES + 2 + 2 * combw_windows() * 128), 1
     if kernel == "affine":  # per stepped value: Z twice (the stepping's dense 40-B copy), the point, a

@@ -1713,7 +1713,7 @@ void check(size_t ndealers, size_t nrecv, size_t dealer_base, size_t recv_base, 
 // PASS 0: both in one launch (the default).  PASS 1 / 2: the same work as two launches that each
 // read ONE comb: pass 1 computes g*s, decides round 4 and parks g*s in acc[p] (160 B), pass 2 adds
 // h*s' to it and decides round 2 -- a split made for the radix-2^11 combs (3.1 MB per base, one
-// XCD's 4-MB L2); the radix-2^17 combs are 134 MB per base (HBM / Infinity Cache) either way.
+// XCD's 4-MB L2); the radix-2^19 combs are 470 MB per base (HBM / Infinity Cache) either way.
 template <int PASS>
 __global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_check_both(size_t ndealers, size_t nrecv, size_t dealer0, size_t dealer_base,
                                                     uint32_t nmod, const uint32_t* __restrict__ s,

@@ -177,16 +177,17 @@ DKG_DEV void comb_mul_add(ge_p3& acc, const sc& s, const uint32_t* tab) {
   }
 }
 
-// Radix-2^17 comb in global memory (134 MB per base: HBM, read through L2 and the 256-MB Infinity
-// Cache): 16 windows B_w = 2^(17 w) B of 65,536 affine Niels entries d B_w (d = 1..65536),
-// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-65536, 65535]: one
-// mixed addition per 17 scalar bits (16 per scalar; radix 2^11 took 24, 2^8 32, the LDS radix-16
-// comb 64), for the bases every kernel shares (g, h).  The checks and commitments are VALU-bound:
-// each window fewer pays more than the misses on the larger tables cost (radix 2^9 .. 2^11:
-// profiles/r04_comb_radix_ab.txt; 2^11 .. 2^17: profiles/r05_comb_radix_ab.txt -- config 5 device
-// time 2^11 -> 2^15 -> 2^17: 303.6 -> 282.2 -> 273.3 ms per batch).
+// Radix-2^19 comb in global memory (470 MB per base: HBM, read through L2 and the 256-MB Infinity
+// Cache): 14 windows B_w = 2^(19 w) B of 262,144 affine Niels entries d B_w (d = 1..2^18),
+// entry-major, 32 words per entry (ypx | ymx | xy2d | 2 pad).  Signed digits in [-2^18, 2^18 - 1]:
+// one mixed addition per 19 scalar bits (14 per scalar; radix 2^17 took 16, 2^11 24, 2^8 32, the
+// LDS radix-16 comb 64), for the bases every kernel shares (g, h).  The checks and commitments are
+// VALU-bound: each window fewer pays more than the misses on the larger tables cost (radix 2^9 ..
+// 2^11: profiles/r04_comb_radix_ab.txt; 2^11 .. 2^17: profiles/r05_comb_radix_ab.txt -- config 5
+// device time 2^11 -> 2^15 -> 2^17: 303.6 -> 282.2 -> 273.3 ms per batch; 2^17 / 2^18 / 2^19:
+// profiles/r06_comb_radix_ab.txt -- config 5 -2.3 ms, the headline -0.4 ms at 2^19, 2^18 flat).
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 17  // -DDKG_COMBW_BITS=11 .. 17: the A/B builds
+#define DKG_COMBW_BITS 19  // -DDKG_COMBW_BITS=11 .. 19: the A/B builds
 #endif
 constexpr int COMBW_BITS = DKG_COMBW_BITS;
 constexpr int COMBW_WINDOWS = 256 / COMBW_BITS + 1;  // the top window absorbs the signed recoding's carry

@@ -116,9 +116,9 @@ constexpr size_t PT_WORDS_H = 40;
 constexpr size_t AFFP_WORDS_H = 32;  // affine addend slot of kernels.hip affine_pieces
 constexpr size_t COMB_BYTES = 30 * 512 * 4;
 #ifndef DKG_COMBW_BITS
-#define DKG_COMBW_BITS 17
+#define DKG_COMBW_BITS 19
 #endif
-// points.h COMBW_WORDS x 4 (radix 2^17: 16 windows x 65,536 entries x 128 B = 134 MB)
+// points.h COMBW_WORDS x 4 (radix 2^19: 14 windows x 262,144 entries x 128 B = 470 MB)
 constexpr size_t COMBW_BYTES =
     (size_t)(256 / DKG_COMBW_BITS + 1) * (1u << (DKG_COMBW_BITS - 1)) * 32 * 4;
 const uint8_t BASEPOINT[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
@@ -2054,7 +2054,7 @@ int dkg_fixed_base_batch(dkg_ctx* ctx, const uint8_t base[32], size_t count, con
   return guarded(ctx, [&] {
     if (count == 0) return DKG_OK;
     const uint32_t* tab = ctx->tab_gw;
-    // the generator and the commitment key have their combs already; another base's comb (134 MB,
+    // the generator and the commitment key have their combs already; another base's comb (470 MB,
     // ~1M entry threads) is built once and kept while the caller passes the same base bytes
     if (base && memcmp(base, BASEPOINT, 32) == 0) {
       base = nullptr;

@@ -83,7 +83,7 @@ int dkg_ctx_set_binomial(dkg_ctx *ctx, int mode);
 /* The fused round-2/4 checks (g*s compared in round 4, + h*s' in round 2): 0 (default) one launch
  * reading both fixed-base combs; 1 two launches that each read one comb, g*s parked in device memory
  * between them.  Mode 1 dates from the radix-2^11 combs (3.1 MB per base, one XCD's 4-MB L2 held
- * one); the radix-2^17 combs (134 MB per base, HBM / Infinity Cache) leave it no cache to win, and
+ * one); the radix-2^19 combs (470 MB per base, HBM / Infinity Cache) leave it no cache to win, and
  * it stays as an A/B option.  Outputs do not depend on it. */
 int dkg_ctx_set_check(dkg_ctx *ctx, int mode);
 /* Verification algorithm of the ceremony drivers (all-receivers views: dkg_ceremony_*, batch, shard):
