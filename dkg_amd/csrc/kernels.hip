@@ -586,98 +586,6 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
   binom_pt_store<NT>(eout, S, (size_t)m * npad + d, x);
 }
 
-// mul_small_ded_lds over two 64-column groups per lane (the same m: two identical chains whose
-// instructions interleave, k_binom_step2); bad[g] collects group g's exceptional additions.
-__device__ __forceinline__ void mul_small_ded_lds2(ge_p3 (&y)[2], uint32_t m, uint32_t* q0, uint32_t* q1,
-                                                   bool (&bad)[2]) {
-  uint32_t pos, neg;
-  const int len = small_recode(m, pos, neg);
-  if (len <= 1) return;
-  {
-    ge_cached xc;
-    ge_to_cached_ded(xc, y[0]);
-    lds_put_cached(q0, xc);
-    ge_to_cached_ded(xc, y[1]);
-    lds_put_cached(q1, xc);
-  }
-#pragma unroll 1
-  for (int i = len - 2; i >= 0; i--) {
-    const uint32_t bit = 1u << i;
-    const bool nz = ((pos | neg) & bit) != 0;
-    ge_dbl_lean(y[0], y[0], nz || i == 0);
-    ge_dbl_lean(y[1], y[1], nz || i == 0);
-    if (nz) {
-      ge_add_ded_lds_s(y[0], y[0], q0, (neg & bit) != 0, 64, i == 0);
-      ge_add_ded_lds_s(y[1], y[1], q1, (neg & bit) != 0, 64, i == 0);
-      bad[0] |= fe_tight_zero(y[0].Z);
-      bad[1] |= fe_tight_zero(y[1].Z);
-    }
-  }
-}
-
-// k_binom_step<true, NT> with TWO 64-column groups per lane (groups 2g, 2g + 1 of a piece; gx2 group
-// pairs per piece): the same m, so the two items' chains are one instruction stream with twice the
-// independent work (ILP 2), at 2 waves per SIMD (20 KB of LDS per wave, ~170 VGPRs).  For the large
-// steps, where a launch has several rounds of waves (runtime.hip picks it by step; the dedicated
-// formula only -- the complete rerun keeps k_binom_step).  Group g marks like k_binom_step's wave.
-template <bool NT>
-__global__ __launch_bounds__(64, 2) void k_binom_step2(int r, int k, size_t npad, size_t N,
-                                                     const uint32_t* __restrict__ C,
-                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
-                                                     size_t pstride, unsigned gx2, unsigned last_piece,
-                                                     int last_off, uint32_t* __restrict__ flags, size_t col_base,
-                                                     size_t dreal, unsigned gw, int fany) {
-  __shared__ uint32_t qs[2 * PT_WORDS * 64];
-  uint32_t* q0 = qs + threadIdx.x;
-  uint32_t* q1 = qs + PT_WORDS * 64 + threadIdx.x;
-  const unsigned piece = blockIdx.x / gx2, grp = 2 * (blockIdx.x - piece * gx2);
-  const size_t d0 = piece * pstride + (size_t)grp * 64 + threadIdx.x, d1 = d0 + 64;
-  const size_t S = N * npad;
-  const int m = r - (int)blockIdx.y;
-  if (m == 0) {
-#pragma unroll 8
-    for (int w = 0; w < PT_WORDS; w++) {
-      binom_st<NT>(eout + w * S + d0, C[w * S + (size_t)k * npad + d0]);
-      binom_st<NT>(eout + w * S + d1, C[w * S + (size_t)k * npad + d1]);
-    }
-    return;
-  }
-  const int re = r - (piece == last_piece ? last_off : 0);
-  if (m > re) return;
-  uint32_t keep = (m == re) ? 0u : 0xffffffffu;  // position re is the identity (k_binom_step)
-  asm volatile("" : "+v"(keep));
-  for (int g = 0; g < 2; g++) {
-    ge_p3 cur;
-    pt_load(cur, ein, S, (size_t)m * npad + (g ? d1 : d0));
-    uint32_t* cw = reinterpret_cast<uint32_t*>(&cur);
-#pragma unroll
-    for (int w = 0; w < PT_WORDS; w++) cw[w] = (cw[w] & keep) | ((w == 10 || w == 20) ? ~keep & 1u : 0u);
-    ge_cached cc;
-    ge_to_cached_ded(cc, cur);
-    lds_put_cached(g ? q1 : q0, cc);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  ge_p3 x[2];
-  pt_load(x[0], ein, S, (size_t)(m - 1) * npad + d0);
-  pt_load(x[1], ein, S, (size_t)(m - 1) * npad + d1);
-  bool bad[2] = {false, false};
-  ge_add_ded_lds(x[0], x[0], q0);  // e_{m-1} + e_m
-  ge_add_ded_lds(x[1], x[1], q1);
-  bad[0] |= fe_tight_zero(x[0].Z);
-  bad[1] |= fe_tight_zero(x[1].Z);
-  mul_small_ded_lds2(x, (uint32_t)m, q0, q1, bad);  // * m
-  for (int g = 0; g < 2; g++) {
-    const size_t gcol = col_base + (size_t)(grp + g) * 64 + threadIdx.x;
-    const bool real = (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
-    if (__ballot(bad[g] && real) != 0 && threadIdx.x == 0)
-      flags[fany ? 0 : (size_t)piece * (pstride / 64) + (col_base / 64) + grp + g] = 1u;
-  }
-  binom_pt_store<NT>(eout, S, (size_t)m * npad + d0, x[0]);
-  uint32_t* eo = eout;  // an opaque copy: the first store's addresses are not kept live
-  asm volatile("" : "+s"(eo));
-  binom_pt_store<NT>(eo, S, (size_t)m * npad + d1, x[1]);
-}
-
 // k_binom_step with lane pairs (split.h): one wave per (position, 32 columns), each column's point
 // held by two lanes that compute half of every field product each -- half the dependent
 // instructions per lane for a latency-bound step (few waves per SIMD), at twice the lanes.
@@ -737,7 +645,7 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
                 hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* flags, size_t col_base,
-                size_t dreal, unsigned gw, bool flag_any, bool nt, bool g2) {
+                size_t dreal, unsigned gw, bool flag_any, bool nt) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
   const dim3 grid((unsigned)(width / 64 * pieces), (unsigned)(r + 1));
@@ -746,17 +654,6 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
                        (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, fl, col_base, dreal, gw ? gw : 64u,
                        fany);
   };
-  if (flags && g2 && (width / 64) % 2 == 0) {  // two column groups per lane (k_binom_step2)
-    const dim3 grid2((unsigned)(width / 128 * pieces), (unsigned)(r + 1));
-    auto go2 = [&](auto kern) {
-      hipLaunchKernelGGL(kern, grid2, dim3(64), 0, stream, (int)r, (int)(N - 1 - r), npad, N, C, in, out, pstride,
-                         (unsigned)(width / 128), (unsigned)(pieces - 1), last_off, flags, col_base, dreal,
-                         gw ? gw : 64u, flag_any ? 1 : 0);
-    };
-    if (nt) go2(k_binom_step2<true>);
-    else go2(k_binom_step2<false>);
-    return;
-  }
   if (flags && nt) go(k_binom_step<true, true>, flags, flag_any ? 1 : 0);
   else if (flags) go(k_binom_step<true, false>, flags, flag_any ? 1 : 0);
   else if (nt) go(k_binom_step<false, true>, nullptr, 0);

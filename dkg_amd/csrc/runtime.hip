@@ -235,9 +235,6 @@ uint32_t* upload_scalars(dkg_ctx* ctx, const char* name, const uint8_t* host, si
   return red;
 }
 
-#ifndef DKG_BINOM_G2_WAVES_DEFAULT
-#define DKG_BINOM_G2_WAVES_DEFAULT 1e30  // never; the round-6 A/B decides
-#endif
 // Nontemporal stores for binomial step r over `columns` table columns (all chunks run their steps
 // together): when the step's rows read + written, 2 (r + 1) columns 160 B, exceed DKG_BINOM_NT_BYTES
 // (kernels.hip binom_pt_store).  The environment variable overrides the default for A/B runs.
@@ -253,18 +250,6 @@ bool binom_nt(size_t r, size_t columns) {
     return e ? atof(e) : DKG_BINOM_NT_BYTES_DEFAULT;
   }();
   return 2.0 * (double)(r + 1) * (double)columns * 160.0 > lim;
-}
-
-// Two column groups per lane (k_binom_step2) for the dedicated steps with at least
-// DKG_BINOM_G2_WAVES waves per SIMD over all chunks (the single-group launch would run several rounds
-// of waves; the paired one halves the waves at twice the work each).  The environment variable
-// overrides the default for A/B runs.
-bool binom_g2(double wps) {
-  static const double lim = [] {
-    const char* e = getenv("DKG_BINOM_G2_WAVES");
-    return e ? atof(e) : DKG_BINOM_G2_WAVES_DEFAULT;
-  }();
-  return wps >= lim;
 }
 
 // After a sync: record the device time of binomial / stepping / check of the last verify_device
@@ -758,7 +743,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
         else
           (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr,
                                                           bany ? bany : bflags, c0, D, (unsigned)gw, bany != nullptr,
-                                                          binom_nt(r, npad * U), binom_g2(wps));
+                                                          binom_nt(r, npad * U));
         std::swap(bin, bout);
       }
       e = bin;
