@@ -1355,3 +1355,43 @@ def test_ceremony_n4096_device(be):
     honest[np.arange(D), np.arange(D)] = SELF  # rank 0 owns dealers 0..D-1: SELF at j == i
     assert np.array_equal(o2.view(D, n).cpu().numpy(), honest)
     assert np.array_equal(o4.view(D, n).cpu().numpy(), honest)
+
+
+_NT_CHILD = r"""
+import json, sys
+sys.path.insert(0, %r)
+import dkg_amd
+c = json.load(open(%r))
+be = dkg_amd.Backend(0)
+be.env_init(c["t"], c["n"], b"Example of a shared string.")
+be.set_split(1)
+be.set_binomial(1)
+H = bytes.fromhex
+r = be.ceremony_verify(H(c["E"]), H(c["A"]), H(c["s"]), H(c["s_prime"]), c["n"], c["t"])
+print(json.dumps({"dec2": "".join(str(x) for x in r.dec2), "dec4": "".join(str(x) for x in r.dec4),
+                  "final_share": r.final_share.hex(), "mpk": r.mpk.hex(), "reruns": be.binomial_reruns()}))
+be.close()
+"""
+
+
+@pytest.mark.parametrize("nt_bytes", ["1e30", "0", "3e5"])
+def test_binomial_store_kinds_env(golden, nt_bytes):
+    """The per-step binomial's rows stored plainly (DKG_BINOM_NT_BYTES=1e30), nontemporally (0, the
+    default) or by step footprint (3e5: steps 1-6 plain, the later ones nontemporal) -- the env
+    knob is read once per process, so each runs in a child: the same decisions, final shares and mpk
+    as the golden ceremony."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "tests", "golden", "ceremony_n64_t31.json")
+    env = dict(os.environ, DKG_BINOM_NT_BYTES=nt_bytes)
+    p = subprocess.run([sys.executable, "-c", _NT_CHILD % (root, path)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    c = golden("ceremony_n64_t31.json")
+    assert got == {"dec2": c["dec2"], "dec4": c["dec4"], "final_share": c["final_share"], "mpk": c["mpk"],
+                   "reruns": 0}
