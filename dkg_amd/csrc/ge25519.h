@@ -349,17 +349,28 @@ DKG_DEV bool ristretto_decode(ge_p3& p, const uint32_t (&w)[8]) {
 }
 
 // Encode to 8 LE words (RFC 9496 ENCODE).
-DKG_DEV void ristretto_encode(uint32_t (&w)[8], const ge_p3& p) {
-  fe u1, u2, t, inv, den1, den2, z_inv, ix0, iy0, ench, x, y, den_inv, sqrtm1, one;
-  fe_ld(sqrtm1, ge_const::SQRT_M1);
-  fe_one(one);
+// The encoding in two halves around its inverse square root, so that a caller can drop the point
+// across the exponentiation and reload it (k_encode: the point's 40 registers are not live during the
+// 265-operation chain).
+DKG_DEV void ristretto_encode_pre(fe& u1, fe& u2, fe& t, const ge_p3& p) {
   fe_add(t, p.Z, p.Y);
   fe_sub(u1, p.Z, p.Y);
   fe_mul(u1, t, u1);                 // (Z+Y)(Z-Y)
   fe_mul(u2, p.X, p.Y);
   fe_sq(t, u2);
   fe_mul(t, t, u1);
+}
+DKG_DEV void ristretto_encode_post(uint32_t (&w)[8], const ge_p3& p, const fe& u1, const fe& u2, const fe& inv);
+DKG_DEV void ristretto_encode(uint32_t (&w)[8], const ge_p3& p) {
+  fe u1, u2, t, inv, one;
+  fe_one(one);
+  ristretto_encode_pre(u1, u2, t, p);
   fe_sqrt_ratio_m1(inv, one, t);
+  ristretto_encode_post(w, p, u1, u2, inv);
+}
+DKG_DEV void ristretto_encode_post(uint32_t (&w)[8], const ge_p3& p, const fe& u1, const fe& u2, const fe& inv) {
+  fe t, den1, den2, z_inv, ix0, iy0, ench, x, y, den_inv, sqrtm1;
+  fe_ld(sqrtm1, ge_const::SQRT_M1);
   fe_mul(den1, inv, u1);
   fe_mul(den2, inv, u2);
   fe_mul(z_inv, den1, den2);

@@ -29,7 +29,10 @@ constexpr int COMB_WORDS = AFF_WORDS * COMB_ENTRIES;  // 15360 words = 61440 B p
 // second copy of the points is needed).
 // With interleaved segments (nseg > 1) dealer i of segment seg goes to column
 // (i / 64) * 64 * nseg + seg * 64 + i % 64, and ok[] is indexed by column * pm_N + k.
-__global__ __launch_bounds__(256) void k_decode(const uint32_t* __restrict__ comp, size_t count,
+#ifndef DKG_DECODE_WAVES
+#define DKG_DECODE_WAVES 2
+#endif
+__global__ __launch_bounds__(256, DKG_DECODE_WAVES) void k_decode(const uint32_t* __restrict__ comp, size_t count,
                                                 uint32_t* __restrict__ ext, size_t stride,
                                                 uint8_t* __restrict__ ok, size_t pm_N, size_t pm_npad,
                                                 uint32_t nseg, uint32_t seg, size_t pm_L, size_t pm_pstride) {
@@ -106,14 +109,29 @@ void gather_points(const uint32_t* src, size_t sstride, size_t step, size_t k0, 
                      count, dst, dstride);
 }
 
-__global__ __launch_bounds__(256) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
+#ifndef DKG_ENCODE_WAVES  // minimum waves per SIMD of k_encode (3: 157 VGPRs, no scratch; 4: 128 + 88 B)
+#define DKG_ENCODE_WAVES 3
+#endif
+__global__ __launch_bounds__(256, DKG_ENCODE_WAVES) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
                                                 size_t count, uint32_t* __restrict__ comp) {
   size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
+  fe u1, u2, t, inv, one;
+  {
+    ge_p3 p;
+    pt_load(p, ext, stride, e);
+    ristretto_encode_pre(u1, u2, t, p);
+  }
+  fe_one(one);
+  fe_sqrt_ratio_m1(inv, one, t);
+  // the point again (160 B from L2 / HBM) rather than 40 registers held across the exponentiation:
+  // an opaque base makes it a real reload
+  const uint32_t* ext2 = ext;
+  asm volatile("" : "+s"(ext2));
   ge_p3 p;
-  pt_load(p, ext, stride, e);
+  pt_load(p, ext2, stride, e);
   uint32_t w[8];
-  ristretto_encode(w, p);
+  ristretto_encode_post(w, p, u1, u2, inv);
   st_words8(comp + 8 * e, w);
 }
 
