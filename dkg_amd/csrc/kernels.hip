@@ -512,8 +512,10 @@ __global__ __launch_bounds__(256) void k_copy_pos(size_t width, size_t npad, siz
 // rows still to be read (the steps above r ~ 105 at n=1024 took 290-330 us, bimodal), while below
 // it the next launch finds the plain-stored rows cached.  runtime.hip picks NT per step by that
 // footprint (binom_nt, DKG_BINOM_NT_BYTES; profiles/r06_binom_levers_ab.txt).
-// A/B knobs of the same kind for the other large table writers (0: plain stores): the stepping's
-// evaluations R and dense Z copy, the normalisation's affine addends, the per-wave binomial
+// A/B knobs of the same kind for the other large table writers (0: plain stores, the default): the
+// stepping's evaluations R and dense Z copy, the normalisation's affine addends, the per-wave binomial,
+// the recombination's output -- each measured neutral on the whole ceremony (round 6, recipe r06d,
+// profiles/r06_binom_levers_ab.txt), so they stay off
 #ifndef DKG_STEP_NT
 #define DKG_STEP_NT 0
 #endif
