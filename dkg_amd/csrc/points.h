@@ -340,6 +340,24 @@ DKG_DEV void ge_to_cached_ded(ge_cached& c, const ge_p3& p) {
   fe_dbl(c.T2d, p.T);       // 2T in the 2dT slot
 }
 DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int stride = 64) {
+#if DKG_FE_PAIR && !defined(DKG_FE_ILP)
+  // the eight products as four independent pairs (fe_mul2: no hazard wait states between the mads)
+  fe a, b, e, h, t, u, qv, qw;
+  fe_sub(t, p.Y, p.X);
+  lds_get_fe(qv, q, 0, stride);  // Y2 + X2
+  fe_add(u, p.Y, p.X);
+  lds_get_fe(qw, q, 1, stride);  // Y2 - X2
+  fe_mul2(a, t, qv, b, u, qw);   // A = (Y1 - X1)(Y2 + X2), B = (Y1 + X1)(Y2 - X2)
+  fe_sub(e, b, a);               // F = B - A <= 1.5*2^27
+  fe_add(h, b, a);               // G = B + A <= 2^27
+  lds_get_fe(qv, q, 3, stride);  // 2 T2
+  lds_get_fe(qw, q, 2, stride);  // 2 Z2
+  fe_mul2(a, p.Z, qv, b, p.T, qw);  // C = 2 Z1 T2, D = 2 T1 Z2
+  fe_add(t, b, a);               // E = D + C <= 2^27
+  fe_sub(b, b, a);               // H = D - C <= 1.5*2^27
+  fe_mul2(r.X, t, e, r.T, t, b);  // X3 = E F, T3 = E H
+  fe_mul2(r.Y, h, b, r.Z, h, e);  // Y3 = G H, Z3 = F G
+#else
   fe a, b, e, h, t, qv;
   fe_sub(t, p.Y, p.X);
   lds_get_fe(qv, q, 0, stride);  // Y2 + X2
@@ -359,6 +377,7 @@ DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int str
   fe_mul(r.Y, h, b);             // Y3 = G H
   fe_mul(r.T, t, b);             // T3 = E H
   fe_mul(r.Z, h, e);             // Z3 = F G  (x19 operands F and H, computed once each)
+#endif
 }
 
 // The dedicated addition with a signed addend and an optional T (the m-chains of the per-wave
