@@ -72,10 +72,29 @@ DKG_DEV void ge_cached_neg(ge_cached& r, const ge_cached& c) {
   fe_carry(r.T2d, r.T2d);
 }
 
+// IL = true (the template argument of the formulas below): the same products, operand for operand,
+// as pairs (fe_mul2 / fe_sq2: two interleaved chains, fewer hazard wait states) at the cost of one
+// more field temporary live; for the kernels with VGPRs to spare (profiles/r06_pair_ab.txt).
 // Additions are written so that (a, b) collapse into (e, h) before (c, d) are formed: at most
 // four field temporaries are live next to the operands (keeps the kernels at <= 128 VGPRs).
 // r = p + q  (8M).  r may alias p.
+template <bool IL = false>
 DKG_DEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
+  if constexpr (IL && DKG_PW) {
+    // the same products, operand for operand, as four pairs (fe_mul2)
+    fe a, b, e, h, t, u;
+    fe_sub(t, p.Y, p.X);
+    fe_add(u, p.Y, p.X);
+    fe_mul2(a, t, q.YmX, b, u, q.YpX);
+    fe_sub(e, b, a);
+    fe_add(h, b, a);
+    fe_mul2(a, p.T, q.T2d, b, p.Z, q.Z2);  // c, d
+    fe_sub(t, b, a);          // f
+    fe_add(b, b, a);          // g
+    fe_mul2(r.X, e, t, r.Y, b, h);
+    fe_mul2(r.Z, b, t, r.T, e, h);
+    return;
+  }
   fe a, b, e, h, t;
   fe_sub(t, p.Y, p.X);      // <= 1.5*2^27
   fe_mul(a, t, q.YmX);
@@ -113,7 +132,26 @@ DKG_DEV void ge_sub(ge_p3& r, const ge_p3& p, const ge_cached& q) {
 }
 
 // r = p + q with q affine Niels (Z = 1): 7M.
+template <bool IL = false>
 DKG_DEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_aff& q) {
+  if constexpr (IL && DKG_PW) {
+    // the four result products as two pairs; A and B stay single (pairing them too pushes the 128-VGPR
+    // comb kernels into scratch)
+    fe a, b, e, h, t;
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, q.ymx);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, q.ypx);
+    fe_sub(e, b, a);
+    fe_add(h, b, a);
+    fe_mul(a, p.T, q.xy2d);   // c
+    fe_dbl(b, p.Z);           // d <= 2^27
+    fe_sub(t, b, a);          // f
+    fe_add(b, b, a);          // g
+    fe_mul2(r.X, t, e, r.Y, h, b);
+    fe_mul2(r.Z, t, b, r.T, h, e);
+    return;
+  }
   fe a, b, e, h, t;
   fe_sub(t, p.Y, p.X);
   fe_mul(a, t, q.ymx);
@@ -150,8 +188,24 @@ DKG_DEV void ge_msub(ge_p3& r, const ge_p3& p, const ge_aff& q) {
 }
 
 // r = 2p (4S + 4M); with_t = false skips T (valid when the next op is another doubling).
-template <bool with_t = true>
+template <bool with_t = true, bool IL = false>
 DKG_DEV void ge_dbl(ge_p3& r, const ge_p3& p) {
+  if constexpr (IL && DKG_PW) {
+    fe a, b, c, e, f, g, h, t;
+    fe_add(t, p.X, p.Y);
+    fe_sq2(a, p.X, b, p.Y);
+    fe_sq2(c, p.Z, t, t);
+    fe_dbl(c, c);
+    fe_add(h, a, b);
+    fe_sub(e, h, t);
+    fe_sub(g, a, b);
+    fe_add(f, c, g);
+    fe_carry(f, f);
+    fe_mul2(r.X, e, f, r.Y, g, h);
+    if (with_t) fe_mul2(r.Z, g, f, r.T, e, h);
+    else fe_mul(r.Z, g, f);
+    return;
+  }
   fe a, b, c, e, f, g, h, t;
   fe_sq(a, p.X);
   fe_sq(b, p.Y);
@@ -171,7 +225,24 @@ DKG_DEV void ge_dbl(ge_p3& r, const ge_p3& p) {
 }
 
 // Doubling with a run-time (wave-uniform) choice of whether T is produced.
+template <bool IL = false>
 DKG_DEV void ge_dbl_rt(ge_p3& r, const ge_p3& p, bool with_t) {
+  if constexpr (IL && DKG_PW) {
+    fe a, b, c, t, h, e, g;
+    fe_add(t, p.X, p.Y);
+    fe_sq2(a, p.X, b, p.Y);
+    fe_sq2(c, p.Z, t, t);
+    fe_dbl(c, c);
+    fe_add(h, a, b);
+    fe_sub(e, h, t);
+    fe_sub(g, a, b);
+    fe_add(c, c, g);
+    fe_carry(c, c);
+    fe_mul2(r.X, e, c, r.Y, g, h);
+    if (with_t) fe_mul2(r.Z, g, c, r.T, e, h);
+    else fe_mul(r.Z, g, c);
+    return;
+  }
   fe a, b, c, t, h, e, g;
   fe_sq(a, p.X);
   fe_sq(b, p.Y);
@@ -191,7 +262,24 @@ DKG_DEV void ge_dbl_rt(ge_p3& r, const ge_p3& p, bool with_t) {
 }
 
 // Doubling with the fewest simultaneously live temporaries (inputs consumed early; r may alias p).
+template <bool IL = false>
 DKG_DEV void ge_dbl_lean(ge_p3& r, const ge_p3& p, bool with_t) {
+  if constexpr (IL && DKG_PW) {
+    fe a, b, t, h, g;
+    fe_sq2(a, p.X, b, p.Y);
+    fe_add(h, a, b);
+    fe_sub(g, a, b);
+    fe_add(a, p.X, p.Y);
+    fe_sq2(t, p.Z, a, a);     // Z^2, (X+Y)^2
+    fe_dbl(t, t);
+    fe_add(t, t, g);
+    fe_carry(t, t);           // f
+    fe_sub(b, h, a);          // e
+    fe_mul2(r.X, b, t, r.Y, g, h);
+    if (with_t) fe_mul2(r.Z, g, t, r.T, b, h);
+    else fe_mul(r.Z, g, t);
+    return;
+  }
   fe a, b, t, h, g;
   fe_sq(a, p.X);
   fe_sq(b, p.Y);
@@ -214,6 +302,7 @@ DKG_DEV void ge_dbl_lean(ge_p3& r, const ge_p3& p, bool with_t) {
 // which of (Y+X, Y-X) multiplies which, and the sign of the 2dT product.
 // with_t = false skips T (one product): valid when the next operation is a doubling, which does not
 // read it.
+template <bool IL = false>
 DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg, bool with_t = true) {
   fe a, b, e, h, t, qa, qb;
 #pragma unroll
@@ -221,23 +310,40 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
     qa.v[i] = neg ? q.YpX.v[i] : q.YmX.v[i];
     qb.v[i] = neg ? q.YmX.v[i] : q.YpX.v[i];
   }
-  fe_sub(t, p.Y, p.X);
-  fe_mul(a, t, qa);
-  fe_add(t, p.Y, p.X);
-  fe_mul(b, t, qb);
+  if constexpr (IL && DKG_PW) {
+    fe u;
+    fe_sub(t, p.Y, p.X);
+    fe_add(u, p.Y, p.X);
+    fe_mul2(a, t, qa, b, u, qb);
+  } else {
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, qa);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, qb);
+  }
   fe_sub(e, b, a);
   fe_add(h, b, a);
-  fe_mul(a, p.T, q.T2d);    // c  (the term whose sign flips with q)
-  fe_mul(b, p.Z, q.Z2);     // d
+  if constexpr (IL && DKG_PW) {
+    fe_mul2(a, p.T, q.T2d, b, p.Z, q.Z2);  // c (the term whose sign flips with q), d
+  } else {
+    fe_mul(a, p.T, q.T2d);  // c  (the term whose sign flips with q)
+    fe_mul(b, p.Z, q.Z2);   // d
+  }
   fe na;
   fe_neg(na, a);            // -c = 2p - c <= 2p limbwise: a valid fe_sub subtrahend as is
   fe_cmov(a, na, neg);      // a = +/-c (limbs <= 2^27)
   fe_sub(t, b, a);          // f = d - (+/-c) <= 1.5*2^27
   fe_add(b, b, a);          // g <= 2^27
-  fe_mul(r.X, e, t);
-  fe_mul(r.Y, b, h);
-  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
-  if (with_t) fe_mul(r.T, e, h);
+  if constexpr (IL && DKG_PW) {
+    fe_mul2(r.X, e, t, r.Y, b, h);
+    if (with_t) fe_mul2(r.Z, b, t, r.T, e, h);
+    else fe_mul(r.Z, b, t);
+  } else {
+    fe_mul(r.X, e, t);
+    fe_mul(r.Y, b, h);
+    fe_mul(r.Z, b, t);      // the x19 operands are F (X, Z) and H (Y, T): computed once each
+    if (with_t) fe_mul(r.T, e, h);
+  }
 }
 
 // r = p + q (neg = false) or p - q (neg = true), q affine Niels (Z = 1): 7M, one code path.  The
@@ -245,6 +351,7 @@ DKG_DEV void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool ne
 // f and g keep ge_add_signed's bounds whatever the sign.  q's fields are second operands only, so
 // they may carry the cached form's uncarried bounds (y+x <= 2^27, y-x <= 2^27.585;
 // tools/fe_bounds.py).
+template <bool IL = false>
 DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg, bool with_t = true) {
   fe a, b, e, h, t, qa, qb;
 #pragma unroll
@@ -252,10 +359,17 @@ DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg,
     qa.v[i] = neg ? q.ypx.v[i] : q.ymx.v[i];
     qb.v[i] = neg ? q.ymx.v[i] : q.ypx.v[i];
   }
-  fe_sub(t, p.Y, p.X);
-  fe_mul(a, t, qa);
-  fe_add(t, p.Y, p.X);
-  fe_mul(b, t, qb);
+  if constexpr (IL && DKG_PW) {
+    fe u;
+    fe_sub(t, p.Y, p.X);
+    fe_add(u, p.Y, p.X);
+    fe_mul2(a, t, qa, b, u, qb);
+  } else {
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, qa);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, qb);
+  }
   fe_sub(e, b, a);
   fe_add(h, b, a);
   fe_mul(a, p.T, q.xy2d);   // c
@@ -266,10 +380,16 @@ DKG_DEV void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_aff& q, bool neg,
   fe_carry(b, b);           // d = 2Z, tight
   fe_sub(t, b, a);          // f = d - (+/-c)
   fe_add(b, b, a);          // g = d + (+/-c)
-  fe_mul(r.X, e, t);
-  fe_mul(r.Y, b, h);
-  fe_mul(r.Z, b, t);        // the x19 operands are F (X, Z) and H (Y, T): computed once each
-  if (with_t) fe_mul(r.T, e, h);
+  if constexpr (IL && DKG_PW) {
+    fe_mul2(r.X, e, t, r.Y, b, h);
+    if (with_t) fe_mul2(r.Z, b, t, r.T, e, h);
+    else fe_mul(r.Z, b, t);
+  } else {
+    fe_mul(r.X, e, t);
+    fe_mul(r.Y, b, h);
+    fe_mul(r.Z, b, t);      // the x19 operands are F (X, Z) and H (Y, T): computed once each
+    if (with_t) fe_mul(r.T, e, h);
+  }
 }
 
 // ---- Ristretto255 (RFC 9496 section 4.3) ----

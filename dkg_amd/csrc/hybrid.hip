@@ -130,6 +130,14 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uin
 // lanes]; the addend of the next nonzero digit is copied into the wave's LDS slot by LDS-DMA
 // (global_load_lds, no VGPRs) right after the previous addition, and lands during the >= 3 doublings
 // in between.  LDS stays one point per wave (4 waves per SIMD, as k_dec_mul).
+// DKG_DEC_W4_WAVES: the launch bound's waves per SIMD (4: <= 128 VGPRs); DKG_DEC_IL: paired
+// products in the chain's doublings and additions (ge25519.h IL).  A/B knobs.
+#ifndef DKG_DEC_W4_WAVES
+#define DKG_DEC_W4_WAVES 4
+#endif
+#ifndef DKG_DEC_IL
+#define DKG_DEC_IL 0
+#endif
 typedef __attribute__((address_space(3))) uint32_t dec_lds_u32;
 typedef __attribute__((address_space(1))) uint32_t dec_g_u32;
 
@@ -144,7 +152,7 @@ DKG_DEV void glds_words(const dec_g_u32* sg, uint32_t* q) {
   }
 }
 
-__global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const uint32_t* __restrict__ sk,
+__global__ __launch_bounds__(64, DKG_DEC_W4_WAVES) void k_dec_mul_w4(size_t D, size_t n, const uint32_t* __restrict__ sk,
                                                       const uint32_t* __restrict__ R_ext, uint32_t* __restrict__ K_ext,
                                                       uint32_t* __restrict__ T, size_t q0) {
   __shared__ uint32_t qs[PT_WORDS * 64];
@@ -240,15 +248,15 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul_w4(size_t D, size_t n, const 
       const int be = __builtin_amdgcn_readfirstlane((int)nzb[e]);
       const int de = __builtin_amdgcn_readfirstlane((int)nzd[e]);
 #pragma unroll 1
-      for (; b > be; b--) ge_dbl_lean(x, x, b - 1 == be);  // T only before the addition
+      for (; b > be; b--) ge_dbl_lean<DKG_DEC_IL != 0>(x, x, b - 1 == be);  // T only before the addition
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the DMA'd addend has landed
       __builtin_amdgcn_s_barrier();
-      ge_add_lds(x, x, qcol, de < 0, 64, be == 0);          // a doubling follows unless be = 0
+      ge_add_lds<DKG_DEC_IL != 0>(x, x, qcol, de < 0, 64, be == 0);  // a doubling follows unless be = 0
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done
       if (e + 1 < nnz) fetch(e + 1);
     }
 #pragma unroll 1
-    for (; b > 0; b--) ge_dbl_lean(x, x, b == 1);          // trailing zero digits
+    for (; b > 0; b--) ge_dbl_lean<DKG_DEC_IL != 0>(x, x, b == 1);  // trailing zero digits
   }
   if (live) pt_store(K_ext, count, idx, x);
 }

@@ -358,8 +358,27 @@ void poly_eval(size_t D, size_t N, const uint32_t* coeffs, size_t M, const uint3
                      out);
 }
 
+// Paired products (ge25519.h, IL = true) per kernel family: the per-step binomial's m-chain, the
+// per-wave binomial's, the recombination's chain, the checks' combs (ge_madd: its result products
+// only).  Off for the binomials: capped at 128 / 168 VGPRs, the pairs push them into scratch
+// (k_binom_step 0 -> 56 B per lane, k_binom_wave 28 -> 84 B; pairing only the result products
+// still spills).  Each is an A/B knob.
+#ifndef DKG_BINOM_IL
+#define DKG_BINOM_IL 0
+#endif
+#ifndef DKG_WAVE_IL
+#define DKG_WAVE_IL 0
+#endif
+#ifndef DKG_AFF_IL
+#define DKG_AFF_IL 1
+#endif
+#ifndef DKG_CHECK_IL
+#define DKG_CHECK_IL 1
+#endif
+
 // ------------------------------------------------------------------ K3a binomial-basis Horner
 // y = m * y, m wave-uniform; q = this lane's column of the wave's 40 x 64-word LDS slot (clobbered).
+template <bool IL = false>
 __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q) {
   uint32_t pos, neg;
   const int len = small_recode(m, pos, neg);
@@ -373,14 +392,15 @@ __device__ __forceinline__ void mul_small_lds(ge_p3& y, uint32_t m, uint32_t* q)
   for (int i = len - 2; i >= 0; i--) {
     const uint32_t bit = 1u << i;
     const bool nz = ((pos | neg) & bit) != 0;
-    ge_dbl_lean(y, y, nz || i == 0);
-    if (nz) ge_add_lds(y, y, q, (neg & bit) != 0, 64, i == 0);  // T only for the result
+    ge_dbl_lean<IL>(y, y, nz || i == 0);
+    if (nz) ge_add_lds<IL>(y, y, q, (neg & bit) != 0, 64, i == 0);  // T only for the result
   }
 }
 
 // mul_small_lds with the dedicated additions (k_binom_wave<.., DED>): the base's cached form needs no
 // product by d; `bad` is set when an addition's Z vanished (then the caller redoes the column group
 // with the complete formula)
+template <bool IL = false>
 __device__ __forceinline__ void mul_small_ded_lds(ge_p3& y, uint32_t m, uint32_t* q, bool& bad) {
   uint32_t pos, neg;
   const int len = small_recode(m, pos, neg);
@@ -394,9 +414,9 @@ __device__ __forceinline__ void mul_small_ded_lds(ge_p3& y, uint32_t m, uint32_t
   for (int i = len - 2; i >= 0; i--) {
     const uint32_t bit = 1u << i;
     const bool nz = ((pos | neg) & bit) != 0;
-    ge_dbl_lean(y, y, nz || i == 0);
+    ge_dbl_lean<IL>(y, y, nz || i == 0);
     if (nz) {
-      ge_add_ded_lds_s(y, y, q, (neg & bit) != 0, 64, i == 0);  // T only for the result
+      ge_add_ded_lds_s<IL>(y, y, q, (neg & bit) != 0, 64, i == 0);  // T only for the result
       bad |= fe_tight_zero(y.Z);
     }
   }
@@ -594,7 +614,7 @@ __global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad,
     bool bad = false;
     ge_add_ded_lds(x, x, q);                   // e_{m-1} + e_m
     bad |= fe_tight_zero(x.Z);
-    mul_small_ded_lds(x, (uint32_t)m, q, bad);  // * m
+    mul_small_ded_lds<DKG_BINOM_IL != 0>(x, (uint32_t)m, q, bad);  // * m
     const size_t gcol = col_base + (size_t)grp * blockDim.x + threadIdx.x;
     const bool real = (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
     if (__ballot(bad && real) != 0 && threadIdx.x == 0)  // fany: one word for the whole table
@@ -786,7 +806,7 @@ __global__ __launch_bounds__(64, PF ? 2 : (CARRY ? DKG_BINOM_WAVE_WAVES : 4)) vo
       if constexpr (DED) {
         ge_add_ded_lds(x, x, q);         // e_{m-1} + e_m
         bad |= fe_tight_zero(x.Z);
-        mul_small_ded_lds(x, (uint32_t)m, q, bad);  // * m
+        mul_small_ded_lds<DKG_WAVE_IL != 0>(x, (uint32_t)m, q, bad);  // * m
       } else {
         ge_add_lds(x, x, q, false);        // e_{m-1} + e_m
         mul_small_lds(x, (uint32_t)m, q);  // * m
@@ -1620,8 +1640,8 @@ DKG_DEV void aff_position(ge_p3& acc, uint64_t w, const uint32_t* qs, const ge_a
     const int e = (int8_t)(w >> (8 * U));
     if (e != 0) {
       const bool t = last || higher_digits64<U, K>(w);  // else a doubling follows: no T
-      if constexpr (U < KL) ge_madd_lds(acc, acc, qs + U * AFF_WORDS * 64 + threadIdx.x, e < 0, 64, t);
-      else ge_madd_signed(acc, acc, qr[U - KL], e < 0, t);
+      if constexpr (U < KL) ge_madd_lds<DKG_AFF_IL != 0>(acc, acc, qs + U * AFF_WORDS * 64 + threadIdx.x, e < 0, 64, t);
+      else ge_madd_signed<DKG_AFF_IL != 0>(acc, acc, qr[U - KL], e < 0, t);
     }
     aff_position<U + 1, K, KL>(acc, w, qs, qr, last);
   }
@@ -1652,7 +1672,7 @@ __global__ __launch_bounds__(64, K == 2 ? 3 : 2) void k_combine_aff(size_t width
     // the bytes of pieces 4..7
     uint64_t w = (uint32_t)__builtin_amdgcn_readfirstlane(dw[b]);
     if constexpr (K > 4) w |= (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(dw1[b]) << 32;
-    if (b != tp) ge_dbl_lean(acc, acc, w != 0 || b == 0);
+    if (b != tp) ge_dbl_lean<DKG_AFF_IL != 0>(acc, acc, w != 0 || b == 0);
     aff_position<0, K, KL>(acc, w, qs, qr, b == 0);
   }
   if (live) pt_store_aos<DKG_COMB_NT != 0>(R, c * nrecv + j, acc);
@@ -1756,7 +1776,7 @@ __global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_check_both(size_t ndeal
     ge_identity(acc);
     sc_load(x, s + 8 * q);
     if (scale) sc_mont_mul(x, x, f);
-    combw_mul_add(acc, x, tab_g);                  // G::generator() * s   (committee.rs:294, :537)
+    combw_mul_add<DKG_CHECK_IL != 0>(acc, x, tab_g);  // G::generator() * s   (committee.rs:294, :537)
     pt_load_aos(r, R, cA * nrecv + j);
     const bool eq = ristretto_eq(acc, r);          // round 4 (:541)
     dec4[q] = self ? 2 : ((dok[cA] && eq) ? 1 : 0);  // missing A: accusation (committee.rs:549-555)
@@ -1769,7 +1789,7 @@ __global__ __launch_bounds__(256, DKG_COMB_WAVES) void k_check_both(size_t ndeal
   }
   sc_load(x, sp + 8 * q);
   if (scale) sc_mont_mul(x, x, f);
-  combw_mul_add(acc, x, tab_h);                    // + h * s'              (committee.rs:292-293)
+  combw_mul_add<DKG_CHECK_IL != 0>(acc, x, tab_h);  // + h * s'              (committee.rs:292-293)
   pt_load_aos(r, R, cE * nrecv + j);
   const bool eq = ristretto_eq(acc, r);            // round 2 (:305)
   dec2[q] = self ? 2 : (dok[cE] ? (eq ? 1 : 0) : 4);  // missing E: disqualified, no complaint (:331-335)

@@ -261,7 +261,7 @@ DKG_DEV void combw_select(ge_aff& r, const uint4 (&e)[8], bool neg, bool zero) {
 // acc += s * B with the radix-2^BITS comb of B.  (Loading each window's entry one window ahead
 // measured no gain -- check 48.0 vs 47.7 ms on config 5 -- and pushed the kernels into scratch at 128
 // VGPRs: profiles/r05_comb_radix_ab.txt.)
-template <int BITS>
+template <int BITS, bool IL = false>
 DKG_DEV void combw_mul_add_r(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
   int carry = 0;
   bool neg, zero;
@@ -273,12 +273,13 @@ DKG_DEV void combw_mul_add_r(ge_p3& acc, const sc& s, const uint32_t* __restrict
     for (int k = 0; k < 8; k++) e[k] = p[k];
     ge_aff r;
     combw_select(r, e, neg, zero);
-    ge_madd(acc, acc, r);
+    ge_madd<IL>(acc, acc, r);
   }
 }
 // the shared bases' combs (g, h: radix 2^DKG_COMBW_BITS)
+template <bool IL = false>
 DKG_DEV void combw_mul_add(ge_p3& acc, const sc& s, const uint32_t* __restrict__ tab) {
-  combw_mul_add_r<COMBW_BITS>(acc, s, tab);
+  combw_mul_add_r<COMBW_BITS, IL>(acc, s, tab);
 }
 
 
@@ -302,8 +303,29 @@ DKG_DEV void lds_get_fe(fe& r, const uint32_t* q, int which, int stride = 64) {
 }
 
 // r = p +/- Q with Q the cached point in LDS; `neg` must be wave-uniform.
+template <bool IL = false>
 DKG_DEV void ge_add_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,
                         bool with_t = true) {
+  if constexpr (IL && DKG_PW) {
+    fe a, b, e, h, t, u, qv, qw;
+    fe_sub(t, p.Y, p.X);
+    lds_get_fe(qv, q, neg ? 0 : 1, stride);
+    fe_add(u, p.Y, p.X);
+    lds_get_fe(qw, q, neg ? 1 : 0, stride);
+    fe_mul2(a, t, qv, b, u, qw);
+    fe_sub(e, b, a);
+    fe_add(h, b, a);
+    lds_get_fe(qv, q, 3, stride);
+    lds_get_fe(qw, q, 2, stride);
+    fe_mul2(a, p.T, qv, b, p.Z, qw);  // c, d
+    if (neg) fe_neg(a, a);
+    fe_sub(t, b, a);          // f
+    fe_add(b, b, a);          // g
+    fe_mul2(r.X, e, t, r.Y, b, h);
+    if (with_t) fe_mul2(r.Z, b, t, r.T, e, h);
+    else fe_mul(r.Z, b, t);
+    return;
+  }
   fe a, b, e, h, t, qv;
   fe_sub(t, p.Y, p.X);
   lds_get_fe(qv, q, neg ? 0 : 1, stride);
@@ -384,8 +406,29 @@ DKG_DEV void ge_add_ded_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, int str
 // binomial): r = p +/- Q, Q as ge_to_cached_ded in LDS, -Q = (Y-X, Y+X, 2Z, -2T) -- the fields
 // swapped and C negated exactly as ge_add_lds does (the same bounds).  `neg` wave-uniform.  Not
 // complete (above): the caller tests r.Z.
+template <bool IL = false>
 DKG_DEV void ge_add_ded_lds_s(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,
                               bool with_t = true) {
+  if constexpr (IL && DKG_PW) {
+    fe a, b, e, h, t, u, qv, qw;
+    fe_sub(t, p.Y, p.X);
+    lds_get_fe(qv, q, neg ? 1 : 0, stride);
+    fe_add(u, p.Y, p.X);
+    lds_get_fe(qw, q, neg ? 0 : 1, stride);
+    fe_mul2(a, t, qv, b, u, qw);   // A, B
+    fe_sub(e, b, a);               // F
+    fe_add(h, b, a);               // G
+    lds_get_fe(qv, q, 3, stride);
+    lds_get_fe(qw, q, 2, stride);
+    fe_mul2(a, p.Z, qv, b, p.T, qw);  // C, D
+    if (neg) fe_neg(a, a);
+    fe_add(t, b, a);               // E
+    fe_sub(b, b, a);               // H
+    fe_mul2(r.X, t, e, r.Y, h, b);
+    if (with_t) fe_mul2(r.Z, h, e, r.T, t, b);
+    else fe_mul(r.Z, h, e);
+    return;
+  }
   fe a, b, e, h, t, qv;
   fe_sub(t, p.Y, p.X);
   lds_get_fe(qv, q, neg ? 1 : 0, stride);
@@ -410,8 +453,30 @@ DKG_DEV void ge_add_ded_lds_s(ge_p3& r, const ge_p3& p, const uint32_t* q, bool 
 
 // r = p +/- Q with Q affine Niels (y+x, y-x, 2dxy) in LDS, read like the cached form above (fields
 // 0, 1, 2): 7M, d = 2Z carried as in ge_madd_signed.  `neg` must be wave-uniform.
+template <bool IL = false>
 DKG_DEV void ge_madd_lds(ge_p3& r, const ge_p3& p, const uint32_t* q, bool neg, int stride = 64,
                          bool with_t = true) {
+  if constexpr (IL && DKG_PW) {
+    fe a, b, e, h, t, u, qv, qw;
+    fe_sub(t, p.Y, p.X);
+    lds_get_fe(qv, q, neg ? 0 : 1, stride);
+    fe_add(u, p.Y, p.X);
+    lds_get_fe(qw, q, neg ? 1 : 0, stride);
+    fe_mul2(a, t, qv, b, u, qw);
+    fe_sub(e, b, a);
+    fe_add(h, b, a);
+    lds_get_fe(qv, q, 2, stride);
+    fe_mul(a, p.T, qv);       // c
+    if (neg) fe_neg(a, a);
+    fe_dbl(b, p.Z);
+    fe_carry(b, b);           // d = 2Z, tight
+    fe_sub(t, b, a);          // f
+    fe_add(b, b, a);          // g
+    fe_mul2(r.X, e, t, r.Y, b, h);
+    if (with_t) fe_mul2(r.Z, b, t, r.T, e, h);
+    else fe_mul(r.Z, b, t);
+    return;
+  }
   fe a, b, e, h, t, qv;
   fe_sub(t, p.Y, p.X);
   lds_get_fe(qv, q, neg ? 0 : 1, stride);

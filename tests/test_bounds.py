@@ -26,6 +26,17 @@ def test_terms_follow_the_header():
         assert F._columns("fe_sq_ps", f, f, "x") == F._columns("fe_sq_cs", f, f, "x")
 
 
+def test_pair_products_are_generated_from_the_singles():
+    """fe_mul2 / fe_sq2 (the interleaved pair products) are generated from fe_mul_ps / fe_sq_ps by
+    tools/gen_fe_pair.py, so the bounds checked above cover them only while the header holds exactly
+    what the generator makes of the current single products."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_fe_pair.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_no_overflow_anywhere():
     tight = F.run()
     assert F.violations == [], F.violations
