@@ -129,14 +129,16 @@ __global__ __launch_bounds__(64, 4) void k_dec_mul(size_t D, size_t n, const uin
 // multiples R, 3R, 5R, 7R (cached form) live in a global table T laid out [wave][4][40 words][64
 // lanes]; the addend of the next nonzero digit is copied into the wave's LDS slot by LDS-DMA
 // (global_load_lds, no VGPRs) right after the previous addition, and lands during the >= 3 doublings
-// in between.  LDS stays one point per wave (4 waves per SIMD, as k_dec_mul).
-// DKG_DEC_W4_WAVES: the launch bound's waves per SIMD (4: <= 128 VGPRs); DKG_DEC_IL: paired
-// products in the chain's doublings and additions (ge25519.h IL).  A/B knobs.
+// in between.  LDS stays one point per wave.
+// DKG_DEC_W4_WAVES: the launch bound's waves per SIMD; DKG_DEC_IL: paired products in the chain's
+// doublings and additions (ge25519.h IL).  3 waves at <= 168 VGPRs with pairs (no scratch in the
+// chain) against 4 at 128 without (24 VGPRs spilled in the table setup): full mode 111.6-111.7 against
+// 112.8-113.0 ms per ceremony, k_dec_mul_w4 18.7-19.1 against 19.5-19.9 ms (profiles/r06_pair_ab.txt).
 #ifndef DKG_DEC_W4_WAVES
-#define DKG_DEC_W4_WAVES 4
+#define DKG_DEC_W4_WAVES 3
 #endif
 #ifndef DKG_DEC_IL
-#define DKG_DEC_IL 0
+#define DKG_DEC_IL 1
 #endif
 typedef __attribute__((address_space(3))) uint32_t dec_lds_u32;
 typedef __attribute__((address_space(1))) uint32_t dec_g_u32;
