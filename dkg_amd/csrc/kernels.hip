@@ -569,8 +569,11 @@ DKG_DEV void binom_pt_store(uint32_t* __restrict__ base, size_t stride, size_t e
 // Z = 0 marks flags[0] (fany: the driver's guard word, runtime.hip with_binom_ded, which reruns the
 // verification with the complete formula) or flags[its (piece, column group)] (binomial_wave_redo
 // rebuilds the marked groups after the last step, DKG_BINOM_STEP_DED=2).
+#ifndef DKG_BINOM_STEP_WAVES  // launch bound of k_binom_step: waves per SIMD (4: <= 128 VGPRs)
+#define DKG_BINOM_STEP_WAVES 4
+#endif
 template <bool DED, bool NT>
-__global__ __launch_bounds__(64, 4) void k_binom_step(int r, int k, size_t npad, size_t N,
+__global__ __launch_bounds__(64, DKG_BINOM_STEP_WAVES) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
                                                     size_t pstride, unsigned gx, unsigned last_piece,
