@@ -425,6 +425,73 @@ DKG_DEV bool fe_sqrt_ratio_m1(fe& r, const fe& u, const fe& v) {
   return correct || flipped;
 }
 
+// Two independent SQRT_RATIO_M1 chains at once (k_encode with DKG_ENCODE_PAIR: the inverse square
+// roots of a lane's two points), every product and square as a pair (fe_mul2 / fe_sq2): the same
+// operations, operand for operand, as fe_sqrt_ratio_m1 on each.
+DKG_DEV void fe_sq_x2(fe (&r)[2], const fe (&a)[2]) { fe_sq2(r[0], a[0], r[1], a[1]); }
+DKG_DEV void fe_mul_x2(fe (&r)[2], const fe (&a)[2], const fe (&b)[2]) {
+  fe_mul2(r[0], a[0], b[0], r[1], a[1], b[1]);
+}
+DKG_DEV void fe_sqn_x2(fe (&r)[2], const fe (&a)[2], int n) {
+  fe_sq_x2(r, a);
+  for (int i = 1; i < n; i++) fe_sq_x2(r, r);
+}
+DKG_DEV void fe_pow22523_x2(fe (&out)[2], const fe (&z)[2]) {
+  fe t0[2], t1[2], t2[2];
+  fe_sq_x2(t0, z);            // 2
+  fe_sqn_x2(t1, t0, 2);       // 8
+  fe_mul_x2(t1, z, t1);       // 9
+  fe_mul_x2(t0, t0, t1);      // 11
+  fe_sq_x2(t0, t0);           // 22
+  fe_mul_x2(t0, t1, t0);      // 2^5 - 1
+  fe_sqn_x2(t1, t0, 5);
+  fe_mul_x2(t0, t1, t0);      // 2^10 - 1
+  fe_sqn_x2(t1, t0, 10);
+  fe_mul_x2(t1, t1, t0);      // 2^20 - 1
+  fe_sqn_x2(t2, t1, 20);
+  fe_mul_x2(t1, t2, t1);      // 2^40 - 1
+  fe_sqn_x2(t1, t1, 10);
+  fe_mul_x2(t0, t1, t0);      // 2^50 - 1
+  fe_sqn_x2(t1, t0, 50);
+  fe_mul_x2(t1, t1, t0);      // 2^100 - 1
+  fe_sqn_x2(t2, t1, 100);
+  fe_mul_x2(t1, t2, t1);      // 2^200 - 1
+  fe_sqn_x2(t1, t1, 50);
+  fe_mul_x2(t0, t1, t0);      // 2^250 - 1
+  fe_sqn_x2(t0, t0, 2);       // 2^252 - 4
+  fe_mul_x2(out, t0, z);      // 2^252 - 3
+}
+// r[k] = SQRT_RATIO_M1(1, v[k]).r (the encoding's inverse square root; was_square is not needed there)
+DKG_DEV void fe_invsqrt_x2(fe (&r)[2], const fe (&v)[2]) {
+  fe v3[2], t[2];
+  fe_sq_x2(v3, v);
+  fe_mul_x2(v3, v3, v);       // v^3
+  fe_sq_x2(t, v3);
+  fe_mul_x2(t, t, v);         // v^7 (= u v^7 with u = 1)
+  fe_pow22523_x2(t, t);       // (v^7)^((p-5)/8)
+  fe_mul_x2(r, t, v3);        // r = v^3 (v^7)^((p-5)/8)
+  fe chk[2];
+  fe_sq_x2(chk, r);
+  fe_mul_x2(chk, chk, v);     // v r^2
+  fe sqrtm1, one, neg_one, neg_i;
+  fe_ld(sqrtm1, ge_const::SQRT_M1);
+  fe_one(one);
+  fe_neg(neg_one, one);
+  fe_carry(neg_one, neg_one);
+  fe_mul(neg_i, neg_one, sqrtm1);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    fe d, r_prime;
+    fe_sub(d, chk[k], neg_one);
+    const bool flipped = fe_iszero(d);
+    fe_sub(d, chk[k], neg_i);
+    const bool flipped_i = fe_iszero(d);
+    fe_mul(r_prime, r[k], sqrtm1);
+    fe_cmov(r[k], r_prime, flipped || flipped_i);
+    fe_abs(r[k], r[k]);
+  }
+}
+
 // Decode 32 bytes (as 8 LE words).  Returns false for a non-canonical / invalid encoding
 // (dalek CompressedRistretto::decompress -> None, groups.rs:78-81).
 DKG_DEV bool ristretto_decode(ge_p3& p, const uint32_t (&w)[8]) {
@@ -481,6 +548,14 @@ DKG_DEV void ristretto_encode_pre(fe& u1, fe& u2, fe& t, const ge_p3& p) {
   fe_mul(t, t, u1);
 }
 DKG_DEV void ristretto_encode_post(uint32_t (&w)[8], const ge_p3& p, const fe& u1, const fe& u2, const fe& inv);
+// u1 = (Z+Y)(Z-Y), u2 = X Y again from the reloaded point (k_encode keeps only t across the chain)
+DKG_DEV void ristretto_encode_u(fe& u1, fe& u2, const ge_p3& p) {
+  fe t;
+  fe_add(t, p.Z, p.Y);
+  fe_sub(u1, p.Z, p.Y);
+  fe_mul(u1, t, u1);
+  fe_mul(u2, p.X, p.Y);
+}
 DKG_DEV void ristretto_encode(uint32_t (&w)[8], const ge_p3& p) {
   fe u1, u2, t, inv, one;
   fe_one(one);

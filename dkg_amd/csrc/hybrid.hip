@@ -27,6 +27,9 @@ namespace dkgk {
 #ifndef DKG_ENC_BS
 #define DKG_ENC_BS 256
 #endif
+#ifndef DKG_ENC_IL  // paired result products in the combs' mixed additions (ge_madd IL; A/B knob)
+#define DKG_ENC_IL 0
+#endif
 __global__ __launch_bounds__(DKG_ENC_BS, DKG_ENC_BS == 256 ? 3 : 1) void k_enc_mul(size_t D, size_t n, const uint32_t* __restrict__ r,
                                                   const uint32_t* __restrict__ tab_gw,
                                                   const uint32_t* __restrict__ tabs_pk, uint32_t* __restrict__ R_ext,
@@ -42,10 +45,10 @@ __global__ __launch_bounds__(DKG_ENC_BS, DKG_ENC_BS == 256 ? 3 : 1) void k_enc_m
   sc_load(x, r + 8 * idx);
   ge_p3 acc;
   ge_identity(acc);
-  combw_mul_add(acc, x, tab_gw);               // e1 = G::generator() * r      (elgamal.rs:141)
+  combw_mul_add<DKG_ENC_IL != 0>(acc, x, tab_gw);  // e1 = G::generator() * r  (elgamal.rs:141)
   pt_store(R_ext, count, idx, acc);
   ge_identity(acc);
-  combw_mul_add_r<DKG_KEY_COMB_BITS>(acc, x, tab_pk);  // symmetric key = pk * r  (elgamal.rs:138-140)
+  combw_mul_add_r<DKG_KEY_COMB_BITS, DKG_ENC_IL != 0>(acc, x, tab_pk);  // key = pk * r  (elgamal.rs:138-140)
   pt_store(K_ext, count, idx, acc);
 }
 

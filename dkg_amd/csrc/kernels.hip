@@ -112,6 +112,48 @@ void gather_points(const uint32_t* src, size_t sstride, size_t step, size_t k0, 
 #ifndef DKG_ENCODE_WAVES  // minimum waves per SIMD of k_encode (3: 157 VGPRs, no scratch; 4: 128 + 88 B)
 #define DKG_ENCODE_WAVES 3
 #endif
+// DKG_ENCODE_RECOMP: only t crosses the inverse square root (u1, u2 recomputed from the reloaded point,
+// two products); DKG_ENCODE_PAIR: each lane encodes points e and e + ceil(count / 2) with the two
+// inverse square roots interleaved (fe_invsqrt_x2).  A/B knobs.
+#ifndef DKG_ENCODE_RECOMP
+#define DKG_ENCODE_RECOMP 0
+#endif
+#ifndef DKG_ENCODE_PAIR
+#define DKG_ENCODE_PAIR 0
+#endif
+#if DKG_ENCODE_PAIR
+__global__ __launch_bounds__(256, DKG_ENCODE_WAVES) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
+                                                size_t count, uint32_t* __restrict__ comp) {
+  const size_t half = (count + 1) / 2;
+  const size_t e0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e0 >= half) return;
+  const size_t e1 = e0 + half;
+  const bool two = e1 < count;  // an odd count's last lane encodes one point (twice)
+  fe t[2], inv[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    ge_p3 p;
+    fe u1, u2;
+    pt_load(p, ext, stride, (k && two) ? e1 : e0);
+    ristretto_encode_pre(u1, u2, t[k], p);
+  }
+  fe_invsqrt_x2(inv, t);
+  const uint32_t* ext2 = ext;
+  asm volatile("" : "+s"(ext2));
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (k && !two) break;
+    const size_t e = k ? e1 : e0;
+    ge_p3 p;
+    pt_load(p, ext2, stride, e);
+    fe u1, u2;
+    ristretto_encode_u(u1, u2, p);
+    uint32_t w[8];
+    ristretto_encode_post(w, p, u1, u2, inv[k]);
+    st_words8(comp + 8 * e, w);
+  }
+}
+#else
 __global__ __launch_bounds__(256, DKG_ENCODE_WAVES) void k_encode(const uint32_t* __restrict__ ext, size_t stride,
                                                 size_t count, uint32_t* __restrict__ comp) {
   size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -130,10 +172,12 @@ __global__ __launch_bounds__(256, DKG_ENCODE_WAVES) void k_encode(const uint32_t
   asm volatile("" : "+s"(ext2));
   ge_p3 p;
   pt_load(p, ext2, stride, e);
+  if (DKG_ENCODE_RECOMP) ristretto_encode_u(u1, u2, p);
   uint32_t w[8];
   ristretto_encode_post(w, p, u1, u2, inv);
   st_words8(comp + 8 * e, w);
 }
+#endif
 
 void decode_points(const uint32_t* comp, size_t count, uint32_t* ext, size_t stride, uint8_t* ok,
                    hipStream_t stream) {
@@ -153,7 +197,8 @@ void decode_position_major(const uint32_t* comp, size_t D, size_t N, size_t npad
 
 void encode_points(const uint32_t* ext, size_t stride, size_t count, uint32_t* comp, hipStream_t stream) {
   if (!count) return;
-  hipLaunchKernelGGL(k_encode, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, stream, ext, stride,
+  const size_t lanes = DKG_ENCODE_PAIR ? (count + 1) / 2 : count;
+  hipLaunchKernelGGL(k_encode, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ext, stride,
                      count, comp);
 }
 
