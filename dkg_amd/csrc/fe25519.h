@@ -98,9 +98,10 @@ DKG_DEV void fe_dbl(fe& r, const fe& a) {
 // previous column, so the carry costs no separate 64-bit add: per column one v_and (full rate) and
 // one v_lshrrev_b64 (half rate) besides the ten half-rate mads (profiles/r02_ubench_intrate3.txt:
 // shifts and 64-bit adds issue at half rate on gfx950, only add/sub/and/or at full rate).  The
-// serial chain costs no issue slots: a wave issues a mad only every ~9.5 cycles anyway
-// (tools/ubench/ilp.hip) and the SIMD interleaves the 4 resident waves and the independent
-// multiplications of each group formula.  The carry-out SGPR pair is unused.
+// serial chain costs few issue slots: a wave issues a mad only every ~9.5 cycles anyway
+// (tools/ubench/ilp.hip) and the SIMD interleaves the resident waves; the s_nop the compiler puts
+// before every mad that reads its own accumulator is mostly hidden by the other waves (the pair
+// products below recover part of it).  The carry-out SGPR pair is unused.
 DKG_DEV void mad_acc(uint64_t& h, uint32_t a, uint32_t b) {
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(h), "=s"(cc) : "v"(a), "v"(b));
@@ -112,9 +113,10 @@ DKG_DEV uint64_t mad_first(uint32_t a, uint32_t b) {
 }
 // The same for the pair products: volatile, so the two chains stay interleaved as written (the
 // compiler would otherwise regroup each chain's mads back to back), and each chain with its own
-// carry-out SGPR pair `cc` (read-write, so the two stay distinct registers): back-to-back VALU writes
-// of ONE SGPR pair, or a mad reading the accumulator the previous instruction wrote, each cost an
-// s_nop wait state; alternating chains and pairs need none.
+// carry-out SGPR pair `cc` (read-write, so the two stay distinct registers).  The hazard recogniser
+// puts one s_nop before each mad that reads its own chain's accumulator, at any distance, and one
+// between back-to-back writes of one SGPR pair: K interleaved chains with K pairs need one s_nop per
+// K mads (two chains: the stepping loop's 731 -> 356; profiles/r06_pair_ab.txt).
 DKG_DEV void mad_acc_v(uint64_t& h, uint32_t a, uint32_t b, uint64_t& cc) {
   asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(h), "+s"(cc) : "v"(a), "v"(b));
 }
