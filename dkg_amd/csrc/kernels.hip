@@ -614,11 +614,14 @@ DKG_DEV void binom_pt_store(uint32_t* __restrict__ base, size_t stride, size_t e
 // Z = 0 marks flags[0] (fany: the driver's guard word, runtime.hip with_binom_ded, which reruns the
 // verification with the complete formula) or flags[its (piece, column group)] (binomial_wave_redo
 // rebuilds the marked groups after the last step, DKG_BINOM_STEP_DED=2).
+// IL: the m-chain's doublings and additions with paired products (ge25519.h IL) under a 2-wave launch
+// bound (<= 256 VGPRs, no scratch), for the steps that leave at most ~2 waves per SIMD anyway (small
+// shards): there a step lasts as long as its longest chain, and pairs shorten the chain's latency.
 #ifndef DKG_BINOM_STEP_WAVES  // launch bound of k_binom_step: waves per SIMD (4: <= 128 VGPRs)
 #define DKG_BINOM_STEP_WAVES 4
 #endif
-template <bool DED, bool NT>
-__global__ __launch_bounds__(64, DKG_BINOM_STEP_WAVES) void k_binom_step(int r, int k, size_t npad, size_t N,
+template <bool DED, bool NT, bool IL = false>
+__global__ __launch_bounds__(64, IL ? 2 : DKG_BINOM_STEP_WAVES) void k_binom_step(int r, int k, size_t npad, size_t N,
                                                     const uint32_t* __restrict__ C,
                                                     const uint32_t* __restrict__ ein, uint32_t* __restrict__ eout,
                                                     size_t pstride, unsigned gx, unsigned last_piece,
@@ -662,14 +665,14 @@ __global__ __launch_bounds__(64, DKG_BINOM_STEP_WAVES) void k_binom_step(int r, 
     bool bad = false;
     ge_add_ded_lds(x, x, q);                   // e_{m-1} + e_m
     bad |= fe_tight_zero(x.Z);
-    mul_small_ded_lds<DKG_BINOM_IL != 0>(x, (uint32_t)m, q, bad);  // * m
+    mul_small_ded_lds<IL || DKG_BINOM_IL != 0>(x, (uint32_t)m, q, bad);  // * m
     const size_t gcol = col_base + (size_t)grp * blockDim.x + threadIdx.x;
     const bool real = (gcol / gw) * 64 + (gcol % gw) % 64 < dreal;
     if (__ballot(bad && real) != 0 && threadIdx.x == 0)  // fany: one word for the whole table
       flags[fany ? 0 : (size_t)piece * (pstride / 64) + (col_base / 64) + grp] = 1u;
   } else {
-    ge_add_lds(x, x, q, false);              // e_{m-1} + e_m
-    mul_small_lds(x, (uint32_t)m, q);        // * m
+    ge_add_lds<IL>(x, x, q, false);          // e_{m-1} + e_m
+    mul_small_lds<IL>(x, (uint32_t)m, q);    // * m
   }
   binom_pt_store<NT>(eout, S, (size_t)m * npad + d, x);
 }
@@ -733,7 +736,7 @@ void binom_init(size_t width, size_t npad, size_t N, const uint32_t* C, uint32_t
 
 void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C, const uint32_t* in, uint32_t* out,
                 hipStream_t stream, size_t pieces, size_t pstride, size_t last_len, uint32_t* flags, size_t col_base,
-                size_t dreal, unsigned gw, bool flag_any, bool nt) {
+                size_t dreal, unsigned gw, bool flag_any, bool nt, bool il) {
   const int last_off = (last_len && last_len < N) ? (int)(N - last_len) : 0;
   // width is a multiple of 64: one wave per (position 0..r, 64 dealers, piece)
   const dim3 grid((unsigned)(width / 64 * pieces), (unsigned)(r + 1));
@@ -742,6 +745,13 @@ void binom_step(size_t r, size_t width, size_t npad, size_t N, const uint32_t* C
                        (unsigned)(width / 64), (unsigned)(pieces - 1), last_off, fl, col_base, dreal, gw ? gw : 64u,
                        fany);
   };
+  if (il) {
+    if (flags && nt) go(k_binom_step<true, true, true>, flags, flag_any ? 1 : 0);
+    else if (flags) go(k_binom_step<true, false, true>, flags, flag_any ? 1 : 0);
+    else if (nt) go(k_binom_step<false, true, true>, nullptr, 0);
+    else go(k_binom_step<false, false, true>, nullptr, 0);
+    return;
+  }
   if (flags && nt) go(k_binom_step<true, true>, flags, flag_any ? 1 : 0);
   else if (flags) go(k_binom_step<true, false>, flags, flag_any ? 1 : 0);
   else if (nt) go(k_binom_step<false, true>, nullptr, 0);

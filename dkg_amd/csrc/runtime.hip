@@ -289,6 +289,25 @@ struct VerifySeg {
 #ifndef DKG_BINOM_ILP_WAVES
 #define DKG_BINOM_ILP_WAVES 1.5
 #endif
+// Product-scanning steps with fewer waves per SIMD than this run k_binom_step<.., IL> (paired
+// products at a 2-wave launch bound); the environment variable DKG_BINOM_IL_WAVES overrides it (A/B).
+#ifndef DKG_BINOM_IL_WAVES_DEFAULT
+#define DKG_BINOM_IL_WAVES_DEFAULT 0.0
+#endif
+double binom_il_waves() {
+  static const double v = [] {
+    const char* e = getenv("DKG_BINOM_IL_WAVES");
+    return e ? atof(e) : DKG_BINOM_IL_WAVES_DEFAULT;
+  }();
+  return v;
+}
+double binom_ilp_waves() {  // DKG_BINOM_ILP_WAVES, overridable the same way (A/B)
+  static const double v = [] {
+    const char* e = getenv("DKG_BINOM_ILP_WAVES");
+    return e ? atof(e) : DKG_BINOM_ILP_WAVES;
+  }();
+  return v;
+}
 // Tables of at least this many 64-column groups (all pieces, all chunks) run the binomial as one
 // launch of per-wave Horner loops (kernels.hip k_binom_wave): each wave then has a long private
 // chain, and 4 rounds of a chip's resident waves keep the last round's tail small.  Fewer groups
@@ -731,7 +750,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
       for (size_t r = 1; r < L; r++) {
         // step r has (r + 1) waves per 64 columns and piece, over all chunks at once
         const double wps = (double)npad / 64 * U * (r + 1) / 1024;  // waves per SIMD, all chunks
-        const bool ilp = use_ilp(ctx, wps < DKG_BINOM_ILP_WAVES);
+        const bool ilp = use_ilp(ctx, wps < binom_ilp_waves());
         // lane pairs (k_binom_pair): by default the steps with under one wave per SIMD, mode 2
         // every step (1-, 2-, 4-, 8-way n=1024 shards 0.2-0.4 ms faster;
         // profiles/r03_binomial_pairs_ab.txt)
@@ -743,7 +762,7 @@ void verify_device(dkg_ctx* ctx, size_t n, size_t t, const VerifySeg* segs, int 
         else
           (ilp ? dkgk_ilp::binom_step : dkgk::binom_step)(r, w, W, L, Cpm + c0, bin, bout, st, U, npad, Lr,
                                                           bany ? bany : bflags, c0, D, (unsigned)gw, bany != nullptr,
-                                                          binom_nt(r, npad * U));
+                                                          binom_nt(r, npad * U), !ilp && wps < binom_il_waves());
         std::swap(bin, bout);
       }
       e = bin;
