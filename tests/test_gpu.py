@@ -1374,12 +1374,16 @@ be.close()
 """
 
 
-@pytest.mark.parametrize("nt_bytes", ["1e30", "0", "3e5"])
-def test_binomial_store_kinds_env(golden, nt_bytes):
+@pytest.mark.parametrize("knobs", [{"DKG_BINOM_NT_BYTES": "1e30"}, {"DKG_BINOM_NT_BYTES": "0"},
+                                   {"DKG_BINOM_NT_BYTES": "3e5"},
+                                   {"DKG_BINOM_IL_WAVES": "1e9", "DKG_BINOM_ILP_WAVES": "0"}],
+                         ids=["plain", "nontemporal", "by_footprint", "paired_chains"])
+def test_binomial_store_kinds_env(golden, knobs):
     """The per-step binomial's rows stored plainly (DKG_BINOM_NT_BYTES=1e30), nontemporally (0, the
-    default) or by step footprint (3e5: steps 1-6 plain, the later ones nontemporal) -- the env
-    knob is read once per process, so each runs in a child: the same decisions, final shares and mpk
-    as the golden ceremony."""
+    default) or by step footprint (3e5: steps 1-6 plain, the later ones nontemporal), and every step
+    on the product-scanning copy with paired m-chains (k_binom_step<.., IL>: DKG_BINOM_IL_WAVES above
+    any step, no column-sum steps) -- the env knobs are read once per process, so each runs in a
+    child: the same decisions, final shares and mpk as the golden ceremony."""
     import json
     import os
     import subprocess
@@ -1387,7 +1391,7 @@ def test_binomial_store_kinds_env(golden, nt_bytes):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "tests", "golden", "ceremony_n64_t31.json")
-    env = dict(os.environ, DKG_BINOM_NT_BYTES=nt_bytes)
+    env = dict(os.environ, **knobs)
     p = subprocess.run([sys.executable, "-c", _NT_CHILD % (root, path)], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
