@@ -631,444 +631,6 @@ DKG_DEV void fe_sq_ps2(fe& ra, const fe& fa, fe& rb, const fe& fb) {
   asm volatile("" : : "s"(cc_a), "s"(cc_b));  // both pairs live to the end: distinct registers
 }
 
-// Four chains: each product's column summed in two accumulators (the carry and the even terms, the
-// odd terms), the two products interleaved.  A mad that reads the accumulator written two
-// instructions before still waits one state; four chains put three instructions in between.
-DKG_DEV void fe_mul_ps4(fe& ra, const fe& fa, const fe& ga, fe& rb, const fe& fb, const fe& gb) {
-  uint64_t cc_ha = 0, cc_hb = 0, cc_la = 0, cc_lb = 0;  // carry-out pairs, one per chain
-  uint64_t h_a, h_b, l_a, l_b;
-  const uint32_t f0_a = fa.v[0], f1_a = fa.v[1], f2_a = fa.v[2], f3_a = fa.v[3], f4_a = fa.v[4];
-  const uint32_t f0_b = fb.v[0], f1_b = fb.v[1], f2_b = fb.v[2], f3_b = fb.v[3], f4_b = fb.v[4];
-  const uint32_t f5_a = fa.v[5], f6_a = fa.v[6], f7_a = fa.v[7], f8_a = fa.v[8], f9_a = fa.v[9];
-  const uint32_t f5_b = fb.v[5], f6_b = fb.v[6], f7_b = fb.v[7], f8_b = fb.v[8], f9_b = fb.v[9];
-  const uint32_t g0_a = ga.v[0], g1_a = ga.v[1], g2_a = ga.v[2], g3_a = ga.v[3], g4_a = ga.v[4];
-  const uint32_t g0_b = gb.v[0], g1_b = gb.v[1], g2_b = gb.v[2], g3_b = gb.v[3], g4_b = gb.v[4];
-  const uint32_t g5_a = ga.v[5], g6_a = ga.v[6], g7_a = ga.v[7], g8_a = ga.v[8], g9_a = ga.v[9];
-  const uint32_t g5_b = gb.v[5], g6_b = gb.v[6], g7_b = gb.v[7], g8_b = gb.v[8], g9_b = gb.v[9];
-  const uint32_t g1_19_a = 19u * g1_a, g2_19_a = 19u * g2_a, g3_19_a = 19u * g3_a, g4_19_a = 19u * g4_a;
-  const uint32_t g1_19_b = 19u * g1_b, g2_19_b = 19u * g2_b, g3_19_b = 19u * g3_b, g4_19_b = 19u * g4_b;
-  const uint32_t g5_19_a = 19u * g5_a, g6_19_a = 19u * g6_a, g7_19_a = 19u * g7_a, g8_19_a = 19u * g8_a;
-  const uint32_t g5_19_b = 19u * g5_b, g6_19_b = 19u * g6_b, g7_19_b = 19u * g7_b, g8_19_b = 19u * g8_b;
-  const uint32_t g9_19_a = 19u * g9_a;
-  const uint32_t g9_19_b = 19u * g9_b;
-  const uint32_t f1_2_a = dbl32(f1_a), f3_2_a = dbl32(f3_a), f5_2_a = dbl32(f5_a), f7_2_a = dbl32(f7_a), f9_2_a = dbl32(f9_a);
-  const uint32_t f1_2_b = dbl32(f1_b), f3_2_b = dbl32(f3_b), f5_2_b = dbl32(f5_b), f7_2_b = dbl32(f7_b), f9_2_b = dbl32(f9_b);
-  h_a = mad_first_v(f0_a, g0_a, cc_ha);
-  h_b = mad_first_v(f0_b, g0_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, g9_19_a, cc_la);
-  l_b = mad_first_v(f1_2_b, g9_19_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g8_19_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g8_19_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, g7_19_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, g7_19_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g6_19_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g6_19_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, g5_19_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, g5_19_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g4_19_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g4_19_b, cc_hb);
-  mad_acc_v(l_a, f7_2_a, g3_19_a, cc_la);
-  mad_acc_v(l_b, f7_2_b, g3_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g2_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g2_19_b, cc_hb);
-  mad_acc_v(l_a, f9_2_a, g1_19_a, cc_la);
-  mad_acc_v(l_b, f9_2_b, g1_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 0, h_a)
-  FE_LIMB(rb, 0, h_b)
-  mad_acc_v(h_a, f0_a, g1_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g1_b, cc_hb);
-  l_a = mad_first_v(f1_a, g0_a, cc_la);
-  l_b = mad_first_v(f1_b, g0_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g9_19_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g9_19_b, cc_hb);
-  mad_acc_v(l_a, f3_a, g8_19_a, cc_la);
-  mad_acc_v(l_b, f3_b, g8_19_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g7_19_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g7_19_b, cc_hb);
-  mad_acc_v(l_a, f5_a, g6_19_a, cc_la);
-  mad_acc_v(l_b, f5_b, g6_19_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g5_19_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g5_19_b, cc_hb);
-  mad_acc_v(l_a, f7_a, g4_19_a, cc_la);
-  mad_acc_v(l_b, f7_b, g4_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g3_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g3_19_b, cc_hb);
-  mad_acc_v(l_a, f9_a, g2_19_a, cc_la);
-  mad_acc_v(l_b, f9_b, g2_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 1, h_a)
-  FE_LIMB(rb, 1, h_b)
-  mad_acc_v(h_a, f0_a, g2_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g2_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, g1_a, cc_la);
-  l_b = mad_first_v(f1_2_b, g1_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g0_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g0_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, g9_19_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, g9_19_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g8_19_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g8_19_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, g7_19_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, g7_19_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g6_19_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g6_19_b, cc_hb);
-  mad_acc_v(l_a, f7_2_a, g5_19_a, cc_la);
-  mad_acc_v(l_b, f7_2_b, g5_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g4_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g4_19_b, cc_hb);
-  mad_acc_v(l_a, f9_2_a, g3_19_a, cc_la);
-  mad_acc_v(l_b, f9_2_b, g3_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 2, h_a)
-  FE_LIMB(rb, 2, h_b)
-  mad_acc_v(h_a, f0_a, g3_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g3_b, cc_hb);
-  l_a = mad_first_v(f1_a, g2_a, cc_la);
-  l_b = mad_first_v(f1_b, g2_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g1_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g1_b, cc_hb);
-  mad_acc_v(l_a, f3_a, g0_a, cc_la);
-  mad_acc_v(l_b, f3_b, g0_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g9_19_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g9_19_b, cc_hb);
-  mad_acc_v(l_a, f5_a, g8_19_a, cc_la);
-  mad_acc_v(l_b, f5_b, g8_19_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g7_19_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g7_19_b, cc_hb);
-  mad_acc_v(l_a, f7_a, g6_19_a, cc_la);
-  mad_acc_v(l_b, f7_b, g6_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g5_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g5_19_b, cc_hb);
-  mad_acc_v(l_a, f9_a, g4_19_a, cc_la);
-  mad_acc_v(l_b, f9_b, g4_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 3, h_a)
-  FE_LIMB(rb, 3, h_b)
-  mad_acc_v(h_a, f0_a, g4_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g4_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, g3_a, cc_la);
-  l_b = mad_first_v(f1_2_b, g3_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g2_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g2_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, g1_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, g1_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g0_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g0_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, g9_19_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, g9_19_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g8_19_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g8_19_b, cc_hb);
-  mad_acc_v(l_a, f7_2_a, g7_19_a, cc_la);
-  mad_acc_v(l_b, f7_2_b, g7_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g6_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g6_19_b, cc_hb);
-  mad_acc_v(l_a, f9_2_a, g5_19_a, cc_la);
-  mad_acc_v(l_b, f9_2_b, g5_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 4, h_a)
-  FE_LIMB(rb, 4, h_b)
-  mad_acc_v(h_a, f0_a, g5_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g5_b, cc_hb);
-  l_a = mad_first_v(f1_a, g4_a, cc_la);
-  l_b = mad_first_v(f1_b, g4_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g3_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g3_b, cc_hb);
-  mad_acc_v(l_a, f3_a, g2_a, cc_la);
-  mad_acc_v(l_b, f3_b, g2_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g1_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g1_b, cc_hb);
-  mad_acc_v(l_a, f5_a, g0_a, cc_la);
-  mad_acc_v(l_b, f5_b, g0_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g9_19_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g9_19_b, cc_hb);
-  mad_acc_v(l_a, f7_a, g8_19_a, cc_la);
-  mad_acc_v(l_b, f7_b, g8_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g7_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g7_19_b, cc_hb);
-  mad_acc_v(l_a, f9_a, g6_19_a, cc_la);
-  mad_acc_v(l_b, f9_b, g6_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 5, h_a)
-  FE_LIMB(rb, 5, h_b)
-  mad_acc_v(h_a, f0_a, g6_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g6_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, g5_a, cc_la);
-  l_b = mad_first_v(f1_2_b, g5_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g4_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g4_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, g3_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, g3_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g2_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g2_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, g1_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, g1_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g0_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g0_b, cc_hb);
-  mad_acc_v(l_a, f7_2_a, g9_19_a, cc_la);
-  mad_acc_v(l_b, f7_2_b, g9_19_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g8_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g8_19_b, cc_hb);
-  mad_acc_v(l_a, f9_2_a, g7_19_a, cc_la);
-  mad_acc_v(l_b, f9_2_b, g7_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 6, h_a)
-  FE_LIMB(rb, 6, h_b)
-  mad_acc_v(h_a, f0_a, g7_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g7_b, cc_hb);
-  l_a = mad_first_v(f1_a, g6_a, cc_la);
-  l_b = mad_first_v(f1_b, g6_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g5_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g5_b, cc_hb);
-  mad_acc_v(l_a, f3_a, g4_a, cc_la);
-  mad_acc_v(l_b, f3_b, g4_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g3_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g3_b, cc_hb);
-  mad_acc_v(l_a, f5_a, g2_a, cc_la);
-  mad_acc_v(l_b, f5_b, g2_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g1_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g1_b, cc_hb);
-  mad_acc_v(l_a, f7_a, g0_a, cc_la);
-  mad_acc_v(l_b, f7_b, g0_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g9_19_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g9_19_b, cc_hb);
-  mad_acc_v(l_a, f9_a, g8_19_a, cc_la);
-  mad_acc_v(l_b, f9_b, g8_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 7, h_a)
-  FE_LIMB(rb, 7, h_b)
-  mad_acc_v(h_a, f0_a, g8_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g8_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, g7_a, cc_la);
-  l_b = mad_first_v(f1_2_b, g7_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g6_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g6_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, g5_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, g5_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g4_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g4_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, g3_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, g3_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g2_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g2_b, cc_hb);
-  mad_acc_v(l_a, f7_2_a, g1_a, cc_la);
-  mad_acc_v(l_b, f7_2_b, g1_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g0_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g0_b, cc_hb);
-  mad_acc_v(l_a, f9_2_a, g9_19_a, cc_la);
-  mad_acc_v(l_b, f9_2_b, g9_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 8, h_a)
-  FE_LIMB(rb, 8, h_b)
-  mad_acc_v(h_a, f0_a, g9_a, cc_ha);
-  mad_acc_v(h_b, f0_b, g9_b, cc_hb);
-  l_a = mad_first_v(f1_a, g8_a, cc_la);
-  l_b = mad_first_v(f1_b, g8_b, cc_lb);
-  mad_acc_v(h_a, f2_a, g7_a, cc_ha);
-  mad_acc_v(h_b, f2_b, g7_b, cc_hb);
-  mad_acc_v(l_a, f3_a, g6_a, cc_la);
-  mad_acc_v(l_b, f3_b, g6_b, cc_lb);
-  mad_acc_v(h_a, f4_a, g5_a, cc_ha);
-  mad_acc_v(h_b, f4_b, g5_b, cc_hb);
-  mad_acc_v(l_a, f5_a, g4_a, cc_la);
-  mad_acc_v(l_b, f5_b, g4_b, cc_lb);
-  mad_acc_v(h_a, f6_a, g3_a, cc_ha);
-  mad_acc_v(h_b, f6_b, g3_b, cc_hb);
-  mad_acc_v(l_a, f7_a, g2_a, cc_la);
-  mad_acc_v(l_b, f7_b, g2_b, cc_lb);
-  mad_acc_v(h_a, f8_a, g1_a, cc_ha);
-  mad_acc_v(h_b, f8_b, g1_b, cc_hb);
-  mad_acc_v(l_a, f9_a, g0_a, cc_la);
-  mad_acc_v(l_b, f9_b, g0_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 9, h_a)
-  FE_LIMB(rb, 9, h_b)
-  FE_FOLD(ra, h_a)
-  FE_FOLD(rb, h_b)
-  asm volatile("" : : "s"(cc_ha), "s"(cc_hb), "s"(cc_la), "s"(cc_lb));  // distinct registers
-}
-
-DKG_DEV void fe_sq_ps4(fe& ra, const fe& fa, fe& rb, const fe& fb) {
-  uint64_t cc_ha = 0, cc_hb = 0, cc_la = 0, cc_lb = 0;  // carry-out pairs, one per chain
-  uint64_t h_a, h_b, l_a, l_b;
-  const uint32_t f0_a = fa.v[0], f1_a = fa.v[1], f2_a = fa.v[2], f3_a = fa.v[3], f4_a = fa.v[4];
-  const uint32_t f0_b = fb.v[0], f1_b = fb.v[1], f2_b = fb.v[2], f3_b = fb.v[3], f4_b = fb.v[4];
-  const uint32_t f5_a = fa.v[5], f6_a = fa.v[6], f7_a = fa.v[7], f8_a = fa.v[8], f9_a = fa.v[9];
-  const uint32_t f5_b = fb.v[5], f6_b = fb.v[6], f7_b = fb.v[7], f8_b = fb.v[8], f9_b = fb.v[9];
-  const uint32_t f0_2_a = dbl32(f0_a), f1_2_a = dbl32(f1_a), f2_2_a = dbl32(f2_a), f3_2_a = dbl32(f3_a), f4_2_a = dbl32(f4_a);
-  const uint32_t f0_2_b = dbl32(f0_b), f1_2_b = dbl32(f1_b), f2_2_b = dbl32(f2_b), f3_2_b = dbl32(f3_b), f4_2_b = dbl32(f4_b);
-  const uint32_t f5_2_a = dbl32(f5_a), f6_2_a = dbl32(f6_a), f7_2_a = dbl32(f7_a), f8_2_a = dbl32(f8_a), f9_2_a = dbl32(f9_a);
-  const uint32_t f5_2_b = dbl32(f5_b), f6_2_b = dbl32(f6_b), f7_2_b = dbl32(f7_b), f8_2_b = dbl32(f8_b), f9_2_b = dbl32(f9_b);
-  const uint32_t f1_4_a = dbl32(f1_2_a), f3_4_a = dbl32(f3_2_a), f5_4_a = dbl32(f5_2_a), f7_4_a = dbl32(f7_2_a);
-  const uint32_t f1_4_b = dbl32(f1_2_b), f3_4_b = dbl32(f3_2_b), f5_4_b = dbl32(f5_2_b), f7_4_b = dbl32(f7_2_b);
-  const uint32_t f5_19_a = 19u * f5_a, f6_19_a = 19u * f6_a, f7_19_a = 19u * f7_a, f8_19_a = 19u * f8_a;
-  const uint32_t f5_19_b = 19u * f5_b, f6_19_b = 19u * f6_b, f7_19_b = 19u * f7_b, f8_19_b = 19u * f8_b;
-  const uint32_t f9_19_a = 19u * f9_a;
-  const uint32_t f9_19_b = 19u * f9_b;
-  h_a = mad_first_v(f0_a, f0_a, cc_ha);
-  h_b = mad_first_v(f0_b, f0_b, cc_hb);
-  l_a = mad_first_v(f1_4_a, f9_19_a, cc_la);
-  l_b = mad_first_v(f1_4_b, f9_19_b, cc_lb);
-  mad_acc_v(h_a, f2_2_a, f8_19_a, cc_ha);
-  mad_acc_v(h_b, f2_2_b, f8_19_b, cc_hb);
-  mad_acc_v(l_a, f3_4_a, f7_19_a, cc_la);
-  mad_acc_v(l_b, f3_4_b, f7_19_b, cc_lb);
-  mad_acc_v(h_a, f4_2_a, f6_19_a, cc_ha);
-  mad_acc_v(h_b, f4_2_b, f6_19_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, f5_19_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, f5_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 0, h_a)
-  FE_LIMB(rb, 0, h_b)
-  mad_acc_v(h_a, f0_2_a, f1_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f1_b, cc_hb);
-  l_a = mad_first_v(f2_2_a, f9_19_a, cc_la);
-  l_b = mad_first_v(f2_2_b, f9_19_b, cc_lb);
-  mad_acc_v(h_a, f3_2_a, f8_19_a, cc_ha);
-  mad_acc_v(h_b, f3_2_b, f8_19_b, cc_hb);
-  mad_acc_v(l_a, f4_2_a, f7_19_a, cc_la);
-  mad_acc_v(l_b, f4_2_b, f7_19_b, cc_lb);
-  mad_acc_v(h_a, f5_2_a, f6_19_a, cc_ha);
-  mad_acc_v(h_b, f5_2_b, f6_19_b, cc_hb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 1, h_a)
-  FE_LIMB(rb, 1, h_b)
-  mad_acc_v(h_a, f0_2_a, f2_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f2_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f1_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f1_b, cc_lb);
-  mad_acc_v(h_a, f3_4_a, f9_19_a, cc_ha);
-  mad_acc_v(h_b, f3_4_b, f9_19_b, cc_hb);
-  mad_acc_v(l_a, f4_2_a, f8_19_a, cc_la);
-  mad_acc_v(l_b, f4_2_b, f8_19_b, cc_lb);
-  mad_acc_v(h_a, f5_4_a, f7_19_a, cc_ha);
-  mad_acc_v(h_b, f5_4_b, f7_19_b, cc_hb);
-  mad_acc_v(l_a, f6_a, f6_19_a, cc_la);
-  mad_acc_v(l_b, f6_b, f6_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 2, h_a)
-  FE_LIMB(rb, 2, h_b)
-  mad_acc_v(h_a, f0_2_a, f3_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f3_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f2_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f2_b, cc_lb);
-  mad_acc_v(h_a, f4_2_a, f9_19_a, cc_ha);
-  mad_acc_v(h_b, f4_2_b, f9_19_b, cc_hb);
-  mad_acc_v(l_a, f5_2_a, f8_19_a, cc_la);
-  mad_acc_v(l_b, f5_2_b, f8_19_b, cc_lb);
-  mad_acc_v(h_a, f6_2_a, f7_19_a, cc_ha);
-  mad_acc_v(h_b, f6_2_b, f7_19_b, cc_hb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 3, h_a)
-  FE_LIMB(rb, 3, h_b)
-  mad_acc_v(h_a, f0_2_a, f4_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f4_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f3_2_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f3_2_b, cc_lb);
-  mad_acc_v(h_a, f2_a, f2_a, cc_ha);
-  mad_acc_v(h_b, f2_b, f2_b, cc_hb);
-  mad_acc_v(l_a, f5_4_a, f9_19_a, cc_la);
-  mad_acc_v(l_b, f5_4_b, f9_19_b, cc_lb);
-  mad_acc_v(h_a, f6_2_a, f8_19_a, cc_ha);
-  mad_acc_v(h_b, f6_2_b, f8_19_b, cc_hb);
-  mad_acc_v(l_a, f7_2_a, f7_19_a, cc_la);
-  mad_acc_v(l_b, f7_2_b, f7_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 4, h_a)
-  FE_LIMB(rb, 4, h_b)
-  mad_acc_v(h_a, f0_2_a, f5_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f5_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f4_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f4_b, cc_lb);
-  mad_acc_v(h_a, f2_2_a, f3_a, cc_ha);
-  mad_acc_v(h_b, f2_2_b, f3_b, cc_hb);
-  mad_acc_v(l_a, f6_2_a, f9_19_a, cc_la);
-  mad_acc_v(l_b, f6_2_b, f9_19_b, cc_lb);
-  mad_acc_v(h_a, f7_2_a, f8_19_a, cc_ha);
-  mad_acc_v(h_b, f7_2_b, f8_19_b, cc_hb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 5, h_a)
-  FE_LIMB(rb, 5, h_b)
-  mad_acc_v(h_a, f0_2_a, f6_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f6_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f5_2_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f5_2_b, cc_lb);
-  mad_acc_v(h_a, f2_2_a, f4_a, cc_ha);
-  mad_acc_v(h_b, f2_2_b, f4_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, f3_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, f3_b, cc_lb);
-  mad_acc_v(h_a, f7_4_a, f9_19_a, cc_ha);
-  mad_acc_v(h_b, f7_4_b, f9_19_b, cc_hb);
-  mad_acc_v(l_a, f8_a, f8_19_a, cc_la);
-  mad_acc_v(l_b, f8_b, f8_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 6, h_a)
-  FE_LIMB(rb, 6, h_b)
-  mad_acc_v(h_a, f0_2_a, f7_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f7_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f6_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f6_b, cc_lb);
-  mad_acc_v(h_a, f2_2_a, f5_a, cc_ha);
-  mad_acc_v(h_b, f2_2_b, f5_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, f4_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, f4_b, cc_lb);
-  mad_acc_v(h_a, f8_2_a, f9_19_a, cc_ha);
-  mad_acc_v(h_b, f8_2_b, f9_19_b, cc_hb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 7, h_a)
-  FE_LIMB(rb, 7, h_b)
-  mad_acc_v(h_a, f0_2_a, f8_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f8_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f7_2_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f7_2_b, cc_lb);
-  mad_acc_v(h_a, f2_2_a, f6_a, cc_ha);
-  mad_acc_v(h_b, f2_2_b, f6_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, f5_2_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, f5_2_b, cc_lb);
-  mad_acc_v(h_a, f4_a, f4_a, cc_ha);
-  mad_acc_v(h_b, f4_b, f4_b, cc_hb);
-  mad_acc_v(l_a, f9_2_a, f9_19_a, cc_la);
-  mad_acc_v(l_b, f9_2_b, f9_19_b, cc_lb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 8, h_a)
-  FE_LIMB(rb, 8, h_b)
-  mad_acc_v(h_a, f0_2_a, f9_a, cc_ha);
-  mad_acc_v(h_b, f0_2_b, f9_b, cc_hb);
-  l_a = mad_first_v(f1_2_a, f8_a, cc_la);
-  l_b = mad_first_v(f1_2_b, f8_b, cc_lb);
-  mad_acc_v(h_a, f2_2_a, f7_a, cc_ha);
-  mad_acc_v(h_b, f2_2_b, f7_b, cc_hb);
-  mad_acc_v(l_a, f3_2_a, f6_a, cc_la);
-  mad_acc_v(l_b, f3_2_b, f6_b, cc_lb);
-  mad_acc_v(h_a, f4_2_a, f5_a, cc_ha);
-  mad_acc_v(h_b, f4_2_b, f5_b, cc_hb);
-  h_a += l_a;
-  h_b += l_b;
-  FE_LIMB(ra, 9, h_a)
-  FE_LIMB(rb, 9, h_b)
-  FE_FOLD(ra, h_a)
-  FE_FOLD(rb, h_b)
-  asm volatile("" : : "s"(cc_ha), "s"(cc_hb), "s"(cc_la), "s"(cc_lb));  // distinct registers
-}
 // ---- END generated pair products
 
 DKG_DEV void fe_mul_small_ps(fe& r, const fe& a, uint32_t k) {
@@ -1220,7 +782,8 @@ DKG_DEV void fe_mul_small(fe& r, const fe& a, uint32_t k) {
 
 // Two independent products at once (the pair versions above; the column-sum flavour already has ten
 // independent chains per product and just runs both).  DKG_FE_PAIR=0 keeps single products, 1 the
-// two-chain interleave, 2 the four-chain split (A/B).
+// two-chain interleave, 2 the four-chain split (A/B only: its functions are generated with
+// tools/gen_fe_pair.py --four; measured 4-5 % slower, profiles/r06_pair_ab.txt).
 #ifndef DKG_FE_PAIR
 #define DKG_FE_PAIR 1
 #endif

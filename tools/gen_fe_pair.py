@@ -4,7 +4,9 @@ Each is the single product (fe_mul_ps / fe_sq_ps) written twice with suffixed lo
 statements interleaved, so consecutive v_mad_u64_u32 belong to different chains; every chain keeps
 its own carry-out SGPR pair (cc_a / cc_b) so the hardware sees no back-to-back write of one SGPR.
 The generated text replaces the block between the BEGIN/END markers (inserted before
-fe_mul_small_ps the first time).  Run from the repository root: python tools/gen_fe_pair.py
+fe_mul_small_ps the first time): python tools/gen_fe_pair.py.  --four adds the four-chain flavour
+fe_mul_ps4 / fe_sq_ps4 (two accumulators per product; DKG_FE_PAIR=2, for A/B builds: measured
+slower); --check only compares.
 """
 import os
 import re
@@ -91,11 +93,12 @@ code=("// Two independent products in one instruction stream (pair versions of f
       "// Generated from the single versions (tools/gen_fe_pair.py); the same terms in the same order.\n")
 code+=gen('fe_mul_ps','fe_mul_ps2','fe& ra, const fe& fa, const fe& ga, fe& rb, const fe& fb, const fe& gb')+'\n\n'
 code+=gen('fe_sq_ps','fe_sq_ps2','fe& ra, const fe& fa, fe& rb, const fe& fb')+'\n\n'
-code+=("// Four chains: each product's column summed in two accumulators (the carry and the even terms, the\n"
-       "// odd terms), the two products interleaved.  A mad that reads the accumulator written two\n"
-       "// instructions before still waits one state; four chains put three instructions in between.\n")
-code+=gen4('fe_mul_ps','fe_mul_ps4','fe& ra, const fe& fa, const fe& ga, fe& rb, const fe& fb, const fe& gb')+'\n\n'
-code+=gen4('fe_sq_ps','fe_sq_ps4','fe& ra, const fe& fa, fe& rb, const fe& fb')+'\n'
+if '--four' in sys.argv:  # the four-chain flavour (DKG_FE_PAIR=2), measured 4-5 % slower: A/B builds only
+    code+=("// Four chains: each product's column summed in two accumulators (the carry and the even terms,\n"
+           "// the odd terms), the two products interleaved: one s_nop per four mads instead of two, for a\n"
+           "// 64-bit add per column (profiles/r06_pair_ab.txt: slower).\n")
+    code+=gen4('fe_mul_ps','fe_mul_ps4','fe& ra, const fe& fa, const fe& ga, fe& rb, const fe& fb, const fe& gb')+'\n\n'
+    code+=gen4('fe_sq_ps','fe_sq_ps4','fe& ra, const fe& fa, fe& rb, const fe& fb')+'\n'
 begin='// ---- BEGIN generated pair products (tools/gen_fe_pair.py)\n'
 end='// ---- END generated pair products\n'
 if begin in s:
